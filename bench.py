@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident decode + 5-tuple ACL classify on MI355X (BASELINE.json metric).
+
+A step = one ppe_classify launch over one resident batch (default config C1: 1M × 64 B IPv4/UDP packets, 256
+five-tuple ACL rules).  Steps rotate over --nbufs distinct batches (inputs + outputs ≈ 84 MB each) so the working
+set exceeds the 256 MiB Infinity Cache and every step streams its packets from HBM.  With --gpus N (launched by
+torch.distributed.run) each rank classifies its own 1M-packet shard (weak scaling, no data-path collective);
+`value` = all packets processed ÷ the slowest rank's time.
+
+Prints ONE JSON line (rank 0).  Also: `roofline` from HIP-event kernel durations on the launch stream, and
+`cpu_baseline` = the oracle's C restatement (tree-walk ACL, run-to-completion pthread shards like mainloop) timed on
+this host's cores (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path[:0] = [str(ROOT / "packet-process-engine_amd"), str(ROOT / "oracle")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (load torch's HIP runtime before libppe_hip.so so both share it)
+
+from ppe import Engine, synth  # noqa: E402
+
+METRIC = "Mpps device-resident decode+ACL classify, 64B & 1500B pkts, 1/2/4/8 GPUs"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+NOW = 1_700_000_000
+
+
+def algorithmic_bytes(stride: int) -> tuple[float, float]:
+    """(read, write) bytes per packet the kernel must move: the 64-B header window + 4-B length
+    read; verdict + flow hash + ACL hit (12 B) + one compacted index (4 B) + the tile count (4 B / 64 packets)
+    written.  Payload bytes past the window are never touched (IMIX included)."""
+    return float(min(stride, 64)) + 4.0, 12.0 + 4.0 + 4.0 / 64.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="C1", choices=sorted(synth.CONFIGS))
+    ap.add_argument("--n", type=int, default=0, help="packets per GPU (default: the config's)")
+    ap.add_argument("--stride", type=int, default=64)
+    ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: > 256 MiB total)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cfgd = synth.CONFIGS[args.config]
+    n = args.n or cfgd["n"]
+    stride = args.stride
+    rules = synth.make_rules(cfgd["rules"])
+    per_buf = n * (stride + 4 + 16)
+    nbufs = args.nbufs or max(2, int(np.ceil(300e6 / per_buf)))
+
+    eng = Engine(local)
+    acl = eng.commit(rules, default_action=1)
+    cfg = eng.cfg(now_seconds=NOW)
+
+    bufs = []
+    lens0 = None
+    for b in range(nbufs):
+        pk = synth.make_packets(n, rules, seed=synth.SEED + 1 + 7919 * (rank * 64 + b), kind=cfgd["kind"],
+                                stride=stride)
+        if lens0 is None:
+            lens0 = pk["len"]
+        hdr = torch.from_numpy(pk["hdr"]).to(dev)
+        lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
+        out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
+               "flow_hash": torch.empty(n, dtype=torch.int32, device=dev),
+               "acl_hit": torch.empty(n, dtype=torch.int32, device=dev),
+               "fw_idx": torch.empty(n, dtype=torch.int32, device=dev),
+               "drop_idx": torch.empty(n, dtype=torch.int32, device=dev),
+               "tile_cnt": torch.empty((n + 63) // 64, dtype=torch.int32, device=dev)}
+        bufs.append((hdr, lens, out, pk if b == 0 else None))
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i):
+        hdr, lens, out, _ = bufs[i % nbufs]
+        eng.classify_torch(hdr, lens, out, cfg=cfg, stream=stream)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    eng.timing(True)
+    eng.timing_read(reset=True)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(i)
+    ev1.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    elapsed_ms = ev0.elapsed_time(ev1)
+    kern_ms, launches = eng.timing_read(reset=True)
+    eng.timing(False)
+    my_ms = max(elapsed_ms, 1e-9)
+    if dist is not None:
+        t = torch.tensor([my_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        my_ms = float(t.item())
+
+    total_pkts = n * args.steps * world
+    mpps = total_pkts / (my_ms / 1e3) / 1e6
+    rd, wr = algorithmic_bytes(stride)
+    kern_avg_ms = kern_ms / max(launches, 1)
+    achieved = (rd + wr) * n / (kern_avg_ms / 1e3) / 1e9
+
+    # ---- parity spot check of the timed buffers (batch 0) against the oracle, 1/16 sample ----
+    parity = None
+    if rank == 0:
+        import pyoracle
+        hdr, lens, out, pk = bufs[0]
+        o = pyoracle.Oracle(rules, default_action=1)
+        m = min(n, 1 << 16)
+        ref = o.classify_batch(pk["hdr"][:m], pk["len"][:m], cfg=o.cfg(now_seconds=NOW), nthreads=8)
+        got_v = out["verdict"][:m].cpu().numpy().view(np.uint32)
+        got_h = out["flow_hash"][:m].cpu().numpy().view(np.uint32)
+        got_a = out["acl_hit"][:m].cpu().numpy()
+        parity = bool(np.array_equal(got_v, ref["verdict"]) and np.array_equal(got_h, ref["flow_hash"])
+                      and np.array_equal(got_a, ref["acl_hit"]))
+
+    # ---- host-inclusive rate (pinned host buffers, H2D + classify + D2H pipeline) ----
+    host_mpps = None
+    if rank == 0 and world == 1 and not args.no_host_inclusive:
+        pk = bufs[0][3]
+        ph = torch.from_numpy(pk["hdr"]).pin_memory()
+        pl = torch.from_numpy(pk["len"].view(np.int32)).pin_memory()
+        res = {k: torch.empty(n, dtype=torch.int32).pin_memory() for k in ("verdict", "flow_hash", "acl_hit")}
+        from ppe import abi
+        import ctypes as C
+        b = abi.Batch(ph.data_ptr(), pl.data_ptr(), None, n, stride)
+        r = abi.Result(res["verdict"].data_ptr(), res["flow_hash"].data_ptr(), res["acl_hit"].data_ptr(),
+                       None, None, None, None)
+        reps = 5
+        eng.lib.ppe_classify_host(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), 1 << 18)
+        th = time.perf_counter()
+        for _ in range(reps):
+            rc = eng.lib.ppe_classify_host(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), 1 << 18)
+            assert rc == 0
+        host_mpps = n * reps / (time.perf_counter() - th) / 1e6
+
+    # ---- CPU baseline: oracle restatement (tree-walk ACL) on this host, rank 0, N = 1 ----
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import pyoracle
+        pk = bufs[0][3]
+        img = eng.image()
+        o = pyoracle.Oracle(rules, default_action=1, image=img)
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        reps = 16
+        o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=thr, use_tree=True)
+        tc = time.perf_counter()
+        for _ in range(reps):
+            o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=thr, use_tree=True)
+        cpu_s = time.perf_counter() - tc
+        t1 = time.perf_counter()
+        o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=1, use_tree=True)
+        one_s = time.perf_counter() - t1
+        cpu = {"value": n * reps / cpu_s / 1e6, "unit": "Mpps", "cores": thr, "kind": "port",
+               "sample": f"{reps} passes over the {n}-packet {args.config} batch ({n * reps} packets), "
+                         f"{thr} pthreads run-to-completion shards; 1-thread rate {n / one_s / 1e6:.2f} Mpps",
+               "single_thread_mpps": n / one_s / 1e6}
+
+    if rank == 0:
+        li = eng.launch_info()
+        line = {
+            "metric": METRIC, "value": round(mpps, 2), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(my_ms / args.steps, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"{args.config}: {n} x {'64B IPv4/UDP' if cfgd['kind'] == 'udp64' else 'IMIX'}"
+                                   f" packets per GPU, {cfgd['rules']} five-tuple ACL rules",
+                       "packets_per_gpu": n, "rules": cfgd["rules"], "window_bytes": stride, "resident_batches": nbufs,
+                       "parallelism": f"batch-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": rd + wr,
+                         "launches_timed": launches},
+            "cpu_baseline": cpu,
+            "host_inclusive_mpps": round(host_mpps, 2) if host_mpps else None,
+            "parity_sample_ok": parity,
+            "acl": {k: acl[k] for k in ("n_rules", "n_nodes", "max_depth", "blob_bytes", "lds_resident")},
+            "launch": li,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,218 @@
+/*
+ * ppe_hip.h — C ABI of the MI355X-native decode + 5-tuple ACL classify engine.
+ *
+ * One call classifies a whole batch of packets on the GPU: Ethernet → [one VLAN tag] → IPv4 → TCP|UDP header parse,
+ * 5-tuple extraction, the symmetric TluHash flow hash and the first-match ACL lookup, with per-reason counters and
+ * per-tile ballot-compacted FW/DROP index lists.  It replaces, for a whole batch at once, the reference's per-mbuf
+ * hot path:
+ *
+ *   Decode(mbuf)                         dataplane/src/decode/decode.c:19-28
+ *   └ DecodeEthernet / DecodeVLAN        dataplane/src/decode/decode-ethernet.c:23-115, decode-vlan.c:23-89
+ *   └ DecodeIPV4 / DecodeIPV4Packet      dataplane/src/decode/decode-ipv4.c:27-247
+ *   └ DecodeUDP / DecodeTCP              dataplane/src/decode/decode-udp.c:16-71, decode-tcp.c:135-222
+ *   └ FlowHandlePacket → flow_hashfn     dataplane/src/flow/flow.c:181-245,271-292, flow/tluhash.h:7-35
+ *     └ (first packet) syn_check, DP_Acl_Lookup   dataplane/src/flow/flow.c:204-243
+ *
+ * Stateless semantics: every packet is treated as the first packet of its flow (flow-table miss), which is the
+ * reference behaviour for the unique-flow inputs of the benchmark configs.  Fragments and
+ * packets whose headers extend past the header window are PUNTed to the host (status PPE_ST_FRAG /
+ * PPE_ST_WINDOW_PUNT); the reference hands fragments to Defrag (decode-ipv4.c:216-239), out of scope here.
+ *
+ * All pointers in ppe_batch_t / ppe_result_t passed to ppe_classify() are DEVICE pointers (hipMalloc / torch
+ * cuda tensors) on the context's device.  ppe_classify_host() takes host pointers and runs the pipelined
+ * H2D → classify → D2H path.  Functions return 0 or a negative errno-style code (PPE_E*).
+ * Thread-compatible per context: one host thread per context (as one run-to-completion core per mainloop).
+ */
+#ifndef PPE_HIP_H
+#define PPE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "ppe_acl.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPE_ABI_VERSION 1
+
+/* error codes (negative return values) */
+#define PPE_OK       0
+#define PPE_EINVAL  (-22)
+#define PPE_ENOMEM  (-12)
+#define PPE_ENODEV  (-19)
+#define PPE_EIO     (-5)
+#define PPE_ENOTSUP (-95)
+
+/* ---- per-packet verdict word: status (bits 0-7) | action (bits 8-15) | flags (bits 16-31) ---- */
+/* status = the terminal reason, one per reference drop/ok reason (dataplane/src/decode/decode-statistic.h:239-327) */
+enum ppe_status {
+    PPE_ST_ACL_FW = 0,            /* ACL passed (hit with action FW, or default FW)      STAT_ACL_FW        flow.c:240   */
+    PPE_ST_ACL_DROP = 1,          /* ACL drop                                             STAT_ACL_DROP      flow.c:234   */
+    PPE_ST_L2_HEADER_ERR = 2,     /* len<14, or all-zero dst/src MAC                      decode-ethernet.c:29-54      */
+    PPE_ST_L2_UNSUPPORT = 3,      /* ethertype not 0x0800/0x8100/0x9100                   decode-ethernet.c:102-111    */
+    PPE_ST_VLAN_HEADER_ERR = 4,   /* len<4 at a VLAN tag                                  decode-vlan.c:28-33          */
+    PPE_ST_VLAN_LAYER_EXCEED = 5, /* second VLAN tag                                      decode-vlan.c:35-39          */
+    PPE_ST_VLAN_UNSUPPORT = 6,    /* inner type not 0x0800/0x8100/0x9100                  decode-vlan.c:76-84          */
+    PPE_ST_IPV4_HEADER_ERR = 7,   /* len<20 or ihl*4<20                                   decode-ipv4.c:30-48          */
+    PPE_ST_IPV4_VERSION_ERR = 8,  /* version != 4                                         decode-ipv4.c:36-40          */
+    PPE_ST_IPV4_LEN_ERR = 9,      /* ip_len<ihl*4 or len<ip_len                           decode-ipv4.c:50-60          */
+    PPE_ST_FRAG_LEN_ERR = 10,     /* fragment with zero payload                           decode-ipv4.c:227-232        */
+    PPE_ST_FRAG = 11,             /* fragment → Defrag (PUNT to host)                     decode-ipv4.c:216-239        */
+    PPE_ST_IPV4_UNSUPPORT = 12,   /* protocol not TCP/UDP                                 decode-ipv4.c:347-357        */
+    PPE_ST_UDP_HEADER_ERR = 13,   /* l4len<8                                              decode-udp.c:18-22           */
+    PPE_ST_UDP_LEN_ERR = 14,      /* uh_len != l4len                                      decode-udp.c:26-36           */
+    PPE_ST_TCP_HEADER_ERR = 15,   /* l4len<20                                             decode-tcp.c:140-144         */
+    PPE_ST_TCP_LEN_ERR = 16,      /* l4len<hlen or (u8)(hlen-20)>40                        decode-tcp.c:148-160         */
+    PPE_ST_FLOW_TCP_NO_SYN_FIRST = 17, /* flow miss, TCP without SYN, syn_check on        flow.c:204-214               */
+    PPE_ST_WINDOW_PUNT = 18,      /* needed header bytes lie beyond the header window (engine-specific PUNT)          */
+    PPE_ST__COUNT = 19
+};
+
+enum ppe_action { PPE_ACT_FW = 0, PPE_ACT_DROP = 1, PPE_ACT_PUNT = 2 };
+
+#define PPE_F_VLAN   0x0001u   /* one VLAN tag decoded (mbuf->vlan_idx == 1)          */
+#define PPE_F_L4     0x0002u   /* 5-tuple valid (reached FlowHandlePacket)            */
+#define PPE_F_TCP    0x0004u
+#define PPE_F_SYN    0x0008u   /* TCP SYN flag set                                    */
+#define PPE_F_ACL    0x0010u   /* ACL consulted (acl_hit is its result)               */
+#define PPE_F_FRAG   0x0020u   /* IPv4 fragment seen                                  */
+
+#define PPE_VERDICT_STATUS(v) ((v) & 0xffu)
+#define PPE_VERDICT_ACTION(v) (((v) >> 8) & 0xffu)
+#define PPE_VERDICT_FLAGS(v)  ((v) >> 16)
+
+/* ---- per-reason counters (sums over every batch since the last clear) ---- */
+enum ppe_counter {
+    PPE_C_L2_HEADERLEN_ERR = 0, PPE_C_L2_UNSUPPORT, PPE_C_L2_RX_OK,
+    PPE_C_VLAN_HEADERLEN_ERR, PPE_C_VLAN_LAYER_EXCEED, PPE_C_VLAN_UNSUPPORT, PPE_C_VLAN_RX_OK,
+    PPE_C_IPV4_HEADERLEN_ERR, PPE_C_IPV4_VERSION_ERR, PPE_C_IPV4_PKTLEN_ERR, PPE_C_IPV4_UNSUPPORT, PPE_C_IPV4_RX_OK,
+    PPE_C_FRAG_FRAGLEN_ERR, PPE_C_FRAG_PUNT,
+    PPE_C_UDP_HEADERLEN_ERR, PPE_C_UDP_PKTLEN_ERR, PPE_C_UDP_RX_OK,
+    PPE_C_TCP_HEADERLEN_ERR, PPE_C_TCP_PKTLEN_ERR, PPE_C_TCP_RX_OK,
+    PPE_C_ACL_DROP, PPE_C_ACL_FW,
+    PPE_C_FLOW_PROC_OK, PPE_C_FLOW_PROC_FAIL, PPE_C_FLOW_TCP_NO_SYN_FIRST,
+    PPE_C_OUT_FW, PPE_C_OUT_DROP, PPE_C_OUT_PUNT, PPE_C_WINDOW_PUNT, PPE_C_PKTS,
+    PPE_C__COUNT /* 30 */
+};
+
+typedef struct {
+    uint64_t c[32];            /* indexed by enum ppe_counter */
+} ppe_counters_t;
+
+/* ---- batch input: structure of arrays, one header window per packet ---- */
+typedef struct {
+    const uint8_t  *hdr;       /* n × stride bytes: the first min(len, stride) bytes of each packet            */
+    const uint32_t *len;       /* n × wire length (mbuf->pkt_totallen; truncated to 16 bits like Decode())      */
+    const uint64_t *ts;        /* optional n × seconds since 1970 (mbuf->timestamp); NULL → cfg->now_seconds    */
+    uint32_t        n;
+    uint32_t        stride;    /* 64 or 128                                                                     */
+} ppe_batch_t;
+
+/* ---- batch output (SoA; any pointer may be NULL to skip that output) ---- */
+typedef struct {
+    uint32_t *verdict;         /* n × verdict word                                                            */
+    uint32_t *flow_hash;       /* n × flow_hashfn(proto,sip,dip,sport,dport); 0 unless PPE_F_L4                */
+    int32_t  *acl_hit;         /* n × lowest matching rule index, -1 on no match / not consulted               */
+    uint32_t *fw_idx;          /* n slots: per 64-packet tile t, the FW packet indices packed at [64t, 64t+k)  */
+    uint32_t *drop_idx;        /* n slots: same for DROP                                                      */
+    uint32_t *tile_cnt;        /* ceil(n/64) × (nfw | ndrop << 8 | npunt << 16)                                */
+    uint32_t *tuple;           /* optional n × 4 words: sip, dip, sport|dport<<16, proto|vlan<<8|payload_len<<16 */
+} ppe_result_t;
+
+typedef struct {
+    uint32_t unsupport_proto_action;  /* 0 drop (default, dp_cmd.c:37), 1 forward                            */
+    uint32_t syn_check;               /* 1 (default, flow.c:26): TCP flow must start with SYN                 */
+    uint64_t now_seconds;             /* timestamp used for rule time windows when batch.ts == NULL           */
+} ppe_cfg_t;
+
+typedef struct {
+    uint32_t n_rules;          /* USED rules in the committed set                                          */
+    uint32_t n_nodes;          /* tree nodes                                                               */
+    uint32_t n_leaves;
+    uint32_t n_leaf_entries;
+    uint32_t max_depth;
+    double   avg_depth;
+    uint32_t blob_bytes;       /* device image size                                                        */
+    uint32_t lds_resident;     /* 1 if the image is staged into LDS by the kernel                          */
+    double   build_ms;
+} ppe_acl_stats_t;
+
+typedef struct ppe_ctx ppe_ctx_t;
+
+int  ppe_abi_version(void);
+/* device = HIP device ordinal */
+int  ppe_ctx_create(int device, ppe_ctx_t **out);
+int  ppe_ctx_destroy(ppe_ctx_t *ctx);
+int  ppe_ctx_device(ppe_ctx_t *ctx);
+
+/* Build the classifier from rules[0..n) (entry i is eligible iff used == NULL || used[i] == USED) and publish it
+ * for subsequent batches (double-buffered: the previous image stays valid for launches already queued).
+ * n may exceed RULE_ENTRY_MAX (extended rule API, up to 1<<24).  default_action: ACL_RULE_ACTION_FW/DROP. */
+int  ppe_rules_commit(ppe_ctx_t *ctx, const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                      uint32_t default_action, ppe_acl_stats_t *stats);
+
+/* Classify one device-resident batch, enqueued on `stream` (a hipStream_t; NULL = the legacy default stream). */
+int  ppe_classify(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
+                  void *stream);
+
+/* Host-resident batch: pipelined H2D → classify → D2H over `chunk`-packet slices on internal streams.
+ * Output pointers are host pointers (NULL to skip).  Blocks until done. */
+int  ppe_classify_host(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
+                       uint32_t chunk);
+
+/* ACL-only lookup over already-decoded 5-tuples (DP_Acl_Lookup, dataplane/src/flow/flow.c:232).
+ * tuple: n × 4 words {sip, dip, sport | dport << 16, proto} — the same layout as ppe_result_t.tuple;
+ * macs (optional): n × 4 words {dmac bytes 0-3, dmac bytes 4-5, smac bytes 0-3, smac bytes 4-5} (little-endian);
+ * ts (optional): n × seconds, else now_seconds.  hit: lowest matching rule index or -1; action: the matched rule's
+ * action word or the default action. */
+typedef struct {
+    const uint32_t *tuple;
+    const uint32_t *macs;
+    const uint64_t *ts;
+    uint32_t        n;
+} ppe_tuples_t;
+int  ppe_acl_lookup(ppe_ctx_t *ctx, const ppe_tuples_t *in, int32_t *hit, uint32_t *action, uint64_t now_seconds,
+                    void *stream);                                   /* device pointers, asynchronous */
+int  ppe_acl_lookup_host(ppe_ctx_t *ctx, const ppe_tuples_t *in, int32_t *hit, uint32_t *action,
+                         uint64_t now_seconds);                      /* host pointers, blocking */
+
+/* Memory helpers for C integrators (device / pinned host buffers on the context's device). */
+void *ppe_dev_alloc(ppe_ctx_t *ctx, size_t bytes);
+void  ppe_dev_free(ppe_ctx_t *ctx, void *p);
+void *ppe_host_alloc(ppe_ctx_t *ctx, size_t bytes);   /* pinned */
+void  ppe_host_free(ppe_ctx_t *ctx, void *p);
+int   ppe_memcpy_h2d(ppe_ctx_t *ctx, void *dst, const void *src, size_t bytes);
+int   ppe_memcpy_d2h(ppe_ctx_t *ctx, void *dst, const void *src, size_t bytes);
+int   ppe_memset_d(ppe_ctx_t *ctx, void *dst, int value, size_t bytes);
+int   ppe_sync(ppe_ctx_t *ctx);
+
+/* Counters: per-workgroup slots in device memory, reduced on read.  Synchronises the device. */
+int  ppe_counters_read(ppe_ctx_t *ctx, ppe_counters_t *out);
+int  ppe_counters_clear(ppe_ctx_t *ctx);
+
+/* Kernel timing with HIP events recorded around each ppe_classify launch on its stream. */
+int  ppe_timing_enable(ppe_ctx_t *ctx, int on);
+/* Synchronises, then returns the sum of launch durations (ms) and the launch count since the last reset. */
+int  ppe_timing_read(ppe_ctx_t *ctx, double *total_ms, uint32_t *launches, int reset);
+
+/* Copy the current device classifier image to host (for tests / tools).  words may be NULL to query size. */
+int  ppe_acl_image(ppe_ctx_t *ctx, uint32_t *words, uint32_t *n_words);
+
+/* Launch geometry in use (for profiling notes). */
+int  ppe_launch_info(ppe_ctx_t *ctx, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes);
+
+/* Human-readable last error of this context (static storage of the ctx). */
+const char *ppe_last_error(ppe_ctx_t *ctx);
+
+/* Host-side classifier compiler (no device needed): rule list → image words (ppe_image.h layout, malloc'd;
+ * free with ppe_acl_free_image).  binth = max rules in a leaf list before splitting (0 → default 4). */
+int  ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                         uint32_t default_action, uint32_t binth, uint32_t **words, uint32_t *n_words,
+                         ppe_acl_stats_t *stats);
+void ppe_acl_free_image(uint32_t *words);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPE_HIP_H */

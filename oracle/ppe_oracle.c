@@ -1,0 +1,515 @@
+/*
+ * ppe_oracle.c — TEST INFRASTRUCTURE ONLY (see ppe_oracle.h).  A sequential restatement of the reference
+ * dataplane, layer by layer, with the reference's check order, uint16_t lengths and big-endian field reads
+ * (the reference targets big-endian cnMIPS64 and reads header fields raw).
+ */
+#include "ppe_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ppe_hip.h"
+#include "../packet-process-engine_amd/csrc/ppe_image.h"
+
+#define DEC_OK 0
+#define DEC_DROP 1
+
+/* the mbuf fields the path touches (dataplane/src/include/mbuf.h:23-87) plus the recorded verdict */
+typedef struct {
+    const uint8_t *frame;
+    uint32_t avail;
+    uint64_t ts;
+    const oracle_cfg_t *cfg;
+    oracle_result_t *r;
+    int vlan_idx;
+    uint8_t smac[6], dmac[6];
+    int decided;
+} omb_t;
+
+static const RCP_BLOCK_ACL_RULE_TUPLE *g_rules;
+static const uint8_t *g_used;
+static uint32_t g_nrules, g_defact = ACL_RULE_ACTION_DROP;
+static const uint32_t *g_img;
+static uint32_t g_img_words;
+
+void oracle_set_rules(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                      uint32_t default_action) {
+    g_rules = rules;
+    g_used = used;
+    g_nrules = n;
+    g_defact = default_action;
+}
+
+void oracle_set_image(const uint32_t *img, uint32_t n_words) {
+    g_img = img;
+    g_img_words = n_words;
+}
+
+/* byte at frame offset `off`, tracking how far into the frame the verdict reads */
+static uint32_t rd8(omb_t *m, const uint8_t *p) {
+    const uint32_t off = (uint32_t)(p - m->frame);
+    if (off + 1 > m->r->reach) m->r->reach = off + 1;
+    return off < m->avail ? p[0] : 0u;
+}
+static uint32_t rd16(omb_t *m, const uint8_t *p) { return (rd8(m, p) << 8) | rd8(m, p + 1); }
+static uint32_t rd32(omb_t *m, const uint8_t *p) { return (rd16(m, p) << 16) | rd16(m, p + 2); }
+
+static void cnt(omb_t *m, int c) { m->r->counters |= 1u << c; }
+
+/* output_fw_proc / output_drop_proc (dataplane/src/output/output.c:106,151): the first call decides */
+static void out_fw(omb_t *m) {
+    if (!m->decided) { m->r->action = PPE_ACT_FW; m->decided = 1; }
+}
+static void out_drop(omb_t *m) {
+    if (!m->decided) { m->r->action = PPE_ACT_DROP; m->decided = 1; }
+}
+static void set_status(omb_t *m, uint32_t st) {
+    if (m->r->status == 0xffu) m->r->status = st;
+}
+
+/* dataplane/src/decode/decode.c:31-45 */
+static void unsupport_proto_handle(omb_t *m) {
+    if (m->cfg->unsupport_proto_action == 1) out_fw(m);
+    else out_drop(m);
+}
+
+/* dataplane/src/flow/tluhash.h:7-23 */
+uint32_t oracle_tluhash(uint32_t u1, uint32_t u2) {
+    uint32_t a = u2 + 0x9e3779b9u, b = u1 + 0x9e3779b9u, c = 0;
+    a = a - b; a = a - c; a = a ^ (c >> 13);
+    b = b - c; b = b - a; b = b ^ (a << 8);
+    c = c - a; c = c - b; c = c ^ (b >> 13);
+    a = a - b; a = a - c; a = a ^ (c >> 12);
+    b = b - c; b = b - a; b = b ^ (a << 16);
+    c = c - a; c = c - b; c = c ^ (b >> 5);
+    a = a - b; a = a - c; a = a ^ (c >> 3);
+    b = b - c; b = b - a; b = b ^ (a << 10);
+    c = c - a; c = c - b; c = c ^ (b >> 15);
+    return c;
+}
+
+/* dataplane/src/flow/tluhash.h:26-35 (argument order: proto, sip, dip, sport, dport) */
+uint32_t oracle_flow_hashfn(uint32_t proto, uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport) {
+    return oracle_tluhash(sip, sport & 0xffffu) ^ oracle_tluhash(dip, dport & 0xffffu) ^
+           oracle_tluhash(proto & 0xffu, 0);
+}
+
+/* ---- ACL (the reference engine is absent) ---- */
+static int prefix_match(uint32_t x, uint32_t rule_ip, uint32_t len) {
+    if (len == 0) return 1;
+    const uint32_t mask = len >= 32 ? 0xffffffffu : ~(0xffffffffu >> len);
+    return ((x ^ rule_ip) & mask) == 0;
+}
+static int mac_zero(const uint8_t *a) { return (a[0] | a[1] | a[2] | a[3] | a[4] | a[5]) == 0; }
+
+static int rule_matches(const RCP_BLOCK_ACL_RULE_TUPLE *r, uint32_t sip, uint32_t dip, uint32_t sport,
+                        uint32_t dport, uint32_t proto, const uint8_t *dmac, const uint8_t *smac, uint64_t ts) {
+    if (!prefix_match(sip, r->sip, r->sip_mask)) return 0;
+    if (!prefix_match(dip, r->dip, r->dip_mask)) return 0;
+    if (sport < r->sport_start || sport > r->sport_end) return 0;
+    if (dport < r->dport_start || dport > r->dport_end) return 0;
+    if (proto < r->protocol_start || proto > r->protocol_end) return 0;
+    if (!mac_zero(r->smac) && memcmp(r->smac, smac, 6) != 0) return 0;
+    if (!mac_zero(r->dmac) && memcmp(r->dmac, dmac, 6) != 0) return 0;
+    if ((r->time_start != 0 || r->time_end != 0) && (ts < r->time_start || ts > r->time_end)) return 0;
+    return 1;
+}
+
+int32_t oracle_acl_linear(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                          const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action) {
+    for (uint32_t i = 0; i < g_nrules; i++) {
+        if (g_used && g_used[i] != RULE_ENTRY_STATUS_USED) continue;
+        if (rule_matches(&g_rules[i], sip, dip, sport, dport, proto, dmac, smac, ts)) {
+            if (action) *action = g_rules[i].action;
+            return (int32_t)i;
+        }
+    }
+    if (action) *action = g_defact;
+    return -1;
+}
+
+static uint32_t mac_lo(const uint8_t *m) {
+    return (uint32_t)m[0] | ((uint32_t)m[1] << 8) | ((uint32_t)m[2] << 16) | ((uint32_t)m[3] << 24);
+}
+static uint32_t mac_hi(const uint8_t *m) { return (uint32_t)m[4] | ((uint32_t)m[5] << 8); }
+
+int32_t oracle_acl_tree(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                        const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action) {
+    const uint32_t *im = g_img;
+    const uint32_t key[5] = {sip, dip, sport, dport, proto};
+    uint32_t node = 0;
+    for (int it = 0; it <= PPE_MAX_DEPTH; it++) {
+        const uint32_t x = im[PPE_IMG_HDR_WORDS + 2 * node], y = im[PPE_IMG_HDR_WORDS + 2 * node + 1];
+        if ((y & 7u) == PPE_NODE_LEAF) {
+            const uint32_t *lf = im + im[PPE_IMG_W_OFFLEAF] + x;
+            for (uint32_t j = 0; j < (y >> 3); j++) {
+                const uint32_t slot = lf[j] & ~PPE_LEAF_CERTAIN;
+                const uint32_t *r = im + im[PPE_IMG_W_OFFRULES] + 8 * slot;
+                int m = (lf[j] & PPE_LEAF_CERTAIN) != 0;
+                if (!m) {
+                    m = sip >= r[0] && sip <= r[1] && dip >= r[2] && dip <= r[3] && sport >= (r[4] & 0xffffu) &&
+                        sport <= (r[4] >> 16) && dport >= (r[5] & 0xffffu) && dport <= (r[5] >> 16) &&
+                        proto >= (r[6] & 0xffu) && proto <= ((r[6] >> 8) & 0xffu);
+                    const uint32_t rs = r[7] >> 29;
+                    const uint32_t *x8 = im + im[PPE_IMG_W_OFFRESID] + 8 * slot;
+                    if (m && (rs & PPE_RESID_DMAC)) m = x8[0] == mac_lo(dmac) && x8[1] == mac_hi(dmac);
+                    if (m && (rs & PPE_RESID_SMAC)) m = x8[2] == mac_lo(smac) && x8[3] == mac_hi(smac);
+                    if (m && (rs & PPE_RESID_TIME)) {
+                        const uint64_t t0 = x8[4] | ((uint64_t)x8[5] << 32), t1 = x8[6] | ((uint64_t)x8[7] << 32);
+                        m = ts >= t0 && ts <= t1;
+                    }
+                }
+                if (m) {
+                    if (action) *action = r[6] >> 16;
+                    return (int32_t)(r[7] & 0x1fffffffu);
+                }
+            }
+            break;
+        }
+        node = (y >> 3) + (key[y & 7u] > x ? 1u : 0u);
+    }
+    if (action) *action = im[PPE_IMG_W_DEFACT];
+    return -1;
+}
+
+/* ---- flow: dataplane/src/flow/flow.c:181-245 (miss path), 271-292 ---- */
+static __thread int t_use_tree;  /* per shard: 1 = walk the image, 0 = linear first match */
+
+static void flow_handle_packet(omb_t *m) {
+    oracle_result_t *r = m->r;
+    r->flags |= PPE_F_L4;
+    r->flow_hash = oracle_flow_hashfn(r->proto, r->sip, r->dip, r->sport, r->dport);  /* flow.c:189 */
+    /* every packet is a flow-table miss (stateless path) */
+    if (m->cfg->syn_check && r->proto == 6 && !(r->flags & PPE_F_SYN)) {  /* flow.c:204-214 */
+        cnt(m, PPE_C_FLOW_TCP_NO_SYN_FIRST);
+        set_status(m, PPE_ST_FLOW_TCP_NO_SYN_FIRST);
+        out_drop(m);  /* FlowHandlePacket :278-284 */
+        cnt(m, PPE_C_FLOW_PROC_FAIL);
+        return;
+    }
+    /* PortScan_Detect disabled (portscan_able = 0) */
+    uint32_t act;
+    r->flags |= PPE_F_ACL;
+    r->acl_hit = t_use_tree ? oracle_acl_tree(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
+                                              m->ts, &act)
+                            : oracle_acl_linear(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
+                                                m->ts, &act);
+    if (act == ACL_RULE_ACTION_DROP) {  /* flow.c:232-237 */
+        cnt(m, PPE_C_ACL_DROP);
+        set_status(m, PPE_ST_ACL_DROP);
+        out_drop(m);
+        cnt(m, PPE_C_FLOW_PROC_FAIL);
+        return;
+    }
+    cnt(m, PPE_C_ACL_FW);  /* flow.c:240 */
+    set_status(m, PPE_ST_ACL_FW);
+    cnt(m, PPE_C_FLOW_PROC_OK);  /* flow.c:309 */
+    out_fw(m);                   /* SELF_TEST, flow.c:376-377 */
+}
+
+/* ---- UDP: dataplane/src/decode/decode-udp.c:16-71 ---- */
+static int decode_udp(omb_t *m, const uint8_t *pkt, uint16_t len) {
+    if (len < 8) {
+        cnt(m, PPE_C_UDP_HEADERLEN_ERR);
+        set_status(m, PPE_ST_UDP_HEADER_ERR);
+        return DEC_DROP;
+    }
+    const uint32_t uh_len = rd16(m, pkt + 4);
+    if (len < uh_len || len != uh_len) {
+        cnt(m, PPE_C_UDP_PKTLEN_ERR);
+        set_status(m, PPE_ST_UDP_LEN_ERR);
+        return DEC_DROP;
+    }
+    m->r->sport = rd16(m, pkt);
+    m->r->dport = rd16(m, pkt + 2);
+    m->r->paylen = (uint16_t)(len - 8);
+    cnt(m, PPE_C_UDP_RX_OK);
+    flow_handle_packet(m);
+    return DEC_OK;
+}
+
+/* dataplane/src/decode/decode-tcp.c:18-131 — only the window-scale option is recorded; no verdict effect */
+static void decode_tcp_options(omb_t *m, const uint8_t *pkt, uint16_t len) {
+    uint16_t plen = len;
+    while (plen) {
+        const uint32_t off = (uint32_t)(pkt - m->frame);
+        const uint8_t t = off < m->avail ? pkt[0] : 0;
+        if (t == 0) break;          /* EOL */
+        if (t == 1) { pkt++; plen--; continue; }  /* NOP */
+        if (plen < 2) break;
+        const uint8_t ol = off + 1 < m->avail ? pkt[1] : 0;
+        if (ol > plen || ol < 2) return;
+        if (t == 3 && ol == 3) m->r->tcp_ws = 1;
+        pkt += ol;
+        plen = (uint16_t)(plen - ol);
+    }
+}
+
+/* ---- TCP: dataplane/src/decode/decode-tcp.c:135-222 ---- */
+static int decode_tcp(omb_t *m, const uint8_t *pkt, uint16_t len) {
+    if (len < 20) {
+        cnt(m, PPE_C_TCP_HEADERLEN_ERR);
+        set_status(m, PPE_ST_TCP_HEADER_ERR);
+        return DEC_DROP;
+    }
+    const uint8_t hlen = (uint8_t)((rd8(m, pkt + 12) >> 4) << 2);
+    if (len < hlen) {
+        cnt(m, PPE_C_TCP_PKTLEN_ERR);
+        set_status(m, PPE_ST_TCP_LEN_ERR);
+        return DEC_DROP;
+    }
+    const uint8_t opt_len = (uint8_t)(hlen - 20);
+    if (opt_len > 40) {
+        cnt(m, PPE_C_TCP_PKTLEN_ERR);
+        set_status(m, PPE_ST_TCP_LEN_ERR);
+        return DEC_DROP;
+    }
+    m->r->flags |= PPE_F_TCP;
+    if (rd8(m, pkt + 13) & 0x02) m->r->flags |= PPE_F_SYN;  /* land / SYN-flood monitors pass at default config */
+    if (opt_len > 0) decode_tcp_options(m, pkt + 20, opt_len);
+    m->r->sport = rd16(m, pkt);
+    m->r->dport = rd16(m, pkt + 2);
+    m->r->paylen = (uint16_t)(len - hlen);
+    cnt(m, PPE_C_TCP_RX_OK);
+    flow_handle_packet(m);
+    return DEC_OK;
+}
+
+/* ---- IPv4: dataplane/src/decode/decode-ipv4.c:27-247 ---- */
+static int decode_ipv4(omb_t *m, const uint8_t *pkt, uint16_t len) {
+    oracle_result_t *r = m->r;
+    if (len < 20) {
+        cnt(m, PPE_C_IPV4_HEADERLEN_ERR);
+        set_status(m, PPE_ST_IPV4_HEADER_ERR);
+        return DEC_DROP;
+    }
+    const uint32_t verhl = rd8(m, pkt);
+    if ((verhl >> 4) != 4) {
+        cnt(m, PPE_C_IPV4_VERSION_ERR);
+        set_status(m, PPE_ST_IPV4_VERSION_ERR);
+        return DEC_DROP;
+    }
+    const uint32_t hl = (verhl & 0x0f) << 2;
+    if (hl < 20) {
+        cnt(m, PPE_C_IPV4_HEADERLEN_ERR);
+        set_status(m, PPE_ST_IPV4_HEADER_ERR);
+        return DEC_DROP;
+    }
+    const uint32_t ip_len = rd16(m, pkt + 2);
+    if (ip_len < hl || len < ip_len) {
+        cnt(m, PPE_C_IPV4_PKTLEN_ERR);
+        set_status(m, PPE_ST_IPV4_LEN_ERR);
+        return DEC_DROP;
+    }
+    r->sip = rd32(m, pkt + 12);
+    r->dip = rd32(m, pkt + 16);
+    r->proto = rd8(m, pkt + 9);
+    const uint32_t ip_off = rd16(m, pkt + 6);
+    if (((ip_off & 0x1fff) > 0 || ((ip_off & 0x2000) >> 13) == 1) && r->proto != 89) {
+        r->flags |= PPE_F_FRAG;
+        const uint16_t frag_len = (uint16_t)(len - hl);
+        if (frag_len == 0) {
+            cnt(m, PPE_C_FRAG_FRAGLEN_ERR);
+            set_status(m, PPE_ST_FRAG_LEN_ERR);
+            return DEC_DROP;
+        }
+        /* Defrag(): stateful, out of scope — the packet is handed to the host (PUNT); Defrag returning NULL
+         * makes DecodeIPV4 return DECODE_OK with no output call */
+        cnt(m, PPE_C_FRAG_PUNT);
+        set_status(m, PPE_ST_FRAG);
+        r->action = PPE_ACT_PUNT;
+        m->decided = 1;
+        return DEC_OK;
+    }
+    const uint16_t l4len = (uint16_t)(ip_len - hl);
+    switch (r->proto) {
+        case 6:
+            cnt(m, PPE_C_IPV4_RX_OK);
+            if (decode_tcp(m, pkt + hl, l4len) != DEC_OK) out_drop(m);
+            return DEC_OK;
+        case 17:
+            cnt(m, PPE_C_IPV4_RX_OK);
+            /* DP_Attack_UdpPacketMonitor passes at default config */
+            if (decode_udp(m, pkt + hl, l4len) != DEC_OK) out_drop(m);
+            return DEC_OK;
+        default:
+            cnt(m, PPE_C_IPV4_UNSUPPORT);
+            set_status(m, PPE_ST_IPV4_UNSUPPORT);
+            unsupport_proto_handle(m);
+            return DEC_OK;
+    }
+}
+
+/* ---- VLAN: dataplane/src/decode/decode-vlan.c:23-89 ---- */
+static int decode_vlan(omb_t *m, const uint8_t *pkt, uint16_t len) {
+    if (len < 4) {
+        cnt(m, PPE_C_VLAN_HEADERLEN_ERR);
+        set_status(m, PPE_ST_VLAN_HEADER_ERR);
+        return DEC_DROP;
+    }
+    if (m->vlan_idx >= 1) {
+        cnt(m, PPE_C_VLAN_LAYER_EXCEED);
+        set_status(m, PPE_ST_VLAN_LAYER_EXCEED);
+        return DEC_DROP;
+    }
+    const uint32_t proto = rd16(m, pkt + 2);
+    m->vlan_idx = 1;
+    m->r->flags |= PPE_F_VLAN;
+    switch (proto) {
+        case 0x0800:
+            cnt(m, PPE_C_VLAN_RX_OK);
+            return decode_ipv4(m, pkt + 4, (uint16_t)(len - 4));
+        case 0x8100:
+        case 0x9100:
+            cnt(m, PPE_C_VLAN_RX_OK);
+            return decode_vlan(m, pkt + 4, (uint16_t)(len - 4));
+        default:
+            cnt(m, PPE_C_VLAN_UNSUPPORT);
+            set_status(m, PPE_ST_VLAN_UNSUPPORT);
+            unsupport_proto_handle(m);
+            return DEC_OK;
+    }
+}
+
+/* ---- Ethernet: dataplane/src/decode/decode-ethernet.c:23-115 ---- */
+static int decode_ethernet(omb_t *m, const uint8_t *pkt, uint16_t len) {
+    if (len < 14) {
+        cnt(m, PPE_C_L2_HEADERLEN_ERR);
+        set_status(m, PPE_ST_L2_HEADER_ERR);
+        return DEC_DROP;
+    }
+    int dz = 1, sz = 1;
+    for (int i = 0; i < 6; i++) {
+        m->dmac[i] = (uint8_t)rd8(m, pkt + i);
+        m->smac[i] = (uint8_t)rd8(m, pkt + 6 + i);
+        dz &= m->dmac[i] == 0;
+        sz &= m->smac[i] == 0;
+    }
+    if (dz || sz) {
+        cnt(m, PPE_C_L2_HEADERLEN_ERR);
+        set_status(m, PPE_ST_L2_HEADER_ERR);
+        return DEC_DROP;
+    }
+    switch (rd16(m, pkt + 12)) {
+        case 0x0800:
+            cnt(m, PPE_C_L2_RX_OK);
+            return decode_ipv4(m, pkt + 14, (uint16_t)(len - 14));
+        case 0x8100:
+        case 0x9100:
+            cnt(m, PPE_C_L2_RX_OK);
+            return decode_vlan(m, pkt + 14, (uint16_t)(len - 14));
+        default:
+            cnt(m, PPE_C_L2_UNSUPPORT);
+            set_status(m, PPE_ST_L2_UNSUPPORT);
+            unsupport_proto_handle(m);
+            return DEC_OK;
+    }
+}
+
+void oracle_classify(const uint8_t *pkt, uint32_t avail, uint32_t len, uint64_t ts, const oracle_cfg_t *cfg,
+                     oracle_result_t *out) {
+    memset(out, 0, sizeof *out);
+    out->status = 0xffu;
+    out->acl_hit = -1;
+    out->action = PPE_ACT_DROP;
+    omb_t m;
+    memset(&m, 0, sizeof m);
+    m.frame = pkt;
+    m.avail = avail;
+    m.ts = ts;
+    m.cfg = cfg;
+    m.r = out;
+    out->counters |= 1u << PPE_C_PKTS;
+    /* Decode(): dataplane/src/decode/decode.c:19-28, len = (uint16_t)pkt_totallen */
+    if (decode_ethernet(&m, pkt, (uint16_t)len) != DEC_OK) out_drop(&m);
+    switch (out->action) {
+        case PPE_ACT_FW: cnt(&m, PPE_C_OUT_FW); break;
+        case PPE_ACT_DROP: cnt(&m, PPE_C_OUT_DROP); break;
+        default: cnt(&m, PPE_C_OUT_PUNT); break;
+    }
+}
+
+/* ---- batch + threads (the CPU baseline: run-to-completion shards, like per-core mainloop, main.c:250) ---- */
+typedef struct {
+    const uint8_t *hdr;
+    uint32_t stride;
+    const uint32_t *len;
+    const uint64_t *ts;
+    uint32_t lo, hi;
+    const oracle_cfg_t *cfg;
+    int use_tree;
+    uint32_t *verdict, *flow_hash, *tuple, *reach;
+    int32_t *acl_hit;
+    uint64_t counters[32];
+} shard_t;
+
+static void *run_shard(void *arg) {
+    shard_t *s = (shard_t *)arg;
+    t_use_tree = s->use_tree;
+    memset(s->counters, 0, sizeof s->counters);
+    for (uint32_t i = s->lo; i < s->hi; i++) {
+        oracle_result_t r;
+        const uint32_t len = s->len[i];
+        const uint32_t avail = len < s->stride ? len : s->stride;
+        oracle_classify(s->hdr + (size_t)i * s->stride, avail, len, s->ts ? s->ts[i] : s->cfg->now_seconds, s->cfg,
+                        &r);
+        if (s->verdict) s->verdict[i] = r.status | (r.action << 8) | (r.flags << 16);
+        if (s->flow_hash) s->flow_hash[i] = r.flow_hash;
+        if (s->acl_hit) s->acl_hit[i] = r.acl_hit;
+        if (s->reach) s->reach[i] = r.reach;
+        if (s->tuple) {
+            s->tuple[4 * (size_t)i + 0] = r.sip;
+            s->tuple[4 * (size_t)i + 1] = r.dip;
+            s->tuple[4 * (size_t)i + 2] = r.sport | (r.dport << 16);
+            s->tuple[4 * (size_t)i + 3] = r.proto | (((r.flags & PPE_F_VLAN) ? 1u : 0u) << 8) | (r.paylen << 16);
+        }
+        for (int c = 0; c < 32; c++)
+            if (r.counters & (1u << c)) s->counters[c]++;
+    }
+    return NULL;
+}
+
+int oracle_classify_batch(const uint8_t *hdr, uint32_t stride, const uint32_t *len, const uint64_t *ts, uint32_t n,
+                          const oracle_cfg_t *cfg, int nthreads, int use_tree, uint32_t *verdict,
+                          uint32_t *flow_hash, int32_t *acl_hit, uint32_t *tuple, uint32_t *reach,
+                          uint64_t *counters) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 512) nthreads = 512;
+    shard_t *sh = (shard_t *)calloc((size_t)nthreads, sizeof(shard_t));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    if (!sh || !th) {
+        free(sh);
+        free(th);
+        return -1;
+    }
+    const uint32_t per = (n + (uint32_t)nthreads - 1) / (uint32_t)nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        shard_t *s = &sh[t];
+        s->hdr = hdr;
+        s->stride = stride;
+        s->len = len;
+        s->ts = ts;
+        s->lo = (uint32_t)t * per < n ? (uint32_t)t * per : n;
+        s->hi = s->lo + per < n ? s->lo + per : n;
+        s->cfg = cfg;
+        s->use_tree = use_tree;
+        s->verdict = verdict;
+        s->flow_hash = flow_hash;
+        s->acl_hit = acl_hit;
+        s->tuple = tuple;
+        s->reach = reach;
+        if (nthreads == 1) run_shard(s);
+        else pthread_create(&th[t], NULL, run_shard, s);
+    }
+    if (nthreads > 1)
+        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    if (counters) {
+        memset(counters, 0, 32 * sizeof(uint64_t));
+        for (int t = 0; t < nthreads; t++)
+            for (int c = 0; c < 32; c++) counters[c] += sh[t].counters[c];
+    }
+    free(sh);
+    free(th);
+    return 0;
+}

@@ -1,0 +1,75 @@
+/*
+ * ppe_oracle.h — TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference's per-packet decode → flow hash →
+ * ACL path, used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.  The product
+ * (libppe_hip.so) never links, loads or calls it.
+ *
+ * Pinning:
+ *   - flow hash: checked against the reference's own dataplane/src/flow/tluhash.h compiled unmodified into
+ *     oracle/_ref/libref_tluhash.so (tests/test_oracle_ref.py) and the two known answers of SURVEY.md §8(a) A9;
+ *   - decode: the reference decoders cannot be built here without stand-ins for the Cavium SDK headers they
+ *     include (cvmx*.h via mbuf.h / oct-common.h), which this task forbids, so decode is pinned by hand-derived
+ *     known-answer packets, one per reason, each citing the reference line it exercises (tests/test_oracle_kat.py);
+ *   - ACL: the reference engine source is absent (dataplane/src/acl/acl.mk:13-15 builds files not in the tree):
+ *     PARITY UNPINNED by reference code; the semantics are the build's definition, frozen by
+ *     tests/golden/ fixtures and hand-written known answers.
+ */
+#ifndef PPE_ORACLE_H
+#define PPE_ORACLE_H
+
+#include <stdint.h>
+#include "ppe_acl.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    uint32_t unsupport_proto_action; /* 0 drop, 1 fw */
+    uint32_t syn_check;
+    uint64_t now_seconds;            /* packet timestamp when ts == NULL */
+} oracle_cfg_t;
+
+typedef struct {
+    uint32_t status;     /* enum ppe_status */
+    uint32_t action;     /* enum ppe_action */
+    uint32_t flags;      /* PPE_F_* */
+    uint32_t flow_hash;  /* flow_hashfn, 0 unless PPE_F_L4 */
+    int32_t acl_hit;     /* -1 unless a rule matched */
+    uint32_t sip, dip, sport, dport, proto, paylen;
+    uint32_t counters;   /* bit i set = counter i (enum ppe_counter) incremented once */
+    uint32_t reach;      /* 1 + highest frame byte offset the verdict depends on */
+    uint32_t tcp_ws;     /* 1 if DecodeTCPOptions recorded a window-scale option (informational) */
+} oracle_result_t;
+
+/* rule set used by oracle_classify (pointer kept; caller owns the memory) */
+void oracle_set_rules(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                      uint32_t default_action);
+/* optional: walk a classifier image (ppe_image.h) instead of the linear first-match scan */
+void oracle_set_image(const uint32_t *img, uint32_t n_words);
+
+uint32_t oracle_tluhash(uint32_t u1, uint32_t u2);
+uint32_t oracle_flow_hashfn(uint32_t proto, uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport);
+
+/* linear first-match ACL (A11): returns the lowest matching USED index or -1; *action = its action or default */
+int32_t oracle_acl_linear(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                          const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action);
+/* decision-tree walk over the image set by oracle_set_image; same contract */
+int32_t oracle_acl_tree(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                        const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action);
+
+/* One packet.  pkt holds at least `avail` bytes of the frame; len is the wire length (pkt_totallen).
+ * Bytes past `avail` read as 0 (the reach field says whether the verdict depended on them). */
+void oracle_classify(const uint8_t *pkt, uint32_t avail, uint32_t len, uint64_t ts, const oracle_cfg_t *cfg,
+                     oracle_result_t *out);
+
+/* Batch over windows (n × stride bytes), optionally multi-threaded (run-to-completion shards like mainloop);
+ * use_tree selects the image walk.  Any output pointer may be NULL.  Returns 0. */
+int oracle_classify_batch(const uint8_t *hdr, uint32_t stride, const uint32_t *len, const uint64_t *ts, uint32_t n,
+                          const oracle_cfg_t *cfg, int nthreads, int use_tree, uint32_t *verdict,
+                          uint32_t *flow_hash, int32_t *acl_hit, uint32_t *tuple, uint32_t *reach,
+                          uint64_t *counters /* [32] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,118 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of the CPU oracle (oracle/liboracle.so) and of the reference's own
+flow hash (oracle/_ref/libref_tluhash.so, built from /root/reference when present).  Used by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker — never by the product path."""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB = ORACLE_DIR / "liboracle.so"
+REF_LIB = ORACLE_DIR / "_ref" / "libref_tluhash.so"
+
+
+class OCfg(C.Structure):
+    _fields_ = [("unsupport_proto_action", C.c_uint32), ("syn_check", C.c_uint32), ("now_seconds", C.c_uint64)]
+
+
+class OResult(C.Structure):
+    _fields_ = [("status", C.c_uint32), ("action", C.c_uint32), ("flags", C.c_uint32), ("flow_hash", C.c_uint32),
+                ("acl_hit", C.c_int32), ("sip", C.c_uint32), ("dip", C.c_uint32), ("sport", C.c_uint32),
+                ("dport", C.c_uint32), ("proto", C.c_uint32), ("paylen", C.c_uint32), ("counters", C.c_uint32),
+                ("reach", C.c_uint32), ("tcp_ws", C.c_uint32)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            raise OSError(f"{LIB} missing: run `make -C oracle`")
+        lib = C.CDLL(str(LIB))
+        vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+        lib.oracle_set_rules.argtypes = [vp, vp, u32, u32]
+        lib.oracle_set_image.argtypes = [vp, u32]
+        lib.oracle_tluhash.argtypes = [u32, u32]
+        lib.oracle_tluhash.restype = u32
+        lib.oracle_flow_hashfn.argtypes = [u32, u32, u32, u32, u32]
+        lib.oracle_flow_hashfn.restype = u32
+        lib.oracle_classify.argtypes = [vp, u32, u32, u64, C.POINTER(OCfg), C.POINTER(OResult)]
+        lib.oracle_classify_batch.argtypes = [vp, u32, vp, vp, u32, C.POINTER(OCfg), C.c_int, C.c_int, vp, vp, vp,
+                                              vp, vp, vp]
+        lib.oracle_classify_batch.restype = C.c_int
+        lib.oracle_acl_linear.argtypes = [u32, u32, u32, u32, u32, vp, vp, u64, C.POINTER(u32)]
+        lib.oracle_acl_linear.restype = C.c_int32
+        lib.oracle_acl_tree.argtypes = [u32, u32, u32, u32, u32, vp, vp, u64, C.POINTER(u32)]
+        lib.oracle_acl_tree.restype = C.c_int32
+        _lib = lib
+    return _lib
+
+
+class Oracle:
+    """Holds references to the rule arrays the C oracle points at."""
+
+    def __init__(self, rules=None, used=None, default_action=1, image=None):
+        self.lib = load()
+        self.set_rules(rules, used, default_action)
+        self.image = None
+        if image is not None:
+            self.set_image(image)
+
+    def set_rules(self, rules, used=None, default_action=1):
+        from ppe.abi import RULE_DTYPE
+        self.rules = np.ascontiguousarray(rules if rules is not None else np.zeros(0, RULE_DTYPE), RULE_DTYPE)
+        self.used = None if used is None else np.ascontiguousarray(used, np.uint8)
+        self.lib.oracle_set_rules(self.rules.ctypes.data if len(self.rules) else None,
+                                  self.used.ctypes.data if self.used is not None else None, len(self.rules),
+                                  int(default_action))
+
+    def set_image(self, image):
+        self.image = np.ascontiguousarray(image, np.uint32)
+        self.lib.oracle_set_image(self.image.ctypes.data, len(self.image))
+
+    @staticmethod
+    def cfg(unsupport_proto_action=0, syn_check=1, now_seconds=0):
+        return OCfg(unsupport_proto_action, syn_check, now_seconds)
+
+    def classify_one(self, pkt: bytes, length=None, ts=0, cfg=None) -> dict:
+        buf = np.frombuffer(bytes(pkt), np.uint8).copy() if len(pkt) else np.zeros(1, np.uint8)
+        r = OResult()
+        self.lib.oracle_classify(buf.ctypes.data, len(pkt), len(pkt) if length is None else int(length), int(ts),
+                                 C.byref(cfg or self.cfg()), C.byref(r))
+        return {k: getattr(r, k) for k, _ in OResult._fields_}
+
+    def classify_batch(self, hdr, lens, ts=None, cfg=None, nthreads=1, use_tree=False):
+        hdr = np.ascontiguousarray(hdr, np.uint8)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        n, stride = hdr.shape
+        out = dict(verdict=np.zeros(n, np.uint32), flow_hash=np.zeros(n, np.uint32),
+                   acl_hit=np.zeros(n, np.int32), tuple=np.zeros((n, 4), np.uint32), reach=np.zeros(n, np.uint32),
+                   counters=np.zeros(32, np.uint64))
+        if ts is not None:
+            ts = np.ascontiguousarray(ts, np.uint64)
+        if use_tree and self.image is None:
+            raise ValueError("use_tree needs set_image()")
+        self.lib.oracle_classify_batch(hdr.ctypes.data, stride, lens.ctypes.data,
+                                       ts.ctypes.data if ts is not None else None, n, C.byref(cfg or self.cfg()),
+                                       int(nthreads), 1 if use_tree else 0, out["verdict"].ctypes.data,
+                                       out["flow_hash"].ctypes.data, out["acl_hit"].ctypes.data,
+                                       out["tuple"].ctypes.data, out["reach"].ctypes.data,
+                                       out["counters"].ctypes.data)
+        return out
+
+
+def ref_hash_lib():
+    """The reference's own flow_hashfn (tluhash.h compiled unmodified), or None when not built here."""
+    if not REF_LIB.exists():
+        return None
+    lib = C.CDLL(str(REF_LIB))
+    lib.ref_flow_hashfn.argtypes = [C.c_uint8, C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16]
+    lib.ref_flow_hashfn.restype = C.c_uint32
+    lib.ref_TluHash.argtypes = [C.c_uint32, C.c_uint32]
+    lib.ref_TluHash.restype = C.c_uint32
+    lib.ref_flow_hashfn_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+    return lib

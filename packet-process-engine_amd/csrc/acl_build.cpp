@@ -1,0 +1,292 @@
+/*
+ * acl_build.cpp — host-side compiler from the PPE rule list to the device classifier image (ppe_image.h).
+ *
+ * Replaces the absent DP_Acl_Load_Rule tree build (called at dataplane/src/common/dp_cmd.c:2019; sources
+ * dp_acl.c/acl64.c missing, dataplane/src/acl/acl.mk:13-15).  Algorithm: HyperSplit-style recursive
+ * partitioning of the 5-D header space (sip, dip, sport, dport, proto), one binary split per node at a rule
+ * boundary, chosen to minimise the larger child's rule count.  Exactness invariant (lowest-index first match,
+ * SURVEY.md §8(a) A11): every node keeps, in ascending rule index, every rule whose box intersects its region,
+ * truncated after the first rule whose box covers the region and has no residual (MAC / time) constraint — no
+ * later rule can ever win inside that region.  A leaf therefore holds exactly the candidates that can match
+ * there, in priority order, and the kernel returns the first one that matches.
+ *
+ * Rule semantics (frozen here; the reference engine is absent):
+ *   entry eligible iff used == NULL || used[i] == RULE_ENTRY_STATUS_USED
+ *   sip matches iff sip_mask == 0 || top sip_mask bits of (pkt.sip ^ rule.sip) are zero   (prefix length 0..32)
+ *   dip likewise; sport/dport/protocol: start <= x <= end (an empty range never matches)
+ *   smac/dmac: all-zero = any, else equal; time: (0,0) = any, else time_start <= ts <= time_end
+ *   action: the rule's action word; the packet is dropped iff it equals ACL_RULE_ACTION_DROP (flow.c:232)
+ */
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <vector>
+
+#include "ppe_hip.h"
+#include "ppe_image.h"
+#include "ppe_internal.h"
+
+namespace {
+
+struct Rule {
+    uint32_t lo[PPE_NDIMS], hi[PPE_NDIMS];
+    uint32_t id;
+    uint32_t action;
+    uint32_t resid;
+    uint32_t slot;
+};
+
+struct Work {
+    uint32_t node;
+    uint32_t depth;
+    uint32_t lo[PPE_NDIMS], hi[PPE_NDIMS];
+    std::vector<uint32_t> rules;  // slots, ascending
+};
+
+inline bool covers(const Rule &r, const uint32_t *lo, const uint32_t *hi) {
+    for (int d = 0; d < PPE_NDIMS; ++d)
+        if (r.lo[d] > lo[d] || r.hi[d] < hi[d]) return false;
+    return true;
+}
+
+inline uint32_t prefix_lo(uint32_t ip, uint32_t len) {
+    return len == 0 ? 0u : (ip & (0xffffffffu << (32 - len)));
+}
+inline uint32_t prefix_hi(uint32_t ip, uint32_t len) {
+    return len == 0 ? 0xffffffffu : (prefix_lo(ip, len) | ~(0xffffffffu << (32 - len)));
+}
+
+inline bool mac_nonzero(const uint8_t *m) {
+    return (m[0] | m[1] | m[2] | m[3] | m[4] | m[5]) != 0;
+}
+inline uint32_t mac_lo(const uint8_t *m) {
+    return (uint32_t)m[0] | ((uint32_t)m[1] << 8) | ((uint32_t)m[2] << 16) | ((uint32_t)m[3] << 24);
+}
+inline uint32_t mac_hi(const uint8_t *m) { return (uint32_t)m[4] | ((uint32_t)m[5] << 8); }
+
+}  // namespace
+
+extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                                   uint32_t default_action, uint32_t binth, uint32_t **words_out,
+                                   uint32_t *n_words_out, ppe_acl_stats_t *st) {
+    if (!words_out || !n_words_out) return PPE_EINVAL;
+    if (n && !rules) return PPE_EINVAL;
+    if (n > (1u << 24)) return PPE_EINVAL;
+    if (binth == 0) binth = 4;
+    auto t0 = std::chrono::steady_clock::now();
+
+    // ---- compile eligible rules to boxes (slot order = ascending rule index) ----
+    std::vector<Rule> R;
+    std::vector<uint32_t> resid_words;
+    R.reserve(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (used && used[i] != RULE_ENTRY_STATUS_USED) continue;
+        const RCP_BLOCK_ACL_RULE_TUPLE &t = rules[i];
+        if (t.sip_mask > 32 || t.dip_mask > 32) return PPE_EINVAL;  // parsers reject these (rule/rule.c:63-73)
+        if (t.sport_start > t.sport_end || t.dport_start > t.dport_end || t.protocol_start > t.protocol_end)
+            continue;  // empty range: can never match
+        Rule r;
+        r.lo[PPE_DIM_SIP] = prefix_lo(t.sip, t.sip_mask);
+        r.hi[PPE_DIM_SIP] = prefix_hi(t.sip, t.sip_mask);
+        r.lo[PPE_DIM_DIP] = prefix_lo(t.dip, t.dip_mask);
+        r.hi[PPE_DIM_DIP] = prefix_hi(t.dip, t.dip_mask);
+        r.lo[PPE_DIM_SPORT] = t.sport_start;
+        r.hi[PPE_DIM_SPORT] = t.sport_end;
+        r.lo[PPE_DIM_DPORT] = t.dport_start;
+        r.hi[PPE_DIM_DPORT] = t.dport_end;
+        r.lo[PPE_DIM_PROTO] = t.protocol_start;
+        r.hi[PPE_DIM_PROTO] = t.protocol_end;
+        r.id = i;
+        r.action = t.action;
+        r.resid = 0;
+        if (mac_nonzero(t.dmac)) r.resid |= PPE_RESID_DMAC;
+        if (mac_nonzero(t.smac)) r.resid |= PPE_RESID_SMAC;
+        if (t.time_start != 0 || t.time_end != 0) r.resid |= PPE_RESID_TIME;
+        r.slot = (uint32_t)R.size();
+        R.push_back(r);
+        uint32_t rw[8] = {mac_lo(t.dmac), mac_hi(t.dmac), mac_lo(t.smac), mac_hi(t.smac),
+                          (uint32_t)t.time_start, (uint32_t)(t.time_start >> 32),
+                          (uint32_t)t.time_end, (uint32_t)(t.time_end >> 32)};
+        resid_words.insert(resid_words.end(), rw, rw + 8);
+    }
+
+    // ---- recursive partitioning, BFS so that children are contiguous and numbered after their parent ----
+    std::vector<uint32_t> nodes;  // 2 words per node
+    std::vector<uint32_t> leaf;
+    const size_t node_budget = (size_t)1 << 23;
+    uint32_t max_depth = 0, n_leaves = 0;
+    double depth_sum = 0;
+
+    std::deque<Work> q;
+    {
+        Work w;
+        w.node = 0;
+        w.depth = 0;
+        w.lo[0] = w.lo[1] = w.lo[2] = w.lo[3] = w.lo[4] = 0;
+        w.hi[0] = w.hi[1] = 0xffffffffu;
+        w.hi[2] = w.hi[3] = 0xffffu;
+        w.hi[4] = 0xffu;
+        w.rules.resize(R.size());
+        for (uint32_t s = 0; s < R.size(); ++s) w.rules[s] = s;
+        q.push_back(std::move(w));
+        nodes.resize(2);
+    }
+
+    std::vector<uint32_t> clo, chi, cand;
+    while (!q.empty()) {
+        Work w = std::move(q.front());
+        q.pop_front();
+
+        // redundancy removal: drop everything after the first unconditional cover of this region
+        std::vector<uint32_t> S;
+        S.reserve(w.rules.size());
+        for (uint32_t s : w.rules) {
+            S.push_back(s);
+            if (R[s].resid == 0 && covers(R[s], w.lo, w.hi)) break;
+        }
+        w.rules.clear();
+        w.rules.shrink_to_fit();
+
+        auto make_leaf = [&](const std::vector<uint32_t> &L) {
+            nodes[2 * w.node + 0] = (uint32_t)leaf.size();
+            nodes[2 * w.node + 1] = ((uint32_t)L.size() << 3) | PPE_NODE_LEAF;
+            for (uint32_t s : L) {
+                uint32_t e = s;
+                if (R[s].resid == 0 && covers(R[s], w.lo, w.hi)) e |= PPE_LEAF_CERTAIN;
+                leaf.push_back(e);
+            }
+            ++n_leaves;
+            depth_sum += w.depth;
+            if (w.depth > max_depth) max_depth = w.depth;
+        };
+
+        const bool first_certain = !S.empty() && R[S[0]].resid == 0 && covers(R[S[0]], w.lo, w.hi);
+        if (S.empty() || first_certain || S.size() <= binth || w.depth + 1 >= PPE_MAX_DEPTH ||
+            nodes.size() / 2 + 2 > node_budget) {
+            if (first_certain) S.resize(1);
+            make_leaf(S);
+            continue;
+        }
+
+        // choose (dim, threshold) minimising (max(|left|,|right|), |left|+|right|)
+        int best_d = -1;
+        uint32_t best_t = 0;
+        size_t best_max = SIZE_MAX, best_sum = SIZE_MAX;
+        for (int d = 0; d < PPE_NDIMS; ++d) {
+            clo.clear();
+            chi.clear();
+            cand.clear();
+            for (uint32_t s : S) {
+                uint32_t l = std::max(R[s].lo[d], w.lo[d]);
+                uint32_t h = std::min(R[s].hi[d], w.hi[d]);
+                clo.push_back(l);
+                chi.push_back(h);
+                if (l > w.lo[d]) cand.push_back(l - 1);
+                if (h < w.hi[d]) cand.push_back(h);
+            }
+            if (cand.empty()) continue;
+            std::sort(clo.begin(), clo.end());
+            std::sort(chi.begin(), chi.end());
+            std::sort(cand.begin(), cand.end());
+            cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+            for (uint32_t t : cand) {
+                size_t left = (size_t)(std::upper_bound(clo.begin(), clo.end(), t) - clo.begin());
+                size_t right = S.size() - (size_t)(std::upper_bound(chi.begin(), chi.end(), t) - chi.begin());
+                size_t mx = std::max(left, right), sm = left + right;
+                if (mx < best_max || (mx == best_max && sm < best_sum)) {
+                    best_max = mx;
+                    best_sum = sm;
+                    best_d = d;
+                    best_t = t;
+                }
+            }
+        }
+        if (best_d < 0) {  // cannot happen: S[0] does not cover the region, so it has a boundary inside it
+            make_leaf(S);
+            continue;
+        }
+
+        const uint32_t left_idx = (uint32_t)(nodes.size() / 2);
+        nodes.resize(nodes.size() + 4);
+        nodes[2 * w.node + 0] = best_t;
+        nodes[2 * w.node + 1] = (left_idx << 3) | (uint32_t)best_d;
+
+        Work L, Rt;
+        L.node = left_idx;
+        Rt.node = left_idx + 1;
+        L.depth = Rt.depth = w.depth + 1;
+        std::memcpy(L.lo, w.lo, sizeof w.lo);
+        std::memcpy(L.hi, w.hi, sizeof w.hi);
+        std::memcpy(Rt.lo, w.lo, sizeof w.lo);
+        std::memcpy(Rt.hi, w.hi, sizeof w.hi);
+        L.hi[best_d] = best_t;
+        Rt.lo[best_d] = best_t + 1;
+        for (uint32_t s : S) {
+            if (R[s].lo[best_d] <= best_t) L.rules.push_back(s);
+            if (R[s].hi[best_d] > best_t) Rt.rules.push_back(s);
+        }
+        q.push_back(std::move(L));
+        q.push_back(std::move(Rt));
+    }
+
+    // ---- assemble the image ----
+    const uint32_t n_nodes = (uint32_t)(nodes.size() / 2);
+    const uint32_t off_nodes = PPE_IMG_HDR_WORDS;
+    const uint32_t off_leaf = off_nodes + 2 * n_nodes;
+    uint32_t off_rules = off_leaf + (uint32_t)leaf.size();
+    off_rules = (off_rules + 7u) & ~7u;
+    const uint32_t off_resid = off_rules + 8u * (uint32_t)R.size();
+    const uint32_t total = off_resid + 8u * (uint32_t)R.size();
+
+    uint32_t *img = (uint32_t *)std::calloc(total ? total : 1, sizeof(uint32_t));
+    if (!img) return PPE_ENOMEM;
+    img[0] = PPE_IMG_MAGIC;
+    img[1] = PPE_IMG_VERSION;
+    img[PPE_IMG_W_NNODES] = n_nodes;
+    img[PPE_IMG_W_NLEAF] = (uint32_t)leaf.size();
+    img[PPE_IMG_W_NRULES] = (uint32_t)R.size();
+    img[PPE_IMG_W_OFFNODES] = off_nodes;
+    img[PPE_IMG_W_OFFLEAF] = off_leaf;
+    img[PPE_IMG_W_OFFRULES] = off_rules;
+    img[PPE_IMG_W_OFFRESID] = off_resid;
+    img[PPE_IMG_W_DEFACT] = default_action;
+    img[PPE_IMG_W_MAXDEPTH] = max_depth;
+    img[PPE_IMG_W_TOTAL] = total;
+    std::memcpy(img + off_nodes, nodes.data(), nodes.size() * sizeof(uint32_t));
+    if (!leaf.empty()) std::memcpy(img + off_leaf, leaf.data(), leaf.size() * sizeof(uint32_t));
+    for (size_t s = 0; s < R.size(); ++s) {
+        const Rule &r = R[s];
+        uint32_t *o = img + off_rules + 8 * s;
+        o[0] = r.lo[PPE_DIM_SIP];
+        o[1] = r.hi[PPE_DIM_SIP];
+        o[2] = r.lo[PPE_DIM_DIP];
+        o[3] = r.hi[PPE_DIM_DIP];
+        o[4] = r.lo[PPE_DIM_SPORT] | (r.hi[PPE_DIM_SPORT] << 16);
+        o[5] = r.lo[PPE_DIM_DPORT] | (r.hi[PPE_DIM_DPORT] << 16);
+        o[6] = r.lo[PPE_DIM_PROTO] | (r.hi[PPE_DIM_PROTO] << 8) | ((r.action & 0xffffu) << 16);
+        o[7] = r.id | (r.resid << 29);
+    }
+    if (!resid_words.empty())
+        std::memcpy(img + off_resid, resid_words.data(), resid_words.size() * sizeof(uint32_t));
+
+    *words_out = img;
+    *n_words_out = total;
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        st->n_rules = (uint32_t)R.size();
+        st->n_nodes = n_nodes;
+        st->n_leaves = n_leaves;
+        st->n_leaf_entries = (uint32_t)leaf.size();
+        st->max_depth = max_depth;
+        st->avg_depth = n_leaves ? depth_sum / n_leaves : 0.0;
+        st->blob_bytes = total * 4u;
+        st->build_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return PPE_OK;
+}
+
+extern "C" void ppe_acl_free_image(uint32_t *words) { std::free(words); }

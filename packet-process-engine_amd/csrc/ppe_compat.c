@@ -1,0 +1,323 @@
+/*
+ * ppe_compat.c — the reference's decoder / ACL / plugin / log entry points as thin shims over the GPU engine.
+ *
+ *   DP_Acl_Rule_Init        main.c:177
+ *   DP_Acl_Load_Rule        dataplane/src/common/dp_cmd.c:2019
+ *   DP_Acl_Rule_Clean       dataplane/src/common/dp_cmd.c:2030
+ *   DP_Acl_Rule_Release     dataplane/src/platform/oct-init.c:755
+ *   DP_Acl_Rule_Commit      the dp_acl_rule_commit protocol, dataplane/src/common/dp_cmd.c:1987-2053
+ *   DP_Acl_Lookup           dataplane/src/flow/flow.c:232
+ *   Decode                  dataplane/src/decode/decode.c:19-28 (burst-queued; see ppe_decode.h)
+ *   reg_fw_alert/DP_Log_Func dataplane/src/common/dp_log.c:12-31
+ *   plugin_modules          dataplane/src/plugin/plugin-mod/plugin.c:8
+ * Every packet decision is made by the HIP kernels; nothing here inspects packet bytes to classify them.
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ppe_decode.h"
+#include "ppe_hip.h"
+
+uint32_t dp_acl_action_default = ACL_RULE_ACTION_DROP;
+int gWstDepth = 0, gAvgDepth = 0, gChildCount = 0, gNumTreeNode = 0, gNumLeafNode = 0;
+uint32_t unsupport_proto_action = 0; /* dataplane/src/common/dp_cmd.c:37 */
+uint32_t syn_check = 1;              /* dataplane/src/flow/flow.c:26 */
+PluginModule plugin_modules[PLUGIN_SIZE];
+
+struct ppe_tree_set {
+    uint32_t generation;
+    ppe_acl_stats_t stats;
+};
+struct ppe_tree_node {
+    uint32_t generation;
+};
+
+static ppe_ctx_t *g_ctx = NULL;
+static uint32_t g_generation = 0;
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+static fw_alert fw_log_fun = NULL;
+static ppe_output_fn out_fw = NULL, out_drop = NULL, out_punt = NULL;
+
+struct ppe_ctx *ppe_compat_ctx(void) { return g_ctx; }
+
+void reg_fw_alert(fw_alert fun) { fw_log_fun = fun; }
+
+void DP_Log_Func(mbuf_t *m) {
+    if (m && fw_log_fun) fw_log_fun((void *)m);
+}
+
+void ppe_set_output_hooks(ppe_output_fn fw, ppe_output_fn drop, ppe_output_fn punt) {
+    out_fw = fw;
+    out_drop = drop;
+    out_punt = punt;
+}
+
+int DP_Acl_Rule_Init(void) {
+    pthread_mutex_lock(&g_lock);
+    int rc = SEC_OK;
+    if (!g_ctx) {
+        const char *d = getenv("PPE_DEVICE");
+        if (ppe_ctx_create(d ? atoi(d) : 0, &g_ctx) != PPE_OK) {
+            g_ctx = NULL;
+            rc = SEC_NO;
+        }
+    }
+    if (rc == SEC_OK && !rule_list && ppe_rule_list_init() != 0) rc = SEC_NO;
+    pthread_mutex_unlock(&g_lock);
+    return rc;
+}
+
+static void publish_stats(const ppe_acl_stats_t *st) {
+    gWstDepth = (int)st->max_depth;
+    gChildCount = (int)st->n_leaves;
+    gAvgDepth = (int)(st->avg_depth * st->n_leaves + 0.5);
+    gNumTreeNode = (int)st->n_nodes;
+    gNumLeafNode = (int)st->n_leaves;
+}
+
+uint32_t DP_Acl_Load_Rule(rule_list_t *rl, TreeSet **tset, TreeNode **tnode) {
+    if (!rl || !g_ctx) return SEC_NO;
+    RCP_BLOCK_ACL_RULE_TUPLE *t = (RCP_BLOCK_ACL_RULE_TUPLE *)malloc(sizeof(*t) * RULE_ENTRY_MAX);
+    uint8_t *used = (uint8_t *)malloc(RULE_ENTRY_MAX);
+    if (!t || !used) {
+        free(t);
+        free(used);
+        return SEC_NO;
+    }
+    for (int i = 0; i < RULE_ENTRY_MAX; i++) {
+        memcpy(&t[i], &rl->rule_entry[i].rule_tuple, sizeof(*t));
+        used[i] = (uint8_t)rl->rule_entry[i].entry_status;
+    }
+    ppe_acl_stats_t st;
+    const int rc = ppe_rules_commit(g_ctx, t, used, RULE_ENTRY_MAX, dp_acl_action_default, &st);
+    free(t);
+    free(used);
+    if (rc != PPE_OK) return SEC_NO;
+    publish_stats(&st);
+    ++g_generation;
+    if (tset) {
+        struct ppe_tree_set *s = (struct ppe_tree_set *)calloc(1, sizeof *s);
+        if (s) {
+            s->generation = g_generation;
+            s->stats = st;
+        }
+        *tset = s;
+    }
+    if (tnode) {
+        struct ppe_tree_node *n = (struct ppe_tree_node *)calloc(1, sizeof *n);
+        if (n) n->generation = g_generation;
+        *tnode = n;
+    }
+    return SEC_OK;
+}
+
+void DP_Acl_Rule_Clean(TreeSet **tset, TreeNode **tnode) {
+    if (tset && *tset) {
+        free(*tset);
+        *tset = NULL;
+    }
+    if (tnode && *tnode) {
+        free(*tnode);
+        *tnode = NULL;
+    }
+}
+
+void DP_Acl_Rule_Release(void) {
+    pthread_mutex_lock(&g_lock);
+    if (g_ctx) ppe_ctx_destroy(g_ctx);
+    g_ctx = NULL;
+    pthread_mutex_unlock(&g_lock);
+}
+
+int DP_Acl_Rule_Commit(void) {
+    if (!g_ctx || !rule_list) return SEC_NO;
+    int rc = SEC_OK;
+    pthread_mutex_lock(&rule_list->rulelist_mutex);
+    if (rule_list->build_status != RULE_BUILD_COMMIT) {
+        TreeSet *ts = NULL;
+        TreeNode *tn = NULL;
+        if (DP_Acl_Load_Rule(rule_list, &ts, &tn) != SEC_OK) rc = SEC_NO;  /* "commit failed" */
+        DP_Acl_Rule_Clean(&ts, &tn);
+        rule_list->build_status = RULE_BUILD_COMMIT;  /* set either way, dp_cmd.c:2048 */
+    }
+    pthread_mutex_unlock(&rule_list->rulelist_mutex);
+    return rc;
+}
+
+static void mbuf_tuple(const mbuf_t *m, uint32_t *tw, uint32_t *mw) {
+    tw[0] = m->ipv4.sip;
+    tw[1] = m->ipv4.dip;
+    tw[2] = (uint32_t)m->sport | ((uint32_t)m->dport << 16);
+    tw[3] = m->proto;
+    const uint8_t *d = m->eth_dst, *s = m->eth_src;
+    mw[0] = (uint32_t)d[0] | ((uint32_t)d[1] << 8) | ((uint32_t)d[2] << 16) | ((uint32_t)d[3] << 24);
+    mw[1] = (uint32_t)d[4] | ((uint32_t)d[5] << 8);
+    mw[2] = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+    mw[3] = (uint32_t)s[4] | ((uint32_t)s[5] << 8);
+}
+
+int DP_Acl_Lookup_Burst(mbuf_t **m, uint32_t n, int *actions) {
+    if (!g_ctx || !m) return PPE_EINVAL;
+    if (n == 0) return PPE_OK;
+    uint32_t *tw = (uint32_t *)malloc((size_t)n * 16), *mw = (uint32_t *)malloc((size_t)n * 16);
+    uint64_t *ts = (uint64_t *)malloc((size_t)n * 8);
+    int32_t *hit = (int32_t *)malloc((size_t)n * 4);
+    uint32_t *act = (uint32_t *)malloc((size_t)n * 4);
+    int rc = PPE_ENOMEM;
+    if (tw && mw && ts && hit && act) {
+        for (uint32_t i = 0; i < n; i++) {
+            mbuf_tuple(m[i], tw + 4 * i, mw + 4 * i);
+            ts[i] = m[i]->timestamp;
+        }
+        ppe_tuples_t in = {tw, mw, ts, n};
+        rc = ppe_acl_lookup_host(g_ctx, &in, hit, act, 0);
+        if (rc == PPE_OK)
+            for (uint32_t i = 0; i < n; i++) {
+                m[i]->ppe_acl_hit = hit[i];
+                if (actions) actions[i] = act[i] == ACL_RULE_ACTION_DROP ? ACL_RULE_ACTION_DROP : ACL_RULE_ACTION_FW;
+            }
+    }
+    free(tw);
+    free(mw);
+    free(ts);
+    free(hit);
+    free(act);
+    return rc;
+}
+
+int DP_Acl_Lookup(mbuf_t *m) {
+    int a = ACL_RULE_ACTION_FW;
+    if (!m || DP_Acl_Lookup_Burst(&m, 1, &a) != PPE_OK) return (int)dp_acl_action_default;
+    return a;
+}
+
+/* ---- Decode burst ---- */
+#define PPE_COMPAT_STRIDE 128u
+static mbuf_t **g_burst = NULL;
+static uint32_t g_burst_n = 0, g_burst_cap = 4096;
+static pthread_mutex_t g_burst_lock = PTHREAD_MUTEX_INITIALIZER;
+
+void Decode_Set_Burst(uint32_t n) {
+    pthread_mutex_lock(&g_burst_lock);
+    if (n) g_burst_cap = n;
+    pthread_mutex_unlock(&g_burst_lock);
+}
+
+/* statuses on which the reference calls DP_Log_Func before dropping */
+static int logged_drop(uint32_t st) {
+    switch (st) {
+        case PPE_ST_L2_HEADER_ERR: case PPE_ST_VLAN_HEADER_ERR: case PPE_ST_IPV4_HEADER_ERR:
+        case PPE_ST_IPV4_VERSION_ERR: case PPE_ST_IPV4_LEN_ERR: case PPE_ST_FRAG_LEN_ERR:
+        case PPE_ST_UDP_HEADER_ERR: case PPE_ST_UDP_LEN_ERR: case PPE_ST_TCP_HEADER_ERR:
+        case PPE_ST_TCP_LEN_ERR: case PPE_ST_ACL_DROP:
+            return 1;
+        default:
+            return 0;
+    }
+}
+
+static int flush_locked(void) {
+    const uint32_t n = g_burst_n;
+    if (n == 0) return 0;
+    if (!g_ctx) return PPE_ENODEV;
+    uint8_t *hdr = (uint8_t *)aligned_alloc(16, (size_t)n * PPE_COMPAT_STRIDE);
+    uint32_t *len = (uint32_t *)malloc((size_t)n * 4), *verdict = (uint32_t *)malloc((size_t)n * 4);
+    uint32_t *fh = (uint32_t *)malloc((size_t)n * 4), *tuple = (uint32_t *)malloc((size_t)n * 16);
+    uint64_t *ts = (uint64_t *)malloc((size_t)n * 8);
+    int32_t *hit = (int32_t *)malloc((size_t)n * 4);
+    int rc = PPE_ENOMEM;
+    if (hdr && len && verdict && fh && tuple && ts && hit) {
+        memset(hdr, 0, (size_t)n * PPE_COMPAT_STRIDE);
+        for (uint32_t i = 0; i < n; i++) {
+            mbuf_t *m = g_burst[i];
+            const uint32_t c = m->pkt_totallen < PPE_COMPAT_STRIDE ? m->pkt_totallen : PPE_COMPAT_STRIDE;
+            if (m->pkt_ptr && c) memcpy(hdr + (size_t)i * PPE_COMPAT_STRIDE, m->pkt_ptr, c);
+            len[i] = m->pkt_totallen;
+            ts[i] = m->timestamp;
+        }
+        ppe_batch_t b = {hdr, len, ts, n, PPE_COMPAT_STRIDE};
+        ppe_result_t r;
+        memset(&r, 0, sizeof r);
+        r.verdict = verdict;
+        r.flow_hash = fh;
+        r.acl_hit = hit;
+        r.tuple = tuple;
+        ppe_cfg_t cfg = {unsupport_proto_action ? 1u : 0u, syn_check ? 1u : 0u, 0};
+        rc = ppe_classify_host(g_ctx, &b, &r, &cfg, 0);
+        if (rc == PPE_OK) {
+            for (uint32_t i = 0; i < n; i++) {
+                mbuf_t *m = g_burst[i];
+                const uint32_t v = verdict[i], st = PPE_VERDICT_STATUS(v), fl = PPE_VERDICT_FLAGS(v);
+                uint8_t *pkt = (uint8_t *)m->pkt_ptr;
+                m->ppe_verdict = v;
+                m->ppe_flow_hash = fh[i];
+                m->ppe_acl_hit = hit[i];
+                m->vlan_idx = (fl & PPE_F_VLAN) ? 1 : 0;
+                if (pkt && m->pkt_totallen >= 14) {
+                    memcpy(m->eth_dst, pkt, 6);
+                    memcpy(m->eth_src, pkt + 6, 6);
+                    m->ethh = pkt;
+                    if (m->vlan_idx) m->vlanh = pkt + 14;
+                }
+                m->ipv4.sip = tuple[4 * i];
+                m->ipv4.dip = tuple[4 * i + 1];
+                m->proto = (uint8_t)tuple[4 * i + 3];
+                if (fl & PPE_F_L4) {
+                    m->sport = (uint16_t)tuple[4 * i + 2];
+                    m->dport = (uint16_t)(tuple[4 * i + 2] >> 16);
+                    m->payload_len = (uint16_t)(tuple[4 * i + 3] >> 16);
+                    m->flags |= PKT_HAS_FLOW;
+                }
+                if (fl & PPE_F_FRAG) m->flags |= PKT_IP_FRAG;
+                switch (PPE_VERDICT_ACTION(v)) {
+                    case PPE_ACT_FW:
+                        if (out_fw) out_fw(m);
+                        break;
+                    case PPE_ACT_DROP:
+                        if (logged_drop(st)) DP_Log_Func(m);
+                        if (out_drop) out_drop(m);
+                        break;
+                    default:
+                        if (out_punt) out_punt(m);
+                        break;
+                }
+            }
+            rc = (int)n;
+        }
+    }
+    free(hdr);
+    free(len);
+    free(verdict);
+    free(fh);
+    free(tuple);
+    free(ts);
+    free(hit);
+    g_burst_n = 0;
+    return rc;
+}
+
+int Decode_Flush(void) {
+    pthread_mutex_lock(&g_burst_lock);
+    const int rc = flush_locked();
+    pthread_mutex_unlock(&g_burst_lock);
+    return rc;
+}
+
+void Decode(mbuf_t *m) {
+    if (!m) return;
+    pthread_mutex_lock(&g_burst_lock);
+    if (!g_burst || g_burst_n >= g_burst_cap) {
+        if (g_burst_n) flush_locked();
+        mbuf_t **nb = (mbuf_t **)realloc(g_burst, sizeof(mbuf_t *) * g_burst_cap);
+        if (!nb) {
+            pthread_mutex_unlock(&g_burst_lock);
+            if (out_drop) out_drop(m);
+            return;
+        }
+        g_burst = nb;
+    }
+    g_burst[g_burst_n++] = m;
+    if (g_burst_n >= g_burst_cap) flush_locked();
+    pthread_mutex_unlock(&g_burst_lock);
+}

@@ -1,0 +1,505 @@
+/*
+ * ppe_engine.hip — host runtime behind the C ABI in include/ppe_hip.h.
+ *
+ * Owns, per context (one per GPU, like one per-core dataplane instance):
+ *   - the double-buffered classifier image (g_acltree_1/2 + running pointer + rwlock-protected swap of
+ *     dataplane/src/common/dp_cmd.c:1963-1985): commit writes the back image only after the last launch that
+ *     read it has completed (HIP event), then flips `running` — the swap happens at a batch boundary;
+ *   - per-workgroup counter slots (the per-core pktstat[] of dataplane/src/decode/decode-statistic.c:4-22);
+ *   - HIP-event kernel timing, and the pipelined host-buffer path (H2D → classify → D2H on 3 streams).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "ppe_hip.h"
+#include "ppe_image.h"
+#include "ppe_internal.h"
+
+namespace {
+
+constexpr int kSlotSets = 4;      // set 0: ppe_classify; 1..3: host pipeline streams
+constexpr int kHostStreams = 3;
+constexpr uint32_t kMaxBlocksPerCU = 8;
+
+struct HostStage {
+    hipStream_t s = nullptr;
+    uint8_t *hdr = nullptr;
+    uint32_t *len = nullptr;
+    uint64_t *ts = nullptr;
+    uint32_t *verdict = nullptr, *fhash = nullptr, *fw = nullptr, *drop = nullptr, *tcnt = nullptr,
+             *tuple = nullptr;
+    int32_t *hit = nullptr;
+    uint32_t cap = 0, stride = 0;
+};
+
+}  // namespace
+
+struct ppe_ctx {
+    int device = 0;
+    uint32_t n_cu = 256;
+    // classifier images
+    uint32_t *d_img[2] = {nullptr, nullptr};
+    size_t img_cap[2] = {0, 0};
+    std::vector<uint32_t> h_img[2];
+    ppe_acl_stats_t stats[2];
+    hipEvent_t img_done[2] = {nullptr, nullptr};
+    bool img_used[2] = {false, false};
+    int running = 0;
+    // counters
+    unsigned long long *d_cslots = nullptr;
+    uint32_t max_grid = 0;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;  // pairs
+    size_t ev_used = 0;
+    // host pipeline
+    HostStage hs[kHostStreams];
+    char err[256] = {0};
+};
+
+namespace {
+
+int fail(ppe_ctx *c, int code, const char *fmt, ...) {
+    if (c) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(c->err, sizeof c->err, fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                           \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) return fail((c), PPE_EIO, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+uint32_t blocks_per_cu(uint32_t img_bytes, bool lds) {
+    if (!lds) return kMaxBlocksPerCU;
+    const uint32_t per_block = 128u + ((img_bytes + 15u) & ~15u);
+    uint32_t b = (160u * 1024u) / per_block;
+    return std::max(1u, std::min(kMaxBlocksPerCU, b));
+}
+
+int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const ppe_acl_stats_t *st) {
+    if (c->img_used[slot]) HIPCHK(c, hipEventSynchronize(c->img_done[slot]));
+    const size_t bytes = (size_t)n_words * 4u;
+    if (bytes > c->img_cap[slot]) {
+        if (c->d_img[slot]) HIPCHK(c, hipFree(c->d_img[slot]));
+        c->d_img[slot] = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_img[slot], bytes + 64));
+        c->img_cap[slot] = bytes;
+    }
+    HIPCHK(c, hipMemcpy(c->d_img[slot], words, bytes, hipMemcpyHostToDevice));
+    c->h_img[slot].assign(words, words + n_words);
+    c->stats[slot] = *st;
+    c->stats[slot].lds_resident = bytes <= PPE_LDS_IMG_MAX ? 1u : 0u;
+    c->img_used[slot] = false;
+    return PPE_OK;
+}
+
+int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg, hipStream_t s,
+           int slot_set, uint32_t idx_base = 0) {
+    const int r = c->running;
+    const uint32_t words = (uint32_t)c->h_img[r].size();
+    const bool lds = (size_t)words * 4u <= PPE_LDS_IMG_MAX;
+    const uint32_t tiles = (in->n + 63u) / 64u;
+    const uint32_t want = (tiles + (PPE_BLOCK / 64) - 1) / (PPE_BLOCK / 64);
+    const uint32_t maxg = c->n_cu * blocks_per_cu(words * 4u, lds);
+    const uint32_t grid = std::max(1u, std::min(want, std::min(maxg, c->max_grid)));
+
+    ppe_kargs a;
+    std::memset(&a, 0, sizeof a);
+    a.hdr = in->hdr;
+    a.len = in->len;
+    a.ts = in->ts;
+    a.n = in->n;
+    a.stride = in->stride;
+    a.verdict = out->verdict;
+    a.fhash = out->flow_hash;
+    a.hit = out->acl_hit;
+    a.fw_idx = out->fw_idx;
+    a.drop_idx = out->drop_idx;
+    a.tile_cnt = out->tile_cnt;
+    a.tuple = out->tuple;
+    a.img = c->d_img[r];
+    a.img_words = words;
+    a.unsup_fw = cfg ? cfg->unsupport_proto_action : 0u;
+    a.syn_check = cfg ? cfg->syn_check : 1u;
+    a.now = cfg ? cfg->now_seconds : 0u;
+    a.default_action = c->h_img[r][PPE_IMG_W_DEFACT];
+    a.idx_base = idx_base;
+    a.cslots = c->d_cslots + (size_t)slot_set * c->max_grid * PPE_CSLOT_WORDS;
+
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing) {
+        if (c->ev_used + 2 > c->ev.size()) {
+            for (int i = 0; i < 256; ++i) {
+                hipEvent_t e;
+                HIPCHK(c, hipEventCreate(&e));
+                c->ev.push_back(e);
+            }
+        }
+        e0 = c->ev[c->ev_used];
+        e1 = c->ev[c->ev_used + 1];
+        c->ev_used += 2;
+        HIPCHK(c, hipEventRecord(e0, s));
+    }
+    const int rc = ppe_launch_classify(&a, grid, lds ? 1 : 0, (void *)s);
+    if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
+    if (c->timing) HIPCHK(c, hipEventRecord(e1, s));
+    HIPCHK(c, hipEventRecord(c->img_done[r], s));
+    c->img_used[r] = true;
+    return PPE_OK;
+}
+
+int check_batch(ppe_ctx *c, const ppe_batch_t *in, const ppe_cfg_t *cfg) {
+    if (!in) return fail(c, PPE_EINVAL, "null batch");
+    if (in->n == 0) return PPE_OK;
+    if (!in->hdr || !in->len) return fail(c, PPE_EINVAL, "hdr/len required");
+    if (in->stride != 64 && in->stride != 128) return fail(c, PPE_EINVAL, "stride must be 64 or 128");
+    if (((uintptr_t)in->hdr & 15u) != 0) return fail(c, PPE_EINVAL, "hdr must be 16-byte aligned");
+    if (cfg && cfg->unsupport_proto_action > 1) return fail(c, PPE_EINVAL, "unsupport_proto_action must be 0/1");
+    if (cfg && cfg->syn_check > 1) return fail(c, PPE_EINVAL, "syn_check must be 0/1");
+    return PPE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppe_abi_version(void) { return PPE_ABI_VERSION; }
+
+const char *ppe_last_error(ppe_ctx_t *ctx) { return ctx ? ctx->err : "null context"; }
+
+int ppe_ctx_create(int device, ppe_ctx_t **out) {
+    if (!out) return PPE_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PPE_ENODEV;
+    if (device < 0 || device >= ndev) return PPE_ENODEV;
+    ppe_ctx *c = new (std::nothrow) ppe_ctx();
+    if (!c) return PPE_ENOMEM;
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess) {
+        delete c;
+        return PPE_ENODEV;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->n_cu = (uint32_t)prop.multiProcessorCount;
+    c->max_grid = c->n_cu * kMaxBlocksPerCU;
+    const size_t cs_bytes = (size_t)kSlotSets * c->max_grid * PPE_CSLOT_WORDS * sizeof(unsigned long long);
+    int rc = PPE_OK;
+    if (hipMalloc(&c->d_cslots, cs_bytes) != hipSuccess || hipMemset(c->d_cslots, 0, cs_bytes) != hipSuccess)
+        rc = PPE_ENOMEM;
+    for (int i = 0; i < 2 && rc == PPE_OK; ++i)
+        if (hipEventCreateWithFlags(&c->img_done[i], hipEventDisableTiming) != hipSuccess) rc = PPE_EIO;
+    if (rc == PPE_OK) {
+        // empty rule set, management default action DROP (mgrplane/src/srv/srvnet/srv_rule.c:84)
+        rc = ppe_rules_commit(c, nullptr, nullptr, 0, ACL_RULE_ACTION_DROP, nullptr);
+    }
+    if (rc != PPE_OK) {
+        ppe_ctx_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return PPE_OK;
+}
+
+int ppe_ctx_destroy(ppe_ctx_t *c) {
+    if (!c) return PPE_EINVAL;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    for (int i = 0; i < 2; ++i) {
+        if (c->d_img[i]) (void)hipFree(c->d_img[i]);
+        if (c->img_done[i]) (void)hipEventDestroy(c->img_done[i]);
+    }
+    if (c->d_cslots) (void)hipFree(c->d_cslots);
+    for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    for (auto &h : c->hs) {
+        if (h.s) (void)hipStreamDestroy(h.s);
+        (void)hipFree(h.hdr);
+        (void)hipFree(h.len);
+        (void)hipFree(h.ts);
+        (void)hipFree(h.verdict);
+        (void)hipFree(h.fhash);
+        (void)hipFree(h.hit);
+        (void)hipFree(h.fw);
+        (void)hipFree(h.drop);
+        (void)hipFree(h.tcnt);
+        (void)hipFree(h.tuple);
+    }
+    delete c;
+    return PPE_OK;
+}
+
+int ppe_ctx_device(ppe_ctx_t *c) { return c ? c->device : PPE_EINVAL; }
+
+int ppe_rules_commit(ppe_ctx_t *c, const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                     uint32_t default_action, ppe_acl_stats_t *stats) {
+    if (!c) return PPE_EINVAL;
+    if (default_action > 0xffffu) return fail(c, PPE_EINVAL, "default action out of range");
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t *words = nullptr, n_words = 0;
+    ppe_acl_stats_t st;
+    const char *bt = getenv("PPE_BINTH");
+    const uint32_t binth = bt ? (uint32_t)atoi(bt) : 0u;
+    int rc = ppe_acl_build_image(rules, used, n, default_action, binth, &words, &n_words, &st);
+    if (rc != PPE_OK) return fail(c, rc, "classifier build failed (%d)", rc);
+    const int back = c->h_img[c->running].empty() ? c->running : 1 - c->running;
+    rc = upload_image(c, back, words, n_words, &st);
+    ppe_acl_free_image(words);
+    if (rc != PPE_OK) return rc;
+    c->running = back;  // publish: later launches read the new image (set_running_acltree, dp_cmd.c:1980-1985)
+    if (stats) *stats = c->stats[back];
+    return PPE_OK;
+}
+
+int ppe_classify(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
+                 void *stream) {
+    if (!c || !out) return PPE_EINVAL;
+    int rc = check_batch(c, in, cfg);
+    if (rc != PPE_OK || in->n == 0) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    return launch(c, in, out, cfg, (hipStream_t)stream, 0);
+}
+
+int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
+                      uint32_t chunk) {
+    if (!c || !out) return PPE_EINVAL;
+    int rc = check_batch(c, in, cfg);
+    if (rc != PPE_OK || in->n == 0) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (chunk == 0) chunk = 1u << 18;
+    chunk = (chunk + 63u) & ~63u;
+    chunk = std::min(chunk, (in->n + 63u) & ~63u);
+    for (auto &h : c->hs) {
+        if (!h.s) HIPCHK(c, hipStreamCreateWithFlags(&h.s, hipStreamNonBlocking));
+        if (h.cap < chunk || h.stride != in->stride) {
+            (void)hipFree(h.hdr); (void)hipFree(h.len); (void)hipFree(h.ts); (void)hipFree(h.verdict); (void)hipFree(h.fhash);
+            (void)hipFree(h.hit); (void)hipFree(h.fw); (void)hipFree(h.drop); (void)hipFree(h.tcnt); (void)hipFree(h.tuple);
+            h = HostStage{h.s};
+            HIPCHK(c, hipMalloc(&h.hdr, (size_t)chunk * in->stride));
+            HIPCHK(c, hipMalloc(&h.len, (size_t)chunk * 4));
+            HIPCHK(c, hipMalloc(&h.ts, (size_t)chunk * 8));
+            HIPCHK(c, hipMalloc(&h.verdict, (size_t)chunk * 4));
+            HIPCHK(c, hipMalloc(&h.fhash, (size_t)chunk * 4));
+            HIPCHK(c, hipMalloc(&h.hit, (size_t)chunk * 4));
+            HIPCHK(c, hipMalloc(&h.fw, (size_t)chunk * 4));
+            HIPCHK(c, hipMalloc(&h.drop, (size_t)chunk * 4));
+            HIPCHK(c, hipMalloc(&h.tcnt, (size_t)(chunk / 64) * 4));
+            HIPCHK(c, hipMalloc(&h.tuple, (size_t)chunk * 16));
+            h.cap = chunk;
+            h.stride = in->stride;
+        }
+    }
+    const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
+    for (uint32_t base = 0, i = 0; base < in->n; base += chunk, ++i) {
+        HostStage &h = c->hs[i % kHostStreams];
+        const uint32_t m = std::min(chunk, in->n - base);
+        HIPCHK(c, hipMemcpyAsync(h.hdr, in->hdr + (size_t)base * in->stride, (size_t)m * in->stride, h2d, h.s));
+        HIPCHK(c, hipMemcpyAsync(h.len, in->len + base, (size_t)m * 4, h2d, h.s));
+        if (in->ts) HIPCHK(c, hipMemcpyAsync(h.ts, in->ts + base, (size_t)m * 8, h2d, h.s));
+        ppe_batch_t b = {h.hdr, h.len, in->ts ? h.ts : nullptr, m, in->stride};
+        ppe_result_t r;
+        r.verdict = out->verdict ? h.verdict : nullptr;
+        r.flow_hash = out->flow_hash ? h.fhash : nullptr;
+        r.acl_hit = out->acl_hit ? h.hit : nullptr;
+        r.fw_idx = out->fw_idx ? h.fw : nullptr;
+        r.drop_idx = out->drop_idx ? h.drop : nullptr;
+        r.tile_cnt = out->tile_cnt ? h.tcnt : nullptr;
+        r.tuple = out->tuple ? h.tuple : nullptr;
+        rc = launch(c, &b, &r, cfg, h.s, 1 + (int)(i % kHostStreams), base);
+        if (rc != PPE_OK) return rc;
+        if (out->verdict) HIPCHK(c, hipMemcpyAsync(out->verdict + base, h.verdict, (size_t)m * 4, d2h, h.s));
+        if (out->flow_hash) HIPCHK(c, hipMemcpyAsync(out->flow_hash + base, h.fhash, (size_t)m * 4, d2h, h.s));
+        if (out->acl_hit) HIPCHK(c, hipMemcpyAsync(out->acl_hit + base, h.hit, (size_t)m * 4, d2h, h.s));
+        if (out->tuple) HIPCHK(c, hipMemcpyAsync(out->tuple + (size_t)base * 4, h.tuple, (size_t)m * 16, d2h, h.s));
+        if (out->tile_cnt)
+            HIPCHK(c, hipMemcpyAsync(out->tile_cnt + base / 64, h.tcnt, (size_t)((m + 63) / 64) * 4, d2h, h.s));
+        // compacted indices carry the batch index (idx_base); chunk is a multiple of 64, so tiles line up
+        if (out->fw_idx) HIPCHK(c, hipMemcpyAsync(out->fw_idx + base, h.fw, (size_t)m * 4, d2h, h.s));
+        if (out->drop_idx) HIPCHK(c, hipMemcpyAsync(out->drop_idx + base, h.drop, (size_t)m * 4, d2h, h.s));
+    }
+    for (auto &h : c->hs) HIPCHK(c, hipStreamSynchronize(h.s));
+    return PPE_OK;
+}
+
+int ppe_acl_lookup(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint32_t *action, uint64_t now_seconds,
+                   void *stream) {
+    if (!c || !in) return PPE_EINVAL;
+    if (in->n == 0) return PPE_OK;
+    if (!in->tuple) return fail(c, PPE_EINVAL, "tuple required");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int r = c->running;
+    const uint32_t words = (uint32_t)c->h_img[r].size();
+    const bool lds = (size_t)words * 4u <= PPE_LDS_IMG_MAX;
+    ppe_tuple_kargs a;
+    std::memset(&a, 0, sizeof a);
+    a.tuple = in->tuple;
+    a.macs = in->macs;
+    a.ts = in->ts;
+    a.n = in->n;
+    a.hit = hit;
+    a.action = action;
+    a.img = c->d_img[r];
+    a.img_words = words;
+    a.default_action = c->h_img[r][PPE_IMG_W_DEFACT];
+    a.now = now_seconds;
+    const uint32_t want = (in->n + PPE_BLOCK - 1) / PPE_BLOCK;
+    const uint32_t grid = std::max(1u, std::min(want, c->n_cu * blocks_per_cu(words * 4u, lds)));
+    const int rc = ppe_launch_acl_tuples(&a, grid, lds ? 1 : 0, stream);
+    if (rc != 0) return fail(c, PPE_EIO, "acl kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
+    HIPCHK(c, hipEventRecord(c->img_done[r], (hipStream_t)stream));
+    c->img_used[r] = true;
+    return PPE_OK;
+}
+
+int ppe_acl_lookup_host(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint32_t *action,
+                        uint64_t now_seconds) {
+    if (!c || !in) return PPE_EINVAL;
+    if (in->n == 0) return PPE_OK;
+    if (!in->tuple) return fail(c, PPE_EINVAL, "tuple required");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t n = in->n;
+    uint8_t *buf = nullptr;
+    const size_t bytes = n * 16 + (in->macs ? n * 16 : 0) + (in->ts ? n * 8 : 0) + n * 8;
+    HIPCHK(c, hipMalloc(&buf, bytes));
+    uint32_t *dt = (uint32_t *)buf;
+    uint8_t *p = buf + n * 16;
+    uint32_t *dm = nullptr;
+    uint64_t *dts = nullptr;
+    if (in->macs) { dm = (uint32_t *)p; p += n * 16; }
+    if (in->ts) { dts = (uint64_t *)p; p += n * 8; }
+    int32_t *dh = (int32_t *)p;
+    uint32_t *da = (uint32_t *)(p + n * 4);
+    int rc = PPE_OK;
+    if (hipMemcpy(dt, in->tuple, n * 16, hipMemcpyHostToDevice) != hipSuccess ||
+        (dm && hipMemcpy(dm, in->macs, n * 16, hipMemcpyHostToDevice) != hipSuccess) ||
+        (dts && hipMemcpy(dts, in->ts, n * 8, hipMemcpyHostToDevice) != hipSuccess))
+        rc = fail(c, PPE_EIO, "tuple upload failed");
+    if (rc == PPE_OK) {
+        ppe_tuples_t d = {dt, dm, dts, in->n};
+        rc = ppe_acl_lookup(c, &d, dh, da, now_seconds, nullptr);
+    }
+    if (rc == PPE_OK && hipDeviceSynchronize() != hipSuccess) rc = fail(c, PPE_EIO, "acl kernel failed");
+    if (rc == PPE_OK && hit && hipMemcpy(hit, dh, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = PPE_EIO;
+    if (rc == PPE_OK && action && hipMemcpy(action, da, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = PPE_EIO;
+    (void)hipFree(buf);
+    return rc;
+}
+
+void *ppe_dev_alloc(ppe_ctx_t *c, size_t bytes) {
+    void *p = nullptr;
+    if (!c || hipSetDevice(c->device) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
+    return p;
+}
+void ppe_dev_free(ppe_ctx_t *c, void *p) {
+    if (c && p && hipSetDevice(c->device) == hipSuccess) (void)hipFree(p);
+}
+void *ppe_host_alloc(ppe_ctx_t *c, size_t bytes) {
+    void *p = nullptr;
+    if (!c || hipSetDevice(c->device) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+void ppe_host_free(ppe_ctx_t *c, void *p) {
+    if (c && p) (void)hipHostFree(p);
+}
+int ppe_memcpy_h2d(ppe_ctx_t *c, void *dst, const void *src, size_t bytes) {
+    if (!c) return PPE_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return PPE_OK;
+}
+int ppe_memcpy_d2h(ppe_ctx_t *c, void *dst, const void *src, size_t bytes) {
+    if (!c) return PPE_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return PPE_OK;
+}
+int ppe_memset_d(ppe_ctx_t *c, void *dst, int value, size_t bytes) {
+    if (!c) return PPE_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemset(dst, value, bytes));
+    return PPE_OK;
+}
+int ppe_sync(ppe_ctx_t *c) {
+    if (!c) return PPE_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    return PPE_OK;
+}
+
+int ppe_counters_read(ppe_ctx_t *c, ppe_counters_t *out) {
+    if (!c || !out) return PPE_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    const size_t words = (size_t)kSlotSets * c->max_grid * PPE_CSLOT_WORDS;
+    std::vector<unsigned long long> h(words);
+    HIPCHK(c, hipMemcpy(h.data(), c->d_cslots, words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    std::memset(out, 0, sizeof *out);
+    for (size_t b = 0; b < (size_t)kSlotSets * c->max_grid; ++b)
+        for (int i = 0; i < PPE_CSLOT_WORDS; ++i) out->c[i] += h[b * PPE_CSLOT_WORDS + i];
+    return PPE_OK;
+}
+
+int ppe_counters_clear(ppe_ctx_t *c) {
+    if (!c) return PPE_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemset(c->d_cslots, 0,
+                        (size_t)kSlotSets * c->max_grid * PPE_CSLOT_WORDS * sizeof(unsigned long long)));
+    return PPE_OK;
+}
+
+int ppe_timing_enable(ppe_ctx_t *c, int on) {
+    if (!c) return PPE_EINVAL;
+    c->timing = on != 0;
+    return PPE_OK;
+}
+
+int ppe_timing_read(ppe_ctx_t *c, double *total_ms, uint32_t *launches, int reset) {
+    if (!c) return PPE_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    double t = 0;
+    for (size_t i = 0; i + 1 < c->ev_used; i += 2) {
+        HIPCHK(c, hipEventSynchronize(c->ev[i + 1]));
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
+        t += ms;
+    }
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = (uint32_t)(c->ev_used / 2);
+    if (reset) c->ev_used = 0;
+    return PPE_OK;
+}
+
+int ppe_acl_image(ppe_ctx_t *c, uint32_t *words, uint32_t *n_words) {
+    if (!c || !n_words) return PPE_EINVAL;
+    const std::vector<uint32_t> &img = c->h_img[c->running];
+    if (words) std::memcpy(words, img.data(), std::min<size_t>(*n_words, img.size()) * 4u);
+    *n_words = (uint32_t)img.size();
+    return PPE_OK;
+}
+
+int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes) {
+    if (!c) return PPE_EINVAL;
+    const uint32_t words = (uint32_t)c->h_img[c->running].size();
+    const bool lds = (size_t)words * 4u <= PPE_LDS_IMG_MAX;
+    if (grid) *grid = std::min(c->n_cu * blocks_per_cu(words * 4u, lds), c->max_grid);
+    if (block) *block = PPE_BLOCK;
+    if (lds_bytes) *lds_bytes = 128u + (lds ? ((words * 4u + 15u) & ~15u) : 0u);
+    return PPE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,59 @@
+/* ppe_internal.h — declarations shared between the engine (host) and the HIP kernel translation unit. */
+#ifndef PPE_INTERNAL_H
+#define PPE_INTERNAL_H
+
+#include <stdint.h>
+
+/* Kernel launch parameters, passed by value. */
+struct ppe_kargs {
+    const uint8_t *hdr;
+    const uint32_t *len;
+    const uint64_t *ts;
+    uint32_t n;
+    uint32_t stride;
+    uint32_t *verdict;
+    uint32_t *fhash;
+    int32_t *hit;
+    uint32_t *fw_idx;
+    uint32_t *drop_idx;
+    uint32_t *tile_cnt;
+    uint32_t *tuple;
+    const uint32_t *img;      /* device classifier image (ppe_image.h) */
+    uint32_t img_words;
+    uint32_t unsup_fw;        /* 1: unsupported protocols are forwarded */
+    uint32_t syn_check;
+    uint32_t default_action;
+    uint64_t now;
+    uint32_t idx_base;        /* added to the packet indices written to fw_idx / drop_idx */
+    unsigned long long *cslots; /* [grid][PPE_CSLOT_WORDS] counter slots, one per workgroup */
+};
+
+struct ppe_tuple_kargs {
+    const uint32_t *tuple;    /* n × {sip, dip, sport | dport << 16, proto} */
+    const uint32_t *macs;     /* optional n × {dmac lo, dmac hi, smac lo, smac hi} */
+    const uint64_t *ts;
+    uint32_t n;
+    int32_t *hit;
+    uint32_t *action;
+    const uint32_t *img;
+    uint32_t img_words;
+    uint32_t default_action;
+    uint64_t now;
+};
+
+#define PPE_CSLOT_WORDS 32
+#define PPE_BLOCK 256
+/* images up to this size are staged into LDS by every workgroup */
+#define PPE_LDS_IMG_MAX (40u * 1024u)
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* Launch the classify kernel. grid = workgroups (persistent), lds_img = stage image in LDS. Returns hipError_t. */
+int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int lds_img, void *stream);
+int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,185 @@
+"""ctypes view of the C ABI in include/ppe_hip.h / ppe_acl.h (test and bench plumbing — the product is the C ABI).
+
+The library is loaded from the package tree (``packet-process-engine_amd/libppe_hip.so``); a missing library raises
+immediately: there is no Python or CPU fallback for any classification.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent.parent          # packet-process-engine_amd/
+REPO_DIR = PKG_DIR.parent
+LIB_PATH = PKG_DIR / "libppe_hip.so"
+
+# ---- constants mirrored from include/ppe_hip.h ----
+PPE_OK = 0
+ST = dict(ACL_FW=0, ACL_DROP=1, L2_HEADER_ERR=2, L2_UNSUPPORT=3, VLAN_HEADER_ERR=4, VLAN_LAYER_EXCEED=5,
+          VLAN_UNSUPPORT=6, IPV4_HEADER_ERR=7, IPV4_VERSION_ERR=8, IPV4_LEN_ERR=9, FRAG_LEN_ERR=10, FRAG=11,
+          IPV4_UNSUPPORT=12, UDP_HEADER_ERR=13, UDP_LEN_ERR=14, TCP_HEADER_ERR=15, TCP_LEN_ERR=16,
+          FLOW_TCP_NO_SYN_FIRST=17, WINDOW_PUNT=18)
+ST_NAME = {v: k for k, v in ST.items()}
+ACT_FW, ACT_DROP, ACT_PUNT = 0, 1, 2
+F_VLAN, F_L4, F_TCP, F_SYN, F_ACL, F_FRAG = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
+COUNTERS = ["l2_headerlen_err", "l2_unsupport", "l2_rx_ok",
+            "vlan_headerlen_err", "vlan_layer_exceed", "vlan_unsupport", "vlan_rx_ok",
+            "ipv4_headerlen_err", "ipv4_version_err", "ipv4_pktlen_err", "ipv4_unsupport", "ipv4_rx_ok",
+            "frag_fraglen_err", "frag_punt",
+            "udp_headerlen_err", "udp_pktlen_err", "udp_rx_ok",
+            "tcp_headerlen_err", "tcp_pktlen_err", "tcp_rx_ok",
+            "acl_drop", "acl_fw",
+            "flow_proc_ok", "flow_proc_fail", "flow_tcp_no_syn_first",
+            "out_fw", "out_drop", "out_punt", "window_punt", "pkts"]
+ACL_RULE_ACTION_FW, ACL_RULE_ACTION_DROP = 0, 1
+RULE_ENTRY_MAX = 10000
+
+# RCP_BLOCK_ACL_RULE_TUPLE, include/rpc-common.h:97-114 (packed, 60 bytes)
+RULE_DTYPE = np.dtype([
+    ("time_start", "<u8"), ("time_end", "<u8"), ("smac", "u1", 6), ("dmac", "u1", 6),
+    ("sport_start", "<u2"), ("sport_end", "<u2"), ("sip", "<u4"), ("dip", "<u4"),
+    ("sip_mask", "<u4"), ("dip_mask", "<u4"), ("dport_start", "<u2"), ("dport_end", "<u2"),
+    ("protocol_start", "u1"), ("protocol_end", "u1"), ("action", "<u2"), ("logable", "<u4"),
+])
+assert RULE_DTYPE.itemsize == 60
+
+
+class Batch(C.Structure):
+    _fields_ = [("hdr", C.c_void_p), ("len", C.c_void_p), ("ts", C.c_void_p), ("n", C.c_uint32),
+                ("stride", C.c_uint32)]
+
+
+class Result(C.Structure):
+    _fields_ = [("verdict", C.c_void_p), ("flow_hash", C.c_void_p), ("acl_hit", C.c_void_p),
+                ("fw_idx", C.c_void_p), ("drop_idx", C.c_void_p), ("tile_cnt", C.c_void_p), ("tuple", C.c_void_p)]
+
+
+class Cfg(C.Structure):
+    _fields_ = [("unsupport_proto_action", C.c_uint32), ("syn_check", C.c_uint32), ("now_seconds", C.c_uint64)]
+
+
+class AclStats(C.Structure):
+    _fields_ = [("n_rules", C.c_uint32), ("n_nodes", C.c_uint32), ("n_leaves", C.c_uint32),
+                ("n_leaf_entries", C.c_uint32), ("max_depth", C.c_uint32), ("avg_depth", C.c_double),
+                ("blob_bytes", C.c_uint32), ("lds_resident", C.c_uint32), ("build_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Counters(C.Structure):
+    _fields_ = [("c", C.c_uint64 * 32)]
+
+    def as_dict(self):
+        return {name: int(self.c[i]) for i, name in enumerate(COUNTERS)}
+
+
+class Tuples(C.Structure):
+    _fields_ = [("tuple", C.c_void_p), ("macs", C.c_void_p), ("ts", C.c_void_p), ("n", C.c_uint32)]
+
+
+# every symbol include/*.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    # ppe_hip.h
+    "ppe_abi_version", "ppe_ctx_create", "ppe_ctx_destroy", "ppe_ctx_device", "ppe_rules_commit", "ppe_classify",
+    "ppe_classify_host", "ppe_acl_lookup", "ppe_acl_lookup_host", "ppe_dev_alloc", "ppe_dev_free",
+    "ppe_host_alloc", "ppe_host_free", "ppe_memcpy_h2d", "ppe_memcpy_d2h", "ppe_memset_d", "ppe_sync",
+    "ppe_counters_read", "ppe_counters_clear", "ppe_timing_enable", "ppe_timing_read", "ppe_acl_image",
+    "ppe_launch_info", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image",
+    # ppe_acl.h
+    "ppe_rule_list_init", "ppe_rule_list_free", "Rule_add", "Rule_del_by_id", "Rule_del_all",
+    "Rule_duplicate_check", "Rule_Load_Line", "ppe_rule_load_file", "DP_Acl_Rule_Init", "DP_Acl_Load_Rule",
+    "DP_Acl_Rule_Clean", "DP_Acl_Rule_Release", "DP_Acl_Rule_Commit",
+    # ppe_decode.h
+    "ppe_set_output_hooks", "Decode", "Decode_Flush", "Decode_Set_Burst", "DP_Acl_Lookup_Burst", "DP_Acl_Lookup",
+    "reg_fw_alert", "DP_Log_Func", "ppe_compat_ctx",
+]
+EXPORTED_DATA = ["rule_list", "dp_acl_action_default", "gWstDepth", "gAvgDepth", "gChildCount", "gNumTreeNode",
+                 "gNumLeafNode", "unsupport_proto_action", "syn_check", "plugin_modules"]
+
+_lib = None
+
+
+def load(path: str | os.PathLike | None = None) -> C.CDLL:
+    """Load libppe_hip.so (raises OSError if it was not built — no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise OSError(f"{p} not found: build it with `make -C packet-process-engine_amd` (no CPU fallback exists)")
+    lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+    vp, u32, i32, u64 = C.c_void_p, C.c_uint32, C.c_int32, C.c_uint64
+    sig = {
+        "ppe_abi_version": ([], C.c_int),
+        "ppe_ctx_create": ([C.c_int, C.POINTER(vp)], C.c_int),
+        "ppe_ctx_destroy": ([vp], C.c_int),
+        "ppe_ctx_device": ([vp], C.c_int),
+        "ppe_rules_commit": ([vp, vp, vp, u32, u32, C.POINTER(AclStats)], C.c_int),
+        "ppe_classify": ([vp, C.POINTER(Batch), C.POINTER(Result), C.POINTER(Cfg), vp], C.c_int),
+        "ppe_classify_host": ([vp, C.POINTER(Batch), C.POINTER(Result), C.POINTER(Cfg), u32], C.c_int),
+        "ppe_acl_lookup": ([vp, C.POINTER(Tuples), vp, vp, u64, vp], C.c_int),
+        "ppe_acl_lookup_host": ([vp, C.POINTER(Tuples), vp, vp, u64], C.c_int),
+        "ppe_dev_alloc": ([vp, C.c_size_t], vp),
+        "ppe_dev_free": ([vp, vp], None),
+        "ppe_host_alloc": ([vp, C.c_size_t], vp),
+        "ppe_host_free": ([vp, vp], None),
+        "ppe_memcpy_h2d": ([vp, vp, vp, C.c_size_t], C.c_int),
+        "ppe_memcpy_d2h": ([vp, vp, vp, C.c_size_t], C.c_int),
+        "ppe_memset_d": ([vp, vp, C.c_int, C.c_size_t], C.c_int),
+        "ppe_sync": ([vp], C.c_int),
+        "ppe_counters_read": ([vp, C.POINTER(Counters)], C.c_int),
+        "ppe_counters_clear": ([vp], C.c_int),
+        "ppe_timing_enable": ([vp, C.c_int], C.c_int),
+        "ppe_timing_read": ([vp, C.POINTER(C.c_double), C.POINTER(u32), C.c_int], C.c_int),
+        "ppe_acl_image": ([vp, vp, C.POINTER(u32)], C.c_int),
+        "ppe_launch_info": ([vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], C.c_int),
+        "ppe_last_error": ([vp], C.c_char_p),
+        "ppe_acl_build_image": ([vp, vp, u32, u32, u32, C.POINTER(C.POINTER(u32)), C.POINTER(u32),
+                                 C.POINTER(AclStats)], C.c_int),
+        "ppe_acl_free_image": ([C.POINTER(u32)], None),
+        "ppe_rule_list_init": ([], C.c_int),
+        "ppe_rule_list_free": ([], None),
+        "Rule_add": ([vp, C.POINTER(u32)], C.c_int),
+        "Rule_del_by_id": ([u32], C.c_int),
+        "Rule_del_all": ([], C.c_int),
+        "Rule_duplicate_check": ([vp], C.c_int),
+        "ppe_rule_load_file": ([C.c_char_p], C.c_int),
+        "DP_Acl_Rule_Init": ([], C.c_int),
+        "DP_Acl_Load_Rule": ([vp, vp, vp], u32),
+        "DP_Acl_Rule_Commit": ([], C.c_int),
+        "DP_Acl_Rule_Release": ([], None),
+        "Decode": ([vp], None),
+        "Decode_Flush": ([], C.c_int),
+        "Decode_Set_Burst": ([u32], None),
+        "DP_Acl_Lookup": ([vp], C.c_int),
+        "DP_Acl_Lookup_Burst": ([vp, u32, vp], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = lib
+    return lib
+
+
+def build_image(rules: np.ndarray, used: np.ndarray | None = None, default_action: int = ACL_RULE_ACTION_DROP,
+                binth: int = 0):
+    """Host-side classifier compiler (no GPU needed): returns (image words as np.uint32, stats dict)."""
+    lib = load()
+    rules = np.ascontiguousarray(rules, dtype=RULE_DTYPE)
+    if used is not None:
+        used = np.ascontiguousarray(used, dtype=np.uint8)
+    words = C.POINTER(C.c_uint32)()
+    nw = C.c_uint32()
+    st = AclStats()
+    rc = lib.ppe_acl_build_image(rules.ctypes.data if len(rules) else None,
+                                 used.ctypes.data if used is not None else None, len(rules), default_action, binth,
+                                 C.byref(words), C.byref(nw), C.byref(st))
+    if rc != 0:
+        raise ValueError(f"ppe_acl_build_image failed: {rc}")
+    img = np.ctypeslib.as_array(words, shape=(nw.value,)).copy()
+    lib.ppe_acl_free_image(words)
+    return img, st.as_dict()

@@ -1,0 +1,162 @@
+"""Thin Python handle over one ppe_ctx_t (one GPU).  Every call goes through libppe_hip.so."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+class PPEError(RuntimeError):
+    pass
+
+
+class Engine:
+    def __init__(self, device: int = 0):
+        self.lib = abi.load()
+        self.ctx = C.c_void_p()
+        rc = self.lib.ppe_ctx_create(int(device), C.byref(self.ctx))
+        if rc != 0:
+            raise PPEError(f"ppe_ctx_create(device={device}) failed: {rc} (is a GPU visible?)")
+        self.device = int(device)
+
+    # ---- lifecycle ----
+    def close(self):
+        if self.ctx:
+            self.lib.ppe_ctx_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc != 0:
+            err = self.lib.ppe_last_error(self.ctx)
+            raise PPEError(f"{what} failed: {rc}: {err.decode() if err else ''}")
+
+    # ---- rules ----
+    def commit(self, rules: np.ndarray, used: np.ndarray | None = None,
+               default_action: int = abi.ACL_RULE_ACTION_DROP) -> dict:
+        rules = np.ascontiguousarray(rules, dtype=abi.RULE_DTYPE)
+        if used is not None:
+            used = np.ascontiguousarray(used, dtype=np.uint8)
+        st = abi.AclStats()
+        rc = self.lib.ppe_rules_commit(self.ctx, rules.ctypes.data if len(rules) else None,
+                                       used.ctypes.data if used is not None else None, len(rules),
+                                       int(default_action), C.byref(st))
+        self._check(rc, "ppe_rules_commit")
+        return st.as_dict()
+
+    def image(self) -> np.ndarray:
+        n = C.c_uint32(0)
+        self._check(self.lib.ppe_acl_image(self.ctx, None, C.byref(n)), "ppe_acl_image")
+        out = np.zeros(n.value, np.uint32)
+        self._check(self.lib.ppe_acl_image(self.ctx, out.ctypes.data, C.byref(n)), "ppe_acl_image")
+        return out
+
+    # ---- classify ----
+    @staticmethod
+    def cfg(unsupport_proto_action=0, syn_check=1, now_seconds=0) -> abi.Cfg:
+        return abi.Cfg(int(unsupport_proto_action), int(syn_check), int(now_seconds))
+
+    def classify_ptrs(self, hdr: int, lens: int, n: int, stride: int, out: dict, cfg: abi.Cfg | None = None,
+                      ts: int | None = None, stream: int | None = None):
+        """Device-pointer form (ppe_classify): enqueue on `stream` (hipStream_t as int) and return."""
+        b = abi.Batch(hdr, lens, ts, int(n), int(stride))
+        r = abi.Result(out.get("verdict"), out.get("flow_hash"), out.get("acl_hit"), out.get("fw_idx"),
+                       out.get("drop_idx"), out.get("tile_cnt"), out.get("tuple"))
+        rc = self.lib.ppe_classify(self.ctx, C.byref(b), C.byref(r), C.byref(cfg or self.cfg()), stream)
+        self._check(rc, "ppe_classify")
+
+    def classify_torch(self, hdr, lens, out: dict, cfg: abi.Cfg | None = None, ts=None, stream=None):
+        """Tensors on this engine's GPU; `out` maps output names to torch tensors (or None)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        stride = hdr.shape[1]
+        ptrs = {k: (v.data_ptr() if v is not None else None) for k, v in out.items()}
+        self.classify_ptrs(hdr.data_ptr(), lens.data_ptr(), lens.numel(), stride, ptrs, cfg,
+                           ts.data_ptr() if ts is not None else None, s.cuda_stream)
+
+    def classify_host(self, hdr: np.ndarray, lens: np.ndarray, ts: np.ndarray | None = None,
+                      cfg: abi.Cfg | None = None, chunk: int = 0, outputs=("verdict", "flow_hash", "acl_hit"),
+                      ) -> dict:
+        """Host-buffer form (ppe_classify_host: pipelined H2D → classify → D2H).  hdr: (n, stride) uint8."""
+        hdr = np.ascontiguousarray(hdr, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n, stride = hdr.shape
+        res = {}
+        if "verdict" in outputs:
+            res["verdict"] = np.zeros(n, np.uint32)
+        if "flow_hash" in outputs:
+            res["flow_hash"] = np.zeros(n, np.uint32)
+        if "acl_hit" in outputs:
+            res["acl_hit"] = np.zeros(n, np.int32)
+        if "fw_idx" in outputs:
+            res["fw_idx"] = np.zeros(n, np.uint32)
+        if "drop_idx" in outputs:
+            res["drop_idx"] = np.zeros(n, np.uint32)
+        if "tile_cnt" in outputs:
+            res["tile_cnt"] = np.zeros((n + 63) // 64, np.uint32)
+        if "tuple" in outputs:
+            res["tuple"] = np.zeros((n, 4), np.uint32)
+        if ts is not None:
+            ts = np.ascontiguousarray(ts, dtype=np.uint64)
+        b = abi.Batch(hdr.ctypes.data, lens.ctypes.data, ts.ctypes.data if ts is not None else None, n, stride)
+        g = lambda k: res[k].ctypes.data if k in res else None  # noqa: E731
+        r = abi.Result(g("verdict"), g("flow_hash"), g("acl_hit"), g("fw_idx"), g("drop_idx"), g("tile_cnt"),
+                       g("tuple"))
+        rc = self.lib.ppe_classify_host(self.ctx, C.byref(b), C.byref(r), C.byref(cfg or self.cfg()), int(chunk))
+        self._check(rc, "ppe_classify_host")
+        return res
+
+    def acl_lookup_host(self, tuple_: np.ndarray, macs: np.ndarray | None = None, ts: np.ndarray | None = None,
+                        now_seconds: int = 0):
+        tuple_ = np.ascontiguousarray(tuple_, dtype=np.uint32)
+        n = tuple_.shape[0]
+        if macs is not None:
+            macs = np.ascontiguousarray(macs, dtype=np.uint32)
+        if ts is not None:
+            ts = np.ascontiguousarray(ts, dtype=np.uint64)
+        hit = np.zeros(n, np.int32)
+        act = np.zeros(n, np.uint32)
+        t = abi.Tuples(tuple_.ctypes.data, macs.ctypes.data if macs is not None else None,
+                       ts.ctypes.data if ts is not None else None, n)
+        self._check(self.lib.ppe_acl_lookup_host(self.ctx, C.byref(t), hit.ctypes.data, act.ctypes.data,
+                                                 int(now_seconds)), "ppe_acl_lookup_host")
+        return hit, act
+
+    # ---- counters / timing ----
+    def counters(self) -> dict:
+        c = abi.Counters()
+        self._check(self.lib.ppe_counters_read(self.ctx, C.byref(c)), "ppe_counters_read")
+        return c.as_dict()
+
+    def clear_counters(self):
+        self._check(self.lib.ppe_counters_clear(self.ctx), "ppe_counters_clear")
+
+    def timing(self, on: bool = True):
+        self._check(self.lib.ppe_timing_enable(self.ctx, 1 if on else 0), "ppe_timing_enable")
+
+    def timing_read(self, reset: bool = True):
+        ms = C.c_double()
+        n = C.c_uint32()
+        self._check(self.lib.ppe_timing_read(self.ctx, C.byref(ms), C.byref(n), 1 if reset else 0),
+                    "ppe_timing_read")
+        return ms.value, n.value
+
+    def launch_info(self) -> dict:
+        g, b, l = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        self._check(self.lib.ppe_launch_info(self.ctx, C.byref(g), C.byref(b), C.byref(l)), "ppe_launch_info")
+        return {"grid": g.value, "block": b.value, "lds_bytes": l.value}
+
+    def sync(self):
+        self._check(self.lib.ppe_sync(self.ctx), "ppe_sync")
+
+
+def decode_verdict(v: np.ndarray):
+    v = np.asarray(v, dtype=np.uint32)
+    return v & 0xFF, (v >> 8) & 0xFF, v >> 16
