@@ -96,9 +96,25 @@ def main():
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
 
+    # pre-built C argument blocks: a step is one ppe_classify call (no per-step Python object building)
+    import ctypes as C
+    from ppe import abi
+    calls = []
+    for hdr, lens, out, _ in bufs:
+        b = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, stride)
+        r = abi.Result(*(out[k].data_ptr() for k in ("verdict", "flow_hash", "acl_hit", "fw_idx", "drop_idx",
+                                                      "tile_cnt")), None)
+        calls.append((C.byref(b), C.byref(r), b, r))
+    cfg_ref = C.byref(cfg)
+    sptr = C.c_void_p(stream.cuda_stream)
+    classify = eng.lib.ppe_classify
+    ctx = eng.ctx
+
     def step(i):
-        hdr, lens, out, _ = bufs[i % nbufs]
-        eng.classify_torch(hdr, lens, out, cfg=cfg, stream=stream)
+        bb, rr, _, _ = calls[i % nbufs]
+        rc = classify(ctx, bb, rr, cfg_ref, sptr)
+        if rc:
+            raise RuntimeError(f"ppe_classify failed: {rc}")
 
     def barrier():
         if dist is not None:

@@ -238,8 +238,11 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     const uint32_t off_leaf = off_nodes + 2 * n_nodes;
     uint32_t off_rules = off_leaf + (uint32_t)leaf.size();
     off_rules = (off_rules + 7u) & ~7u;
+    // residual (MAC / time) records only when some rule has one: the kernel reads them only for such rules
+    bool any_resid = false;
+    for (const Rule &r : R) any_resid |= r.resid != 0;
     const uint32_t off_resid = off_rules + 8u * (uint32_t)R.size();
-    const uint32_t total = off_resid + 8u * (uint32_t)R.size();
+    const uint32_t total = off_resid + (any_resid ? 8u * (uint32_t)R.size() : 0u);
 
     uint32_t *img = (uint32_t *)std::calloc(total ? total : 1, sizeof(uint32_t));
     if (!img) return PPE_ENOMEM;
@@ -269,8 +272,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         o[6] = r.lo[PPE_DIM_PROTO] | (r.hi[PPE_DIM_PROTO] << 8) | ((r.action & 0xffffu) << 16);
         o[7] = r.id | (r.resid << 29);
     }
-    if (!resid_words.empty())
-        std::memcpy(img + off_resid, resid_words.data(), resid_words.size() * sizeof(uint32_t));
+    if (any_resid) std::memcpy(img + off_resid, resid_words.data(), resid_words.size() * sizeof(uint32_t));
 
     *words_out = img;
     *n_words_out = total;

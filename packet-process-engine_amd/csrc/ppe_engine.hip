@@ -82,14 +82,26 @@ int fail(ppe_ctx *c, int code, const char *fmt, ...) {
     } while (0)
 
 uint32_t blocks_per_cu(uint32_t img_bytes, bool lds) {
+    static const uint32_t env_bpc = [] {
+        const char *e = getenv("PPE_BLOCKS_PER_CU");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 && v <= (int)kMaxBlocksPerCU ? (uint32_t)v : 0u;
+    }();
+    if (env_bpc) {
+        if (!lds) return env_bpc;
+        const uint32_t fit = (160u * 1024u) / (128u + ((img_bytes + 1023u) & ~1023u));
+        return std::max(1u, std::min(env_bpc, fit));
+    }
     if (!lds) return kMaxBlocksPerCU;
-    const uint32_t per_block = 128u + ((img_bytes + 15u) & ~15u);
+    const uint32_t per_block = 128u + ((img_bytes + 1023u) & ~1023u);
     uint32_t b = (160u * 1024u) / per_block;
     return std::max(1u, std::min(kMaxBlocksPerCU, b));
 }
 
 int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const ppe_acl_stats_t *st) {
-    if (c->img_used[slot]) HIPCHK(c, hipEventSynchronize(c->img_done[slot]));
+    // the back image may still be read by launches queued before the previous swap: wait for them (commits are
+    // control-plane events; launches themselves record nothing)
+    if (c->img_used[slot]) HIPCHK(c, hipDeviceSynchronize());
     const size_t bytes = (size_t)n_words * 4u;
     if (bytes > c->img_cap[slot]) {
         if (c->d_img[slot]) HIPCHK(c, hipFree(c->d_img[slot]));
@@ -155,9 +167,14 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
     const int rc = ppe_launch_classify(&a, grid, lds ? 1 : 0, (void *)s);
     if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
     if (c->timing) HIPCHK(c, hipEventRecord(e1, s));
-    HIPCHK(c, hipEventRecord(c->img_done[r], s));
     c->img_used[r] = true;
     return PPE_OK;
+}
+
+hipError_t use_device(ppe_ctx *c) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == c->device) return hipSuccess;
+    return hipSetDevice(c->device);
 }
 
 int check_batch(ppe_ctx *c, const ppe_batch_t *in, const ppe_cfg_t *cfg) {
@@ -268,7 +285,7 @@ int ppe_classify(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, c
     if (!c || !out) return PPE_EINVAL;
     int rc = check_batch(c, in, cfg);
     if (rc != PPE_OK || in->n == 0) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, use_device(c));
     return launch(c, in, out, cfg, (hipStream_t)stream, 0);
 }
 
@@ -358,7 +375,6 @@ int ppe_acl_lookup(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint32_t 
     const uint32_t grid = std::max(1u, std::min(want, c->n_cu * blocks_per_cu(words * 4u, lds)));
     const int rc = ppe_launch_acl_tuples(&a, grid, lds ? 1 : 0, stream);
     if (rc != 0) return fail(c, PPE_EIO, "acl kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
-    HIPCHK(c, hipEventRecord(c->img_done[r], (hipStream_t)stream));
     c->img_used[r] = true;
     return PPE_OK;
 }
@@ -498,7 +514,7 @@ int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds
     const bool lds = (size_t)words * 4u <= PPE_LDS_IMG_MAX;
     if (grid) *grid = std::min(c->n_cu * blocks_per_cu(words * 4u, lds), c->max_grid);
     if (block) *block = PPE_BLOCK;
-    if (lds_bytes) *lds_bytes = 128u + (lds ? ((words * 4u + 15u) & ~15u) : 0u);
+    if (lds_bytes) *lds_bytes = 128u + (lds ? ((words * 4u + 1023u) & ~1023u) : 0u);
     return PPE_OK;
 }
 

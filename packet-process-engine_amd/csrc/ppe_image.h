@@ -23,7 +23,7 @@
  *  rule (8 words, 32-B aligned), slot order == ascending rule index:
  *      sip_lo, sip_hi, dip_lo, dip_hi, sport_lo | sport_hi << 16, dport_lo | dport_hi << 16,
  *      proto_lo | proto_hi << 8 | action << 16, rule_index | resid << 29
- *  resid (8 words per slot; meaningful only when resid != 0):
+ *  resid (8 words per slot; present only when at least one rule has a residual field, read only for those):
  *      dmac bytes 0-3 (LE), dmac bytes 4-5, smac bytes 0-3, smac bytes 4-5,
  *      time_start lo, hi, time_end lo, hi
  *      resid bits: 1 = dmac must equal, 2 = smac must equal, 4 = time_start <= ts <= time_end

@@ -46,170 +46,126 @@ __device__ __forceinline__ uint32_t flow_hashfn(uint32_t proto, uint32_t sip, ui
     return tlu_hash(sip, sport) ^ tlu_hash(dip, dport) ^ tlu_hash(proto, 0);
 }
 
-struct Pkt {
-    uint32_t st, act, flags, cb;
+#define CB(x) (1u << (x))
+#define ST_ACL 0xffu  // decode passed: the ACL decides
+
+// counter index of each terminal status (enum ppe_status → enum ppe_counter), 5 bits per entry
+__device__ __forceinline__ uint32_t reason_counter(uint32_t st) {
+    constexpr uint64_t K0 =  // st 0..11
+        ((uint64_t)PPE_C_ACL_FW << 0) | ((uint64_t)PPE_C_ACL_DROP << 5) | ((uint64_t)PPE_C_L2_HEADERLEN_ERR << 10) |
+        ((uint64_t)PPE_C_L2_UNSUPPORT << 15) | ((uint64_t)PPE_C_VLAN_HEADERLEN_ERR << 20) |
+        ((uint64_t)PPE_C_VLAN_LAYER_EXCEED << 25) | ((uint64_t)PPE_C_VLAN_UNSUPPORT << 30) |
+        ((uint64_t)PPE_C_IPV4_HEADERLEN_ERR << 35) | ((uint64_t)PPE_C_IPV4_VERSION_ERR << 40) |
+        ((uint64_t)PPE_C_IPV4_PKTLEN_ERR << 45) | ((uint64_t)PPE_C_FRAG_FRAGLEN_ERR << 50) |
+        ((uint64_t)PPE_C_FRAG_PUNT << 55);
+    constexpr uint64_t K1 =  // st 12..18
+        ((uint64_t)PPE_C_IPV4_UNSUPPORT << 0) | ((uint64_t)PPE_C_UDP_HEADERLEN_ERR << 5) |
+        ((uint64_t)PPE_C_UDP_PKTLEN_ERR << 10) | ((uint64_t)PPE_C_TCP_HEADERLEN_ERR << 15) |
+        ((uint64_t)PPE_C_TCP_PKTLEN_ERR << 20) | ((uint64_t)PPE_C_FLOW_TCP_NO_SYN_FIRST << 25) |
+        ((uint64_t)PPE_C_WINDOW_PUNT << 30);
+    const bool lo = st < 12u;
+    return (uint32_t)(((lo ? K0 : K1) >> (5u * (lo ? st : st - 12u))) & 31u);
+}
+
+struct Dec {
+    uint32_t st, flags, cb;
     uint32_t sip, dip, sport, dport, proto, paylen;
-    uint32_t acl;  // 1: flow miss path reached the ACL
 };
 
-#define CB(x) (1u << (x))
-
-// Decode of one packet.  w[0..15] = first 64 bytes (little-endian dwords), row = the packet's window in global
-// memory (for fields past byte 63), stride = window size.
-__device__ __forceinline__ void decode(const uint32_t (&w)[16], uint32_t len32, const uint8_t *row,
-                                       uint32_t stride, uint32_t unsup_act, uint32_t syn_check, Pkt &k) {
+// Decode of one packet, straight-line: every check of the reference is evaluated, then the terminal status is
+// chosen by applying the checks in REVERSE order of the reference's control flow, so the first failing check
+// (the one the reference returns on) wins.  w[0..15] = first 64 bytes (little-endian dwords); row = the packet's
+// window in global memory (read only for L4 headers behind IPv4 options).
+__device__ __forceinline__ Dec decode(const uint32_t (&w)[16], uint32_t len32, const uint8_t *row, uint32_t stride,
+                                      uint32_t syn_check) {
+    Dec k;
     const uint32_t len = len32 & 0xffffu;  // Decode passes (uint16_t)pkt_totallen, decode.c:22
-    k.cb = CB(PPE_C_PKTS);
-    k.flags = 0;
-    k.acl = 0;
-    k.sip = k.dip = k.sport = k.dport = k.proto = k.paylen = 0;
-    k.act = PPE_ACT_DROP;
-
     // ---- Ethernet: dataplane/src/decode/decode-ethernet.c:23-115 ----
-    if (len < 14) {  // :29-34
-        k.st = PPE_ST_L2_HEADER_ERR; k.cb |= CB(PPE_C_L2_HEADERLEN_ERR); return;
-    }
-    const bool dst_zero = (w[0] == 0u) && ((w[1] & 0xffffu) == 0u);  // :38-44
-    const bool src_zero = ((w[1] >> 16) == 0u) && (w[2] == 0u);      // :45-51
-    if (dst_zero || src_zero) {
-        k.st = PPE_ST_L2_HEADER_ERR; k.cb |= CB(PPE_C_L2_HEADERLEN_ERR); return;
-    }
+    const bool bad_len = len < 14u;                               // :29-34
+    const bool dz = (w[0] | (w[1] & 0xffffu)) == 0u;              // :38-44 dst MAC all zero
+    const bool sz = ((w[1] >> 16) | w[2]) == 0u;                  // :45-51 src MAC all zero
     const uint32_t etype = be16_lo(w[3]);
-    uint32_t v, l3len;
-    if (etype == 0x0800u) {  // :75-79
-        k.cb |= CB(PPE_C_L2_RX_OK);
-        v = 0;
-        l3len = len - 14u;
-    } else if (etype == 0x8100u || etype == 0x9100u) {  // :96-101 → decode-vlan.c:23-89
-        k.cb |= CB(PPE_C_L2_RX_OK);
-        const uint32_t vlen = len - 14u;
-        if (vlen < 4u) {  // decode-vlan.c:28-33
-            k.st = PPE_ST_VLAN_HEADER_ERR; k.cb |= CB(PPE_C_VLAN_HEADERLEN_ERR); return;
-        }
-        k.flags |= PPE_F_VLAN;  // vlan_idx = 1, decode-vlan.c:46
-        const uint32_t itype = be16_lo(w[4]);
-        if (itype == 0x0800u) {  // :49-53
-            k.cb |= CB(PPE_C_VLAN_RX_OK);
-            v = 1;
-            l3len = vlen - 4u;
-        } else if (itype == 0x8100u || itype == 0x9100u) {  // :70-75 recurse: len check, then vlan_idx >= 1
-            k.cb |= CB(PPE_C_VLAN_RX_OK);
-            if (vlen - 4u < 4u) {
-                k.st = PPE_ST_VLAN_HEADER_ERR; k.cb |= CB(PPE_C_VLAN_HEADERLEN_ERR);
-            } else {
-                k.st = PPE_ST_VLAN_LAYER_EXCEED; k.cb |= CB(PPE_C_VLAN_LAYER_EXCEED);
-            }
-            return;
-        } else {  // :76-84 unsupported → Decode_unsupport_proto_handle (decode.c:31-45)
-            k.st = PPE_ST_VLAN_UNSUPPORT; k.cb |= CB(PPE_C_VLAN_UNSUPPORT); k.act = unsup_act; return;
-        }
-    } else {  // :102-111
-        k.st = PPE_ST_L2_UNSUPPORT; k.cb |= CB(PPE_C_L2_UNSUPPORT); k.act = unsup_act; return;
-    }
-
-    // ---- IPv4: dataplane/src/decode/decode-ipv4.c:27-79, 86-247.  L3 starts at byte 14 + 4v = 4*(3+v) + 2.
-    // D[i] = dword (3 + v + i) of the window, i.e. the dwords covering the L3/L4 headers.  Blended with a mask
-    // rather than `v ? w[4+i] : w[3+i]`, which the compiler turns into a dynamic index (scratch).
+    const bool is_ip = etype == 0x0800u;                          // :75
+    const bool is_vl = (etype | 0x1000u) == 0x9100u;              // 0x8100 or 0x9100, :96-97
+    const bool l2_ok = !(bad_len || dz || sz) && (is_ip || is_vl);
+    // ---- VLAN: dataplane/src/decode/decode-vlan.c:23-89 ----
+    const uint32_t vlen = len - 14u;
+    const uint32_t itype = be16_lo(w[4]);
+    const bool v_ip = itype == 0x0800u, v_vl = (itype | 0x1000u) == 0x9100u;
+    const uint32_t v = is_vl ? 1u : 0u;
+    const uint32_t l3len = vlen - 4u * v;
+    // ---- IPv4: dataplane/src/decode/decode-ipv4.c:27-247.  L3 starts at byte 14 + 4v = 4*(3+v) + 2.
+    // D[i] = dword (3 + v + i); a mask blend, not `v ? w[4+i] : w[3+i]` (folded into a dynamic index → scratch)
     const uint32_t vm = 0u - v;
     uint32_t D[10];
 #pragma unroll
     for (int i = 0; i < 10; ++i) D[i] = (w[3 + i] & ~vm) | (w[4 + i] & vm);
-    if (l3len < 20u) {  // :30-34
-        k.st = PPE_ST_IPV4_HEADER_ERR; k.cb |= CB(PPE_C_IPV4_HEADERLEN_ERR); return;
-    }
     const uint32_t verhl = (D[0] >> 16) & 0xffu;
-    if ((verhl >> 4) != 4u) {  // :36-40
-        k.st = PPE_ST_IPV4_VERSION_ERR; k.cb |= CB(PPE_C_IPV4_VERSION_ERR); return;
-    }
     const uint32_t hlen = (verhl & 0xfu) << 2;
-    if (hlen < 20u) {  // :44-48
-        k.st = PPE_ST_IPV4_HEADER_ERR; k.cb |= CB(PPE_C_IPV4_HEADERLEN_ERR); return;
-    }
     const uint32_t iplen = be16_lo(D[1]);
-    if (iplen < hlen || l3len < iplen) {  // :50-60
-        k.st = PPE_ST_IPV4_LEN_ERR; k.cb |= CB(PPE_C_IPV4_PKTLEN_ERR); return;
-    }
-    k.sip = __builtin_bswap32((D[3] >> 16) | (D[4] << 16));  // :62 src_addr at L3+12
-    k.dip = __builtin_bswap32((D[4] >> 16) | (D[5] << 16));  // :63 dst_addr at L3+16
-    k.proto = D[2] >> 24;                                     // :97 ip_proto at L3+9
-    const uint32_t ipoff = be16_lo(D[2]);                     // ip_off at L3+6
-    if ((ipoff & 0x3fffu) != 0u && k.proto != 89u) {          // IPV4_IS_FRAGMENT && !OSPF, :102
-        k.flags |= PPE_F_FRAG;
-        if (((l3len - hlen) & 0xffffu) == 0u) {  // frag_len == 0, :109-114
-            k.st = PPE_ST_FRAG_LEN_ERR; k.cb |= CB(PPE_C_FRAG_FRAGLEN_ERR); return;
-        }
-        k.st = PPE_ST_FRAG; k.cb |= CB(PPE_C_FRAG_PUNT); k.act = PPE_ACT_PUNT; return;  // Defrag → host
-    }
-    const bool is_tcp = k.proto == 6u, is_udp = k.proto == 17u;
-    if (!is_tcp && !is_udp) {  // :233-243
-        k.st = PPE_ST_IPV4_UNSUPPORT; k.cb |= CB(PPE_C_IPV4_UNSUPPORT); k.act = unsup_act; return;
-    }
-    k.cb |= CB(PPE_C_IPV4_RX_OK);
+    const uint32_t sip = __builtin_bswap32((D[3] >> 16) | (D[4] << 16));  // src_addr, L3+12
+    const uint32_t dip = __builtin_bswap32((D[4] >> 16) | (D[5] << 16));  // dst_addr, L3+16
+    const uint32_t proto = D[2] >> 24;                                     // ip_proto, L3+9
+    const uint32_t ipoff = be16_lo(D[2]);                                  // ip_off, L3+6
+    const bool l3_in = l2_ok && (is_ip || (vlen >= 4u && v_ip));
+    const bool ip_ok = l3_in && l3len >= 20u && (verhl >> 4) == 4u && hlen >= 20u && iplen >= hlen && l3len >= iplen;
+    const bool frag = (ipoff & 0x3fffu) != 0u && proto != 89u;             // IPV4_IS_FRAGMENT && !OSPF, :102
+    const bool is_tcp = proto == 6u, is_udp = proto == 17u;
+    const bool l4_in = ip_ok && !frag && (is_tcp || is_udp);
     const uint32_t l4len = (iplen - hlen) & 0xffffu;
     const uint32_t l4off = 14u + 4u * v + hlen;
-    const bool fast = hlen == 20u;  // L4 at byte 34+4v: fields from registers
-    uint32_t sport, dport, x;
-    if (is_udp) {
-        // ---- UDP: dataplane/src/decode/decode-udp.c:16-49 ----
-        if (l4len < 8u) {  // :18-22
-            k.st = PPE_ST_UDP_HEADER_ERR; k.cb |= CB(PPE_C_UDP_HEADERLEN_ERR); return;
-        }
-        if (fast) {
-            sport = be16_hi(D[5]);
-            dport = be16_lo(D[6]);
-            x = be16_hi(D[6]);
-        } else {
-            if (l4off + 6u > stride) {
-                k.st = PPE_ST_WINDOW_PUNT; k.cb |= CB(PPE_C_WINDOW_PUNT); k.act = PPE_ACT_PUNT; return;
-            }
-            const uint16_t *q = (const uint16_t *)(row + l4off);
-            sport = bswap16(q[0]);
-            dport = bswap16(q[1]);
-            x = bswap16(q[2]);
-        }
-        if (l4len != x) {  // l4len < uh_len, l4len != uh_len: :26-36
-            k.st = PPE_ST_UDP_LEN_ERR; k.cb |= CB(PPE_C_UDP_PKTLEN_ERR); return;
-        }
-        k.cb |= CB(PPE_C_UDP_RX_OK);
-        k.paylen = l4len - 8u;
-    } else {
-        // ---- TCP: dataplane/src/decode/decode-tcp.c:135-190 ----
-        if (l4len < 20u) {  // :140-144
-            k.st = PPE_ST_TCP_HEADER_ERR; k.cb |= CB(PPE_C_TCP_HEADERLEN_ERR); return;
-        }
-        if (fast) {
-            sport = be16_hi(D[5]);
-            dport = be16_lo(D[6]);
-            x = D[8] >> 16;  // byte 12 = th_offx2, byte 13 = th_flags
-        } else {
-            if (l4off + 14u > stride) {
-                k.st = PPE_ST_WINDOW_PUNT; k.cb |= CB(PPE_C_WINDOW_PUNT); k.act = PPE_ACT_PUNT; return;
-            }
-            const uint16_t *q = (const uint16_t *)(row + l4off);
-            sport = bswap16(q[0]);
-            dport = bswap16(q[1]);
-            x = q[6];
-        }
-        const uint32_t thl = ((x & 0xffu) >> 4) << 2;  // uint8_t hlen, :148
-        if (l4len < thl || ((thl - 20u) & 0xffu) > 40u) {  // :149-160
-            k.st = PPE_ST_TCP_LEN_ERR; k.cb |= CB(PPE_C_TCP_PKTLEN_ERR); return;
-        }
-        k.flags |= PPE_F_TCP;
-        if ((x >> 8) & 0x02u) k.flags |= PPE_F_SYN;  // TCP_IS_SYN, decode-tcp.h:313
-        k.cb |= CB(PPE_C_TCP_RX_OK);
-        k.paylen = l4len - thl;
+    const bool fast = hlen == 20u;  // L4 at byte 34+4v: every field below byte 52, in registers
+    const bool win_short = !fast && (l4off + (is_tcp ? 14u : 6u) > stride);
+    uint32_t sport = be16_hi(D[5]), dport = be16_lo(D[6]);
+    uint32_t x = is_tcp ? (D[8] >> 16) : be16_hi(D[6]);  // TCP: offx2 | flags << 8;  UDP: uh_len
+    if (l4_in && !fast && !win_short) {  // IPv4 options: L4 header at a data-dependent offset
+        const uint16_t *q = (const uint16_t *)(row + l4off);
+        sport = bswap16(q[0]);
+        dport = bswap16(q[1]);
+        x = is_tcp ? (uint32_t)q[6] : bswap16(q[2]);
     }
-    k.sport = sport;
-    k.dport = dport;
-    k.flags |= PPE_F_L4;
+    // ---- UDP: dataplane/src/decode/decode-udp.c:16-49;  TCP: dataplane/src/decode/decode-tcp.c:135-190 ----
+    const uint32_t thl = ((x & 0xffu) >> 4) << 2;  // uint8_t hlen, decode-tcp.c:148
+    const bool syn = ((x >> 8) & 0x02u) != 0u;     // TCP_IS_SYN, decode-tcp.h:313
+    uint32_t st_tcp = (syn_check && !syn) ? (uint32_t)PPE_ST_FLOW_TCP_NO_SYN_FIRST : ST_ACL;  // flow.c:204-214
+    st_tcp = (l4len < thl || ((thl - 20u) & 0xffu) > 40u) ? (uint32_t)PPE_ST_TCP_LEN_ERR : st_tcp;  // :149-160
+    st_tcp = win_short ? (uint32_t)PPE_ST_WINDOW_PUNT : st_tcp;
+    st_tcp = l4len < 20u ? (uint32_t)PPE_ST_TCP_HEADER_ERR : st_tcp;  // :140-144
+    uint32_t st_udp = l4len != x ? (uint32_t)PPE_ST_UDP_LEN_ERR : ST_ACL;  // :26-36
+    st_udp = win_short ? (uint32_t)PPE_ST_WINDOW_PUNT : st_udp;
+    st_udp = l4len < 8u ? (uint32_t)PPE_ST_UDP_HEADER_ERR : st_udp;  // :18-22
+    uint32_t st = is_tcp ? st_tcp : (is_udp ? st_udp : (uint32_t)PPE_ST_IPV4_UNSUPPORT);  // decode-ipv4.c:233-243
+    st = frag ? ((((l3len - hlen) & 0xffffu) == 0u) ? (uint32_t)PPE_ST_FRAG_LEN_ERR : (uint32_t)PPE_ST_FRAG) : st;
+    st = (iplen < hlen || l3len < iplen) ? (uint32_t)PPE_ST_IPV4_LEN_ERR : st;  // decode-ipv4.c:50-60
+    st = hlen < 20u ? (uint32_t)PPE_ST_IPV4_HEADER_ERR : st;                    // :44-48
+    st = (verhl >> 4) != 4u ? (uint32_t)PPE_ST_IPV4_VERSION_ERR : st;           // :36-40
+    st = l3len < 20u ? (uint32_t)PPE_ST_IPV4_HEADER_ERR : st;                   // :30-34
+    // VLAN tag (decode-vlan.c): len check, then the inner type; a second tag recurses: len check, vlan_idx >= 1
+    uint32_t st_v = v_ip ? st
+                         : (v_vl ? ((vlen - 4u < 4u) ? (uint32_t)PPE_ST_VLAN_HEADER_ERR
+                                                     : (uint32_t)PPE_ST_VLAN_LAYER_EXCEED)
+                                 : (uint32_t)PPE_ST_VLAN_UNSUPPORT);
+    st_v = vlen < 4u ? (uint32_t)PPE_ST_VLAN_HEADER_ERR : st_v;
+    st = is_vl ? st_v : (is_ip ? st : (uint32_t)PPE_ST_L2_UNSUPPORT);
+    st = (bad_len || dz || sz) ? (uint32_t)PPE_ST_L2_HEADER_ERR : st;
 
-    // ---- FlowHandlePacket miss path: dataplane/src/flow/flow.c:204-243 ----
-    if (is_tcp && syn_check && !(k.flags & PPE_F_SYN)) {
-        k.st = PPE_ST_FLOW_TCP_NO_SYN_FIRST;
-        k.cb |= CB(PPE_C_FLOW_TCP_NO_SYN_FIRST) | CB(PPE_C_FLOW_PROC_FAIL);
-        return;
-    }
-    k.acl = 1;  // status decided by the ACL
+    const bool l4_ok = st == ST_ACL || st == PPE_ST_FLOW_TCP_NO_SYN_FIRST;  // reached FlowHandlePacket
+    k.st = st;
+    k.flags = (l2_ok && is_vl && vlen >= 4u ? PPE_F_VLAN : 0u) | (l4_ok ? PPE_F_L4 : 0u) |
+              (l4_ok && is_tcp ? PPE_F_TCP : 0u) | (l4_ok && is_tcp && syn ? PPE_F_SYN : 0u) |
+              (ip_ok && frag ? PPE_F_FRAG : 0u);
+    k.cb = CB(PPE_C_PKTS) | (st != ST_ACL ? CB(reason_counter(st)) : 0u) | (l2_ok ? CB(PPE_C_L2_RX_OK) : 0u) |
+           (l2_ok && is_vl && vlen >= 4u && (v_ip || v_vl) ? CB(PPE_C_VLAN_RX_OK) : 0u) |
+           (l4_in ? CB(PPE_C_IPV4_RX_OK) : 0u) | (l4_ok && is_udp ? CB(PPE_C_UDP_RX_OK) : 0u) |
+           (l4_ok && is_tcp ? CB(PPE_C_TCP_RX_OK) : 0u) |
+           (st == PPE_ST_FLOW_TCP_NO_SYN_FIRST ? CB(PPE_C_FLOW_PROC_FAIL) : 0u);
+    k.sip = ip_ok ? sip : 0u;
+    k.dip = ip_ok ? dip : 0u;
+    k.proto = ip_ok ? proto : 0u;
+    k.sport = l4_ok ? sport : 0u;
+    k.dport = l4_ok ? dport : 0u;
+    k.paylen = l4_ok ? (is_tcp ? l4len - thl : l4len - 8u) : 0u;
+    return k;
 }
 
 // First-match decision-tree lookup over the classifier image (ppe_image.h).  `im` points either into LDS or to
@@ -220,8 +176,8 @@ __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ im, uint
                                            uint32_t off_resid, uint32_t default_action, const uint32_t sip,
                                            const uint32_t dip, const uint32_t sport, const uint32_t dport,
                                            const uint32_t proto, uint32_t dmac_lo, uint32_t dmac_hi,
-                                           uint32_t smac_lo, uint32_t smac_hi, uint64_t ts, int32_t &hit,
-                                           uint32_t &action) {
+                                           uint32_t smac_lo, uint32_t smac_hi, const uint64_t *tsp, uint32_t p,
+                                           uint64_t now, int32_t &hit, uint32_t &action) {
     const uint2 *nodes = (const uint2 *)(im + PPE_IMG_HDR_WORDS);
     uint2 nd = nodes[0];
 #pragma unroll 1
@@ -257,7 +213,8 @@ __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ im, uint
                 const uint4 c = xp[0], t = xp[1];
                 if (rs & PPE_RESID_DMAC) m = m && c.x == dmac_lo && c.y == dmac_hi;
                 if (rs & PPE_RESID_SMAC) m = m && c.z == smac_lo && c.w == smac_hi;
-                if (rs & PPE_RESID_TIME) {
+                if (rs & PPE_RESID_TIME) {  // the packet timestamp is only fetched for time-window rules
+                    const uint64_t ts = tsp ? tsp[p] : now;
                     const uint64_t t0 = (uint64_t)t.x | ((uint64_t)t.y << 32);
                     const uint64_t t1 = (uint64_t)t.z | ((uint64_t)t.w << 32);
                     m = m && ts >= t0 && ts <= t1;
@@ -272,6 +229,21 @@ __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ im, uint
     }
 }
 
+// Copy the classifier image into LDS with LDS-DMA (global_load_lds_dwordx4): every 1-KB piece of the image is in
+// flight at once, no VGPR round trip.  Each wave-instruction writes 64 × 16 B at a wave-uniform LDS base, so the
+// LDS region is padded to a multiple of 1 KB and the (clamped) tail lanes write into the padding.
+__device__ __forceinline__ void stage_image(const uint32_t *img, uint32_t *lds, uint32_t words, uint32_t tid) {
+    typedef __attribute__((address_space(1))) const void *gptr_t;
+    typedef __attribute__((address_space(3))) void *lptr_t;
+    const uint32_t n4 = (words + 3u) >> 2;
+    const uint32_t lane = tid & 63u;
+    for (uint32_t base = (tid >> 6) * 64u; base < n4; base += PPE_BLOCK) {
+        const uint32_t i = min(base + lane, n4 - 1u);
+        __builtin_amdgcn_global_load_lds((gptr_t)(img + 4u * i), (lptr_t)(lds + 4u * base), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <bool LDS_IMG>
 __global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -279,12 +251,7 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
     uint32_t *limg = smem + 32;  // staged classifier image
     const uint32_t tid = threadIdx.x;
     if (tid < 32) lcnt[tid] = 0;
-    if (LDS_IMG) {
-        const uint4 *src = (const uint4 *)a.img;
-        uint4 *dst = (uint4 *)limg;
-        const uint32_t n4 = (a.img_words + 3u) >> 2;
-        for (uint32_t i = tid; i < n4; i += PPE_BLOCK) dst[i] = src[i];
-    }
+    if (LDS_IMG) stage_image(a.img, limg, a.img_words, tid);
     __syncthreads();
     const uint32_t *im = LDS_IMG ? (const uint32_t *)limg : a.img;
     const uint32_t off_leaf = a.img[PPE_IMG_W_OFFLEAF];
@@ -294,57 +261,64 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t lane = tid & 63u;
     const uint32_t ntiles = (a.n + 63u) >> 6;
     const uint32_t stride_waves = gridDim.x * (PPE_BLOCK / 64);
-    const uint32_t unsup_act = a.unsup_fw ? (uint32_t)PPE_ACT_FW : (uint32_t)PPE_ACT_DROP;
+    // action of each terminal status, 2 bits per status: FW for ACL_FW, PUNT for fragments / short windows, the
+    // configured action for unsupported protocols (Decode_unsupport_proto_handle, decode.c:31-45), else DROP
+    uint64_t act_table = 0;
+#pragma unroll
+    for (uint32_t st = 0; st < PPE_ST__COUNT; ++st) {
+        const uint64_t ac = st == PPE_ST_ACL_FW ? PPE_ACT_FW
+                          : (st == PPE_ST_L2_UNSUPPORT || st == PPE_ST_VLAN_UNSUPPORT || st == PPE_ST_IPV4_UNSUPPORT)
+                              ? (a.unsup_fw ? PPE_ACT_FW : PPE_ACT_DROP)
+                          : (st == PPE_ST_FRAG || st == PPE_ST_WINDOW_PUNT) ? PPE_ACT_PUNT : PPE_ACT_DROP;
+        act_table |= ac << (2u * st);
+    }
     uint32_t my_cnt = 0;  // lane b (< PPE_C__COUNT) accumulates counter b of this wave
 
-    for (uint32_t tile = blockIdx.x * (PPE_BLOCK / 64) + (tid >> 6); tile < ntiles; tile += stride_waves) {
+    // software pipeline: the next tile's header window is loaded while the current one is classified
+    uint32_t tile = blockIdx.x * (PPE_BLOCK / 64) + (tid >> 6);
+    uint4 q0, q1, q2, q3;
+    uint32_t qlen;
+    {
+        const uint32_t p = min((tile << 6) + lane, a.n - 1u);  // clamped: loads are unconditional (no phi → no wait)
+        const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)p * a.stride);
+        q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
+        qlen = a.len[p];
+    }
+    for (; tile < ntiles; tile += stride_waves) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < a.n;
-        uint32_t w[16];
-        uint32_t len = 0;
-        const uint8_t *row = a.hdr + (size_t)p * a.stride;
-        if (valid) {
-            const uint4 *r4 = (const uint4 *)row;
-            const uint4 q0 = r4[0], q1 = r4[1], q2 = r4[2], q3 = r4[3];
-            w[0] = q0.x; w[1] = q0.y; w[2] = q0.z; w[3] = q0.w;
-            w[4] = q1.x; w[5] = q1.y; w[6] = q1.z; w[7] = q1.w;
-            w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
-            w[12] = q3.x; w[13] = q3.y; w[14] = q3.z; w[15] = q3.w;
-            len = a.len[p];
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) w[i] = 0;
+        const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+        const uint32_t len = valid ? qlen : 0u;
+        {
+            const uint32_t np = min(((tile + stride_waves) << 6) + lane, a.n - 1u);
+            const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)np * a.stride);
+            q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
+            qlen = a.len[np];
         }
+        const uint8_t *row = a.hdr + (size_t)p * a.stride;
+        Dec k = decode(w, len, row, a.stride, a.syn_check);
 
-        Pkt k;
-        decode(w, len, row, a.stride, unsup_act, a.syn_check, k);
-        if (!valid) k.acl = 0;
-
-        uint32_t fh = 0;
+        uint32_t fh = 0, act;
         int32_t hit = -1;
         if (k.flags & PPE_F_L4) fh = flow_hashfn(k.proto, k.sip, k.dip, k.sport, k.dport);
-        if (k.acl) {
-            const uint64_t ts = a.ts ? a.ts[p] : a.now;
-            uint32_t act;
+        if (valid && k.st == ST_ACL) {
+            uint32_t rule_act;
             // dmac = bytes 0-5, smac = bytes 6-11 (EthernetHdr, decode-ethernet.h:23-27)
             acl_lookup(im, off_leaf, off_rules, off_resid, a.default_action, k.sip, k.dip, k.sport, k.dport,
-                       k.proto, w[0], w[1] & 0xffffu,
-                       (w[1] >> 16) | (w[2] << 16), w[2] >> 16, ts, hit, act);
+                       k.proto, w[0], w[1] & 0xffffu, (w[1] >> 16) | (w[2] << 16), w[2] >> 16, a.ts, p, a.now, hit,
+                       rule_act);
+            const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
+            k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
             k.flags |= PPE_F_ACL;
-            if (act == ACL_RULE_ACTION_DROP) {  // flow.c:232-237
-                k.st = PPE_ST_ACL_DROP;
-                k.act = PPE_ACT_DROP;
-                k.cb |= CB(PPE_C_ACL_DROP) | CB(PPE_C_FLOW_PROC_FAIL);
-            } else {  // flow.c:238-243, FlowHandlePacket :309
-                k.st = PPE_ST_ACL_FW;
-                k.act = PPE_ACT_FW;
-                k.cb |= CB(PPE_C_ACL_FW) | CB(PPE_C_FLOW_PROC_OK);
-            }
+            k.cb |= drop ? (CB(PPE_C_ACL_DROP) | CB(PPE_C_FLOW_PROC_FAIL)) : (CB(PPE_C_ACL_FW) | CB(PPE_C_FLOW_PROC_OK));
         }
-        k.cb |= k.act == PPE_ACT_FW ? CB(PPE_C_OUT_FW) : (k.act == PPE_ACT_DROP ? CB(PPE_C_OUT_DROP) : CB(PPE_C_OUT_PUNT));
+        const uint32_t st = k.st;
+        act = (uint32_t)(act_table >> (2u * st)) & 3u;
+        k.cb |= act == PPE_ACT_FW ? CB(PPE_C_OUT_FW) : (act == PPE_ACT_DROP ? CB(PPE_C_OUT_DROP) : CB(PPE_C_OUT_PUNT));
 
         if (valid) {
-            if (a.verdict) a.verdict[p] = k.st | (k.act << 8) | (k.flags << 16);
+            if (a.verdict) a.verdict[p] = st | (act << 8) | (k.flags << 16);
             if (a.fhash) a.fhash[p] = fh;
             if (a.hit) a.hit[p] = hit;
             if (a.tuple) {
@@ -358,11 +332,11 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
         }
 
         // ---- wave-ballot compaction of FW / DROP indices into this tile's 64-slot segment ----
-        const bool is_fw = valid && k.act == PPE_ACT_FW;
-        const bool is_drop = valid && k.act == PPE_ACT_DROP;
+        const bool is_fw = valid && act == PPE_ACT_FW;
+        const bool is_drop = valid && act == PPE_ACT_DROP;
         const uint64_t bfw = __ballot(is_fw);
         const uint64_t bdr = __ballot(is_drop);
-        const uint64_t bpu = __ballot(valid && k.act == PPE_ACT_PUNT);
+        const uint64_t bpu = __ballot(valid && act == PPE_ACT_PUNT);
         if (a.fw_idx && is_fw) {
             const uint32_t pos =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(bfw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bfw, 0u));
@@ -379,7 +353,7 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
 
         // ---- per-reason counters: one ballot per reason, lane b keeps reason b ----
         const uint32_t cb = valid ? k.cb : 0u;
-#pragma unroll
+#pragma unroll 2
         for (int b = 0; b < PPE_C__COUNT; ++b) {
             const uint32_t c = (uint32_t)__popcll(__ballot((cb >> b) & 1u));
             my_cnt += lane == (uint32_t)b ? c : 0u;
@@ -398,10 +372,7 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t tid = threadIdx.x;
     if (LDS_IMG) {
-        const uint4 *src = (const uint4 *)a.img;
-        uint4 *dst = (uint4 *)smem;
-        const uint32_t n4 = (a.img_words + 3u) >> 2;
-        for (uint32_t i = tid; i < n4; i += PPE_BLOCK) dst[i] = src[i];
+        stage_image(a.img, smem, a.img_words, tid);
         __syncthreads();
     }
     const uint32_t *im = LDS_IMG ? (const uint32_t *)smem : a.img;
@@ -412,11 +383,10 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
         const uint4 t = ((const uint4 *)a.tuple)[i];
         uint4 m = make_uint4(0, 0, 0, 0);
         if (a.macs) m = ((const uint4 *)a.macs)[i];
-        const uint64_t ts = a.ts ? a.ts[i] : a.now;
         int32_t hit;
         uint32_t act;
         acl_lookup(im, off_leaf, off_rules, off_resid, a.default_action, t.x, t.y, t.z & 0xffffu, t.z >> 16,
-                   t.w & 0xffu, m.x, m.y, m.z, m.w, ts, hit, act);
+                   t.w & 0xffu, m.x, m.y, m.z, m.w, a.ts, i, a.now, hit, act);
         if (a.hit) a.hit[i] = hit;
         if (a.action) a.action[i] = act;
     }
@@ -427,7 +397,7 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
 extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int lds_img, void *stream) {
     const size_t base = 32 * sizeof(uint32_t);
     if (lds_img) {
-        const size_t shmem = base + (((size_t)a->img_words * 4u + 15u) & ~(size_t)15u);
+        const size_t shmem = base + (((size_t)a->img_words * 4u + 1023u) & ~(size_t)1023u);
         hipLaunchKernelGGL(ppe_classify_kernel<true>, dim3(grid), dim3(PPE_BLOCK), shmem, (hipStream_t)stream, *a);
     } else {
         hipLaunchKernelGGL(ppe_classify_kernel<false>, dim3(grid), dim3(PPE_BLOCK), base, (hipStream_t)stream, *a);
@@ -437,7 +407,7 @@ extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int lds_im
 
 extern "C" int ppe_launch_acl_tuples(const ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream) {
     if (lds_img) {
-        const size_t shmem = ((size_t)a->img_words * 4u + 15u) & ~(size_t)15u;
+        const size_t shmem = ((size_t)a->img_words * 4u + 1023u) & ~(size_t)1023u;
         hipLaunchKernelGGL(ppe_acl_tuple_kernel<true>, dim3(grid), dim3(PPE_BLOCK), shmem, (hipStream_t)stream, *a);
     } else {
         hipLaunchKernelGGL(ppe_acl_tuple_kernel<false>, dim3(grid), dim3(PPE_BLOCK), 0, (hipStream_t)stream, *a);
