@@ -81,21 +81,46 @@ int fail(ppe_ctx *c, int code, const char *fmt, ...) {
         if (e_ != hipSuccess) return fail((c), PPE_EIO, "%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
-uint32_t blocks_per_cu(uint32_t img_bytes, bool lds) {
-    static const uint32_t env_bpc = [] {
-        const char *e = getenv("PPE_BLOCKS_PER_CU");
-        const int v = e ? atoi(e) : 0;
-        return v > 0 && v <= (int)kMaxBlocksPerCU ? (uint32_t)v : 0u;
+int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+
+// Kernel variant knobs (defaults = the fastest measured on MI355X):
+//   PPE_PREFETCH  1 = next-tile register prefetch            (default 0)
+//   PPE_BLOCK     workgroup size 256 / 512 / 1024           (default 256)
+//   PPE_LDS_IMG   0 = read the classifier image from global memory (L1/L2) instead of staging it in LDS
+bool use_prefetch() {
+    static const bool p = env_int("PPE_PREFETCH", 0) != 0;
+    return p;
+}
+uint32_t block_size() {
+    static const uint32_t b = [] {
+        const int v = env_int("PPE_BLOCK", 256);
+        return (uint32_t)(v == 512 || v == 1024 ? v : 256);
     }();
-    if (env_bpc) {
-        if (!lds) return env_bpc;
+    return b;
+}
+bool lds_image_ok(uint32_t img_bytes) {
+    static const int mode = env_int("PPE_LDS_IMG", 1);
+    return mode != 0 && img_bytes <= PPE_LDS_IMG_MAX;
+}
+
+// Resident workgroups per CU for the classify kernel with this image: the occupancy API's answer (register and
+// LDS limits) unless PPE_BLOCKS_PER_CU overrides it.  The persistent grid is CUs × this, so no workgroup waits for
+// a second round.
+uint32_t blocks_per_cu(uint32_t img_bytes, bool lds) {
+    static const int env_bpc = env_int("PPE_BLOCKS_PER_CU", 0);
+    if (env_bpc > 0 && env_bpc <= (int)kMaxBlocksPerCU) {
+        if (!lds) return (uint32_t)env_bpc;
         const uint32_t fit = (160u * 1024u) / (128u + ((img_bytes + 1023u) & ~1023u));
-        return std::max(1u, std::min(env_bpc, fit));
+        return std::max(1u, std::min((uint32_t)env_bpc, fit));  // env override assumes 256-thread blocks
     }
+    const int occ = ppe_classify_occupancy(img_bytes / 4u, lds ? 1 : 0, use_prefetch() ? 1 : 0, (int)block_size());
+    if (occ > 0) return std::min<uint32_t>((uint32_t)occ, kMaxBlocksPerCU);
     if (!lds) return kMaxBlocksPerCU;
     const uint32_t per_block = 128u + ((img_bytes + 1023u) & ~1023u);
-    uint32_t b = (160u * 1024u) / per_block;
-    return std::max(1u, std::min(kMaxBlocksPerCU, b));
+    return std::max(1u, std::min(kMaxBlocksPerCU * 256u / block_size(), (160u * 1024u) / per_block));
 }
 
 int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const ppe_acl_stats_t *st) {
@@ -112,7 +137,7 @@ int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const 
     HIPCHK(c, hipMemcpy(c->d_img[slot], words, bytes, hipMemcpyHostToDevice));
     c->h_img[slot].assign(words, words + n_words);
     c->stats[slot] = *st;
-    c->stats[slot].lds_resident = bytes <= PPE_LDS_IMG_MAX ? 1u : 0u;
+    c->stats[slot].lds_resident = lds_image_ok((uint32_t)bytes) ? 1u : 0u;
     c->img_used[slot] = false;
     return PPE_OK;
 }
@@ -121,9 +146,10 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
            int slot_set, uint32_t idx_base = 0) {
     const int r = c->running;
     const uint32_t words = (uint32_t)c->h_img[r].size();
-    const bool lds = (size_t)words * 4u <= PPE_LDS_IMG_MAX;
+    const bool lds = lds_image_ok(words * 4u);
+    const uint32_t wpb = block_size() / 64u;
     const uint32_t tiles = (in->n + 63u) / 64u;
-    const uint32_t want = (tiles + (PPE_BLOCK / 64) - 1) / (PPE_BLOCK / 64);
+    const uint32_t want = (tiles + wpb - 1) / wpb;
     const uint32_t maxg = c->n_cu * blocks_per_cu(words * 4u, lds);
     const uint32_t grid = std::max(1u, std::min(want, std::min(maxg, c->max_grid)));
 
@@ -164,7 +190,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
         c->ev_used += 2;
         HIPCHK(c, hipEventRecord(e0, s));
     }
-    const int rc = ppe_launch_classify(&a, grid, lds ? 1 : 0, (void *)s);
+    const int rc = ppe_launch_classify(&a, grid, lds ? 1 : 0, use_prefetch() ? 1 : 0, (int)block_size(), (void *)s);
     if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
     if (c->timing) HIPCHK(c, hipEventRecord(e1, s));
     c->img_used[r] = true;
@@ -511,9 +537,9 @@ int ppe_acl_image(ppe_ctx_t *c, uint32_t *words, uint32_t *n_words) {
 int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes) {
     if (!c) return PPE_EINVAL;
     const uint32_t words = (uint32_t)c->h_img[c->running].size();
-    const bool lds = (size_t)words * 4u <= PPE_LDS_IMG_MAX;
+    const bool lds = lds_image_ok(words * 4u);
     if (grid) *grid = std::min(c->n_cu * blocks_per_cu(words * 4u, lds), c->max_grid);
-    if (block) *block = PPE_BLOCK;
+    if (block) *block = block_size();
     if (lds_bytes) *lds_bytes = 128u + (lds ? ((words * 4u + 1023u) & ~1023u) : 0u);
     return PPE_OK;
 }

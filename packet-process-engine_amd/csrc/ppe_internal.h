@@ -50,7 +50,9 @@ struct ppe_tuple_kargs {
 extern "C" {
 #endif
 /* Launch the classify kernel. grid = workgroups (persistent), lds_img = stage image in LDS. Returns hipError_t. */
-int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int lds_img, void *stream);
+int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int lds_img, int prefetch, int block,
+                        void *stream);
+int ppe_classify_occupancy(uint32_t img_words, int lds_img, int prefetch, int block);
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
 #ifdef __cplusplus
 }

@@ -19,6 +19,12 @@
 #include "ppe_image.h"
 #include "ppe_internal.h"
 
+// Diagnostic ablation builds only (make ablate): bit 0 skip the ACL walk, bit 1 skip counters, bit 2 skip the
+// compaction, bit 3 skip the flow hash.  The product build has PPE_ABLATE == 0.
+#ifndef PPE_ABLATE
+#define PPE_ABLATE 0
+#endif
+
 namespace {
 
 __device__ __forceinline__ uint32_t be16_lo(uint32_t w) { return ((w & 0xffu) << 8) | ((w >> 8) & 0xffu); }
@@ -26,7 +32,7 @@ __device__ __forceinline__ uint32_t be16_hi(uint32_t w) { return ((w >> 8) & 0xf
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
 
 // dataplane/src/flow/tluhash.h:7-23 (one Jenkins lookup2 mix with c = 0)
-__device__ __forceinline__ uint32_t tlu_hash(uint32_t u1, uint32_t u2) {
+__host__ __device__ constexpr uint32_t tlu_hash(uint32_t u1, uint32_t u2) {
     uint32_t a = u2 + 0x9e3779b9u, b = u1 + 0x9e3779b9u, c = 0;
     a -= b; a -= c; a ^= (c >> 13);
     b -= c; b -= a; b ^= (a << 8);
@@ -40,10 +46,13 @@ __device__ __forceinline__ uint32_t tlu_hash(uint32_t u1, uint32_t u2) {
     return c;
 }
 
-// dataplane/src/flow/tluhash.h:26-35
-__device__ __forceinline__ uint32_t flow_hashfn(uint32_t proto, uint32_t sip, uint32_t dip, uint32_t sport,
-                                                uint32_t dport) {
-    return tlu_hash(sip, sport) ^ tlu_hash(dip, dport) ^ tlu_hash(proto, 0);
+// dataplane/src/flow/tluhash.h:26-35.  Only TCP/UDP packets reach the flow engine, so the protocol term
+// TluHash(proto, 0) is one of two compile-time constants.
+constexpr uint32_t kProtoHashTcp = tlu_hash(6u, 0u);
+constexpr uint32_t kProtoHashUdp = tlu_hash(17u, 0u);
+__device__ __forceinline__ uint32_t flow_hashfn_l4(bool tcp, uint32_t sip, uint32_t dip, uint32_t sport,
+                                                   uint32_t dport) {
+    return tlu_hash(sip, sport) ^ tlu_hash(dip, dport) ^ (tcp ? kProtoHashTcp : kProtoHashUdp);
 }
 
 #define CB(x) (1u << (x))
@@ -232,35 +241,46 @@ __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ im, uint
 // Copy the classifier image into LDS with LDS-DMA (global_load_lds_dwordx4): every 1-KB piece of the image is in
 // flight at once, no VGPR round trip.  Each wave-instruction writes 64 × 16 B at a wave-uniform LDS base, so the
 // LDS region is padded to a multiple of 1 KB and the (clamped) tail lanes write into the padding.
+template <int BLOCK>
 __device__ __forceinline__ void stage_image(const uint32_t *img, uint32_t *lds, uint32_t words, uint32_t tid) {
     typedef __attribute__((address_space(1))) const void *gptr_t;
     typedef __attribute__((address_space(3))) void *lptr_t;
     const uint32_t n4 = (words + 3u) >> 2;
     const uint32_t lane = tid & 63u;
-    for (uint32_t base = (tid >> 6) * 64u; base < n4; base += PPE_BLOCK) {
+    for (uint32_t base = (tid >> 6) * 64u; base < n4; base += BLOCK) {
         const uint32_t i = min(base + lane, n4 - 1u);
         __builtin_amdgcn_global_load_lds((gptr_t)(img + 4u * i), (lptr_t)(lds + 4u * base), 16, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool LDS_IMG>
-__global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
+template <bool LDS_IMG, bool PREFETCH, int BLOCK>
+__global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *lcnt = smem;       // [32] per-reason counters of this workgroup
     uint32_t *limg = smem + 32;  // staged classifier image
     const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t ntiles = (a.n + 63u) >> 6;
+    uint32_t tile = blockIdx.x * (BLOCK / 64) + (tid >> 6);
+    // the first tile's header window is requested before the image staging, so the two latencies overlap
+    uint4 q0, q1, q2, q3;
+    uint32_t qlen;
+    {
+        const uint32_t p = min((tile << 6) + lane, a.n - 1u);  // clamped: loads are unconditional (no phi → no wait)
+        const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)p * a.stride);
+        q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
+        qlen = a.len[p];
+    }
     if (tid < 32) lcnt[tid] = 0;
-    if (LDS_IMG) stage_image(a.img, limg, a.img_words, tid);
+    if (LDS_IMG) stage_image<BLOCK>(a.img, limg, a.img_words, tid);
     __syncthreads();
     const uint32_t *im = LDS_IMG ? (const uint32_t *)limg : a.img;
     const uint32_t off_leaf = a.img[PPE_IMG_W_OFFLEAF];
     const uint32_t off_rules = a.img[PPE_IMG_W_OFFRULES];
     const uint32_t off_resid = a.img[PPE_IMG_W_OFFRESID];
 
-    const uint32_t lane = tid & 63u;
-    const uint32_t ntiles = (a.n + 63u) >> 6;
-    const uint32_t stride_waves = gridDim.x * (PPE_BLOCK / 64);
+    const uint32_t stride_waves = gridDim.x * (BLOCK / 64);
     // action of each terminal status, 2 bits per status: FW for ACL_FW, PUNT for fragments / short windows, the
     // configured action for unsupported protocols (Decode_unsupport_proto_handle, decode.c:31-45), else DROP
     uint64_t act_table = 0;
@@ -274,23 +294,21 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
     }
     uint32_t my_cnt = 0;  // lane b (< PPE_C__COUNT) accumulates counter b of this wave
 
-    // software pipeline: the next tile's header window is loaded while the current one is classified
-    uint32_t tile = blockIdx.x * (PPE_BLOCK / 64) + (tid >> 6);
-    uint4 q0, q1, q2, q3;
-    uint32_t qlen;
-    {
-        const uint32_t p = min((tile << 6) + lane, a.n - 1u);  // clamped: loads are unconditional (no phi → no wait)
-        const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)p * a.stride);
-        q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
-        qlen = a.len[p];
-    }
-    for (; tile < ntiles; tile += stride_waves) {
+    // PREFETCH: the next tile's window is loaded while the current one is classified; otherwise each tile is
+    // loaded at the top of its iteration (the first one above, before the staging)
+    for (bool first = true; tile < ntiles; tile += stride_waves, first = false) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < a.n;
+        if (!PREFETCH && !first) {
+            const uint32_t pc = min(p, a.n - 1u);
+            const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)pc * a.stride);
+            q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
+            qlen = a.len[pc];
+        }
         const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                                 q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
         const uint32_t len = valid ? qlen : 0u;
-        {
+        if (PREFETCH) {
             const uint32_t np = min(((tile + stride_waves) << 6) + lane, a.n - 1u);
             const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)np * a.stride);
             q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
@@ -301,8 +319,12 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
 
         uint32_t fh = 0, act;
         int32_t hit = -1;
-        if (k.flags & PPE_F_L4) fh = flow_hashfn(k.proto, k.sip, k.dip, k.sport, k.dport);
-        if (valid && k.st == ST_ACL) {
+        if (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4)) fh = flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport);
+        if ((PPE_ABLATE & 1) && valid && k.st == ST_ACL) {
+            k.st = PPE_ST_ACL_FW;
+            k.flags |= PPE_F_ACL;
+        }
+        if (!(PPE_ABLATE & 1) && valid && k.st == ST_ACL) {
             uint32_t rule_act;
             // dmac = bytes 0-5, smac = bytes 6-11 (EthernetHdr, decode-ethernet.h:23-27)
             acl_lookup(im, off_leaf, off_rules, off_resid, a.default_action, k.sip, k.dip, k.sport, k.dport,
@@ -332,6 +354,8 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
         }
 
         // ---- wave-ballot compaction of FW / DROP indices into this tile's 64-slot segment ----
+        if (PPE_ABLATE & 4) goto skip_compact;
+        {
         const bool is_fw = valid && act == PPE_ACT_FW;
         const bool is_drop = valid && act == PPE_ACT_DROP;
         const uint64_t bfw = __ballot(is_fw);
@@ -350,13 +374,18 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_classify_kernel(ppe_kargs a) {
         if (a.tile_cnt && lane == 0)
             a.tile_cnt[tile] = (uint32_t)__popcll(bfw) | ((uint32_t)__popcll(bdr) << 8) |
                                ((uint32_t)__popcll(bpu) << 16);
+        }
+    skip_compact:
 
-        // ---- per-reason counters: one ballot per reason, lane b keeps reason b ----
-        const uint32_t cb = valid ? k.cb : 0u;
-#pragma unroll 2
-        for (int b = 0; b < PPE_C__COUNT; ++b) {
-            const uint32_t c = (uint32_t)__popcll(__ballot((cb >> b) & 1u));
-            my_cnt += lane == (uint32_t)b ? c : 0u;
+        // ---- per-reason counters: one iteration per DISTINCT counter pattern in the wave (typically 2-3: the
+        // ACL-forward path, the ACL-drop path, a malformed packet); lane b keeps counter b ----
+        const uint32_t cb = k.cb;
+        uint64_t todo = (PPE_ABLATE & 2) ? 0ull : __ballot(valid);
+        while (todo) {
+            const uint32_t pat = __builtin_amdgcn_readlane(cb, (uint32_t)__builtin_ctzll(todo));
+            const uint64_t same = __ballot(cb == pat) & todo;
+            todo &= ~same;
+            my_cnt += ((pat >> lane) & 1u) * (uint32_t)__popcll(same);
         }
     }
 
@@ -372,7 +401,7 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t tid = threadIdx.x;
     if (LDS_IMG) {
-        stage_image(a.img, smem, a.img_words, tid);
+        stage_image<PPE_BLOCK>(a.img, smem, a.img_words, tid);
         __syncthreads();
     }
     const uint32_t *im = LDS_IMG ? (const uint32_t *)smem : a.img;
@@ -394,15 +423,58 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
 
 }  // namespace
 
-extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int lds_img, void *stream) {
-    const size_t base = 32 * sizeof(uint32_t);
-    if (lds_img) {
-        const size_t shmem = base + (((size_t)a->img_words * 4u + 1023u) & ~(size_t)1023u);
-        hipLaunchKernelGGL(ppe_classify_kernel<true>, dim3(grid), dim3(PPE_BLOCK), shmem, (hipStream_t)stream, *a);
-    } else {
-        hipLaunchKernelGGL(ppe_classify_kernel<false>, dim3(grid), dim3(PPE_BLOCK), base, (hipStream_t)stream, *a);
-    }
+template <bool L, bool P, int B>
+static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t s) {
+    hipLaunchKernelGGL((ppe_classify_kernel<L, P, B>), dim3(grid), dim3(B), shmem, s, *a);
     return (int)hipGetLastError();
+}
+
+template <bool L, bool P, int B>
+static int occ_t(size_t shmem) {
+    int nb = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<L, P, B>, B, shmem) == hipSuccess
+               ? nb : -1;
+}
+
+static size_t classify_shmem(uint32_t img_words, int lds_img) {
+    const size_t base = 32 * sizeof(uint32_t);
+    return lds_img ? base + (((size_t)img_words * 4u + 1023u) & ~(size_t)1023u) : base;
+}
+
+// variant = (lds_img, prefetch, block ∈ {256, 512, 1024})
+#define PPE_DISPATCH(FN, ...)                                                                         \
+    do {                                                                                              \
+        if (lds_img) {                                                                                \
+            if (prefetch) {                                                                           \
+                if (block == 1024) return FN<true, true, 1024>(__VA_ARGS__);                          \
+                if (block == 512) return FN<true, true, 512>(__VA_ARGS__);                            \
+                return FN<true, true, 256>(__VA_ARGS__);                                              \
+            }                                                                                         \
+            if (block == 1024) return FN<true, false, 1024>(__VA_ARGS__);                             \
+            if (block == 512) return FN<true, false, 512>(__VA_ARGS__);                               \
+            return FN<true, false, 256>(__VA_ARGS__);                                                 \
+        }                                                                                             \
+        if (prefetch) {                                                                               \
+            if (block == 1024) return FN<false, true, 1024>(__VA_ARGS__);                             \
+            if (block == 512) return FN<false, true, 512>(__VA_ARGS__);                               \
+            return FN<false, true, 256>(__VA_ARGS__);                                                 \
+        }                                                                                             \
+        if (block == 1024) return FN<false, false, 1024>(__VA_ARGS__);                                \
+        if (block == 512) return FN<false, false, 512>(__VA_ARGS__);                                  \
+        return FN<false, false, 256>(__VA_ARGS__);                                                    \
+    } while (0)
+
+extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int lds_img, int prefetch, int block,
+                                   void *stream) {
+    const size_t shmem = classify_shmem(a->img_words, lds_img);
+    hipStream_t s = (hipStream_t)stream;
+    PPE_DISPATCH(launch_t, a, grid, shmem, s);
+}
+
+// resident workgroups per CU for the kernel variant (the persistent grid is sized to exactly fill the chip)
+extern "C" int ppe_classify_occupancy(uint32_t img_words, int lds_img, int prefetch, int block) {
+    const size_t shmem = classify_shmem(img_words, lds_img);
+    PPE_DISPATCH(occ_t, shmem);
 }
 
 extern "C" int ppe_launch_acl_tuples(const ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream) {

@@ -107,7 +107,7 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    p = Path(path) if path else Path(os.environ.get("PPE_LIB", LIB_PATH))
     if not p.exists():
         raise OSError(f"{p} not found: build it with `make -C packet-process-engine_amd` (no CPU fallback exists)")
     lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)

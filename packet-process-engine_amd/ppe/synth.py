@@ -25,7 +25,7 @@ CONFIGS = {
 }
 
 MAC_POOL = 16
-N_MALFORMED_KINDS = 23
+N_MALFORMED_KINDS = 24
 
 
 def _mac_pool(rng):
@@ -279,4 +279,7 @@ def _malform(hdr, lens, i, k, rng, stride):
                 h[o + 13] = 0x02
         else:
             h[l3] = 0x4F  # ip_len < 60 → IPV4_LEN_ERR
+    elif k == 23:   # TCP segment shorter than its 20-B header → TCP_HEADER_ERR
+        h[l3 + 9] = 6
+        _set16(h, l3 + 2, 20 + int(rng.integers(0, 20)))
 

@@ -1,0 +1,100 @@
+"""The host classifier compiler (product code, runs without a GPU): walking its image must give exactly the
+linear first-match result for every packet, across rule-set shapes."""
+import numpy as np
+import pytest
+
+import pyoracle
+from ppe import abi, synth
+from ppe.abi import RULE_DTYPE
+
+NOW = 1_700_000_000
+
+
+def compare(rules, used, pk, default_action=1, binth=0, cfg=None):
+    img, st = abi.build_image(rules, used, default_action, binth)
+    o = pyoracle.Oracle(rules, used, default_action=default_action, image=img)
+    cfg = cfg or o.cfg(0, 1, NOW)
+    lin = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4)
+    tree = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4, use_tree=True)
+    for k in ("verdict", "acl_hit", "flow_hash", "counters"):
+        assert np.array_equal(lin[k], tree[k]), k
+    return img, st, lin
+
+
+@pytest.mark.parametrize("binth", [1, 2, 4, 16])
+@pytest.mark.parametrize("nrules,resid", [(16, 0.0), (256, 0.0), (300, 0.3), (1024, 0.1)])
+def test_tree_equals_linear(nrules, resid, binth):
+    rules = synth.make_rules(nrules, seed=nrules + binth, resid_frac=resid, any_ip_frac=0.1)
+    pk = synth.make_packets(6000, rules, seed=5, kind="imix", stride=128, malformed_frac=0.05, with_ts=True)
+    img, st, lin = compare(rules, None, pk, binth=binth)
+    assert st["n_rules"] == nrules
+    assert st["max_depth"] < 60
+    assert (lin["acl_hit"] >= 0).sum() > 500
+
+
+def test_golden_rules_tree(golden):
+    pk = {"hdr": golden["hdr"], "len": golden["len"], "ts": golden["ts"]}
+    for binth in (1, 4):
+        _, _, lin = compare(golden["rules"], golden["used"], pk, binth=binth)
+        assert np.array_equal(lin["verdict"], golden["a_verdict"])
+
+
+def test_heavily_overlapping_wildcards():
+    rng = np.random.default_rng(3)
+    n = 400
+    r = np.zeros(n, RULE_DTYPE)
+    r["sip_mask"] = rng.choice([0, 8, 16], n)
+    r["sip"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) & 0xFFFF0000
+    r["dip_mask"] = rng.choice([0, 4], n)
+    r["dip"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    lo = rng.integers(0, 60000, n)
+    r["dport_start"], r["dport_end"] = lo, lo + rng.integers(0, 5000, n)
+    r["sport_end"] = 65535
+    r["protocol_start"], r["protocol_end"] = 0, 255
+    r["action"] = rng.integers(0, 2, n)
+    pk = synth.make_packets(8000, r, seed=9, stride=128, hit_frac=0.9)
+    compare(r, None, pk, default_action=0)
+
+
+def test_default_action_and_empty_set():
+    pk = synth.make_packets(2000, np.zeros(0, RULE_DTYPE), seed=2, stride=128)
+    for da in (0, 1):
+        img, st, lin = compare(np.zeros(0, RULE_DTYPE), None, pk, default_action=da)
+        assert st["n_nodes"] == 1 and (lin["acl_hit"] == -1).all()
+
+
+def test_used_mask_and_empty_ranges():
+    rules = synth.make_rules(200, seed=4)
+    rules["sport_start"][::7] = 60000
+    rules["sport_end"][::7] = 10  # empty: never matches
+    used = (np.arange(200) % 5 != 0).astype(np.uint8)
+    pk = synth.make_packets(5000, rules, seed=8, stride=128)
+    _, st, _ = compare(rules, used, pk)
+    assert st["n_rules"] == int(((np.arange(200) % 5 != 0) & (np.arange(200) % 7 != 0)).sum())
+
+
+def test_bad_mask_rejected():
+    rules = synth.make_rules(4)
+    rules["sip_mask"][2] = 33
+    with pytest.raises(ValueError):
+        abi.build_image(rules)
+
+
+def test_large_ruleset_builds_bounded():
+    rules = synth.make_rules(65536)
+    img, st = abi.build_image(rules, default_action=1, binth=1)
+    assert st["n_rules"] == 65536 and st["max_depth"] < 60
+    assert len(img) * 4 == st["blob_bytes"] < 64 << 20
+    pk = synth.make_packets(3000, rules, seed=1, stride=128)
+    o = pyoracle.Oracle(rules, default_action=1, image=img)
+    lin = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=8)
+    tree = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=8, use_tree=True)
+    assert np.array_equal(lin["acl_hit"], tree["acl_hit"])
+
+
+def test_image_layout():
+    rules = synth.make_rules(64)
+    img, st = abi.build_image(rules)
+    assert img[0] == 0x41455050 and img[1] == 1
+    assert img[2] == st["n_nodes"] and img[4] == 64 and img[11] == len(img)
+    assert img[7] % 8 == 0  # rules 32-B aligned

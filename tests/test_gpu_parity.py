@@ -1,0 +1,280 @@
+"""GPU parity: the HIP path (libppe_hip.so through the C ABI) against the oracle and the committed fixtures.
+
+Bar: bit-exact verdict word, flow hash, ACL hit index, 5-tuple and counters (integer work — no tolerance)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import torch  # noqa: E402  (loads the HIP runtime first)
+
+import pyoracle  # noqa: E402
+from ppe import Engine, abi, synth  # noqa: E402
+from ppe.abi import ST  # noqa: E402
+
+NOW = 1_700_000_000
+DEV = torch.device("cuda:0")
+OUTS = ("verdict", "flow_hash", "acl_hit", "fw_idx", "drop_idx", "tile_cnt", "tuple")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def gpu_classify(eng, hdr, lens, ts=None, cfg=None, outs=OUTS):
+    n = len(lens)
+    th = torch.from_numpy(np.ascontiguousarray(hdr)).to(DEV)
+    tl = torch.from_numpy(np.ascontiguousarray(lens, np.uint32).view(np.int32)).to(DEV)
+    tt = torch.from_numpy(np.ascontiguousarray(ts, np.uint64).view(np.int64)).to(DEV) if ts is not None else None
+    shapes = {"tile_cnt": ((n + 63) // 64,), "tuple": (n, 4)}
+    out = {k: torch.full(shapes.get(k, (n,)), -7, dtype=torch.int32, device=DEV) if k in outs else None
+           for k in OUTS}
+    eng.classify_torch(th, tl, out, cfg=cfg or eng.cfg(now_seconds=NOW), ts=tt)
+    torch.cuda.synchronize()
+    res = {}
+    for k, v in out.items():
+        if v is None:
+            continue
+        a = v.cpu().numpy()
+        res[k] = a if k == "acl_hit" else a.view(np.uint32)
+    return res
+
+
+def assert_same(got, ref, keys=("verdict", "flow_hash", "acl_hit", "tuple")):
+    for k in keys:
+        g, r = got[k], ref[k]
+        if not np.array_equal(g, r):
+            bad = np.nonzero((g != r).reshape(len(g), -1).any(axis=1))[0]
+            raise AssertionError(f"{k}: {len(bad)} mismatches, first {bad[:5].tolist()}: gpu={g[bad[:3]].tolist()} "
+                                 f"ref={r[bad[:3]].tolist()}")
+
+
+def check_compaction(res, n):
+    v = res["verdict"]
+    act = (v >> 8) & 0xFF
+    tc = res["tile_cnt"]
+    for t in range((n + 63) // 64):
+        lo, hi = 64 * t, min(n, 64 * t + 64)
+        fw = np.nonzero(act[lo:hi] == 0)[0] + lo
+        dr = np.nonzero(act[lo:hi] == 1)[0] + lo
+        pu = np.nonzero(act[lo:hi] == 2)[0] + lo
+        assert tc[t] == len(fw) | (len(dr) << 8) | (len(pu) << 16), t
+        assert np.array_equal(res["fw_idx"][lo:lo + len(fw)], fw), t
+        assert np.array_equal(res["drop_idx"][lo:lo + len(dr)], dr), t
+
+
+# ---------------------------------------------------------------- fixtures frozen in tests/golden
+@pytest.mark.parametrize("tag,cfg", [("a", (0, 1)), ("b", (1, 0))])
+def test_golden_fixture_device_path(eng, golden, tag, cfg):
+    g = golden
+    eng.commit(g["rules"], g["used"], default_action=1)
+    eng.clear_counters()
+    res = gpu_classify(eng, g["hdr"], g["len"], g["ts"], eng.cfg(cfg[0], cfg[1], int(g["now"])))
+    assert_same(res, {k: g[f"{tag}_{k}"] for k in ("verdict", "flow_hash", "acl_hit", "tuple")})
+    check_compaction(res, len(g["len"]))
+    cnt = eng.counters()
+    assert [cnt[n] for n in abi.COUNTERS] == g[f"{tag}_counters"][:30].tolist()
+
+
+def test_golden_fixture_host_pipeline(eng, golden):
+    g = golden
+    eng.commit(g["rules"], g["used"], default_action=1)
+    for chunk in (64, 1000, 0):
+        res = eng.classify_host(g["hdr"], g["len"], ts=g["ts"], cfg=eng.cfg(0, 1, int(g["now"])), chunk=chunk,
+                                outputs=OUTS)
+        assert_same(res, {k: g[f"a_{k}"] for k in ("verdict", "flow_hash", "acl_hit", "tuple")})
+        check_compaction(res, len(g["len"]))
+
+
+def test_flow_hash_matches_reference_tluhash(eng, ref_hash):
+    """Packets built from the reference-hashed tuples: the GPU flow hash equals the value the reference's own
+    dataplane/src/flow/tluhash.h produced (fixture made by tests/golden/gen_golden.py from oracle/_ref)."""
+    tup, want = ref_hash["tuple"], ref_hash["hash"]
+    sel = np.nonzero((tup[:, 3] == 6) | (tup[:, 3] == 17))[0]
+    n = len(sel)
+    hdr = np.zeros((n, 64), np.uint8)
+    lens = np.full(n, 64, np.uint32)
+    for j, i in enumerate(sel):
+        sip, dip, ports, proto = (int(x) for x in tup[i])
+        sp, dp = ports & 0xFFFF, ports >> 16
+        h = hdr[j]
+        h[0:12] = [2, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2]
+        h[12:14] = [8, 0]
+        h[14], h[16:18], h[23] = 0x45, [0, 50], proto
+        h[26:30] = list(sip.to_bytes(4, "big"))
+        h[30:34] = list(dip.to_bytes(4, "big"))
+        h[34:38] = list(sp.to_bytes(2, "big")) + list(dp.to_bytes(2, "big"))
+        if proto == 17:
+            h[38:40] = [0, 30]
+        else:
+            h[46], h[47] = 0x50, 0x02
+    eng.commit(np.zeros(0, abi.RULE_DTYPE), default_action=0)
+    res = gpu_classify(eng, hdr, lens)
+    assert ((res["verdict"] & 0xFF) == ST["ACL_FW"]).all()
+    assert np.array_equal(res["flow_hash"], want[sel])
+
+
+# ---------------------------------------------------------------- seeded random batches per benchmark config
+@pytest.mark.parametrize("cfgname,n", [("C0", 10_000), ("C1", 200_000), ("C2", 200_000)])
+def test_config_batches_vs_oracle(eng, cfgname, n):
+    c = synth.CONFIGS[cfgname]
+    rules = synth.make_rules(c["rules"])
+    pk = synth.make_packets(n, rules, seed=31, kind=c["kind"], stride=128)
+    eng.commit(rules, default_action=1)
+    res = gpu_classify(eng, pk["hdr"], pk["len"])
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    assert_same(res, ref)
+    check_compaction(res, n)
+
+
+def test_c3_64k_rules_vs_oracle(eng):
+    rules = synth.make_rules(65536)
+    pk = synth.make_packets(100_000, rules, seed=32, stride=64)
+    st = eng.commit(rules, default_action=1)
+    assert st["n_rules"] == 65536
+    res = gpu_classify(eng, pk["hdr"], pk["len"])
+    img = eng.image()
+    o = pyoracle.Oracle(rules, default_action=1, image=img)
+    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16, use_tree=True)
+    assert_same(res, ref)
+    lin = o.classify_batch(pk["hdr"][:3000], pk["len"][:3000], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    assert np.array_equal(res["acl_hit"][:3000], lin["acl_hit"])
+
+
+def test_residual_rules_with_timestamps(eng):
+    rules = synth.make_rules(512, seed=40, resid_frac=0.5, any_ip_frac=0.2)
+    pk = synth.make_packets(50_000, rules, seed=41, kind="imix", stride=128, with_ts=True, hit_frac=0.9)
+    eng.commit(rules, default_action=0)
+    res = gpu_classify(eng, pk["hdr"], pk["len"], ts=pk["ts"])
+    o = pyoracle.Oracle(rules, default_action=0)
+    ref = o.classify_batch(pk["hdr"], pk["len"], ts=pk["ts"], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    assert_same(res, ref)
+    # and the batch-wide timestamp (ts == NULL → cfg.now_seconds)
+    res = gpu_classify(eng, pk["hdr"], pk["len"])
+    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    assert_same(res, ref)
+
+
+def test_window_64_punts_exactly_where_headers_exceed_it(eng):
+    rules = synth.make_rules(256, seed=50)
+    pk = synth.make_packets(60_000, rules, seed=51, kind="imix", stride=128, malformed_frac=0.3)
+    eng.commit(rules, default_action=1)
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    res = gpu_classify(eng, np.ascontiguousarray(pk["hdr"][:, :64]), pk["len"])
+    need = ref["reach"] > 64
+    st = res["verdict"] & 0xFF
+    assert need.sum() > 10
+    assert (st[need] == ST["WINDOW_PUNT"]).all()
+    assert (((res["verdict"][need] >> 8) & 0xFF) == 2).all()
+    ok = ~need
+    for k in ("verdict", "flow_hash", "acl_hit"):
+        assert np.array_equal(res[k][ok], ref[k][ok]), k
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 129, 1000])
+def test_ragged_sizes(eng, n):
+    rules = synth.make_rules(32, seed=60)
+    pk = synth.make_packets(n, rules, seed=61, kind="imix", stride=128, malformed_frac=0.2)
+    eng.commit(rules, default_action=1)
+    res = gpu_classify(eng, pk["hdr"], pk["len"])
+    o = pyoracle.Oracle(rules, default_action=1)
+    assert_same(res, o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW)))
+    check_compaction(res, n)
+
+
+def test_argument_errors(eng):
+    lib = eng.lib
+    buf = torch.zeros(4096, dtype=torch.uint8, device=DEV)
+    lens = torch.zeros(16, dtype=torch.int32, device=DEV)
+    r = abi.Result()
+    cfg = eng.cfg()
+    b = abi.Batch(buf.data_ptr() + 4, lens.data_ptr(), None, 16, 64)  # misaligned window array
+    assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == -22
+    b = abi.Batch(buf.data_ptr(), lens.data_ptr(), None, 16, 96)  # unsupported stride
+    assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == -22
+    bad = eng.cfg(unsupport_proto_action=2)
+    b = abi.Batch(buf.data_ptr(), lens.data_ptr(), None, 16, 64)
+    assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(bad), None) == -22
+    b = abi.Batch(buf.data_ptr(), lens.data_ptr(), None, 0, 64)  # empty batch is a no-op
+    assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == 0
+
+
+def test_acl_tuple_lookup_api(eng):
+    rules = synth.make_rules(300, seed=70, resid_frac=0.3)
+    pk = synth.make_packets(20_000, rules, seed=71, stride=128, with_ts=True, hit_frac=0.9)
+    eng.commit(rules, default_action=1)
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"], pk["len"], ts=pk["ts"], cfg=o.cfg(0, 1, NOW))
+    l4 = (ref["verdict"] >> 16) & 0x10 != 0  # PPE_F_ACL: the packets whose ACL result the oracle computed
+    tup = ref["tuple"][l4].copy()
+    tup[:, 3] &= 0xFF
+    h = pk["hdr"][l4]
+    macs = np.zeros((len(tup), 4), np.uint32)
+    macs[:, 0] = h[:, 0:4].copy().view("<u4")[:, 0]
+    macs[:, 1] = h[:, 4].astype(np.uint32) | (h[:, 5].astype(np.uint32) << 8)
+    macs[:, 2] = h[:, 6:10].copy().view("<u4")[:, 0]
+    macs[:, 3] = h[:, 10].astype(np.uint32) | (h[:, 11].astype(np.uint32) << 8)
+    hit, act = eng.acl_lookup_host(tup, macs, pk["ts"][l4])
+    assert np.array_equal(hit, ref["acl_hit"][l4])
+    want = np.where(hit >= 0, rules["action"][np.maximum(hit, 0)], 1)
+    assert np.array_equal(act, want)
+
+
+def test_commit_double_buffer_and_determinism(eng):
+    rules_a = synth.make_rules(256, seed=80)
+    rules_b = synth.make_rules(256, seed=81)
+    pk = synth.make_packets(300_000, rules_a, seed=82, stride=64)
+    eng.commit(rules_a, default_action=1)
+    r1 = gpu_classify(eng, pk["hdr"], pk["len"])
+    r2 = gpu_classify(eng, pk["hdr"], pk["len"])
+    for k in r1:
+        assert np.array_equal(r1[k], r2[k]), k  # deterministic, including the compaction order
+    eng.commit(rules_b, default_action=0)
+    rb = gpu_classify(eng, pk["hdr"], pk["len"])
+    o = pyoracle.Oracle(rules_b, default_action=0)
+    assert_same(rb, o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16))
+    eng.commit(rules_a, default_action=1)
+    ra = gpu_classify(eng, pk["hdr"], pk["len"])
+    assert np.array_equal(ra["acl_hit"], r1["acl_hit"])
+
+
+def test_full_size_properties_c1(eng):
+    """1M packets (the C1 bench batch): counters sum to n, every packet is in exactly one compaction class,
+    the two halves classified separately equal the whole, and the flow hash is direction-symmetric."""
+    c = synth.CONFIGS["C1"]
+    rules = synth.make_rules(c["rules"])
+    n = c["n"]
+    pk = synth.make_packets(n, rules, stride=64)
+    eng.commit(rules, default_action=1)
+    eng.clear_counters()
+    whole = gpu_classify(eng, pk["hdr"], pk["len"])
+    cnt = eng.counters()
+    assert cnt["pkts"] == n and cnt["out_fw"] + cnt["out_drop"] + cnt["out_punt"] == n
+    assert cnt["acl_fw"] + cnt["acl_drop"] == int((((whole["verdict"] >> 16) & 0x10) != 0).sum())
+    half = n // 2  # tile aligned
+    a = gpu_classify(eng, pk["hdr"][:half], pk["len"][:half])
+    b = gpu_classify(eng, pk["hdr"][half:], pk["len"][half:])
+    for k in ("verdict", "flow_hash", "acl_hit"):
+        assert np.array_equal(np.concatenate([a[k], b[k]]), whole[k]), k
+    # swap source and destination (addresses and ports) of every well-formed UDP packet: same flow hash
+    h = pk["hdr"].copy()
+    h[:, 26:30], h[:, 30:34] = pk["hdr"][:, 30:34], pk["hdr"][:, 26:30]
+    h[:, 34:36], h[:, 36:38] = pk["hdr"][:, 36:38], pk["hdr"][:, 34:36]
+    sw = gpu_classify(eng, h, pk["len"])
+    l4 = (((whole["verdict"] >> 16) & 0x2) != 0) & (pk["kinds"] == -1)  # well-formed: ports at bytes 34-37
+    assert l4.sum() > 0.9 * n
+    assert np.array_equal(sw["flow_hash"][l4], whole["flow_hash"][l4])
+    # and a 1/16 sample bit-exact against the oracle
+    o = pyoracle.Oracle(rules, default_action=1)
+    idx = slice(0, n, 16)
+    ref = o.classify_batch(pk["hdr"][idx], pk["len"][idx], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    for k in ("verdict", "flow_hash", "acl_hit"):
+        assert np.array_equal(whole[k][idx], ref[k]), k

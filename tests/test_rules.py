@@ -1,0 +1,119 @@
+"""Rule store + '@' rule-file parser (include/rule.h, rule/rule.c semantics) through the C ABI — host code only."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from ppe import abi
+from ppe.abi import RULE_DTYPE
+
+RULE_OK, RULE_FULL, RULE_EXIST, RULE_NOT_EXIST = 0, 1, 2, 3
+
+
+class RuleEntry(C.Structure):
+    _pack_ = 1
+    _fields_ = [("entry_status", C.c_int8), ("tuple", C.c_uint8 * 60)]
+
+
+class RuleList(C.Structure):  # include/acl_rule.h:34-41 on x86-64
+    _fields_ = [("rule_def_act", C.c_uint32), ("rule_entry_free", C.c_int), ("build_status", C.c_int),
+                ("mutex", C.c_uint64 * 5), ("rule_entry", RuleEntry * abi.RULE_ENTRY_MAX)]
+
+
+@pytest.fixture()
+def lib():
+    lib = abi.load()
+    lib.ppe_rule_list_free()
+    assert lib.ppe_rule_list_init() == 0
+    yield lib
+    lib.ppe_rule_list_free()
+
+
+def rl(lib) -> RuleList:
+    p = C.c_void_p.in_dll(lib, "rule_list")
+    return RuleList.from_address(p.value)
+
+
+def one(**kw):
+    r = np.zeros(1, RULE_DTYPE)
+    r["sport_end"] = r["dport_end"] = 65535
+    r["protocol_end"] = 255
+    for k, v in kw.items():
+        r[k] = v
+    return r
+
+
+def add(lib, r):
+    rid = C.c_uint32(99999)
+    rc = lib.Rule_add(r.ctypes.data, C.byref(rid))
+    return rc, rid.value
+
+
+def test_layout_and_init(lib):
+    assert C.sizeof(RuleEntry) == 61 and C.sizeof(RuleList) == 56 + 61 * 10000
+    L = rl(lib)
+    assert L.rule_def_act == 1 and L.rule_entry_free == 10000 and L.build_status == 1  # srv_rule.c:84-86
+
+
+def test_add_dup_del_first_free(lib):
+    a, b = one(sip=0x0A000000, sip_mask=8), one(dip=0x0B000000, dip_mask=8)
+    assert add(lib, a) == (RULE_OK, 0)
+    assert rl(lib).build_status == 0  # UNCOMMIT
+    assert add(lib, a)[0] == RULE_EXIST  # memcmp duplicate, rule/rule.c:363-368
+    assert add(lib, b) == (RULE_OK, 1)
+    assert lib.Rule_del_by_id(0) == RULE_OK
+    assert lib.Rule_del_by_id(0) == RULE_NOT_EXIST
+    assert lib.Rule_del_by_id(123456) == RULE_NOT_EXIST
+    assert add(lib, a) == (RULE_OK, 0)  # first free index wins, rule/rule.c:13-23
+    L = rl(lib)
+    assert L.rule_entry_free == 9998
+    assert bytes(L.rule_entry[1].tuple) == b.tobytes()
+    assert lib.Rule_del_all() == RULE_OK
+    assert rl(lib).rule_entry_free == 10000
+    assert lib.Rule_del_by_id(1) == RULE_NOT_EXIST
+
+
+def test_full(lib):
+    r = one()
+    for i in range(abi.RULE_ENTRY_MAX):
+        r["sport_start"] = i
+        assert add(lib, r)[0] == RULE_OK
+    r["sport_start"] = 60000
+    assert add(lib, r)[0] == RULE_FULL
+
+
+RULE_FILE = """# comment lines and anything before the at-sign are skipped (rule/rule.c:202-213)
+@ 00:00:00:00:00:00 02:aa:bb:cc:dd:ee 10.0.0.0/8 192.168.1.1/32 0 : 65535 80 : 80 17 : 17 0 0 1 1
+@ 00:00:00:00:00:00 00:00:00:00:00:00 0.0.0.0/0 0.0.0.0/0 1024 : 2048 0 : 65535 0 : 255 1700000000 1700000100 0 0
+"""
+
+
+def test_rule_file_parser(lib, tmp_path):
+    f = tmp_path / "rule_config"
+    f.write_text(RULE_FILE)
+    assert lib.ppe_rule_load_file(str(f).encode()) == 2
+    L = rl(lib)
+    t0 = np.frombuffer(bytes(L.rule_entry[0].tuple), RULE_DTYPE)[0]
+    assert t0["sip"] == 0x0A000000 and t0["sip_mask"] == 8 and t0["dip"] == 0xC0A80101 and t0["dip_mask"] == 32
+    assert (t0["dport_start"], t0["dport_end"]) == (80, 80) and t0["protocol_start"] == 17
+    assert list(t0["dmac"]) == [0x02, 0xAA, 0xBB, 0xCC, 0xDD, 0xEE] and t0["action"] == 1 and t0["logable"] == 1
+    t1 = np.frombuffer(bytes(L.rule_entry[1].tuple), RULE_DTYPE)[0]
+    assert (t1["time_start"], t1["time_end"]) == (1700000000, 1700000100)
+    assert (t1["sport_start"], t1["sport_end"]) == (1024, 2048)
+
+
+@pytest.mark.parametrize("line", [
+    "@ 00:00:00:00:00:00 00:00:00:00:00:00 0.0.0.0/8 0.0.0.0/0 0 : 1 0 : 1 0 : 1 0 0 0 0",   # ip 0 with mask != 0
+    "@ 00:00:00:00:00:00 00:00:00:00:00:00 1.0.0.0/33 0.0.0.0/0 0 : 1 0 : 1 0 : 1 0 0 0 0",  # mask > 32
+    "@ 00:00:00:00:00:00 00:00:00:00:00:00 1.0.0.0/8 0.0.0.0/0 9 : 1 0 : 1 0 : 1 0 0 0 0",   # sport start > end
+    "@ 00:00:00:00:00:00 00:00:00:00:00:00 1.0.0.0/8 0.0.0.0/0 0 : 1 0 : 1 9 : 1 0 0 0 0",   # proto start > end
+    "@ 00:00:00:00:00:00 00:00:00:00:00:00 1.0.0.0/8 0.0.0.0/0 0 : 1 0 : 1 0 : 1 0 0 2 0",   # action not 0/1
+    "@ 00:00:00:00:00:00 00:00:00:00:00:00 1.0.0.0/8 0.0.0.0/0 0 : 1 0 : 1 0 : 1 0 0 0 7",   # log not 0/1
+    "@ 00:00:00:00:00 00:00:00:00:00:00 1.0.0.0/8 0.0.0.0/0 0 : 1 0 : 1 0 : 1 0 0 0 0",      # short MAC
+    "@ 00:00:00:00:00:00 00:00:00:00:00:00 1.0.0.0-8 0.0.0.0/0 0 : 1 0 : 1 0 : 1 0 0 0 0",   # no slash
+])
+def test_rule_file_rejects(lib, tmp_path, line):
+    f = tmp_path / "bad"
+    f.write_text(line + "\n")
+    assert lib.ppe_rule_load_file(str(f).encode()) == -1
+    assert rl(lib).rule_entry_free == 10000
