@@ -123,19 +123,22 @@ def main():
 
     for i in range(args.warmup):
         step(i)
-    barrier()
-    eng.timing(True)
-    eng.timing_read(reset=True)
+    # timed region 1 (value): K back-to-back launches, barrier + synchronize on both sides, no per-launch events
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
-    t0 = time.perf_counter()
     ev0.record(stream)
     for i in range(args.steps):
         step(i)
     ev1.record(stream)
     barrier()
-    wall = time.perf_counter() - t0
     elapsed_ms = ev0.elapsed_time(ev1)
+    # timed region 2 (roofline): the same K launches with HIP events recorded around each launch on its stream
+    eng.timing(True)
+    eng.timing_read(reset=True)
+    barrier()
+    for i in range(args.steps):
+        step(i)
+    barrier()
     kern_ms, launches = eng.timing_read(reset=True)
     eng.timing(False)
     my_ms = max(elapsed_ms, 1e-9)
@@ -161,8 +164,11 @@ def main():
         got_v = out["verdict"][:m].cpu().numpy().view(np.uint32)
         got_h = out["flow_hash"][:m].cpu().numpy().view(np.uint32)
         got_a = out["acl_hit"][:m].cpu().numpy()
-        parity = bool(np.array_equal(got_v, ref["verdict"]) and np.array_equal(got_h, ref["flow_hash"])
-                      and np.array_equal(got_a, ref["acl_hit"]))
+        # packets whose headers reach past the window must be WINDOW_PUNT; every other one bit-exact
+        far = ref["reach"] > stride
+        ok = ~far
+        parity = bool(np.array_equal(got_v[ok], ref["verdict"][ok]) and np.array_equal(got_h[ok], ref["flow_hash"][ok])
+                      and np.array_equal(got_a[ok], ref["acl_hit"][ok]) and ((got_v[far] & 0xFF) == 18).all())
 
     # ---- host-inclusive rate (pinned host buffers, H2D + classify + D2H pipeline) ----
     host_mpps = None

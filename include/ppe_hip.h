@@ -199,6 +199,17 @@ int  ppe_timing_read(ppe_ctx_t *ctx, double *total_ms, uint32_t *launches, int r
 /* Copy the current device classifier image to host (for tests / tools).  words may be NULL to query size. */
 int  ppe_acl_image(ppe_ctx_t *ctx, uint32_t *words, uint32_t *n_words);
 
+/* Launch tuning of the classify kernel for this context.  Defaults come from the fastest measured variant (and the
+ * PPE_BLOCK / PPE_BLOCKS_PER_CU / PPE_PREFETCH / PPE_LDS_IMG environment variables); 0 = automatic. */
+typedef struct {
+    uint32_t block;          /* workgroup size 256, 512 or 1024; 0 = chosen per classifier image   */
+    uint32_t blocks_per_cu;  /* persistent-grid workgroups per CU; 0 = occupancy API              */
+    uint32_t prefetch;       /* reserved, must be 0 (register prefetch measured slower)            */
+    uint32_t lds_image;      /* 1 = stage the image (or its top) in LDS, 0 = read it from global   */
+} ppe_tuning_t;
+int  ppe_set_tuning(ppe_ctx_t *ctx, const ppe_tuning_t *t);
+int  ppe_get_tuning(ppe_ctx_t *ctx, ppe_tuning_t *t);
+
 /* Launch geometry in use (for profiling notes). */
 int  ppe_launch_info(ppe_ctx_t *ctx, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes);
 

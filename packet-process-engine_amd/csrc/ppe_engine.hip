@@ -60,6 +60,7 @@ struct ppe_ctx {
     size_t ev_used = 0;
     // host pipeline
     HostStage hs[kHostStreams];
+    ppe_tuning_t tune;
     char err[256] = {0};
 };
 
@@ -86,41 +87,67 @@ int env_int(const char *name, int dflt) {
     return e && *e ? atoi(e) : dflt;
 }
 
-// Kernel variant knobs (defaults = the fastest measured on MI355X):
-//   PPE_PREFETCH  1 = next-tile register prefetch            (default 0)
-//   PPE_BLOCK     workgroup size 256 / 512 / 1024           (default 256)
-//   PPE_LDS_IMG   0 = read the classifier image from global memory (L1/L2) instead of staging it in LDS
-bool use_prefetch() {
-    static const bool p = env_int("PPE_PREFETCH", 0) != 0;
-    return p;
-}
-uint32_t block_size() {
-    static const uint32_t b = [] {
-        const int v = env_int("PPE_BLOCK", 256);
-        return (uint32_t)(v == 512 || v == 1024 ? v : 256);
-    }();
-    return b;
-}
-bool lds_image_ok(uint32_t img_bytes) {
-    static const int mode = env_int("PPE_LDS_IMG", 1);
-    return mode != 0 && img_bytes <= PPE_LDS_IMG_MAX;
+// Kernel variant knobs live per context (ppe_set_tuning); the defaults are the fastest measured on MI355X
+//  and can be overridden by PPE_BLOCK / PPE_BLOCKS_PER_CU / PPE_LDS_IMG.
+ppe_tuning_t default_tuning() {
+    ppe_tuning_t t;
+    const int b = env_int("PPE_BLOCK", 0);
+    t.block = (uint32_t)(b == 256 || b == 512 || b == 1024 ? b : 0);  // 0 = chosen per image
+    const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
+    t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
+    t.prefetch = 0;
+    t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
+    return t;
 }
 
-// Resident workgroups per CU for the classify kernel with this image: the occupancy API's answer (register and
-// LDS limits) unless PPE_BLOCKS_PER_CU overrides it.  The persistent grid is CUs × this, so no workgroup waits for
-// a second round.
-uint32_t blocks_per_cu(uint32_t img_bytes, bool lds) {
-    static const int env_bpc = env_int("PPE_BLOCKS_PER_CU", 0);
-    if (env_bpc > 0 && env_bpc <= (int)kMaxBlocksPerCU) {
-        if (!lds) return (uint32_t)env_bpc;
-        const uint32_t fit = (160u * 1024u) / (128u + ((img_bytes + 1023u) & ~1023u));
-        return std::max(1u, std::min((uint32_t)env_bpc, fit));  // env override assumes 256-thread blocks
+// How the classify kernel holds the classifier image (see IMG_* in ppe_kernels.hip).
+struct StagePlan {
+    int mode;            // 0 global, 1 whole image in LDS, 2 prefix in LDS
+    uint32_t block;
+    uint32_t lds_words, lds_nodes, leaf_lds;
+};
+
+StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
+    StagePlan p = {0, c->tune.block ? c->tune.block : 256u, 0, 0, 0};
+    const uint32_t words = (uint32_t)img.size(), bytes = words * 4u;
+    if (!c->tune.lds_image) return p;
+    if (bytes <= PPE_LDS_IMG_SMALL && (c->tune.block == 0 || c->tune.block == 256)) {
+        p.mode = 1;  // small image: 256-thread workgroups, 8 per CU, each with its own copy
+        p.block = 256;
+        p.lds_words = words;
+        return p;
     }
-    const int occ = ppe_classify_occupancy(img_bytes / 4u, lds ? 1 : 0, use_prefetch() ? 1 : 0, (int)block_size());
-    if (occ > 0) return std::min<uint32_t>((uint32_t)occ, kMaxBlocksPerCU);
-    if (!lds) return kMaxBlocksPerCU;
-    const uint32_t per_block = 128u + ((img_bytes + 1023u) & ~1023u);
-    return std::max(1u, std::min(kMaxBlocksPerCU * 256u / block_size(), (160u * 1024u) / per_block));
+    p.block = c->tune.block ? c->tune.block : 1024u;
+    // LDS per workgroup when the CU holds 2048 / block workgroups (32 waves), minus counters and 1-KB rounding
+    const uint32_t budget = std::min<uint32_t>(PPE_LDS_IMG_MAX, (160u * 1024u) / (2048u / p.block) - 1152u);
+    const uint32_t off_rules = img[PPE_IMG_W_OFFRULES], n_nodes = img[PPE_IMG_W_NNODES];
+    if (bytes <= budget) {
+        p.mode = 1;
+        p.lds_words = words;
+    } else if (off_rules * 4u <= budget) {  // every node and leaf list; rule records from global (L2)
+        p.mode = 2;
+        p.lds_words = off_rules;
+        p.lds_nodes = n_nodes;
+        p.leaf_lds = 1;
+    } else {  // the top of the tree (BFS order) fills the budget
+        p.mode = 2;
+        p.lds_nodes = std::min(n_nodes, (budget / 4u - PPE_IMG_HDR_WORDS) / 2u);
+        p.lds_words = PPE_IMG_HDR_WORDS + 2u * p.lds_nodes;
+        p.leaf_lds = 0;
+    }
+    return p;
+}
+
+// Resident workgroups per CU: the occupancy API's answer (register and LDS limits) unless the tuning fixes it.
+// The persistent grid is CUs × this, so no workgroup waits for a second round.
+uint32_t blocks_per_cu(const ppe_ctx *c, const StagePlan &p) {
+    const uint32_t cap = kMaxBlocksPerCU * 256u / p.block;
+    const uint32_t lds_fit =
+        p.mode ? (160u * 1024u) / (128u + ((p.lds_words * 4u + 1023u) & ~1023u)) : cap;
+    if (c->tune.blocks_per_cu) return std::max(1u, std::min(c->tune.blocks_per_cu, std::min(cap, lds_fit)));
+    const int occ = ppe_classify_occupancy(p.lds_words, p.mode, (int)p.block);
+    if (occ > 0) return std::min<uint32_t>((uint32_t)occ, cap);
+    return std::max(1u, std::min(cap, lds_fit));
 }
 
 int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const ppe_acl_stats_t *st) {
@@ -137,7 +164,7 @@ int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const 
     HIPCHK(c, hipMemcpy(c->d_img[slot], words, bytes, hipMemcpyHostToDevice));
     c->h_img[slot].assign(words, words + n_words);
     c->stats[slot] = *st;
-    c->stats[slot].lds_resident = lds_image_ok((uint32_t)bytes) ? 1u : 0u;
+    c->stats[slot].lds_resident = (uint32_t)stage_plan(c, c->h_img[slot]).mode;
     c->img_used[slot] = false;
     return PPE_OK;
 }
@@ -146,11 +173,11 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
            int slot_set, uint32_t idx_base = 0) {
     const int r = c->running;
     const uint32_t words = (uint32_t)c->h_img[r].size();
-    const bool lds = lds_image_ok(words * 4u);
-    const uint32_t wpb = block_size() / 64u;
+    const StagePlan plan = stage_plan(c, c->h_img[r]);
+    const uint32_t wpb = plan.block / 64u;
     const uint32_t tiles = (in->n + 63u) / 64u;
     const uint32_t want = (tiles + wpb - 1) / wpb;
-    const uint32_t maxg = c->n_cu * blocks_per_cu(words * 4u, lds);
+    const uint32_t maxg = c->n_cu * blocks_per_cu(c, plan);
     const uint32_t grid = std::max(1u, std::min(want, std::min(maxg, c->max_grid)));
 
     ppe_kargs a;
@@ -174,6 +201,9 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
     a.now = cfg ? cfg->now_seconds : 0u;
     a.default_action = c->h_img[r][PPE_IMG_W_DEFACT];
     a.idx_base = idx_base;
+    a.lds_words = plan.lds_words;
+    a.lds_nodes = plan.lds_nodes;
+    a.leaf_lds = plan.leaf_lds;
     a.cslots = c->d_cslots + (size_t)slot_set * c->max_grid * PPE_CSLOT_WORDS;
 
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -188,11 +218,9 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
         e0 = c->ev[c->ev_used];
         e1 = c->ev[c->ev_used + 1];
         c->ev_used += 2;
-        HIPCHK(c, hipEventRecord(e0, s));
     }
-    const int rc = ppe_launch_classify(&a, grid, lds ? 1 : 0, use_prefetch() ? 1 : 0, (int)block_size(), (void *)s);
+    const int rc = ppe_launch_classify(&a, grid, plan.mode, (int)plan.block, (void *)s, (void *)e0, (void *)e1);
     if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
-    if (c->timing) HIPCHK(c, hipEventRecord(e1, s));
     c->img_used[r] = true;
     return PPE_OK;
 }
@@ -239,6 +267,7 @@ int ppe_ctx_create(int device, ppe_ctx_t **out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->n_cu = (uint32_t)prop.multiProcessorCount;
     c->max_grid = c->n_cu * kMaxBlocksPerCU;
+    c->tune = default_tuning();
     const size_t cs_bytes = (size_t)kSlotSets * c->max_grid * PPE_CSLOT_WORDS * sizeof(unsigned long long);
     int rc = PPE_OK;
     if (hipMalloc(&c->d_cslots, cs_bytes) != hipSuccess || hipMemset(c->d_cslots, 0, cs_bytes) != hipSuccess)
@@ -398,7 +427,7 @@ int ppe_acl_lookup(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint32_t 
     a.default_action = c->h_img[r][PPE_IMG_W_DEFACT];
     a.now = now_seconds;
     const uint32_t want = (in->n + PPE_BLOCK - 1) / PPE_BLOCK;
-    const uint32_t grid = std::max(1u, std::min(want, c->n_cu * blocks_per_cu(words * 4u, lds)));
+    const uint32_t grid = std::max(1u, std::min(want, c->n_cu * 8u));
     const int rc = ppe_launch_acl_tuples(&a, grid, lds ? 1 : 0, stream);
     if (rc != 0) return fail(c, PPE_EIO, "acl kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
     c->img_used[r] = true;
@@ -526,6 +555,24 @@ int ppe_timing_read(ppe_ctx_t *c, double *total_ms, uint32_t *launches, int rese
     return PPE_OK;
 }
 
+int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
+    if (!c || !t) return PPE_EINVAL;
+    if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
+        return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
+    if (t->prefetch) return fail(c, PPE_EINVAL, "register prefetch is not built (measured slower; DESIGN.md)");
+    if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 8");
+    c->tune = *t;
+    c->tune.prefetch = t->prefetch ? 1u : 0u;
+    c->tune.lds_image = t->lds_image ? 1u : 0u;
+    return PPE_OK;
+}
+
+int ppe_get_tuning(ppe_ctx_t *c, ppe_tuning_t *t) {
+    if (!c || !t) return PPE_EINVAL;
+    *t = c->tune;
+    return PPE_OK;
+}
+
 int ppe_acl_image(ppe_ctx_t *c, uint32_t *words, uint32_t *n_words) {
     if (!c || !n_words) return PPE_EINVAL;
     const std::vector<uint32_t> &img = c->h_img[c->running];
@@ -536,11 +583,10 @@ int ppe_acl_image(ppe_ctx_t *c, uint32_t *words, uint32_t *n_words) {
 
 int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes) {
     if (!c) return PPE_EINVAL;
-    const uint32_t words = (uint32_t)c->h_img[c->running].size();
-    const bool lds = lds_image_ok(words * 4u);
-    if (grid) *grid = std::min(c->n_cu * blocks_per_cu(words * 4u, lds), c->max_grid);
-    if (block) *block = block_size();
-    if (lds_bytes) *lds_bytes = 128u + (lds ? ((words * 4u + 1023u) & ~1023u) : 0u);
+    const StagePlan plan = stage_plan(c, c->h_img[c->running]);
+    if (grid) *grid = std::min(c->n_cu * blocks_per_cu(c, plan), c->max_grid);
+    if (block) *block = plan.block;
+    if (lds_bytes) *lds_bytes = 128u + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u);
     return PPE_OK;
 }
 

@@ -25,6 +25,9 @@ struct ppe_kargs {
     uint32_t default_action;
     uint64_t now;
     uint32_t idx_base;        /* added to the packet indices written to fw_idx / drop_idx */
+    uint32_t lds_words;       /* image words staged in LDS (IMG_LDS: all; IMG_SPLIT: header + top nodes [+ leaves]) */
+    uint32_t lds_nodes;       /* IMG_SPLIT: nodes [0, lds_nodes) are in LDS                                         */
+    uint32_t leaf_lds;        /* IMG_SPLIT: the leaf lists are in LDS too                                             */
     unsigned long long *cslots; /* [grid][PPE_CSLOT_WORDS] counter slots, one per workgroup */
 };
 
@@ -43,16 +46,19 @@ struct ppe_tuple_kargs {
 
 #define PPE_CSLOT_WORDS 32
 #define PPE_BLOCK 256
-/* images up to this size are staged into LDS by every workgroup */
-#define PPE_LDS_IMG_MAX (40u * 1024u)
+/* LDS available to the staged classifier image per workgroup: small images with 256-thread workgroups (8 per CU),
+ * larger ones with 1024-thread workgroups (2 per CU, so 2 × (128 B + image) ≤ 160 KiB) */
+#define PPE_LDS_IMG_SMALL (20u * 1024u)
+#define PPE_LDS_IMG_MAX (78u * 1024u)
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 /* Launch the classify kernel. grid = workgroups (persistent), lds_img = stage image in LDS. Returns hipError_t. */
-int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int lds_img, int prefetch, int block,
-                        void *stream);
-int ppe_classify_occupancy(uint32_t img_words, int lds_img, int prefetch, int block);
+/* mode: 0 image in global memory, 1 whole image in LDS, 2 prefix in LDS (see ppe_kernels.hip) */
+int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int block, void *stream, void *ev_start,
+                        void *ev_stop);
+int ppe_classify_occupancy(uint32_t lds_words, int mode, int block);
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
 #ifdef __cplusplus
 }

@@ -14,6 +14,7 @@
  * No MFMA: integer bitfield / compare work bound by HBM bandwidth.
  */
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "ppe_hip.h"
 #include "ppe_image.h"
@@ -23,6 +24,9 @@
 // compaction, bit 3 skip the flow hash.  The product build has PPE_ABLATE == 0.
 #ifndef PPE_ABLATE
 #define PPE_ABLATE 0
+#endif
+#ifndef PPE_HOIST  // experiment switch: request the first tile before the image staging (measured 1 µs slower)
+#define PPE_HOIST 0
 #endif
 
 namespace {
@@ -177,38 +181,41 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[16], uint32_t len32, c
     return k;
 }
 
-// First-match decision-tree lookup over the classifier image (ppe_image.h).  `im` points either into LDS or to
-// global memory; after inlining the address space is inferred from the caller.
-// The 5-tuple arrives as scalars (not struct fields): a select between fields of an in-memory struct is folded
-// into a dynamically indexed load, which sends the whole struct to scratch.
-__device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ im, uint32_t off_leaf, uint32_t off_rules,
-                                           uint32_t off_resid, uint32_t default_action, const uint32_t sip,
-                                           const uint32_t dip, const uint32_t sport, const uint32_t dport,
-                                           const uint32_t proto, uint32_t dmac_lo, uint32_t dmac_hi,
-                                           uint32_t smac_lo, uint32_t smac_hi, const uint64_t *tsp, uint32_t p,
-                                           uint64_t now, int32_t &hit, uint32_t &action) {
-    const uint2 *nodes = (const uint2 *)(im + PPE_IMG_HDR_WORDS);
-    uint2 nd = nodes[0];
-#pragma unroll 1
-    for (int it = 0; it < PPE_MAX_DEPTH && (nd.y & 7u) != PPE_NODE_LEAF; ++it) {
-        const uint32_t d = nd.y & 7u;
-        uint32_t key = proto;
-        key = d == PPE_DIM_SIP ? sip : key;
-        key = d == PPE_DIM_DIP ? dip : key;
-        key = d == PPE_DIM_SPORT ? sport : key;
-        key = d == PPE_DIM_DPORT ? dport : key;
-        nd = nodes[(nd.y >> 3) + (key > nd.x ? 1u : 0u)];
-    }
-    hit = -1;
-    action = default_action;
-    if ((nd.y & 7u) != PPE_NODE_LEAF) return;  // unreachable for a builder-made image
+// Image staging modes of the classify kernel:
+//   IMG_GLOBAL  the whole classifier image is read from global memory (L1/L2/MALL-cached)
+//   IMG_LDS     the whole image is staged in LDS
+//   IMG_SPLIT   a prefix is staged: tree nodes [0, lds_nodes) (BFS order: the top of the tree) and, when it fits,
+//               the leaf lists; deeper nodes, leaf lists that did not fit and the rule records come from global
+#define IMG_GLOBAL 0
+#define IMG_LDS 1
+#define IMG_SPLIT 2
+
+__device__ __forceinline__ uint32_t node_key(uint32_t d, uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport,
+                                             uint32_t proto) {
+    uint32_t key = proto;
+    key = d == PPE_DIM_SIP ? sip : key;
+    key = d == PPE_DIM_DIP ? dip : key;
+    key = d == PPE_DIM_SPORT ? sport : key;
+    key = d == PPE_DIM_DPORT ? dport : key;
+    return key;
+}
+
+#define NODE_IS_LEAF(nd) (((nd).y & 7u) == PPE_NODE_LEAF)
+#define NODE_CHILD(nd, key) (((nd).y >> 3) + ((key) > (nd).x ? 1u : 0u))
+
+// Scan one leaf's candidate list in priority order; the first rule that matches wins (lowest index).  `lf`, `rules`
+// and `resid` may each point into LDS or global memory (address space inferred after inlining).
+__device__ __forceinline__ void leaf_scan(uint2 nd, const uint32_t *__restrict__ lf, const uint32_t *__restrict__ rules,
+                                          const uint32_t *__restrict__ resid, uint32_t sip, uint32_t dip, uint32_t sport,
+                                          uint32_t dport, uint32_t proto, uint32_t dmac_lo, uint32_t dmac_hi,
+                                          uint32_t smac_lo, uint32_t smac_hi, const uint64_t *tsp, uint32_t p,
+                                          uint64_t now, int32_t &hit, uint32_t &action) {
     const uint32_t cnt = nd.y >> 3;
-    const uint32_t *lf = im + off_leaf + nd.x;
 #pragma unroll 1
     for (uint32_t j = 0; j < cnt; ++j) {
         const uint32_t e = lf[j];
         const uint32_t slot = e & ~PPE_LEAF_CERTAIN;
-        const uint4 *rp = (const uint4 *)(im + off_rules + 8u * slot);
+        const uint4 *rp = (const uint4 *)(rules + 8u * slot);
         const uint4 a = rp[0], b = rp[1];
         bool m = (e & PPE_LEAF_CERTAIN) != 0u;
         if (!m) {
@@ -218,7 +225,7 @@ __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ im, uint
                 proto >= (b.z & 0xffu) && proto <= ((b.z >> 8) & 0xffu);
             const uint32_t rs = b.w >> 29;
             if (m && rs) {
-                const uint4 *xp = (const uint4 *)(im + off_resid + 8u * slot);
+                const uint4 *xp = (const uint4 *)(resid + 8u * slot);
                 const uint4 c = xp[0], t = xp[1];
                 if (rs & PPE_RESID_DMAC) m = m && c.x == dmac_lo && c.y == dmac_hi;
                 if (rs & PPE_RESID_SMAC) m = m && c.z == smac_lo && c.w == smac_hi;
@@ -238,6 +245,57 @@ __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ im, uint
     }
 }
 
+// First-match decision-tree lookup over the classifier image (ppe_image.h).  The 5-tuple arrives as scalars (not
+// struct fields): a select between fields of an in-memory struct is folded into a dynamically indexed load, which
+// sends the whole struct to scratch.
+template <int MODE>
+__device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ gimg, const uint32_t *__restrict__ limg,
+                                           uint32_t lds_nodes, uint32_t leaf_lds, uint32_t off_leaf,
+                                           uint32_t off_rules, uint32_t off_resid, uint32_t default_action,
+                                           const uint32_t sip, const uint32_t dip, const uint32_t sport,
+                                           const uint32_t dport, const uint32_t proto, uint32_t dmac_lo,
+                                           uint32_t dmac_hi, uint32_t smac_lo, uint32_t smac_hi,
+                                           const uint64_t *tsp, uint32_t p, uint64_t now, int32_t &hit,
+                                           uint32_t &action) {
+    const uint2 *gn = (const uint2 *)(gimg + PPE_IMG_HDR_WORDS);
+    uint2 nd;
+    int it = 0;
+    if (MODE == IMG_GLOBAL) {
+        nd = gn[0];
+#pragma unroll 1
+        for (; it < PPE_MAX_DEPTH && !NODE_IS_LEAF(nd); ++it)
+            nd = gn[NODE_CHILD(nd, node_key(nd.y & 7u, sip, dip, sport, dport, proto))];
+    } else {
+        const uint2 *ln = (const uint2 *)(limg + PPE_IMG_HDR_WORDS);
+        nd = ln[0];
+        uint32_t node = 0;
+#pragma unroll 1
+        for (; it < PPE_MAX_DEPTH && !NODE_IS_LEAF(nd); ++it) {
+            node = NODE_CHILD(nd, node_key(nd.y & 7u, sip, dip, sport, dport, proto));
+            if (MODE == IMG_SPLIT && node >= lds_nodes) break;  // below the staged top of the tree
+            nd = ln[node];
+        }
+        if (MODE == IMG_SPLIT && !NODE_IS_LEAF(nd)) {
+            nd = gn[node];
+#pragma unroll 1
+            for (; it < PPE_MAX_DEPTH && !NODE_IS_LEAF(nd); ++it)
+                nd = gn[NODE_CHILD(nd, node_key(nd.y & 7u, sip, dip, sport, dport, proto))];
+        }
+    }
+    hit = -1;
+    action = default_action;
+    if (!NODE_IS_LEAF(nd)) return;  // unreachable for a builder-made image
+    if (MODE == IMG_LDS)
+        leaf_scan(nd, limg + off_leaf + nd.x, limg + off_rules, limg + off_resid, sip, dip, sport, dport, proto,
+                  dmac_lo, dmac_hi, smac_lo, smac_hi, tsp, p, now, hit, action);
+    else if (MODE == IMG_SPLIT && leaf_lds)
+        leaf_scan(nd, limg + off_leaf + nd.x, gimg + off_rules, gimg + off_resid, sip, dip, sport, dport, proto,
+                  dmac_lo, dmac_hi, smac_lo, smac_hi, tsp, p, now, hit, action);
+    else
+        leaf_scan(nd, gimg + off_leaf + nd.x, gimg + off_rules, gimg + off_resid, sip, dip, sport, dport, proto,
+                  dmac_lo, dmac_hi, smac_lo, smac_hi, tsp, p, now, hit, action);
+}
+
 // Copy the classifier image into LDS with LDS-DMA (global_load_lds_dwordx4): every 1-KB piece of the image is in
 // flight at once, no VGPR round trip.  Each wave-instruction writes 64 × 16 B at a wave-uniform LDS base, so the
 // LDS region is padded to a multiple of 1 KB and the (clamped) tail lanes write into the padding.
@@ -254,7 +312,7 @@ __device__ __forceinline__ void stage_image(const uint32_t *img, uint32_t *lds, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool LDS_IMG, bool PREFETCH, int BLOCK>
+template <int MODE, bool PREFETCH, int BLOCK>
 __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *lcnt = smem;       // [32] per-reason counters of this workgroup
@@ -263,19 +321,18 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t lane = tid & 63u;
     const uint32_t ntiles = (a.n + 63u) >> 6;
     uint32_t tile = blockIdx.x * (BLOCK / 64) + (tid >> 6);
-    // the first tile's header window is requested before the image staging, so the two latencies overlap
+    // PPE_HOIST: request the first tile's header window before the image staging (A/B: slower, kept off)
     uint4 q0, q1, q2, q3;
     uint32_t qlen;
-    {
+    if (PPE_HOIST || PREFETCH) {
         const uint32_t p = min((tile << 6) + lane, a.n - 1u);  // clamped: loads are unconditional (no phi → no wait)
         const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)p * a.stride);
         q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
         qlen = a.len[p];
     }
     if (tid < 32) lcnt[tid] = 0;
-    if (LDS_IMG) stage_image<BLOCK>(a.img, limg, a.img_words, tid);
+    if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img, limg, a.lds_words, tid);
     __syncthreads();
-    const uint32_t *im = LDS_IMG ? (const uint32_t *)limg : a.img;
     const uint32_t off_leaf = a.img[PPE_IMG_W_OFFLEAF];
     const uint32_t off_rules = a.img[PPE_IMG_W_OFFRULES];
     const uint32_t off_resid = a.img[PPE_IMG_W_OFFRESID];
@@ -299,7 +356,7 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     for (bool first = true; tile < ntiles; tile += stride_waves, first = false) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < a.n;
-        if (!PREFETCH && !first) {
+        if (!PREFETCH && (!first || !PPE_HOIST)) {
             const uint32_t pc = min(p, a.n - 1u);
             const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)pc * a.stride);
             q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
@@ -327,9 +384,9 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
         if (!(PPE_ABLATE & 1) && valid && k.st == ST_ACL) {
             uint32_t rule_act;
             // dmac = bytes 0-5, smac = bytes 6-11 (EthernetHdr, decode-ethernet.h:23-27)
-            acl_lookup(im, off_leaf, off_rules, off_resid, a.default_action, k.sip, k.dip, k.sport, k.dport,
-                       k.proto, w[0], w[1] & 0xffffu, (w[1] >> 16) | (w[2] << 16), w[2] >> 16, a.ts, p, a.now, hit,
-                       rule_act);
+            acl_lookup<MODE>(a.img, limg, a.lds_nodes, a.leaf_lds, off_leaf, off_rules, off_resid, a.default_action,
+                             k.sip, k.dip, k.sport, k.dport, k.proto, w[0], w[1] & 0xffffu,
+                             (w[1] >> 16) | (w[2] << 16), w[2] >> 16, a.ts, p, a.now, hit, rule_act);
             const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
             k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
             k.flags |= PPE_F_ACL;
@@ -404,7 +461,6 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
         stage_image<PPE_BLOCK>(a.img, smem, a.img_words, tid);
         __syncthreads();
     }
-    const uint32_t *im = LDS_IMG ? (const uint32_t *)smem : a.img;
     const uint32_t off_leaf = a.img[PPE_IMG_W_OFFLEAF];
     const uint32_t off_rules = a.img[PPE_IMG_W_OFFRULES];
     const uint32_t off_resid = a.img[PPE_IMG_W_OFFRESID];
@@ -414,8 +470,13 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
         if (a.macs) m = ((const uint4 *)a.macs)[i];
         int32_t hit;
         uint32_t act;
-        acl_lookup(im, off_leaf, off_rules, off_resid, a.default_action, t.x, t.y, t.z & 0xffffu, t.z >> 16,
-                   t.w & 0xffu, m.x, m.y, m.z, m.w, a.ts, i, a.now, hit, act);
+        if (LDS_IMG)
+            acl_lookup<IMG_LDS>(a.img, smem, 0, 0, off_leaf, off_rules, off_resid, a.default_action, t.x, t.y,
+                                t.z & 0xffffu, t.z >> 16, t.w & 0xffu, m.x, m.y, m.z, m.w, a.ts, i, a.now, hit, act);
+        else
+            acl_lookup<IMG_GLOBAL>(a.img, smem, 0, 0, off_leaf, off_rules, off_resid, a.default_action, t.x, t.y,
+                                   t.z & 0xffffu, t.z >> 16, t.w & 0xffu, m.x, m.y, m.z, m.w, a.ts, i, a.now, hit,
+                                   act);
         if (a.hit) a.hit[i] = hit;
         if (a.action) a.action[i] = act;
     }
@@ -423,57 +484,54 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
 
 }  // namespace
 
-template <bool L, bool P, int B>
-static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t s) {
-    hipLaunchKernelGGL((ppe_classify_kernel<L, P, B>), dim3(grid), dim3(B), shmem, s, *a);
+template <int M, int B>
+static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    // hipExtLaunchKernelGGL's events are the dispatch packet's own start/end timestamps (what rocprofv3 reports),
+    // unlike hipEventRecord markers around the launch
+    hipExtLaunchKernelGGL((ppe_classify_kernel<M, false, B>), dim3(grid), dim3(B), shmem, s, e0, e1, 0, *a);
     return (int)hipGetLastError();
 }
 
-template <bool L, bool P, int B>
+template <int M, int B>
 static int occ_t(size_t shmem) {
     int nb = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<L, P, B>, B, shmem) == hipSuccess
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, false, B>, B, shmem) == hipSuccess
                ? nb : -1;
 }
 
-static size_t classify_shmem(uint32_t img_words, int lds_img) {
+static size_t classify_shmem(uint32_t lds_words, int mode) {
     const size_t base = 32 * sizeof(uint32_t);
-    return lds_img ? base + (((size_t)img_words * 4u + 1023u) & ~(size_t)1023u) : base;
+    return mode != IMG_GLOBAL ? base + (((size_t)lds_words * 4u + 1023u) & ~(size_t)1023u) : base;
 }
 
-// variant = (lds_img, prefetch, block ∈ {256, 512, 1024})
 #define PPE_DISPATCH(FN, ...)                                                                         \
     do {                                                                                              \
-        if (lds_img) {                                                                                \
-            if (prefetch) {                                                                           \
-                if (block == 1024) return FN<true, true, 1024>(__VA_ARGS__);                          \
-                if (block == 512) return FN<true, true, 512>(__VA_ARGS__);                            \
-                return FN<true, true, 256>(__VA_ARGS__);                                              \
-            }                                                                                         \
-            if (block == 1024) return FN<true, false, 1024>(__VA_ARGS__);                             \
-            if (block == 512) return FN<true, false, 512>(__VA_ARGS__);                               \
-            return FN<true, false, 256>(__VA_ARGS__);                                                 \
+        if (mode == IMG_LDS) {                                                                        \
+            if (block == 1024) return FN<IMG_LDS, 1024>(__VA_ARGS__);                                 \
+            if (block == 512) return FN<IMG_LDS, 512>(__VA_ARGS__);                                   \
+            return FN<IMG_LDS, 256>(__VA_ARGS__);                                                     \
         }                                                                                             \
-        if (prefetch) {                                                                               \
-            if (block == 1024) return FN<false, true, 1024>(__VA_ARGS__);                             \
-            if (block == 512) return FN<false, true, 512>(__VA_ARGS__);                               \
-            return FN<false, true, 256>(__VA_ARGS__);                                                 \
+        if (mode == IMG_SPLIT) {                                                                      \
+            if (block == 1024) return FN<IMG_SPLIT, 1024>(__VA_ARGS__);                               \
+            if (block == 512) return FN<IMG_SPLIT, 512>(__VA_ARGS__);                                 \
+            return FN<IMG_SPLIT, 256>(__VA_ARGS__);                                                   \
         }                                                                                             \
-        if (block == 1024) return FN<false, false, 1024>(__VA_ARGS__);                                \
-        if (block == 512) return FN<false, false, 512>(__VA_ARGS__);                                  \
-        return FN<false, false, 256>(__VA_ARGS__);                                                    \
+        if (block == 1024) return FN<IMG_GLOBAL, 1024>(__VA_ARGS__);                                  \
+        if (block == 512) return FN<IMG_GLOBAL, 512>(__VA_ARGS__);                                    \
+        return FN<IMG_GLOBAL, 256>(__VA_ARGS__);                                                      \
     } while (0)
 
-extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int lds_img, int prefetch, int block,
-                                   void *stream) {
-    const size_t shmem = classify_shmem(a->img_words, lds_img);
+extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, int block, void *stream,
+                                   void *ev_start, void *ev_stop) {
+    const size_t shmem = classify_shmem(a->lds_words, mode);
     hipStream_t s = (hipStream_t)stream;
-    PPE_DISPATCH(launch_t, a, grid, shmem, s);
+    hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
+    PPE_DISPATCH(launch_t, a, grid, shmem, s, e0, e1);
 }
 
 // resident workgroups per CU for the kernel variant (the persistent grid is sized to exactly fill the chip)
-extern "C" int ppe_classify_occupancy(uint32_t img_words, int lds_img, int prefetch, int block) {
-    const size_t shmem = classify_shmem(img_words, lds_img);
+extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int block) {
+    const size_t shmem = classify_shmem(lds_words, mode);
     PPE_DISPATCH(occ_t, shmem);
 }
 

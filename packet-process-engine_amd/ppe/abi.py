@@ -76,6 +76,17 @@ class Counters(C.Structure):
         return {name: int(self.c[i]) for i, name in enumerate(COUNTERS)}
 
 
+class Tuning(C.Structure):
+    _fields_ = [("block", C.c_uint32), ("blocks_per_cu", C.c_uint32), ("prefetch", C.c_uint32),
+                ("lds_image", C.c_uint32)]
+
+    def __init__(self, block=0, blocks_per_cu=0, prefetch=0, lds_image=1):
+        super().__init__(block, blocks_per_cu, prefetch, lds_image)
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Tuples(C.Structure):
     _fields_ = [("tuple", C.c_void_p), ("macs", C.c_void_p), ("ts", C.c_void_p), ("n", C.c_uint32)]
 
@@ -87,7 +98,8 @@ EXPORTS = [
     "ppe_classify_host", "ppe_acl_lookup", "ppe_acl_lookup_host", "ppe_dev_alloc", "ppe_dev_free",
     "ppe_host_alloc", "ppe_host_free", "ppe_memcpy_h2d", "ppe_memcpy_d2h", "ppe_memset_d", "ppe_sync",
     "ppe_counters_read", "ppe_counters_clear", "ppe_timing_enable", "ppe_timing_read", "ppe_acl_image",
-    "ppe_launch_info", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image",
+    "ppe_launch_info", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
+    "ppe_get_tuning",
     # ppe_acl.h
     "ppe_rule_list_init", "ppe_rule_list_free", "Rule_add", "Rule_del_by_id", "Rule_del_all",
     "Rule_duplicate_check", "Rule_Load_Line", "ppe_rule_load_file", "DP_Acl_Rule_Init", "DP_Acl_Load_Rule",
@@ -108,9 +120,21 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
     if _lib is not None and path is None:
         return _lib
     p = Path(path) if path else Path(os.environ.get("PPE_LIB", LIB_PATH))
+    lib = _open(p, C.RTLD_GLOBAL)
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def load_variant(path: str | os.PathLike) -> C.CDLL:
+    """Load another build of the library side by side (RTLD_LOCAL), for in-process A/B timing."""
+    return _open(Path(path), C.RTLD_LOCAL)
+
+
+def _open(p: Path, mode) -> C.CDLL:
     if not p.exists():
         raise OSError(f"{p} not found: build it with `make -C packet-process-engine_amd` (no CPU fallback exists)")
-    lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(str(p), mode=mode)
     vp, u32, i32, u64 = C.c_void_p, C.c_uint32, C.c_int32, C.c_uint64
     sig = {
         "ppe_abi_version": ([], C.c_int),
@@ -137,6 +161,8 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         "ppe_acl_image": ([vp, vp, C.POINTER(u32)], C.c_int),
         "ppe_launch_info": ([vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], C.c_int),
         "ppe_last_error": ([vp], C.c_char_p),
+        "ppe_set_tuning": ([vp, C.POINTER(Tuning)], C.c_int),
+        "ppe_get_tuning": ([vp, C.POINTER(Tuning)], C.c_int),
         "ppe_acl_build_image": ([vp, vp, u32, u32, u32, C.POINTER(C.POINTER(u32)), C.POINTER(u32),
                                  C.POINTER(AclStats)], C.c_int),
         "ppe_acl_free_image": ([C.POINTER(u32)], None),
@@ -161,7 +187,6 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res
-    _lib = lib
     return lib
 
 

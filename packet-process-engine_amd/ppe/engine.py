@@ -13,8 +13,8 @@ class PPEError(RuntimeError):
 
 
 class Engine:
-    def __init__(self, device: int = 0):
-        self.lib = abi.load()
+    def __init__(self, device: int = 0, lib=None):
+        self.lib = lib or abi.load()
         self.ctx = C.c_void_p()
         rc = self.lib.ppe_ctx_create(int(device), C.byref(self.ctx))
         if rc != 0:
@@ -147,6 +147,16 @@ class Engine:
         self._check(self.lib.ppe_timing_read(self.ctx, C.byref(ms), C.byref(n), 1 if reset else 0),
                     "ppe_timing_read")
         return ms.value, n.value
+
+    def tuning(self, **kw) -> dict:
+        """Read (and with keyword arguments, set) the launch tuning: block, blocks_per_cu, prefetch, lds_image."""
+        t = abi.Tuning()
+        self._check(self.lib.ppe_get_tuning(self.ctx, C.byref(t)), "ppe_get_tuning")
+        if kw:
+            for k, v in kw.items():
+                setattr(t, k, int(v))
+            self._check(self.lib.ppe_set_tuning(self.ctx, C.byref(t)), "ppe_set_tuning")
+        return t.as_dict()
 
     def launch_info(self) -> dict:
         g, b, l = C.c_uint32(), C.c_uint32(), C.c_uint32()

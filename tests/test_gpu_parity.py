@@ -205,6 +205,30 @@ def test_argument_errors(eng):
     assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(bad), None) == -22
     b = abi.Batch(buf.data_ptr(), lens.data_ptr(), None, 0, 64)  # empty batch is a no-op
     assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == 0
+    t = abi.Tuning(block=300)
+    assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
+
+
+@pytest.mark.parametrize("tune", [dict(lds_image=0), dict(block=512), dict(block=1024), dict(block=256)])
+def test_every_staging_mode_and_block_matches(eng, tune):
+    """All image placements (global / whole image in LDS / split prefix) and workgroup sizes give identical
+    results: C4-sized rules (split mode by default) and C1-sized rules (whole image in LDS)."""
+    for nrules in (256, 4096):
+        rules = synth.make_rules(nrules, seed=nrules)
+        pk = synth.make_packets(100_000, rules, seed=3, kind="imix", stride=128)
+        eng.commit(rules, default_action=1)
+        base = gpu_classify(eng, pk["hdr"], pk["len"])
+        old = eng.tuning()
+        try:
+            eng.tuning(**tune)
+            res = gpu_classify(eng, pk["hdr"], pk["len"])
+        finally:
+            eng.tuning(**old)
+        for k in base:
+            assert np.array_equal(base[k], res[k]), (nrules, tune, k)
+        o = pyoracle.Oracle(rules, default_action=1)
+        ref = o.classify_batch(pk["hdr"][:5000], pk["len"][:5000], cfg=o.cfg(0, 1, NOW), nthreads=16)
+        assert np.array_equal(res["acl_hit"][:5000], ref["acl_hit"])
 
 
 def test_acl_tuple_lookup_api(eng):

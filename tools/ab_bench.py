@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""In-process A/B timing of kernel variants (different library builds and/or tunings) on the same resident data,
+interleaved over rounds so device clock and thermal drift hit every variant alike (cdna_hip_programming.md §5.4
+rule 24).  Prints median / min kernel time and step time per variant.
+
+  python tools/ab_bench.py --config C1 --variant base=packet-process-engine_amd/libppe_hip.so \
+      --variant b512=packet-process-engine_amd/libppe_hip.so:block=512
+"""
+import argparse
+import ctypes as C
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "packet-process-engine_amd"), str(ROOT / "oracle")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from ppe import Engine, abi, synth  # noqa: E402
+
+NOW = 1_700_000_000
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C1")
+    ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--stride", type=int, default=64)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--nbufs", type=int, default=4)
+    ap.add_argument("--binth", type=int, default=0)
+    ap.add_argument("--variant", action="append", required=True, help="name=libpath[:key=val,...]")
+    ap.add_argument("--check", action="store_true", help="compare every variant's outputs with the first")
+    args = ap.parse_args()
+    if args.binth:
+        import os
+        os.environ["PPE_BINTH"] = str(args.binth)
+
+    c = synth.CONFIGS[args.config]
+    n = args.n or c["n"]
+    rules = synth.make_rules(c["rules"])
+    dev = torch.device("cuda:0")
+    bufs = []
+    for b in range(args.nbufs):
+        pk = synth.make_packets(n, rules, seed=synth.SEED + 1 + 7919 * b, kind=c["kind"], stride=args.stride)
+        hdr = torch.from_numpy(pk["hdr"]).to(dev)
+        lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
+        outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(5)] + \
+               [torch.empty((n + 63) // 64, dtype=torch.int32, device=dev)]
+        bufs.append((hdr, lens, outs))
+    libs = {}
+    variants = []
+    for spec in args.variant:
+        name, rest = spec.split("=", 1)
+        path, _, kv = rest.partition(":")
+        path = str(Path(path).resolve())
+        if path not in libs:
+            libs[path] = abi.load_variant(path)
+        eng = Engine(0, lib=libs[path])
+        eng.commit(rules, default_action=1)
+        if kv:
+            eng.tuning(**{k: int(v) for k, v in (x.split("=") for x in kv.split(","))})
+        calls = []
+        for hdr, lens, outs in bufs:
+            bb = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, args.stride)
+            rr = abi.Result(*(o.data_ptr() for o in outs), None)
+            calls.append((bb, rr))
+        variants.append(dict(name=name, eng=eng, calls=calls, kern=[], step=[]))
+    cfg = Engine.cfg(now_seconds=NOW)
+    stream = torch.cuda.current_stream(dev)
+    sp = C.c_void_p(stream.cuda_stream)
+
+    def run(v, steps, timed):
+        fn, ctx = v["eng"].lib.ppe_classify, v["eng"].ctx
+        if timed:
+            v["eng"].timing(True)
+            v["eng"].timing_read(reset=True)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for i in range(steps):
+            bb, rr = v["calls"][i % len(v["calls"])]
+            assert fn(ctx, C.byref(bb), C.byref(rr), C.byref(cfg), sp) == 0
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if timed:
+            kms, nl = v["eng"].timing_read(reset=True)
+            v["eng"].timing(False)
+            v["kern"].append(kms / nl * 1e3)
+            v["step"].append(e0.elapsed_time(e1) / steps * 1e3)
+
+    ref = None
+    for v in variants:
+        run(v, 3, False)
+        if args.check:
+            got = [o.cpu().numpy().copy() for o in bufs[0][2]]
+            if ref is None:
+                ref = got
+            else:
+                same = all(np.array_equal(a, b) for a, b in zip(ref[:3], got[:3]))
+                print(f"{v['name']}: outputs {'identical' if same else 'DIFFER'} to {variants[0]['name']}")
+    for r in range(args.rounds):
+        order = variants[r % len(variants):] + variants[:r % len(variants)]
+        for v in order:
+            run(v, args.steps, True)
+    res = {}
+    for v in variants:
+        k, s = v["kern"], v["step"]
+        res[v["name"]] = {"kern_med_us": round(statistics.median(k), 3), "kern_min_us": round(min(k), 3),
+                          "step_med_us": round(statistics.median(s), 3), "mpps_med": round(n / statistics.median(s), 1),
+                          "tuning": v["eng"].tuning(), "launch": v["eng"].launch_info()}
+        print(f"{v['name']:>12s}: kernel med {res[v['name']]['kern_med_us']:8.3f} us  min {min(k):8.3f}  "
+              f"step med {statistics.median(s):8.3f} us  ({n / statistics.median(s):9.1f} Mpps)  "
+              f"{res[v['name']]['launch']}")
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
