@@ -200,24 +200,24 @@ int  ppe_timing_read(ppe_ctx_t *ctx, double *total_ms, uint32_t *launches, int r
 int  ppe_acl_image(ppe_ctx_t *ctx, uint32_t *words, uint32_t *n_words);
 
 /* Launch tuning of the classify kernel for this context.  Defaults come from the fastest measured variant (and the
- * PPE_BLOCK / PPE_BLOCKS_PER_CU / PPE_PREFETCH / PPE_LDS_IMG environment variables); 0 = automatic. */
+ * PPE_BLOCK / PPE_BLOCKS_PER_CU / PPE_PIPELINE / PPE_LDS_IMG environment variables); 0 = automatic. */
 typedef struct {
     uint32_t block;          /* workgroup size 256, 512 or 1024; 0 = chosen per classifier image   */
-    uint32_t blocks_per_cu;  /* persistent-grid workgroups per CU; 0 = occupancy API              */
-    uint32_t prefetch;       /* reserved, must be 0 (register prefetch measured slower)            */
+    uint32_t blocks_per_cu;  /* workgroups per CU (<= 32); 0 = resident count from the occupancy API */
+    uint32_t pipeline;       /* LDS-DMA next-tile packet pipeline: 0 = automatic, 1 = off, 2 = on  */
     uint32_t lds_image;      /* 1 = stage the image (or its top) in LDS, 0 = read it from global   */
 } ppe_tuning_t;
 int  ppe_set_tuning(ppe_ctx_t *ctx, const ppe_tuning_t *t);
 int  ppe_get_tuning(ppe_ctx_t *ctx, ppe_tuning_t *t);
 
-/* Launch geometry in use (for profiling notes). */
-int  ppe_launch_info(ppe_ctx_t *ctx, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes);
+/* Launch geometry in use (for profiling notes).  variant = image mode (0 global, 1 LDS, 2 split) | pipeline << 4. */
+int  ppe_launch_info(ppe_ctx_t *ctx, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes, uint32_t *variant);
 
 /* Human-readable last error of this context (static storage of the ctx). */
 const char *ppe_last_error(ppe_ctx_t *ctx);
 
 /* Host-side classifier compiler (no device needed): rule list → image words (ppe_image.h layout, malloc'd;
- * free with ppe_acl_free_image).  binth = max rules in a leaf list before splitting (0 → default 4). */
+ * free with ppe_acl_free_image).  binth = max rules in a leaf list before splitting (0 → default 1). */
 int  ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
                          uint32_t default_action, uint32_t binth, uint32_t **words, uint32_t *n_words,
                          ppe_acl_stats_t *stats);

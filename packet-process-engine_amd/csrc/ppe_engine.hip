@@ -25,7 +25,10 @@ namespace {
 
 constexpr int kSlotSets = 4;      // set 0: ppe_classify; 1..3: host pipeline streams
 constexpr int kHostStreams = 3;
-constexpr uint32_t kMaxBlocksPerCU = 8;
+#ifndef PPE_PIPE_DEFAULT
+#define PPE_PIPE_DEFAULT 1
+#endif
+constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 
 struct HostStage {
     hipStream_t s = nullptr;
@@ -95,31 +98,39 @@ ppe_tuning_t default_tuning() {
     t.block = (uint32_t)(b == 256 || b == 512 || b == 1024 ? b : 0);  // 0 = chosen per image
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
-    t.prefetch = 0;
+    const int pl = env_int("PPE_PIPELINE", 0);
+    t.pipeline = pl == 1 || pl == 2 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     return t;
 }
 
-// How the classify kernel holds the classifier image (see IMG_* in ppe_kernels.hip).
+// How the classify kernel holds the classifier image (see IMG_* in ppe_kernels.hip) and whether it runs the LDS-DMA
+// packet pipeline.
 struct StagePlan {
     int mode;            // 0 global, 1 whole image in LDS, 2 prefix in LDS
+    int pipe;            // 1 = LDS-DMA next-tile pipeline
     uint32_t block;
     uint32_t lds_words, lds_nodes, leaf_lds;
 };
 
-StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
-    StagePlan p = {0, c->tune.block ? c->tune.block : 256u, 0, 0, 0};
+// LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves): 160 KiB shared, minus
+// the counters, the 1-KB rounding of the staged image and the pipeline's per-wave packet slots
+uint32_t image_budget(uint32_t block, bool pipe) {
+    const uint32_t per_wg = (160u * 1024u) / (2048u / block);
+    const uint32_t fixed = 1152u + (pipe ? ppe_classify_pipe_lds((int)block) : 0u);
+    return per_wg > fixed ? std::min<uint32_t>(PPE_LDS_IMG_MAX, per_wg - fixed) : 0u;
+}
+
+StagePlan stage_plan_for(const ppe_ctx *c, const std::vector<uint32_t> &img, bool pipe) {
     const uint32_t words = (uint32_t)img.size(), bytes = words * 4u;
-    if (!c->tune.lds_image) return p;
-    if (bytes <= PPE_LDS_IMG_SMALL && (c->tune.block == 0 || c->tune.block == 256)) {
-        p.mode = 1;  // small image: 256-thread workgroups, 8 per CU, each with its own copy
-        p.block = 256;
-        p.lds_words = words;
+    StagePlan p = {0, pipe ? 1 : 0, c->tune.block ? c->tune.block : 1024u, 0, 0, 0};
+    if (!c->tune.lds_image) {
+        if (!c->tune.block && !pipe) p.block = 256;
         return p;
     }
-    p.block = c->tune.block ? c->tune.block : 1024u;
-    // LDS per workgroup when the CU holds 2048 / block workgroups (32 waves), minus counters and 1-KB rounding
-    const uint32_t budget = std::min<uint32_t>(PPE_LDS_IMG_MAX, (160u * 1024u) / (2048u / p.block) - 1152u);
+    // without the pipeline a small image goes with 256-thread workgroups (8 per CU, each with its own copy)
+    if (!c->tune.block && !pipe && bytes <= image_budget(256, false)) p.block = 256;
+    const uint32_t budget = image_budget(p.block, pipe);
     const uint32_t off_rules = img[PPE_IMG_W_OFFRULES], n_nodes = img[PPE_IMG_W_NNODES];
     if (bytes <= budget) {
         p.mode = 1;
@@ -129,7 +140,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
         p.lds_words = off_rules;
         p.lds_nodes = n_nodes;
         p.leaf_lds = 1;
-    } else {  // the top of the tree (BFS order) fills the budget
+    } else if (budget >= 4u * (PPE_IMG_HDR_WORDS + 2u * 64u)) {  // the top of the tree (BFS order) fills the budget
         p.mode = 2;
         p.lds_nodes = std::min(n_nodes, (budget / 4u - PPE_IMG_HDR_WORDS) / 2u);
         p.lds_words = PPE_IMG_HDR_WORDS + 2u * p.lds_nodes;
@@ -138,16 +149,25 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
     return p;
 }
 
+// The LDS-DMA pipeline runs only with the whole image in LDS (see PPE_DISPATCH); when the image with the pipeline's
+// slots does not fit, the plan falls back to the non-pipelined kernel.
+StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
+    const bool pipe = c->tune.pipeline == 2 || (c->tune.pipeline == 0 && PPE_PIPE_DEFAULT);
+    if (pipe && c->tune.lds_image) {
+        const StagePlan p = stage_plan_for(c, img, true);
+        if (p.mode == 1) return p;
+    }
+    return stage_plan_for(c, img, false);
+}
+
 // Resident workgroups per CU: the occupancy API's answer (register and LDS limits) unless the tuning fixes it.
 // The persistent grid is CUs × this, so no workgroup waits for a second round.
 uint32_t blocks_per_cu(const ppe_ctx *c, const StagePlan &p) {
     const uint32_t cap = kMaxBlocksPerCU * 256u / p.block;
-    const uint32_t lds_fit =
-        p.mode ? (160u * 1024u) / (128u + ((p.lds_words * 4u + 1023u) & ~1023u)) : cap;
-    if (c->tune.blocks_per_cu) return std::max(1u, std::min(c->tune.blocks_per_cu, std::min(cap, lds_fit)));
-    const int occ = ppe_classify_occupancy(p.lds_words, p.mode, (int)p.block);
+    if (c->tune.blocks_per_cu) return std::max(1u, std::min(c->tune.blocks_per_cu, cap));  // may exceed residency
+    const int occ = ppe_classify_occupancy(p.lds_words, p.mode, p.pipe, (int)p.block);
     if (occ > 0) return std::min<uint32_t>((uint32_t)occ, cap);
-    return std::max(1u, std::min(cap, lds_fit));
+    return 1u;
 }
 
 int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const ppe_acl_stats_t *st) {
@@ -204,6 +224,9 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
     a.lds_words = plan.lds_words;
     a.lds_nodes = plan.lds_nodes;
     a.leaf_lds = plan.leaf_lds;
+    a.off_leaf = c->h_img[r][PPE_IMG_W_OFFLEAF];
+    a.off_rules = c->h_img[r][PPE_IMG_W_OFFRULES];
+    a.off_resid = c->h_img[r][PPE_IMG_W_OFFRESID];
     a.cslots = c->d_cslots + (size_t)slot_set * c->max_grid * PPE_CSLOT_WORDS;
 
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -219,7 +242,8 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
         e1 = c->ev[c->ev_used + 1];
         c->ev_used += 2;
     }
-    const int rc = ppe_launch_classify(&a, grid, plan.mode, (int)plan.block, (void *)s, (void *)e0, (void *)e1);
+    const int rc =
+        ppe_launch_classify(&a, grid, plan.mode, plan.pipe, (int)plan.block, (void *)s, (void *)e0, (void *)e1);
     if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
     c->img_used[r] = true;
     return PPE_OK;
@@ -559,10 +583,10 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->prefetch) return fail(c, PPE_EINVAL, "register prefetch is not built (measured slower; DESIGN.md)");
-    if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 8");
+    if (t->pipeline > 2) return fail(c, PPE_EINVAL, "pipeline must be 0 (auto), 1 (off) or 2 (on)");
+    if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     c->tune = *t;
-    c->tune.prefetch = t->prefetch ? 1u : 0u;
+    c->tune.pipeline = t->pipeline;
     c->tune.lds_image = t->lds_image ? 1u : 0u;
     return PPE_OK;
 }
@@ -581,12 +605,15 @@ int ppe_acl_image(ppe_ctx_t *c, uint32_t *words, uint32_t *n_words) {
     return PPE_OK;
 }
 
-int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes) {
+int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes, uint32_t *variant) {
     if (!c) return PPE_EINVAL;
     const StagePlan plan = stage_plan(c, c->h_img[c->running]);
     if (grid) *grid = std::min(c->n_cu * blocks_per_cu(c, plan), c->max_grid);
     if (block) *block = plan.block;
-    if (lds_bytes) *lds_bytes = 128u + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u);
+    if (lds_bytes)
+        *lds_bytes = 128u + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u) +
+                     (plan.pipe ? ppe_classify_pipe_lds((int)plan.block) : 0u);
+    if (variant) *variant = (uint32_t)plan.mode | ((uint32_t)plan.pipe << 4);
     return PPE_OK;
 }
 

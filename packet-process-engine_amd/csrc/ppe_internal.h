@@ -28,6 +28,8 @@ struct ppe_kargs {
     uint32_t lds_words;       /* image words staged in LDS (IMG_LDS: all; IMG_SPLIT: header + top nodes [+ leaves]) */
     uint32_t lds_nodes;       /* IMG_SPLIT: nodes [0, lds_nodes) are in LDS                                         */
     uint32_t leaf_lds;        /* IMG_SPLIT: the leaf lists are in LDS too                                             */
+    uint32_t off_leaf, off_rules, off_resid; /* image section offsets (words), from the image header: kernel arguments
+                                                so the loop holds no vector load the LDS-DMA pipeline would wait on */
     unsigned long long *cslots; /* [grid][PPE_CSLOT_WORDS] counter slots, one per workgroup */
 };
 
@@ -56,9 +58,10 @@ extern "C" {
 #endif
 /* Launch the classify kernel. grid = workgroups (persistent), lds_img = stage image in LDS. Returns hipError_t. */
 /* mode: 0 image in global memory, 1 whole image in LDS, 2 prefix in LDS (see ppe_kernels.hip) */
-int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int block, void *stream, void *ev_start,
-                        void *ev_stop);
-int ppe_classify_occupancy(uint32_t lds_words, int mode, int block);
+int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, void *stream,
+                        void *ev_start, void *ev_stop);
+int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block);
+uint32_t ppe_classify_pipe_lds(int block);
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
 #ifdef __cplusplus
 }

@@ -25,11 +25,11 @@
 #ifndef PPE_ABLATE
 #define PPE_ABLATE 0
 #endif
-#ifndef PPE_HOIST  // experiment switch: request the first tile before the image staging (measured 1 µs slower)
-#define PPE_HOIST 0
-#endif
 
 namespace {
+
+typedef __attribute__((address_space(1))) const void *gptr_t;
+typedef __attribute__((address_space(3))) void *lptr_t;
 
 __device__ __forceinline__ uint32_t be16_lo(uint32_t w) { return ((w & 0xffu) << 8) | ((w >> 8) & 0xffu); }
 __device__ __forceinline__ uint32_t be16_hi(uint32_t w) { return ((w >> 8) & 0xff00u) | (w >> 24); }
@@ -80,6 +80,58 @@ __device__ __forceinline__ uint32_t reason_counter(uint32_t st) {
     return (uint32_t)(((lo ? K0 : K1) >> (5u * (lo ? st : st - 12u))) & 31u);
 }
 
+// Synchronous global loads for the rare paths (IPv4 options, time-window rules).  Inline asm with its own wait: the
+// compiler then tracks no pending VMEM result across the tile loop, so it never puts a conservative vmcnt(0) -
+// which would also wait for the next tile's in-flight LDS-DMA - at the top of the loop.
+__device__ __forceinline__ void ld_l4_sync(const uint8_t *q, uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
+    asm volatile(
+        "global_load_ushort %0, %4, off\n\t"
+        "global_load_ushort %1, %4, off offset:2\n\t"
+        "global_load_ushort %2, %4, off offset:4\n\t"
+        "global_load_ushort %3, %4, off offset:12\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+        : "v"(q)
+        : "memory");
+}
+__device__ __forceinline__ void ld_mac_sync(const uint8_t *q, uint32_t &a, uint32_t &b, uint32_t &c) {
+    typedef uint32_t v3u __attribute__((ext_vector_type(3)));
+    v3u v;
+    asm volatile("global_load_dwordx3 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(q) : "memory");
+    a = v.x;
+    b = v.y;
+    c = v.z;
+}
+__device__ __forceinline__ uint64_t ld_u64_sync(const uint64_t *q) {
+    uint64_t v;
+    asm volatile("global_load_dwordx2 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(q) : "memory");
+    return v;
+}
+
+// Where a residual MAC rule gets the packet's MACs: re-read from the header window (classify kernel: rare path, keeps
+// the MACs out of registers during the tree walk) or given by value (tuple kernel).
+struct MacFromWindow {
+    const uint8_t *hdr;
+    uint32_t p, stride;
+    __device__ __forceinline__ void get(uint32_t &dlo, uint32_t &dhi, uint32_t &slo, uint32_t &shi) const {
+        uint32_t w0, w1, w2;  // dmac = bytes 0-5, smac = bytes 6-11 (EthernetHdr, decode-ethernet.h:23-27)
+        ld_mac_sync(hdr + (size_t)p * stride, w0, w1, w2);
+        dlo = w0;
+        dhi = w1 & 0xffffu;
+        slo = (w1 >> 16) | (w2 << 16);
+        shi = w2 >> 16;
+    }
+};
+struct MacValues {
+    uint32_t dlo, dhi, slo, shi;
+    __device__ __forceinline__ void get(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) const {
+        a = dlo;
+        b = dhi;
+        c = slo;
+        d = shi;
+    }
+};
+
 struct Dec {
     uint32_t st, flags, cb;
     uint32_t sip, dip, sport, dport, proto, paylen;
@@ -89,7 +141,7 @@ struct Dec {
 // chosen by applying the checks in REVERSE order of the reference's control flow, so the first failing check
 // (the one the reference returns on) wins.  w[0..15] = first 64 bytes (little-endian dwords); row = the packet's
 // window in global memory (read only for L4 headers behind IPv4 options).
-__device__ __forceinline__ Dec decode(const uint32_t (&w)[16], uint32_t len32, const uint8_t *row, uint32_t stride,
+__device__ __forceinline__ Dec decode(const uint32_t (&w)[16], uint32_t len32, const uint8_t *hdr, uint32_t p, uint32_t stride,
                                       uint32_t syn_check) {
     Dec k;
     const uint32_t len = len32 & 0xffffu;  // Decode passes (uint16_t)pkt_totallen, decode.c:22
@@ -132,10 +184,11 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[16], uint32_t len32, c
     uint32_t sport = be16_hi(D[5]), dport = be16_lo(D[6]);
     uint32_t x = is_tcp ? (D[8] >> 16) : be16_hi(D[6]);  // TCP: offx2 | flags << 8;  UDP: uh_len
     if (l4_in && !fast && !win_short) {  // IPv4 options: L4 header at a data-dependent offset
-        const uint16_t *q = (const uint16_t *)(row + l4off);
-        sport = bswap16(q[0]);
-        dport = bswap16(q[1]);
-        x = is_tcp ? (uint32_t)q[6] : bswap16(q[2]);
+        uint32_t h0, h1, h2, h6;
+        ld_l4_sync(hdr + (size_t)p * stride + l4off, h0, h1, h2, h6);
+        sport = bswap16(h0);
+        dport = bswap16(h1);
+        x = is_tcp ? h6 : bswap16(h2);
     }
     // ---- UDP: dataplane/src/decode/decode-udp.c:16-49;  TCP: dataplane/src/decode/decode-tcp.c:135-190 ----
     const uint32_t thl = ((x & 0xffu) >> 4) << 2;  // uint8_t hlen, decode-tcp.c:148
@@ -205,10 +258,10 @@ __device__ __forceinline__ uint32_t node_key(uint32_t d, uint32_t sip, uint32_t 
 
 // Scan one leaf's candidate list in priority order; the first rule that matches wins (lowest index).  `lf`, `rules`
 // and `resid` may each point into LDS or global memory (address space inferred after inlining).
+template <class Mac>
 __device__ __forceinline__ void leaf_scan(uint2 nd, const uint32_t *__restrict__ lf, const uint32_t *__restrict__ rules,
                                           const uint32_t *__restrict__ resid, uint32_t sip, uint32_t dip, uint32_t sport,
-                                          uint32_t dport, uint32_t proto, uint32_t dmac_lo, uint32_t dmac_hi,
-                                          uint32_t smac_lo, uint32_t smac_hi, const uint64_t *tsp, uint32_t p,
+                                          uint32_t dport, uint32_t proto, const Mac &mac, const uint64_t *tsp, uint32_t p,
                                           uint64_t now, int32_t &hit, uint32_t &action) {
     const uint32_t cnt = nd.y >> 3;
 #pragma unroll 1
@@ -227,10 +280,14 @@ __device__ __forceinline__ void leaf_scan(uint2 nd, const uint32_t *__restrict__
             if (m && rs) {
                 const uint4 *xp = (const uint4 *)(resid + 8u * slot);
                 const uint4 c = xp[0], t = xp[1];
-                if (rs & PPE_RESID_DMAC) m = m && c.x == dmac_lo && c.y == dmac_hi;
-                if (rs & PPE_RESID_SMAC) m = m && c.z == smac_lo && c.w == smac_hi;
+                if (rs & (PPE_RESID_DMAC | PPE_RESID_SMAC)) {
+                    uint32_t dmac_lo, dmac_hi, smac_lo, smac_hi;
+                    mac.get(dmac_lo, dmac_hi, smac_lo, smac_hi);
+                    if (rs & PPE_RESID_DMAC) m = m && c.x == dmac_lo && c.y == dmac_hi;
+                    if (rs & PPE_RESID_SMAC) m = m && c.z == smac_lo && c.w == smac_hi;
+                }
                 if (rs & PPE_RESID_TIME) {  // the packet timestamp is only fetched for time-window rules
-                    const uint64_t ts = tsp ? tsp[p] : now;
+                    const uint64_t ts = tsp ? ld_u64_sync(tsp + p) : now;
                     const uint64_t t0 = (uint64_t)t.x | ((uint64_t)t.y << 32);
                     const uint64_t t1 = (uint64_t)t.z | ((uint64_t)t.w << 32);
                     m = m && ts >= t0 && ts <= t1;
@@ -248,13 +305,12 @@ __device__ __forceinline__ void leaf_scan(uint2 nd, const uint32_t *__restrict__
 // First-match decision-tree lookup over the classifier image (ppe_image.h).  The 5-tuple arrives as scalars (not
 // struct fields): a select between fields of an in-memory struct is folded into a dynamically indexed load, which
 // sends the whole struct to scratch.
-template <int MODE>
+template <int MODE, class Mac>
 __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ gimg, const uint32_t *__restrict__ limg,
                                            uint32_t lds_nodes, uint32_t leaf_lds, uint32_t off_leaf,
                                            uint32_t off_rules, uint32_t off_resid, uint32_t default_action,
                                            const uint32_t sip, const uint32_t dip, const uint32_t sport,
-                                           const uint32_t dport, const uint32_t proto, uint32_t dmac_lo,
-                                           uint32_t dmac_hi, uint32_t smac_lo, uint32_t smac_hi,
+                                           const uint32_t dport, const uint32_t proto, const Mac &mac,
                                            const uint64_t *tsp, uint32_t p, uint64_t now, int32_t &hit,
                                            uint32_t &action) {
     const uint2 *gn = (const uint2 *)(gimg + PPE_IMG_HDR_WORDS);
@@ -287,13 +343,13 @@ __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ gimg, co
     if (!NODE_IS_LEAF(nd)) return;  // unreachable for a builder-made image
     if (MODE == IMG_LDS)
         leaf_scan(nd, limg + off_leaf + nd.x, limg + off_rules, limg + off_resid, sip, dip, sport, dport, proto,
-                  dmac_lo, dmac_hi, smac_lo, smac_hi, tsp, p, now, hit, action);
+                  mac, tsp, p, now, hit, action);
     else if (MODE == IMG_SPLIT && leaf_lds)
         leaf_scan(nd, limg + off_leaf + nd.x, gimg + off_rules, gimg + off_resid, sip, dip, sport, dport, proto,
-                  dmac_lo, dmac_hi, smac_lo, smac_hi, tsp, p, now, hit, action);
+                  mac, tsp, p, now, hit, action);
     else
         leaf_scan(nd, gimg + off_leaf + nd.x, gimg + off_rules, gimg + off_resid, sip, dip, sport, dport, proto,
-                  dmac_lo, dmac_hi, smac_lo, smac_hi, tsp, p, now, hit, action);
+                  mac, tsp, p, now, hit, action);
 }
 
 // Copy the classifier image into LDS with LDS-DMA (global_load_lds_dwordx4): every 1-KB piece of the image is in
@@ -301,8 +357,6 @@ __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ gimg, co
 // LDS region is padded to a multiple of 1 KB and the (clamped) tail lanes write into the padding.
 template <int BLOCK>
 __device__ __forceinline__ void stage_image(const uint32_t *img, uint32_t *lds, uint32_t words, uint32_t tid) {
-    typedef __attribute__((address_space(1))) const void *gptr_t;
-    typedef __attribute__((address_space(3))) void *lptr_t;
     const uint32_t n4 = (words + 3u) >> 2;
     const uint32_t lane = tid & 63u;
     for (uint32_t base = (tid >> 6) * 64u; base < n4; base += BLOCK) {
@@ -312,32 +366,146 @@ __device__ __forceinline__ void stage_image(const uint32_t *img, uint32_t *lds, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int MODE, bool PREFETCH, int BLOCK>
+// LDS-DMA packet pipeline (PIPE): each wave owns one 3.5-KB LDS slot.  While tile t is classified from registers,
+// tile t+1 is already on its way from HBM into the slot via global_load_lds (no VGPRs held, no wait), so the next
+// HBM fetch overlaps this tile's decode / tree walk.  Slot layout (bytes): [0, 3072) the first 48 B of each of the 64
+// windows (48-B rows: ds_read_b128 per lane is bank-conflict free), [3072, 3328) bytes 48..51 of each window,
+// [3328, 3584) the 64 wire lengths.  Bytes 52..63 are never needed on the fast path (hlen == 20); IPv4-options
+// packets read their L4 header from the window in global memory, as without the pipeline.
+#define PIPE_SLOT_BYTES 3584u
+#define PIPE_W12_OFF 3072u
+#define PIPE_LEN_OFF 3328u
+
+// Issue the five DMA ops of tile `t` into the slot at LDS byte address `slot` (wave-uniform).  Lane l of op k (< 3)
+// fetches 16-B chunk (64k+l) % 3 of packet (64k+l) / 3; op 3 fetches bytes 48..51, op 4 the length.  In asm, like
+// pipe_read: compiler-visible LDS-DMA makes the compiler (a) hoist the per-lane 64-bit addresses out of the tile loop
+// (spilled to scratch, and every scratch reload then waits for the DMA in flight) and (b) track the DMA as pending
+// VMEM.  Full tiles use the saddr form (uniform 64-bit tile base + 32-bit lane offset); M0 is saved and restored
+// because the compiler reserves it.  No instruction offsets: an LDS-DMA op adds its offset to the LDS address too.
+__device__ __forceinline__ uint32_t launder(uint32_t x) {  // opaque copy: stops loop-invariant hoisting
+    uint32_t y;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+    return y;
+}
+
+__device__ __forceinline__ void pipe_issue(const ppe_kargs &a, uint32_t t, uint32_t slot, uint32_t lane_) {
+    const uint32_t base = t << 6;
+    const uint32_t lane = launder(lane_);
+    uint32_t off[3];
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+        const uint32_t idx = 64u * k + lane;
+        const uint32_t pk = (idx * 0xAAABu) >> 17;  // idx / 3 for idx < 192
+        off[k] = pk * a.stride + 16u * (idx - 3u * pk);
+    }
+    uint32_t m0save;
+    if (base + 64u <= a.n) {  // full tile
+        const uint8_t *tb = a.hdr + (size_t)base * a.stride;
+        const uint32_t *lb = a.len + base;
+        asm volatile(
+            "s_mov_b32 %[sv], m0\n\t"
+            "s_mov_b32 m0, %[s0]\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %[o0], %[tb]\n\t"
+            "s_add_u32 m0, %[s0], 0x400\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %[o1], %[tb]\n\t"
+            "s_add_u32 m0, %[s0], 0x800\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %[o2], %[tb]\n\t"
+            "s_add_u32 m0, %[s0], 0xc00\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dword %[o3], %[tb]\n\t"
+            "s_add_u32 m0, %[s0], 0xd00\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dword %[ol], %[lb]\n\t"
+            "s_mov_b32 m0, %[sv]"
+            : [sv] "=&s"(m0save)
+            : [s0] "s"(slot), [o0] "v"(off[0]), [o1] "v"(off[1]), [o2] "v"(off[2]), [o3] "v"(lane * a.stride + 48u),
+              [ol] "v"(lane * 4u), [tb] "s"(tb), [lb] "s"(lb)
+            : "memory");
+        return;
+    }
+    // the batch's partial last tile: clamp to the last packet, 64-bit per-lane addresses
+    const uint32_t last = a.n - 1u;
+    const uint8_t *g[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+        const uint32_t idx = 64u * k + lane;
+        const uint32_t pk = (idx * 0xAAABu) >> 17;
+        g[k] = a.hdr + (size_t)min(base + pk, last) * a.stride + (off[k] - pk * a.stride);
+    }
+    const uint32_t p = min(base + lane, last);
+    g[3] = a.hdr + (size_t)p * a.stride + 48u;
+    const uint32_t *gl = a.len + p;
+    asm volatile(
+        "s_mov_b32 %[sv], m0\n\t"
+        "s_mov_b32 m0, %[s0]\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %[g0], off\n\t"
+        "s_add_u32 m0, %[s0], 0x400\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %[g1], off\n\t"
+        "s_add_u32 m0, %[s0], 0x800\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %[g2], off\n\t"
+        "s_add_u32 m0, %[s0], 0xc00\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %[g3], off\n\t"
+        "s_add_u32 m0, %[s0], 0xd00\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %[gl], off\n\t"
+        "s_mov_b32 m0, %[sv]"
+        : [sv] "=&s"(m0save)
+        : [s0] "s"(slot), [g0] "v"(g[0]), [g1] "v"(g[1]), [g2] "v"(g[2]), [g3] "v"(g[3]), [gl] "v"(gl)
+        : "memory");
+}
+
+// Wait for every outstanding VMEM op of this wave (the slot's DMA, issued one tile earlier, and the previous tile's
+// stores), then read this lane's packet from the slot.  In asm: the compiler cannot see which LDS bytes the DMA
+// writes and would otherwise wait for it before every LDS access to the slot.
+__device__ __forceinline__ void pipe_read(uint32_t slot, uint32_t lane, uint4 &q0, uint4 &q1, uint4 &q2, uint32_t &w12,
+                                          uint32_t &len) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u r0, r1, r2;
+    const uint32_t row = slot + 48u * lane, col = slot + 4u * lane;
+    asm volatile(
+        "s_waitcnt vmcnt(0)\n\t"
+        "ds_read_b128 %0, %5\n\t"
+        "ds_read_b128 %1, %5 offset:16\n\t"
+        "ds_read_b128 %2, %5 offset:32\n\t"
+        "ds_read_b32 %3, %6 offset:3072\n\t"
+        "ds_read_b32 %4, %6 offset:3328\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(w12), "=&v"(len)
+        : "v"(row), "v"(col)
+        : "memory");
+    q0 = make_uint4(r0.x, r0.y, r0.z, r0.w);
+    q1 = make_uint4(r1.x, r1.y, r1.z, r1.w);
+    q2 = make_uint4(r2.x, r2.y, r2.z, r2.w);
+}
+
+template <int MODE, bool PIPE, int BLOCK>
 __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    // a separate LDS object from the image: the compiler then knows the slot DMA never aliases image reads
+    __shared__ __attribute__((aligned(16))) uint32_t ring[PIPE ? BLOCK / 64 : 1][PIPE ? PIPE_SLOT_BYTES / 4 : 1];
     uint32_t *lcnt = smem;       // [32] per-reason counters of this workgroup
     uint32_t *limg = smem + 32;  // staged classifier image
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t ntiles = (a.n + 63u) >> 6;
-    uint32_t tile = blockIdx.x * (BLOCK / 64) + (tid >> 6);
-    // PPE_HOIST: request the first tile's header window before the image staging (A/B: slower, kept off)
-    uint4 q0, q1, q2, q3;
-    uint32_t qlen;
-    if (PPE_HOIST || PREFETCH) {
-        const uint32_t p = min((tile << 6) + lane, a.n - 1u);  // clamped: loads are unconditional (no phi → no wait)
-        const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)p * a.stride);
-        q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
-        qlen = a.len[p];
-    }
+    const uint32_t stride_waves = gridDim.x * (BLOCK / 64);
+    uint32_t tile = blockIdx.x * (BLOCK / 64) + wv;
+    const uint32_t slot = PIPE ? (uint32_t)(uintptr_t)(lptr_t)&ring[wv][0] : 0u;
+    if (PIPE && tile < ntiles) pipe_issue(a, tile, slot, lane);  // in flight during the image staging
+
     if (tid < 32) lcnt[tid] = 0;
     if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img, limg, a.lds_words, tid);
     __syncthreads();
-    const uint32_t off_leaf = a.img[PPE_IMG_W_OFFLEAF];
-    const uint32_t off_rules = a.img[PPE_IMG_W_OFFRULES];
-    const uint32_t off_resid = a.img[PPE_IMG_W_OFFRESID];
+    const uint32_t off_leaf = a.off_leaf, off_rules = a.off_rules, off_resid = a.off_resid;
 
-    const uint32_t stride_waves = gridDim.x * (BLOCK / 64);
     // action of each terminal status, 2 bits per status: FW for ACL_FW, PUNT for fragments / short windows, the
     // configured action for unsupported protocols (Decode_unsupport_proto_handle, decode.c:31-45), else DROP
     uint64_t act_table = 0;
@@ -351,28 +519,27 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     }
     uint32_t my_cnt = 0;  // lane b (< PPE_C__COUNT) accumulates counter b of this wave
 
-    // PREFETCH: the next tile's window is loaded while the current one is classified; otherwise each tile is
-    // loaded at the top of its iteration (the first one above, before the staging)
-    for (bool first = true; tile < ntiles; tile += stride_waves, first = false) {
+    // current tile's window: bytes 0..51 (w[0..12]) and the wire length
+    uint4 q0, q1, q2;
+    uint32_t w12, qlen;
+    if (PIPE && tile < ntiles) {
+        pipe_read(slot, lane, q0, q1, q2, w12, qlen);
+        if (tile + stride_waves < ntiles) pipe_issue(a, tile + stride_waves, slot, lane);
+    }
+    for (; tile < ntiles; tile += stride_waves) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < a.n;
-        if (!PREFETCH && (!first || !PPE_HOIST)) {
+        if (!PIPE) {
             const uint32_t pc = min(p, a.n - 1u);
             const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)pc * a.stride);
-            q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
+            q0 = r4[0]; q1 = r4[1]; q2 = r4[2];
+            w12 = ((const uint32_t *)r4)[12];
             qlen = a.len[pc];
         }
         const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                                q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+                                q2.x, q2.y, q2.z, q2.w, w12, 0u, 0u, 0u};
         const uint32_t len = valid ? qlen : 0u;
-        if (PREFETCH) {
-            const uint32_t np = min(((tile + stride_waves) << 6) + lane, a.n - 1u);
-            const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)np * a.stride);
-            q0 = r4[0]; q1 = r4[1]; q2 = r4[2]; q3 = r4[3];
-            qlen = a.len[np];
-        }
-        const uint8_t *row = a.hdr + (size_t)p * a.stride;
-        Dec k = decode(w, len, row, a.stride, a.syn_check);
+        Dec k = decode(w, len, a.hdr, p, a.stride, a.syn_check);
 
         uint32_t fh = 0, act;
         int32_t hit = -1;
@@ -383,10 +550,9 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
         }
         if (!(PPE_ABLATE & 1) && valid && k.st == ST_ACL) {
             uint32_t rule_act;
-            // dmac = bytes 0-5, smac = bytes 6-11 (EthernetHdr, decode-ethernet.h:23-27)
+            const MacFromWindow mac = {a.hdr, p, a.stride};
             acl_lookup<MODE>(a.img, limg, a.lds_nodes, a.leaf_lds, off_leaf, off_rules, off_resid, a.default_action,
-                             k.sip, k.dip, k.sport, k.dport, k.proto, w[0], w[1] & 0xffffu,
-                             (w[1] >> 16) | (w[2] << 16), w[2] >> 16, a.ts, p, a.now, hit, rule_act);
+                             k.sip, k.dip, k.sport, k.dport, k.proto, mac, a.ts, p, a.now, hit, rule_act);
             const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
             k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
             k.flags |= PPE_F_ACL;
@@ -395,6 +561,10 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
         const uint32_t st = k.st;
         act = (uint32_t)(act_table >> (2u * st)) & 3u;
         k.cb |= act == PPE_ACT_FW ? CB(PPE_C_OUT_FW) : (act == PPE_ACT_DROP ? CB(PPE_C_OUT_DROP) : CB(PPE_C_OUT_PUNT));
+
+        // next tile: its DMA has had this whole tile's compute to land; take it into registers and start the one
+        // after (the stores below are issued after this wait, so it never waits on this tile's own stores)
+        if (PIPE && tile + stride_waves < ntiles) pipe_read(slot, lane, q0, q1, q2, w12, qlen);
 
         if (valid) {
             if (a.verdict) a.verdict[p] = st | (act << 8) | (k.flags << 16);
@@ -444,6 +614,9 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
             todo &= ~same;
             my_cnt += ((pat >> lane) & 1u) * (uint32_t)__popcll(same);
         }
+        // the slot was emptied by pipe_read above; refill it with the tile after next (issued here, where little
+        // is live, rather than right after the read)
+        if (PIPE && tile + 2u * stride_waves < ntiles) pipe_issue(a, tile + 2u * stride_waves, slot, lane);
     }
 
     if (lane < PPE_C__COUNT && my_cnt) atomicAdd(&lcnt[lane], my_cnt);
@@ -470,13 +643,13 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
         if (a.macs) m = ((const uint4 *)a.macs)[i];
         int32_t hit;
         uint32_t act;
+        const MacValues mac = {m.x, m.y, m.z, m.w};
         if (LDS_IMG)
             acl_lookup<IMG_LDS>(a.img, smem, 0, 0, off_leaf, off_rules, off_resid, a.default_action, t.x, t.y,
-                                t.z & 0xffffu, t.z >> 16, t.w & 0xffu, m.x, m.y, m.z, m.w, a.ts, i, a.now, hit, act);
+                                t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i, a.now, hit, act);
         else
             acl_lookup<IMG_GLOBAL>(a.img, smem, 0, 0, off_leaf, off_rules, off_resid, a.default_action, t.x, t.y,
-                                   t.z & 0xffffu, t.z >> 16, t.w & 0xffu, m.x, m.y, m.z, m.w, a.ts, i, a.now, hit,
-                                   act);
+                                   t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i, a.now, hit, act);
         if (a.hit) a.hit[i] = hit;
         if (a.action) a.action[i] = act;
     }
@@ -484,18 +657,18 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
 
 }  // namespace
 
-template <int M, int B>
+template <int M, bool P, int B>
 static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     // hipExtLaunchKernelGGL's events are the dispatch packet's own start/end timestamps (what rocprofv3 reports),
     // unlike hipEventRecord markers around the launch
-    hipExtLaunchKernelGGL((ppe_classify_kernel<M, false, B>), dim3(grid), dim3(B), shmem, s, e0, e1, 0, *a);
+    hipExtLaunchKernelGGL((ppe_classify_kernel<M, P, B>), dim3(grid), dim3(B), shmem, s, e0, e1, 0, *a);
     return (int)hipGetLastError();
 }
 
-template <int M, int B>
+template <int M, bool P, int B>
 static int occ_t(size_t shmem) {
     int nb = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, false, B>, B, shmem) == hipSuccess
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, P, B>, B, shmem) == hipSuccess
                ? nb : -1;
 }
 
@@ -504,24 +677,27 @@ static size_t classify_shmem(uint32_t lds_words, int mode) {
     return mode != IMG_GLOBAL ? base + (((size_t)lds_words * 4u + 1023u) & ~(size_t)1023u) : base;
 }
 
-#define PPE_DISPATCH(FN, ...)                                                                         \
-    do {                                                                                              \
-        if (mode == IMG_LDS) {                                                                        \
-            if (block == 1024) return FN<IMG_LDS, 1024>(__VA_ARGS__);                                 \
-            if (block == 512) return FN<IMG_LDS, 512>(__VA_ARGS__);                                   \
-            return FN<IMG_LDS, 256>(__VA_ARGS__);                                                     \
-        }                                                                                             \
-        if (mode == IMG_SPLIT) {                                                                      \
-            if (block == 1024) return FN<IMG_SPLIT, 1024>(__VA_ARGS__);                               \
-            if (block == 512) return FN<IMG_SPLIT, 512>(__VA_ARGS__);                                 \
-            return FN<IMG_SPLIT, 256>(__VA_ARGS__);                                                   \
-        }                                                                                             \
-        if (block == 1024) return FN<IMG_GLOBAL, 1024>(__VA_ARGS__);                                  \
-        if (block == 512) return FN<IMG_GLOBAL, 512>(__VA_ARGS__);                                    \
-        return FN<IMG_GLOBAL, 256>(__VA_ARGS__);                                                      \
+#define PPE_DISPATCH_B(FN, M, P, ...)                                \
+    do {                                                             \
+        if (block == 1024) return FN<M, P, 1024>(__VA_ARGS__);       \
+        if (block == 512) return FN<M, P, 512>(__VA_ARGS__);         \
+        return FN<M, P, 256>(__VA_ARGS__);                           \
+    } while (0)
+#define PPE_DISPATCH_P(FN, M, ...)                                   \
+    do {                                                             \
+        if (pipe) PPE_DISPATCH_B(FN, M, true, __VA_ARGS__);          \
+        PPE_DISPATCH_B(FN, M, false, __VA_ARGS__);                   \
+    } while (0)
+// the pipeline is built for the whole-image-in-LDS variant only: with tree nodes or rules read from global memory
+// every such load waits (in-order vmcnt) for the next tile's DMA, which defeats the overlap
+#define PPE_DISPATCH(FN, ...)                                        \
+    do {                                                             \
+        if (mode == IMG_LDS) PPE_DISPATCH_P(FN, IMG_LDS, __VA_ARGS__);     \
+        if (mode == IMG_SPLIT) PPE_DISPATCH_B(FN, IMG_SPLIT, false, __VA_ARGS__); \
+        PPE_DISPATCH_B(FN, IMG_GLOBAL, false, __VA_ARGS__);          \
     } while (0)
 
-extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, int block, void *stream,
+extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, void *stream,
                                    void *ev_start, void *ev_stop) {
     const size_t shmem = classify_shmem(a->lds_words, mode);
     hipStream_t s = (hipStream_t)stream;
@@ -530,10 +706,13 @@ extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, 
 }
 
 // resident workgroups per CU for the kernel variant (the persistent grid is sized to exactly fill the chip)
-extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int block) {
+extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block) {
     const size_t shmem = classify_shmem(lds_words, mode);
     PPE_DISPATCH(occ_t, shmem);
 }
+
+// static LDS of the pipelined kernel (the per-wave DMA slots), for the engine's LDS budget
+extern "C" uint32_t ppe_classify_pipe_lds(int block) { return (uint32_t)(block / 64) * PIPE_SLOT_BYTES; }
 
 extern "C" int ppe_launch_acl_tuples(const ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream) {
     if (lds_img) {

@@ -77,11 +77,11 @@ class Counters(C.Structure):
 
 
 class Tuning(C.Structure):
-    _fields_ = [("block", C.c_uint32), ("blocks_per_cu", C.c_uint32), ("prefetch", C.c_uint32),
+    _fields_ = [("block", C.c_uint32), ("blocks_per_cu", C.c_uint32), ("pipeline", C.c_uint32),
                 ("lds_image", C.c_uint32)]
 
-    def __init__(self, block=0, blocks_per_cu=0, prefetch=0, lds_image=1):
-        super().__init__(block, blocks_per_cu, prefetch, lds_image)
+    def __init__(self, block=0, blocks_per_cu=0, pipeline=0, lds_image=1):
+        super().__init__(block, blocks_per_cu, pipeline, lds_image)
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -159,7 +159,7 @@ def _open(p: Path, mode) -> C.CDLL:
         "ppe_timing_enable": ([vp, C.c_int], C.c_int),
         "ppe_timing_read": ([vp, C.POINTER(C.c_double), C.POINTER(u32), C.c_int], C.c_int),
         "ppe_acl_image": ([vp, vp, C.POINTER(u32)], C.c_int),
-        "ppe_launch_info": ([vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], C.c_int),
+        "ppe_launch_info": ([vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], C.c_int),
         "ppe_last_error": ([vp], C.c_char_p),
         "ppe_set_tuning": ([vp, C.POINTER(Tuning)], C.c_int),
         "ppe_get_tuning": ([vp, C.POINTER(Tuning)], C.c_int),

@@ -149,7 +149,7 @@ class Engine:
         return ms.value, n.value
 
     def tuning(self, **kw) -> dict:
-        """Read (and with keyword arguments, set) the launch tuning: block, blocks_per_cu, prefetch, lds_image."""
+        """Read (and with keyword arguments, set) the launch tuning: block, blocks_per_cu, pipeline, lds_image."""
         t = abi.Tuning()
         self._check(self.lib.ppe_get_tuning(self.ctx, C.byref(t)), "ppe_get_tuning")
         if kw:
@@ -159,9 +159,11 @@ class Engine:
         return t.as_dict()
 
     def launch_info(self) -> dict:
-        g, b, l = C.c_uint32(), C.c_uint32(), C.c_uint32()
-        self._check(self.lib.ppe_launch_info(self.ctx, C.byref(g), C.byref(b), C.byref(l)), "ppe_launch_info")
-        return {"grid": g.value, "block": b.value, "lds_bytes": l.value}
+        g, b, l, v = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32()
+        self._check(self.lib.ppe_launch_info(self.ctx, C.byref(g), C.byref(b), C.byref(l), C.byref(v)),
+                    "ppe_launch_info")
+        return {"grid": g.value, "block": b.value, "lds_bytes": l.value,
+                "image": ("global", "lds", "split")[v.value & 15], "pipeline": bool(v.value >> 4)}
 
     def sync(self):
         self._check(self.lib.ppe_sync(self.ctx), "ppe_sync")
