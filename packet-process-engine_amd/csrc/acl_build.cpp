@@ -117,7 +117,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     std::vector<uint32_t> nodes;  // 2 words per node
     std::vector<uint32_t> leaf;
     const size_t node_budget = (size_t)1 << 23;
-    uint32_t max_depth = 0, n_leaves = 0;
+    uint32_t max_depth = 0, n_leaves = 0, max_leaf = 0;
     double depth_sum = 0;
 
     std::deque<Work> q;
@@ -159,6 +159,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
                 leaf.push_back(e);
             }
             ++n_leaves;
+            max_leaf = std::max(max_leaf, (uint32_t)L.size());
             depth_sum += w.depth;
             if (w.depth > max_depth) max_depth = w.depth;
         };
@@ -257,6 +258,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     img[PPE_IMG_W_OFFRESID] = off_resid;
     img[PPE_IMG_W_DEFACT] = default_action;
     img[PPE_IMG_W_MAXDEPTH] = max_depth;
+    img[PPE_IMG_W_MAXLEAF] = max_leaf;
     img[PPE_IMG_W_TOTAL] = total;
     std::memcpy(img + off_nodes, nodes.data(), nodes.size() * sizeof(uint32_t));
     if (!leaf.empty()) std::memcpy(img + off_leaf, leaf.data(), leaf.size() * sizeof(uint32_t));

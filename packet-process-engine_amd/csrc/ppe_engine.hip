@@ -26,7 +26,7 @@ namespace {
 constexpr int kSlotSets = 4;      // set 0: ppe_classify; 1..3: host pipeline streams
 constexpr int kHostStreams = 3;
 #ifndef PPE_PIPE_DEFAULT
-#define PPE_PIPE_DEFAULT 1
+#define PPE_PIPE_DEFAULT 0  // measured slower on C1 (26.4 vs 23.0 us): kept as tuning pipeline=2
 #endif
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 
@@ -50,6 +50,7 @@ struct ppe_ctx {
     uint32_t *d_img[2] = {nullptr, nullptr};
     size_t img_cap[2] = {0, 0};
     std::vector<uint32_t> h_img[2];
+    std::vector<uint32_t> level_end[2];  // per image: number of tree nodes at depth <= d (BFS order)
     ppe_acl_stats_t stats[2];
     hipEvent_t img_done[2] = {nullptr, nullptr};
     bool img_used[2] = {false, false};
@@ -114,10 +115,10 @@ struct StagePlan {
 };
 
 // LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves): 160 KiB shared, minus
-// the counters, the 1-KB rounding of the staged image and the pipeline's per-wave packet slots
+// the counter bins, the 1-KB rounding of the staged image and the pipeline's per-wave packet slots
 uint32_t image_budget(uint32_t block, bool pipe) {
     const uint32_t per_wg = (160u * 1024u) / (2048u / block);
-    const uint32_t fixed = 1152u + (pipe ? ppe_classify_pipe_lds((int)block) : 0u);
+    const uint32_t fixed = PPE_LDS_FIXED + 1024u + (pipe ? ppe_classify_pipe_lds((int)block) : 0u);
     return per_wg > fixed ? std::min<uint32_t>(PPE_LDS_IMG_MAX, per_wg - fixed) : 0u;
 }
 
@@ -183,6 +184,19 @@ int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const 
     }
     HIPCHK(c, hipMemcpy(c->d_img[slot], words, bytes, hipMemcpyHostToDevice));
     c->h_img[slot].assign(words, words + n_words);
+    // BFS node order: the nodes of depth <= d are exactly [0, level_end[d])
+    {
+        std::vector<uint32_t> &le = c->level_end[slot];
+        le.clear();
+        const uint32_t nn = words[PPE_IMG_W_NNODES];
+        std::vector<uint8_t> depth(nn, 0);
+        for (uint32_t k = 0; k < nn; ++k) {
+            const uint32_t y = words[PPE_IMG_HDR_WORDS + 2u * k + 1u];
+            if ((y & 7u) != PPE_NODE_LEAF) depth[(y >> 3)] = depth[(y >> 3) + 1u] = (uint8_t)(depth[k] + 1u);
+            if (le.size() <= depth[k]) le.resize(depth[k] + 1u, 0u);
+            le[depth[k]] = k + 1u;
+        }
+    }
     c->stats[slot] = *st;
     c->stats[slot].lds_resident = (uint32_t)stage_plan(c, c->h_img[slot]).mode;
     c->img_used[slot] = false;
@@ -222,7 +236,16 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
     a.default_action = c->h_img[r][PPE_IMG_W_DEFACT];
     a.idx_base = idx_base;
     a.lds_words = plan.lds_words;
-    a.lds_nodes = plan.lds_nodes;
+    a.max_depth = c->h_img[r][PPE_IMG_W_MAXDEPTH];
+    a.max_leaf = c->h_img[r][PPE_IMG_W_MAXLEAF];
+    if (plan.mode == 1) {
+        a.lds_iters = a.max_depth;
+    } else if (plan.mode == 2) {  // levels 1..L all inside the staged prefix [0, lds_nodes)
+        const std::vector<uint32_t> &le = c->level_end[r];
+        uint32_t L = 0;
+        while (L + 1u < le.size() && le[L + 1u] <= plan.lds_nodes) ++L;
+        a.lds_iters = std::min(L, a.max_depth);
+    }
     a.leaf_lds = plan.leaf_lds;
     a.off_leaf = c->h_img[r][PPE_IMG_W_OFFLEAF];
     a.off_rules = c->h_img[r][PPE_IMG_W_OFFRULES];
@@ -611,7 +634,7 @@ int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds
     if (grid) *grid = std::min(c->n_cu * blocks_per_cu(c, plan), c->max_grid);
     if (block) *block = plan.block;
     if (lds_bytes)
-        *lds_bytes = 128u + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u) +
+        *lds_bytes = PPE_LDS_FIXED + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u) +
                      (plan.pipe ? ppe_classify_pipe_lds((int)plan.block) : 0u);
     if (variant) *variant = (uint32_t)plan.mode | ((uint32_t)plan.pipe << 4);
     return PPE_OK;

@@ -12,7 +12,8 @@
  *  word 1   PPE_IMG_VERSION
  *  word 2   n_nodes           word 3  n_leaf_entries      word 4  n_rules (slots)
  *  word 5   off_nodes         word 6  off_leaf            word 7  off_rules       word 8  off_resid   (word offsets)
- *  word 9   default_action    word 10 max_depth           word 11 total words     word 12..15 reserved
+ *  word 9   default_action    word 10 max_depth           word 11 total words     word 12 max leaf entries
+ *  word 13..15 reserved
  *
  *  node (2 words, 8-B aligned):
  *      internal: x = threshold, y = (left << 3) | dim      dim 0 sip, 1 dip, 2 sport, 3 dport, 4 proto
@@ -45,6 +46,7 @@
 #define PPE_IMG_W_DEFACT   9
 #define PPE_IMG_W_MAXDEPTH 10
 #define PPE_IMG_W_TOTAL    11
+#define PPE_IMG_W_MAXLEAF  12
 
 #define PPE_NODE_LEAF 7u
 #define PPE_DIM_SIP   0u

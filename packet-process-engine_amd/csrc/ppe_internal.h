@@ -26,7 +26,9 @@ struct ppe_kargs {
     uint64_t now;
     uint32_t idx_base;        /* added to the packet indices written to fw_idx / drop_idx */
     uint32_t lds_words;       /* image words staged in LDS (IMG_LDS: all; IMG_SPLIT: header + top nodes [+ leaves]) */
-    uint32_t lds_nodes;       /* IMG_SPLIT: nodes [0, lds_nodes) are in LDS                                         */
+    uint32_t lds_iters;       /* walk levels whose nodes are all in LDS (IMG_LDS: max_depth; IMG_SPLIT: BFS prefix)  */
+    uint32_t max_depth;       /* deepest leaf: uniform trip count of the tree walk                                    */
+    uint32_t max_leaf;        /* longest leaf candidate list: uniform trip count of the leaf scan                     */
     uint32_t leaf_lds;        /* IMG_SPLIT: the leaf lists are in LDS too                                             */
     uint32_t off_leaf, off_rules, off_resid; /* image section offsets (words), from the image header: kernel arguments
                                                 so the loop holds no vector load the LDS-DMA pipeline would wait on */
@@ -47,6 +49,7 @@ struct ppe_tuple_kargs {
 };
 
 #define PPE_CSLOT_WORDS 32
+#define PPE_LDS_FIXED 1152u /* classify kernel LDS before the image: 256 counter bins + 32 counters (u32) */
 #define PPE_BLOCK 256
 /* LDS available to the staged classifier image per workgroup: small images with 256-thread workgroups (8 per CU),
  * larger ones with 1024-thread workgroups (2 per CU, so 2 × (128 B + image) ≤ 160 KiB) */

@@ -132,8 +132,35 @@ struct MacValues {
     }
 };
 
+// Per-reason counters are a function of the final (status, VLAN / TCP / L4 flags) of a packet, so the kernel only
+// counts packets per bin key = status | VLAN << 5 | TCP << 6 | L4 << 7 (one LDS add per packet) and expands each
+// non-empty bin into counter increments once per workgroup.  The rules (same as the reference's pktstat updates):
+//   every packet: PKTS and its terminal reason (decode-statistic.h:239-327; ACL_FW / ACL_DROP for the ACL path)
+//   L2_RX_OK unless the Ethernet layer failed; VLAN_RX_OK for a parsed tag that was not of an unsupported type;
+//   IPV4_RX_OK when the packet reached the TCP/UDP decoder; UDP_RX_OK / TCP_RX_OK when it reached the flow engine;
+//   FLOW_PROC_OK / _FAIL by the flow engine's outcome; OUT_FW / OUT_DROP / OUT_PUNT by the action.
+#define PPE_NBINS 256u
+__device__ __forceinline__ uint32_t bin_counters(uint32_t key, uint64_t act_table) {
+    const uint32_t st = key & 31u;
+    const bool vl = (key >> 5) & 1u, tcp = (key >> 6) & 1u, l4 = (key >> 7) & 1u;
+    uint32_t cb = CB(PPE_C_PKTS) | CB(reason_counter(st));
+    if (st != PPE_ST_L2_HEADER_ERR && st != PPE_ST_L2_UNSUPPORT) cb |= CB(PPE_C_L2_RX_OK);
+    if (vl && st != PPE_ST_VLAN_UNSUPPORT) cb |= CB(PPE_C_VLAN_RX_OK);
+    const bool l4_in = st == PPE_ST_ACL_FW || st == PPE_ST_ACL_DROP || st == PPE_ST_UDP_HEADER_ERR ||
+                       st == PPE_ST_UDP_LEN_ERR || st == PPE_ST_TCP_HEADER_ERR || st == PPE_ST_TCP_LEN_ERR ||
+                       st == PPE_ST_FLOW_TCP_NO_SYN_FIRST || st == PPE_ST_WINDOW_PUNT;
+    if (l4_in) cb |= CB(PPE_C_IPV4_RX_OK);
+    if (l4 && !tcp) cb |= CB(PPE_C_UDP_RX_OK);
+    if (tcp) cb |= CB(PPE_C_TCP_RX_OK);
+    if (st == PPE_ST_FLOW_TCP_NO_SYN_FIRST || st == PPE_ST_ACL_DROP) cb |= CB(PPE_C_FLOW_PROC_FAIL);
+    if (st == PPE_ST_ACL_FW) cb |= CB(PPE_C_FLOW_PROC_OK);
+    const uint32_t act = (uint32_t)(act_table >> (2u * st)) & 3u;
+    cb |= act == PPE_ACT_FW ? CB(PPE_C_OUT_FW) : (act == PPE_ACT_DROP ? CB(PPE_C_OUT_DROP) : CB(PPE_C_OUT_PUNT));
+    return cb;
+}
+
 struct Dec {
-    uint32_t st, flags, cb;
+    uint32_t st, flags;
     uint32_t sip, dip, sport, dport, proto, paylen;
 };
 
@@ -220,11 +247,6 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[16], uint32_t len32, c
     k.flags = (l2_ok && is_vl && vlen >= 4u ? PPE_F_VLAN : 0u) | (l4_ok ? PPE_F_L4 : 0u) |
               (l4_ok && is_tcp ? PPE_F_TCP : 0u) | (l4_ok && is_tcp && syn ? PPE_F_SYN : 0u) |
               (ip_ok && frag ? PPE_F_FRAG : 0u);
-    k.cb = CB(PPE_C_PKTS) | (st != ST_ACL ? CB(reason_counter(st)) : 0u) | (l2_ok ? CB(PPE_C_L2_RX_OK) : 0u) |
-           (l2_ok && is_vl && vlen >= 4u && (v_ip || v_vl) ? CB(PPE_C_VLAN_RX_OK) : 0u) |
-           (l4_in ? CB(PPE_C_IPV4_RX_OK) : 0u) | (l4_ok && is_udp ? CB(PPE_C_UDP_RX_OK) : 0u) |
-           (l4_ok && is_tcp ? CB(PPE_C_TCP_RX_OK) : 0u) |
-           (st == PPE_ST_FLOW_TCP_NO_SYN_FIRST ? CB(PPE_C_FLOW_PROC_FAIL) : 0u);
     k.sip = ip_ok ? sip : 0u;
     k.dip = ip_ok ? dip : 0u;
     k.proto = ip_ok ? proto : 0u;
@@ -256,100 +278,111 @@ __device__ __forceinline__ uint32_t node_key(uint32_t d, uint32_t sip, uint32_t 
 #define NODE_IS_LEAF(nd) (((nd).y & 7u) == PPE_NODE_LEAF)
 #define NODE_CHILD(nd, key) (((nd).y >> 3) + ((key) > (nd).x ? 1u : 0u))
 
-// Scan one leaf's candidate list in priority order; the first rule that matches wins (lowest index).  `lf`, `rules`
-// and `resid` may each point into LDS or global memory (address space inferred after inlining).
+// Classifier geometry for one launch (host-computed from the image header, ppe_image.h).
+struct AclGeo {
+    uint32_t lds_iters;   // walk levels whose nodes are all staged in LDS (IMG_LDS: max_depth, IMG_GLOBAL: 0)
+    uint32_t max_depth;   // deepest leaf
+    uint32_t max_leaf;    // longest leaf candidate list
+    uint32_t off_leaf, off_rules, off_resid;
+    uint32_t leaf_lds;    // leaf lists in LDS (IMG_LDS always; IMG_SPLIT when they fit)
+    uint32_t default_action;
+};
+
+// One level of the walk for every lane: a lane already at a leaf stays there (and re-reads it), so the loops below
+// have a wave-uniform trip count and no per-lane exit: no exec-mask bookkeeping per level.
+template <class N>
+__device__ __forceinline__ void walk_level(const N *nodes, uint32_t &node, uint2 &nd, uint32_t sip, uint32_t dip,
+                                           uint32_t sport, uint32_t dport, uint32_t proto) {
+    const uint32_t child = NODE_CHILD(nd, node_key(nd.y & 7u, sip, dip, sport, dport, proto));
+    node = NODE_IS_LEAF(nd) ? node : child;
+    nd = nodes[node];
+}
+
+// Scan a leaf's candidate list in priority order; the first rule that matches wins (lowest index).  max_leaf
+// uniform iterations: a lane whose list is shorter, or that has matched, keeps reading a valid entry and ignores it.
+// `lf`, `rules` and `resid` may each point into LDS or global memory (address space inferred after inlining).
 template <class Mac>
-__device__ __forceinline__ void leaf_scan(uint2 nd, const uint32_t *__restrict__ lf, const uint32_t *__restrict__ rules,
-                                          const uint32_t *__restrict__ resid, uint32_t sip, uint32_t dip, uint32_t sport,
-                                          uint32_t dport, uint32_t proto, const Mac &mac, const uint64_t *tsp, uint32_t p,
-                                          uint64_t now, int32_t &hit, uint32_t &action) {
+__device__ __forceinline__ void leaf_scan(uint2 nd, uint32_t max_leaf, const uint32_t *__restrict__ lf,
+                                          const uint32_t *__restrict__ rules, const uint32_t *__restrict__ resid,
+                                          uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                                          const Mac &mac, const uint64_t *tsp, uint32_t p, uint64_t now,
+                                          int32_t &hit, uint32_t &action) {
     const uint32_t cnt = nd.y >> 3;
+    bool done = false;
 #pragma unroll 1
-    for (uint32_t j = 0; j < cnt; ++j) {
-        const uint32_t e = lf[j];
+    for (uint32_t j = 0; j < max_leaf; ++j) {
+        const bool live = !done && j < cnt;
+        const uint32_t e = lf[live ? nd.x + j : 0u];  // entry 0 exists whenever max_leaf > 0
         const uint32_t slot = e & ~PPE_LEAF_CERTAIN;
         const uint4 *rp = (const uint4 *)(rules + 8u * slot);
         const uint4 a = rp[0], b = rp[1];
-        bool m = (e & PPE_LEAF_CERTAIN) != 0u;
-        if (!m) {
-            m = sip >= a.x && sip <= a.y && dip >= a.z && dip <= a.w &&
-                sport >= (b.x & 0xffffu) && sport <= (b.x >> 16) &&
-                dport >= (b.y & 0xffffu) && dport <= (b.y >> 16) &&
-                proto >= (b.z & 0xffu) && proto <= ((b.z >> 8) & 0xffu);
-            const uint32_t rs = b.w >> 29;
-            if (m && rs) {
-                const uint4 *xp = (const uint4 *)(resid + 8u * slot);
-                const uint4 c = xp[0], t = xp[1];
-                if (rs & (PPE_RESID_DMAC | PPE_RESID_SMAC)) {
-                    uint32_t dmac_lo, dmac_hi, smac_lo, smac_hi;
-                    mac.get(dmac_lo, dmac_hi, smac_lo, smac_hi);
-                    if (rs & PPE_RESID_DMAC) m = m && c.x == dmac_lo && c.y == dmac_hi;
-                    if (rs & PPE_RESID_SMAC) m = m && c.z == smac_lo && c.w == smac_hi;
-                }
-                if (rs & PPE_RESID_TIME) {  // the packet timestamp is only fetched for time-window rules
-                    const uint64_t ts = tsp ? ld_u64_sync(tsp + p) : now;
-                    const uint64_t t0 = (uint64_t)t.x | ((uint64_t)t.y << 32);
-                    const uint64_t t1 = (uint64_t)t.z | ((uint64_t)t.w << 32);
-                    m = m && ts >= t0 && ts <= t1;
-                }
+        const bool box = sip >= a.x && sip <= a.y && dip >= a.z && dip <= a.w &&
+                         sport >= (b.x & 0xffffu) && sport <= (b.x >> 16) &&
+                         dport >= (b.y & 0xffffu) && dport <= (b.y >> 16) &&
+                         proto >= (b.z & 0xffu) && proto <= ((b.z >> 8) & 0xffu);
+        bool m = live && ((e & PPE_LEAF_CERTAIN) != 0u || box);
+        const uint32_t rs = b.w >> 29;
+        if (m && rs && (e & PPE_LEAF_CERTAIN) == 0u) {  // residual MAC / time fields: rare
+            const uint4 *xp = (const uint4 *)(resid + 8u * slot);
+            const uint4 c = xp[0], t = xp[1];
+            if (rs & (PPE_RESID_DMAC | PPE_RESID_SMAC)) {
+                uint32_t dmac_lo, dmac_hi, smac_lo, smac_hi;
+                mac.get(dmac_lo, dmac_hi, smac_lo, smac_hi);
+                if (rs & PPE_RESID_DMAC) m = m && c.x == dmac_lo && c.y == dmac_hi;
+                if (rs & PPE_RESID_SMAC) m = m && c.z == smac_lo && c.w == smac_hi;
+            }
+            if (rs & PPE_RESID_TIME) {  // the packet timestamp is only fetched for time-window rules
+                const uint64_t ts = tsp ? ld_u64_sync(tsp + p) : now;
+                const uint64_t t0 = (uint64_t)t.x | ((uint64_t)t.y << 32);
+                const uint64_t t1 = (uint64_t)t.z | ((uint64_t)t.w << 32);
+                m = m && ts >= t0 && ts <= t1;
             }
         }
-        if (m) {
-            hit = (int32_t)(b.w & 0x1fffffffu);
-            action = b.z >> 16;
-            return;
-        }
+        hit = m ? (int32_t)(b.w & 0x1fffffffu) : hit;
+        action = m ? b.z >> 16 : action;
+        done = done || m;
     }
 }
 
-// First-match decision-tree lookup over the classifier image (ppe_image.h).  The 5-tuple arrives as scalars (not
-// struct fields): a select between fields of an in-memory struct is folded into a dynamically indexed load, which
-// sends the whole struct to scratch.
+// First-match decision-tree lookup over the classifier image.  The 5-tuple arrives as scalars (not struct fields):
+// a select between fields of an in-memory struct is folded into a dynamically indexed load, which sends the whole
+// struct to scratch.  Levels [0, lds_iters) read the staged top of the tree from LDS, the rest from global memory.
 template <int MODE, class Mac>
 __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ gimg, const uint32_t *__restrict__ limg,
-                                           uint32_t lds_nodes, uint32_t leaf_lds, uint32_t off_leaf,
-                                           uint32_t off_rules, uint32_t off_resid, uint32_t default_action,
-                                           const uint32_t sip, const uint32_t dip, const uint32_t sport,
-                                           const uint32_t dport, const uint32_t proto, const Mac &mac,
-                                           const uint64_t *tsp, uint32_t p, uint64_t now, int32_t &hit,
-                                           uint32_t &action) {
+                                           const AclGeo &g, const uint32_t sip, const uint32_t dip,
+                                           const uint32_t sport, const uint32_t dport, const uint32_t proto,
+                                           const Mac &mac, const uint64_t *tsp, uint32_t p, uint64_t now,
+                                           int32_t &hit, uint32_t &action) {
     const uint2 *gn = (const uint2 *)(gimg + PPE_IMG_HDR_WORDS);
+    const uint2 *ln = (const uint2 *)(limg + PPE_IMG_HDR_WORDS);
+    uint32_t node = 0, it = 0;
     uint2 nd;
-    int it = 0;
     if (MODE == IMG_GLOBAL) {
         nd = gn[0];
-#pragma unroll 1
-        for (; it < PPE_MAX_DEPTH && !NODE_IS_LEAF(nd); ++it)
-            nd = gn[NODE_CHILD(nd, node_key(nd.y & 7u, sip, dip, sport, dport, proto))];
     } else {
-        const uint2 *ln = (const uint2 *)(limg + PPE_IMG_HDR_WORDS);
         nd = ln[0];
-        uint32_t node = 0;
 #pragma unroll 1
-        for (; it < PPE_MAX_DEPTH && !NODE_IS_LEAF(nd); ++it) {
+        for (; it < g.lds_iters; ++it) walk_level(ln, node, nd, sip, dip, sport, dport, proto);
+    }
+    if (MODE != IMG_LDS) {  // below the staged top: per-lane exit (a finished lane must not keep reading L2/HBM)
+#pragma unroll 1
+        for (; it < g.max_depth && !NODE_IS_LEAF(nd); ++it) {
             node = NODE_CHILD(nd, node_key(nd.y & 7u, sip, dip, sport, dport, proto));
-            if (MODE == IMG_SPLIT && node >= lds_nodes) break;  // below the staged top of the tree
-            nd = ln[node];
-        }
-        if (MODE == IMG_SPLIT && !NODE_IS_LEAF(nd)) {
             nd = gn[node];
-#pragma unroll 1
-            for (; it < PPE_MAX_DEPTH && !NODE_IS_LEAF(nd); ++it)
-                nd = gn[NODE_CHILD(nd, node_key(nd.y & 7u, sip, dip, sport, dport, proto))];
         }
     }
     hit = -1;
-    action = default_action;
-    if (!NODE_IS_LEAF(nd)) return;  // unreachable for a builder-made image
+    action = g.default_action;
+    // every lane is at a leaf now (max_depth = the deepest leaf of the builder's tree)
     if (MODE == IMG_LDS)
-        leaf_scan(nd, limg + off_leaf + nd.x, limg + off_rules, limg + off_resid, sip, dip, sport, dport, proto,
-                  mac, tsp, p, now, hit, action);
-    else if (MODE == IMG_SPLIT && leaf_lds)
-        leaf_scan(nd, limg + off_leaf + nd.x, gimg + off_rules, gimg + off_resid, sip, dip, sport, dport, proto,
-                  mac, tsp, p, now, hit, action);
+        leaf_scan(nd, g.max_leaf, limg + g.off_leaf, limg + g.off_rules, limg + g.off_resid, sip, dip, sport, dport,
+                  proto, mac, tsp, p, now, hit, action);
+    else if (MODE == IMG_SPLIT && g.leaf_lds)
+        leaf_scan(nd, g.max_leaf, limg + g.off_leaf, gimg + g.off_rules, gimg + g.off_resid, sip, dip, sport, dport,
+                  proto, mac, tsp, p, now, hit, action);
     else
-        leaf_scan(nd, gimg + off_leaf + nd.x, gimg + off_rules, gimg + off_resid, sip, dip, sport, dport, proto,
-                  mac, tsp, p, now, hit, action);
+        leaf_scan(nd, g.max_leaf, gimg + g.off_leaf, gimg + g.off_rules, gimg + g.off_resid, sip, dip, sport, dport,
+                  proto, mac, tsp, p, now, hit, action);
 }
 
 // Copy the classifier image into LDS with LDS-DMA (global_load_lds_dwordx4): every 1-KB piece of the image is in
@@ -490,8 +523,9 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     // a separate LDS object from the image: the compiler then knows the slot DMA never aliases image reads
     __shared__ __attribute__((aligned(16))) uint32_t ring[PIPE ? BLOCK / 64 : 1][PIPE ? PIPE_SLOT_BYTES / 4 : 1];
-    uint32_t *lcnt = smem;       // [32] per-reason counters of this workgroup
-    uint32_t *limg = smem + 32;  // staged classifier image
+    uint32_t *bins = smem;                   // [PPE_NBINS] packets per (status, flags) bin of this workgroup
+    uint32_t *lcnt = smem + PPE_NBINS;       // [32] per-reason counters of this workgroup
+    uint32_t *limg = smem + PPE_NBINS + 32;  // staged classifier image
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -501,10 +535,11 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t slot = PIPE ? (uint32_t)(uintptr_t)(lptr_t)&ring[wv][0] : 0u;
     if (PIPE && tile < ntiles) pipe_issue(a, tile, slot, lane);  // in flight during the image staging
 
-    if (tid < 32) lcnt[tid] = 0;
+    for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) smem[i] = 0;
     if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img, limg, a.lds_words, tid);
     __syncthreads();
-    const uint32_t off_leaf = a.off_leaf, off_rules = a.off_rules, off_resid = a.off_resid;
+    const AclGeo geo = {a.lds_iters, a.max_depth, a.max_leaf, a.off_leaf, a.off_rules, a.off_resid, a.leaf_lds,
+                        a.default_action};
 
     // action of each terminal status, 2 bits per status: FW for ACL_FW, PUNT for fragments / short windows, the
     // configured action for unsupported protocols (Decode_unsupport_proto_handle, decode.c:31-45), else DROP
@@ -517,7 +552,6 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
                           : (st == PPE_ST_FRAG || st == PPE_ST_WINDOW_PUNT) ? PPE_ACT_PUNT : PPE_ACT_DROP;
         act_table |= ac << (2u * st);
     }
-    uint32_t my_cnt = 0;  // lane b (< PPE_C__COUNT) accumulates counter b of this wave
 
     // current tile's window: bytes 0..51 (w[0..12]) and the wire length
     uint4 q0, q1, q2;
@@ -551,16 +585,14 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
         if (!(PPE_ABLATE & 1) && valid && k.st == ST_ACL) {
             uint32_t rule_act;
             const MacFromWindow mac = {a.hdr, p, a.stride};
-            acl_lookup<MODE>(a.img, limg, a.lds_nodes, a.leaf_lds, off_leaf, off_rules, off_resid, a.default_action,
-                             k.sip, k.dip, k.sport, k.dport, k.proto, mac, a.ts, p, a.now, hit, rule_act);
+            acl_lookup<MODE>(a.img, limg, geo, k.sip, k.dip, k.sport, k.dport, k.proto, mac, a.ts, p, a.now, hit,
+                             rule_act);
             const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
             k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
             k.flags |= PPE_F_ACL;
-            k.cb |= drop ? (CB(PPE_C_ACL_DROP) | CB(PPE_C_FLOW_PROC_FAIL)) : (CB(PPE_C_ACL_FW) | CB(PPE_C_FLOW_PROC_OK));
         }
         const uint32_t st = k.st;
         act = (uint32_t)(act_table >> (2u * st)) & 3u;
-        k.cb |= act == PPE_ACT_FW ? CB(PPE_C_OUT_FW) : (act == PPE_ACT_DROP ? CB(PPE_C_OUT_DROP) : CB(PPE_C_OUT_PUNT));
 
         // next tile: its DMA has had this whole tile's compute to land; take it into registers and start the one
         // after (the stores below are issued after this wait, so it never waits on this tile's own stores)
@@ -580,46 +612,45 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
             }
         }
 
-        // ---- wave-ballot compaction of FW / DROP indices into this tile's 64-slot segment ----
-        if (PPE_ABLATE & 4) goto skip_compact;
-        {
-        const bool is_fw = valid && act == PPE_ACT_FW;
-        const bool is_drop = valid && act == PPE_ACT_DROP;
-        const uint64_t bfw = __ballot(is_fw);
-        const uint64_t bdr = __ballot(is_drop);
-        const uint64_t bpu = __ballot(valid && act == PPE_ACT_PUNT);
-        if (a.fw_idx && is_fw) {
-            const uint32_t pos =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(bfw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bfw, 0u));
-            a.fw_idx[(tile << 6) + pos] = p + a.idx_base;
+        // ---- wave-ballot compaction of FW / DROP indices into this tile's 64-slot segment of each list ----
+        if (!(PPE_ABLATE & 4)) {
+            const bool is_fw = valid && act == PPE_ACT_FW;
+            const bool is_drop = valid && act == PPE_ACT_DROP;
+            const uint64_t bfw = __ballot(is_fw);
+            const uint64_t bdr = __ballot(is_drop);
+            const uint32_t pfw = __builtin_amdgcn_mbcnt_hi((uint32_t)(bfw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bfw, 0u));
+            const uint32_t pdr = __builtin_amdgcn_mbcnt_hi((uint32_t)(bdr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bdr, 0u));
+            if (a.fw_idx && a.drop_idx) {  // both lists: one store instruction
+                uint32_t *dst = is_fw ? a.fw_idx : a.drop_idx;
+                if (is_fw || is_drop) dst[(tile << 6) + (is_fw ? pfw : pdr)] = p + a.idx_base;
+            } else {
+                if (a.fw_idx && is_fw) a.fw_idx[(tile << 6) + pfw] = p + a.idx_base;
+                if (a.drop_idx && is_drop) a.drop_idx[(tile << 6) + pdr] = p + a.idx_base;
+            }
+            const uint32_t nv = (uint32_t)__popcll(__ballot(valid));  // (a ballot outside the lane-0 branch)
+            if (a.tile_cnt && lane == 0) {
+                const uint32_t nfw = (uint32_t)__popcll(bfw), ndr = (uint32_t)__popcll(bdr);
+                a.tile_cnt[tile] = nfw | (ndr << 8) | ((nv - nfw - ndr) << 16);
+            }
         }
-        if (a.drop_idx && is_drop) {
-            const uint32_t pos =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(bdr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bdr, 0u));
-            a.drop_idx[(tile << 6) + pos] = p + a.idx_base;
-        }
-        if (a.tile_cnt && lane == 0)
-            a.tile_cnt[tile] = (uint32_t)__popcll(bfw) | ((uint32_t)__popcll(bdr) << 8) |
-                               ((uint32_t)__popcll(bpu) << 16);
-        }
-    skip_compact:
 
-        // ---- per-reason counters: one iteration per DISTINCT counter pattern in the wave (typically 2-3: the
-        // ACL-forward path, the ACL-drop path, a malformed packet); lane b keeps counter b ----
-        const uint32_t cb = k.cb;
-        uint64_t todo = (PPE_ABLATE & 2) ? 0ull : __ballot(valid);
-        while (todo) {
-            const uint32_t pat = __builtin_amdgcn_readlane(cb, (uint32_t)__builtin_ctzll(todo));
-            const uint64_t same = __ballot(cb == pat) & todo;
-            todo &= ~same;
-            my_cnt += ((pat >> lane) & 1u) * (uint32_t)__popcll(same);
-        }
+        // ---- per-reason counters: one LDS add per packet into its (status, flags) bin ----
+        if (!(PPE_ABLATE & 2) && valid)
+            atomicAdd(&bins[st | ((k.flags & PPE_F_VLAN) ? 32u : 0u) | ((k.flags & PPE_F_TCP) ? 64u : 0u) |
+                            ((k.flags & PPE_F_L4) ? 128u : 0u)],
+                      1u);
         // the slot was emptied by pipe_read above; refill it with the tile after next (issued here, where little
         // is live, rather than right after the read)
         if (PIPE && tile + 2u * stride_waves < ntiles) pipe_issue(a, tile + 2u * stride_waves, slot, lane);
     }
 
-    if (lane < PPE_C__COUNT && my_cnt) atomicAdd(&lcnt[lane], my_cnt);
+    __syncthreads();
+    for (uint32_t b = tid; b < PPE_NBINS; b += BLOCK) {  // expand the bins into counter increments
+        const uint32_t c = bins[b];
+        if (c) {
+            for (uint32_t cb = bin_counters(b, act_table); cb; cb &= cb - 1u) atomicAdd(&lcnt[__builtin_ctz(cb)], c);
+        }
+    }
     __syncthreads();
     if (tid < PPE_C__COUNT) a.cslots[(size_t)blockIdx.x * PPE_CSLOT_WORDS + tid] += lcnt[tid];
 }
@@ -634,9 +665,9 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
         stage_image<PPE_BLOCK>(a.img, smem, a.img_words, tid);
         __syncthreads();
     }
-    const uint32_t off_leaf = a.img[PPE_IMG_W_OFFLEAF];
-    const uint32_t off_rules = a.img[PPE_IMG_W_OFFRULES];
-    const uint32_t off_resid = a.img[PPE_IMG_W_OFFRESID];
+    const uint32_t depth = a.img[PPE_IMG_W_MAXDEPTH];
+    const AclGeo geo = {LDS_IMG ? depth : 0u, depth, a.img[PPE_IMG_W_MAXLEAF], a.img[PPE_IMG_W_OFFLEAF],
+                        a.img[PPE_IMG_W_OFFRULES], a.img[PPE_IMG_W_OFFRESID], LDS_IMG ? 1u : 0u, a.default_action};
     for (uint32_t i = blockIdx.x * PPE_BLOCK + tid; i < a.n; i += gridDim.x * PPE_BLOCK) {
         const uint4 t = ((const uint4 *)a.tuple)[i];
         uint4 m = make_uint4(0, 0, 0, 0);
@@ -645,11 +676,11 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
         uint32_t act;
         const MacValues mac = {m.x, m.y, m.z, m.w};
         if (LDS_IMG)
-            acl_lookup<IMG_LDS>(a.img, smem, 0, 0, off_leaf, off_rules, off_resid, a.default_action, t.x, t.y,
-                                t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i, a.now, hit, act);
+            acl_lookup<IMG_LDS>(a.img, smem, geo, t.x, t.y, t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i, a.now,
+                                hit, act);
         else
-            acl_lookup<IMG_GLOBAL>(a.img, smem, 0, 0, off_leaf, off_rules, off_resid, a.default_action, t.x, t.y,
-                                   t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i, a.now, hit, act);
+            acl_lookup<IMG_GLOBAL>(a.img, smem, geo, t.x, t.y, t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i,
+                                   a.now, hit, act);
         if (a.hit) a.hit[i] = hit;
         if (a.action) a.action[i] = act;
     }
@@ -673,7 +704,7 @@ static int occ_t(size_t shmem) {
 }
 
 static size_t classify_shmem(uint32_t lds_words, int mode) {
-    const size_t base = 32 * sizeof(uint32_t);
+    const size_t base = (PPE_NBINS + 32u) * sizeof(uint32_t);  // counter bins + per-reason counters
     return mode != IMG_GLOBAL ? base + (((size_t)lds_words * 4u + 1023u) & ~(size_t)1023u) : base;
 }
 

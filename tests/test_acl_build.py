@@ -98,3 +98,6 @@ def test_image_layout():
     assert img[0] == 0x41455050 and img[1] == 1
     assert img[2] == st["n_nodes"] and img[4] == 64 and img[11] == len(img)
     assert img[7] % 8 == 0  # rules 32-B aligned
+    nodes = img[16:16 + 2 * img[2]].reshape(-1, 2)
+    leaves = nodes[(nodes[:, 1] & 7) == 7]
+    assert img[10] >= 1 and img[12] == (leaves[:, 1] >> 3).max()  # max depth, max leaf entries
