@@ -141,9 +141,11 @@ int32_t oracle_acl_tree(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dpo
     uint32_t node = 0;
     for (int it = 0; it <= PPE_MAX_DEPTH; it++) {
         const uint32_t x = im[PPE_IMG_HDR_WORDS + 2 * node], y = im[PPE_IMG_HDR_WORDS + 2 * node + 1];
-        if ((y & 7u) == PPE_NODE_LEAF) {
-            const uint32_t *lf = im + im[PPE_IMG_W_OFFLEAF] + x;
-            for (uint32_t j = 0; j < (y >> 3); j++) {
+        if (PPE_NODE_DIM(y) == PPE_NODE_LEAF) {
+            uint32_t first = x, cnt = y & 0xffu;
+            if (cnt == PPE_LEAF_CNT_ESC) cnt = im[im[PPE_IMG_W_OFFLEAF] + first++];
+            const uint32_t *lf = im + im[PPE_IMG_W_OFFLEAF] + first;
+            for (uint32_t j = 0; j < cnt; j++) {
                 const uint32_t slot = lf[j] & ~PPE_LEAF_CERTAIN;
                 const uint32_t *r = im + im[PPE_IMG_W_OFFRULES] + 8 * slot;
                 int m = (lf[j] & PPE_LEAF_CERTAIN) != 0;
@@ -167,7 +169,7 @@ int32_t oracle_acl_tree(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dpo
             }
             break;
         }
-        node = (y >> 3) + (key[y & 7u] > x ? 1u : 0u);
+        node = (y >> PPE_NODE_CHILD_SHIFT) + (key[PPE_NODE_DIM(y)] > x ? 1u : 0u);
     }
     if (action) *action = im[PPE_IMG_W_DEFACT];
     return -1;

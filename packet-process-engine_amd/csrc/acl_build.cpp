@@ -116,7 +116,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     // ---- recursive partitioning, BFS so that children are contiguous and numbered after their parent ----
     std::vector<uint32_t> nodes;  // 2 words per node
     std::vector<uint32_t> leaf;
-    const size_t node_budget = (size_t)1 << 23;
+    const size_t node_budget = PPE_NODE_MAX - 2;
     uint32_t max_depth = 0, n_leaves = 0, max_leaf = 0;
     double depth_sum = 0;
 
@@ -151,8 +151,11 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         w.rules.shrink_to_fit();
 
         auto make_leaf = [&](const std::vector<uint32_t> &L) {
+            const uint32_t cnt = (uint32_t)L.size();
             nodes[2 * w.node + 0] = (uint32_t)leaf.size();
-            nodes[2 * w.node + 1] = ((uint32_t)L.size() << 3) | PPE_NODE_LEAF;
+            nodes[2 * w.node + 1] =
+                (w.node << PPE_NODE_CHILD_SHIFT) | (PPE_NODE_LEAF << 8) | std::min(cnt, PPE_LEAF_CNT_ESC);
+            if (cnt >= PPE_LEAF_CNT_ESC) leaf.push_back(cnt);  // long list: its length leads the entries
             for (uint32_t s : L) {
                 uint32_t e = s;
                 if (R[s].resid == 0 && covers(R[s], w.lo, w.hi)) e |= PPE_LEAF_CERTAIN;
@@ -213,7 +216,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         const uint32_t left_idx = (uint32_t)(nodes.size() / 2);
         nodes.resize(nodes.size() + 4);
         nodes[2 * w.node + 0] = best_t;
-        nodes[2 * w.node + 1] = (left_idx << 3) | (uint32_t)best_d;
+        nodes[2 * w.node + 1] = (left_idx << PPE_NODE_CHILD_SHIFT) | ((uint32_t)best_d << 8);
 
         Work L, Rt;
         L.node = left_idx;

@@ -26,7 +26,8 @@ namespace {
 constexpr int kSlotSets = 4;      // set 0: ppe_classify; 1..3: host pipeline streams
 constexpr int kHostStreams = 3;
 #ifndef PPE_PIPE_DEFAULT
-#define PPE_PIPE_DEFAULT 0  // measured slower on C1 (26.4 vs 23.0 us): kept as tuning pipeline=2
+// next-tile fetch of the classify kernel (PF_* in ppe_kernels.hip): 0 none, 1 register double buffer, 2 LDS-DMA
+#define PPE_PF_DEFAULT 0  // none: register (28.3 us) and LDS-DMA (24.4) prefetch measured slower on C1 (22.2)
 #endif
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 
@@ -65,6 +66,7 @@ struct ppe_ctx {
     // host pipeline
     HostStage hs[kHostStreams];
     ppe_tuning_t tune;
+    unsigned long long *trace = nullptr;  // ppe_debug_trace
     char err[256] = {0};
 };
 
@@ -100,7 +102,7 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl == 1 || pl == 2 ? (uint32_t)pl : 0u;
+    t.pipeline = pl >= 1 && pl <= 3 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     return t;
 }
@@ -109,31 +111,41 @@ ppe_tuning_t default_tuning() {
 // packet pipeline.
 struct StagePlan {
     int mode;            // 0 global, 1 whole image in LDS, 2 prefix in LDS
-    int pipe;            // 1 = LDS-DMA next-tile pipeline
+    int pipe;            // next-tile fetch: 0 none, 1 register double buffer, 2 LDS-DMA slot
     uint32_t block;
     uint32_t lds_words, lds_nodes, leaf_lds;
 };
 
 // LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves): 160 KiB shared, minus
-// the counter bins, the 1-KB rounding of the staged image and the pipeline's per-wave packet slots
-uint32_t image_budget(uint32_t block, bool pipe) {
+// the counter bins, the 1-KB rounding of the staged image, the pipeline's per-wave packet slots and (whole image in
+// LDS) the per-wave walk keys
+uint32_t image_budget(uint32_t block, bool pipe, bool keys) {
     const uint32_t per_wg = (160u * 1024u) / (2048u / block);
-    const uint32_t fixed = PPE_LDS_FIXED + 1024u + (pipe ? ppe_classify_pipe_lds((int)block) : 0u);
+    const uint32_t fixed = PPE_LDS_FIXED + 1024u + (pipe ? ppe_classify_pipe_lds((int)block) : 0u) +
+                           (keys ? ppe_classify_keys_lds((int)block) : 0u);
     return per_wg > fixed ? std::min<uint32_t>(PPE_LDS_IMG_MAX, per_wg - fixed) : 0u;
 }
 
-StagePlan stage_plan_for(const ppe_ctx *c, const std::vector<uint32_t> &img, bool pipe) {
+StagePlan stage_plan_for(const ppe_ctx *c, const std::vector<uint32_t> &img, int pf) {
+    const bool pipe = pf == 2;
     const uint32_t words = (uint32_t)img.size(), bytes = words * 4u;
-    StagePlan p = {0, pipe ? 1 : 0, c->tune.block ? c->tune.block : 1024u, 0, 0, 0};
+    StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0, 0};
     if (!c->tune.lds_image) {
         if (!c->tune.block && !pipe) p.block = 256;
         return p;
     }
-    // without the pipeline a small image goes with 256-thread workgroups (8 per CU, each with its own copy)
-    if (!c->tune.block && !pipe && bytes <= image_budget(256, false)) p.block = 256;
-    const uint32_t budget = image_budget(p.block, pipe);
+    // the whole image in LDS: the smallest workgroup (most copies per CU) whose share holds it
+    if (!c->tune.block) {
+        for (uint32_t b : {256u, 512u, 1024u}) {
+            if (bytes <= image_budget(b, pipe, true)) {
+                p.block = b;
+                break;
+            }
+        }
+    }
     const uint32_t off_rules = img[PPE_IMG_W_OFFRULES], n_nodes = img[PPE_IMG_W_NNODES];
-    if (bytes <= budget) {
+    const uint32_t budget = image_budget(p.block, pipe, false);
+    if (bytes <= image_budget(p.block, pipe, true)) {
         p.mode = 1;
         p.lds_words = words;
     } else if (off_rules * 4u <= budget) {  // every node and leaf list; rule records from global (L2)
@@ -153,12 +165,14 @@ StagePlan stage_plan_for(const ppe_ctx *c, const std::vector<uint32_t> &img, boo
 // The LDS-DMA pipeline runs only with the whole image in LDS (see PPE_DISPATCH); when the image with the pipeline's
 // slots does not fit, the plan falls back to the non-pipelined kernel.
 StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
-    const bool pipe = c->tune.pipeline == 2 || (c->tune.pipeline == 0 && PPE_PIPE_DEFAULT);
-    if (pipe && c->tune.lds_image) {
-        const StagePlan p = stage_plan_for(c, img, true);
+    // tuning.pipeline: 0 automatic, 1 none, 2 LDS-DMA, 3 register double buffer
+    static const int kPf[4] = {PPE_PF_DEFAULT, 0, 2, 1};
+    const int pf = kPf[c->tune.pipeline & 3u];
+    if (pf == 2 && c->tune.lds_image) {
+        const StagePlan p = stage_plan_for(c, img, 2);
         if (p.mode == 1) return p;
     }
-    return stage_plan_for(c, img, false);
+    return stage_plan_for(c, img, pf == 2 ? 0 : pf);
 }
 
 // Resident workgroups per CU: the occupancy API's answer (register and LDS limits) unless the tuning fixes it.
@@ -192,7 +206,8 @@ int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const 
         std::vector<uint8_t> depth(nn, 0);
         for (uint32_t k = 0; k < nn; ++k) {
             const uint32_t y = words[PPE_IMG_HDR_WORDS + 2u * k + 1u];
-            if ((y & 7u) != PPE_NODE_LEAF) depth[(y >> 3)] = depth[(y >> 3) + 1u] = (uint8_t)(depth[k] + 1u);
+            const uint32_t ch = y >> PPE_NODE_CHILD_SHIFT;
+            if (PPE_NODE_DIM(y) != PPE_NODE_LEAF) depth[ch] = depth[ch + 1u] = (uint8_t)(depth[k] + 1u);
             if (le.size() <= depth[k]) le.resize(depth[k] + 1u, 0u);
             le[depth[k]] = k + 1u;
         }
@@ -251,6 +266,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
     a.off_rules = c->h_img[r][PPE_IMG_W_OFFRULES];
     a.off_resid = c->h_img[r][PPE_IMG_W_OFFRESID];
     a.cslots = c->d_cslots + (size_t)slot_set * c->max_grid * PPE_CSLOT_WORDS;
+    a.trace = c->trace;
 
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
@@ -606,11 +622,18 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline > 2) return fail(c, PPE_EINVAL, "pipeline must be 0 (auto), 1 (off) or 2 (on)");
+    if (t->pipeline > 3)
+        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto), 1 (none), 2 (LDS-DMA) or 3 (register prefetch)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     c->tune = *t;
     c->tune.pipeline = t->pipeline;
     c->tune.lds_image = t->lds_image ? 1u : 0u;
+    return PPE_OK;
+}
+
+int ppe_debug_trace(ppe_ctx_t *c, void *dev_buf) {
+    if (!c) return PPE_EINVAL;
+    c->trace = (unsigned long long *)dev_buf;
     return PPE_OK;
 }
 
@@ -635,7 +658,8 @@ int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds
     if (block) *block = plan.block;
     if (lds_bytes)
         *lds_bytes = PPE_LDS_FIXED + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u) +
-                     (plan.pipe ? ppe_classify_pipe_lds((int)plan.block) : 0u);
+                     (plan.mode == 1 ? ppe_classify_keys_lds((int)plan.block) : 0u) +
+                     (plan.pipe == 2 ? ppe_classify_pipe_lds((int)plan.block) : 0u);
     if (variant) *variant = (uint32_t)plan.mode | ((uint32_t)plan.pipe << 4);
     return PPE_OK;
 }

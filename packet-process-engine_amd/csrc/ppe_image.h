@@ -15,10 +15,15 @@
  *  word 9   default_action    word 10 max_depth           word 11 total words     word 12 max leaf entries
  *  word 13..15 reserved
  *
- *  node (2 words, 8-B aligned):
- *      internal: x = threshold, y = (left << 3) | dim      dim 0 sip, 1 dip, 2 sport, 3 dport, 4 proto
+ *  node (2 words, 8-B aligned):  y = (child << 11) | (dim << 8) | count
+ *      internal: x = threshold, child = left, dim 0 sip, 1 dip, 2 sport, 3 dport, 4 proto, count 0
  *                key <= threshold → left, key > threshold → left + 1
- *      leaf:     x = first leaf entry (index into the leaf array), y = (count << 3) | 7
+ *      leaf:     dim = PPE_NODE_LEAF (5): the walk's key slot 5 holds 0, so "key > x" is false and the walk stays
+ *                at child = the leaf itself (a fixed point: every lane can walk max_depth levels without a per-lane
+ *                exit).  x = first leaf entry; count = number of entries, or PPE_LEAF_CNT_ESC when the count is
+ *                stored in leaf entry x and the entries start at x + 1.
+ *      The field positions let the walk form the key's LDS offset as y & 0x700 (slot stride 256 B) and the child's
+ *      byte offset as (y >> 8) & ~7.
  *  leaf entry (1 word): rule slot | (certain << 31)      certain: the rule's 5-tuple box covers the leaf's region
  *                                                          and it has no residual field, so it matches unchecked
  *  rule (8 words, 32-B aligned), slot order == ascending rule index:
@@ -33,7 +38,7 @@
 #define PPE_IMAGE_H
 
 #define PPE_IMG_MAGIC   0x41455050u /* "PPEA" */
-#define PPE_IMG_VERSION 1u
+#define PPE_IMG_VERSION 2u
 #define PPE_IMG_HDR_WORDS 16u
 
 #define PPE_IMG_W_NNODES   2
@@ -48,7 +53,11 @@
 #define PPE_IMG_W_TOTAL    11
 #define PPE_IMG_W_MAXLEAF  12
 
-#define PPE_NODE_LEAF 7u
+#define PPE_NODE_LEAF 5u          /* leaf marker in the dim field; also the index of the walk's zero key slot */
+#define PPE_NODE_CHILD_SHIFT 11u
+#define PPE_NODE_DIM(y) (((y) >> 8) & 7u)
+#define PPE_NODE_MAX (1u << 21)   /* child index field: 21 bits */
+#define PPE_LEAF_CNT_ESC 255u     /* count field value meaning "count stored in the first leaf word" */
 #define PPE_DIM_SIP   0u
 #define PPE_DIM_DIP   1u
 #define PPE_DIM_SPORT 2u

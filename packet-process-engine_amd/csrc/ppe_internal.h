@@ -33,6 +33,7 @@ struct ppe_kargs {
     uint32_t off_leaf, off_rules, off_resid; /* image section offsets (words), from the image header: kernel arguments
                                                 so the loop holds no vector load the LDS-DMA pipeline would wait on */
     unsigned long long *cslots; /* [grid][PPE_CSLOT_WORDS] counter slots, one per workgroup */
+    unsigned long long *trace;  /* diagnostic builds (PPE_TRACE) only: per-wave phase timestamps, else unused */
 };
 
 struct ppe_tuple_kargs {
@@ -65,6 +66,7 @@ int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int 
                         void *ev_start, void *ev_stop);
 int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block);
 uint32_t ppe_classify_pipe_lds(int block);
+uint32_t ppe_classify_keys_lds(int block);
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
 #ifdef __cplusplus
 }

@@ -25,6 +25,20 @@
 #ifndef PPE_ABLATE
 #define PPE_ABLATE 0
 #endif
+// Diagnostic builds only (make variant NAME=trace VFLAGS=-DPPE_TRACE=1): lane 0 of every wave writes shader-clock
+// timestamps (s_memrealtime, 100 MHz) of its phases to kargs.trace, 32 words per wave (tools/trace_analyze.py):
+//   [0] kernel entry  [1] image staged  [2 + 5i + k] tile iteration i < 4: k 0 loop top, 1 window in registers,
+//   2 decoded + hashed, 3 ACL done, 4 outputs + counters issued   [22] after the loop  [31] tiles processed
+#ifndef PPE_TRACE
+#define PPE_TRACE 0
+#endif
+#define TRACE_AT(idx)                                                                      \
+    do {                                                                                   \
+        if (PPE_TRACE) {                                                                   \
+            const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                            \
+            if (lane == 0 && a.trace) a.trace[(size_t)twave * 32u + (idx)] = t_;          \
+        }                                                                                  \
+    } while (0)
 
 namespace {
 
@@ -265,9 +279,11 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[16], uint32_t len32, c
 #define IMG_LDS 1
 #define IMG_SPLIT 2
 
+// key of dimension d held in registers (walks that read nodes from global memory); d == PPE_NODE_LEAF gives 0
 __device__ __forceinline__ uint32_t node_key(uint32_t d, uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport,
                                              uint32_t proto) {
-    uint32_t key = proto;
+    uint32_t key = 0u;
+    key = d == PPE_DIM_PROTO ? proto : key;
     key = d == PPE_DIM_SIP ? sip : key;
     key = d == PPE_DIM_DIP ? dip : key;
     key = d == PPE_DIM_SPORT ? sport : key;
@@ -275,9 +291,14 @@ __device__ __forceinline__ uint32_t node_key(uint32_t d, uint32_t sip, uint32_t 
     return key;
 }
 
-#define NODE_IS_LEAF(nd) (((nd).y & 7u) == PPE_NODE_LEAF)
-#define NODE_CHILD(nd, key) (((nd).y >> 3) + ((key) > (nd).x ? 1u : 0u))
+#define NODE_IS_LEAF(nd) (PPE_NODE_DIM((nd).y) == PPE_NODE_LEAF)
+#define NODE_CHILD(nd, key) (((nd).y >> PPE_NODE_CHILD_SHIFT) + ((key) > (nd).x ? 1u : 0u))
 
+// Per-lane walk keys in LDS (IMG_LDS): each wave owns KEY_SLOTS x 64 words, slot d = dimension d of every lane
+// ([slot][lane]: a read with per-lane slots is bank-conflict free), slot PPE_NODE_LEAF = 0.  A level then costs one
+// LDS read for the key instead of a 5-way register select.
+#define KEY_SLOTS 6u
+#define KEY_WAVE_WORDS (KEY_SLOTS * 64u)
 // Classifier geometry for one launch (host-computed from the image header, ppe_image.h).
 struct AclGeo {
     uint32_t lds_iters;   // walk levels whose nodes are all staged in LDS (IMG_LDS: max_depth, IMG_GLOBAL: 0)
@@ -288,14 +309,12 @@ struct AclGeo {
     uint32_t default_action;
 };
 
-// One level of the walk for every lane: a lane already at a leaf stays there (and re-reads it), so the loops below
-// have a wave-uniform trip count and no per-lane exit: no exec-mask bookkeeping per level.
-template <class N>
-__device__ __forceinline__ void walk_level(const N *nodes, uint32_t &node, uint2 &nd, uint32_t sip, uint32_t dip,
-                                           uint32_t sport, uint32_t dport, uint32_t proto) {
-    const uint32_t child = NODE_CHILD(nd, node_key(nd.y & 7u, sip, dip, sport, dport, proto));
-    node = NODE_IS_LEAF(nd) ? node : child;
-    nd = nodes[node];
+// One level of the walk for every lane, keys from LDS: a leaf's dimension is the zero key slot, so a lane already at a
+// leaf stays there (ppe_image.h): a wave-uniform trip count, no per-lane exit, no exec-mask bookkeeping per level.
+__device__ __forceinline__ void walk_level_lds(const uint2 *nodes, const uint32_t *keys, uint2 &nd) {
+    const uint32_t key = *(const uint32_t *)((const char *)keys + (nd.y & 0x700u));          // slot dim, this lane
+    const uint32_t off = ((nd.y >> 8) & ~7u) + (key > nd.x ? 8u : 0u);                       // child byte offset
+    nd = *(const uint2 *)((const char *)nodes + off);
 }
 
 // Scan a leaf's candidate list in priority order; the first rule that matches wins (lowest index).  max_leaf
@@ -307,12 +326,13 @@ __device__ __forceinline__ void leaf_scan(uint2 nd, uint32_t max_leaf, const uin
                                           uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
                                           const Mac &mac, const uint64_t *tsp, uint32_t p, uint64_t now,
                                           int32_t &hit, uint32_t &action) {
-    const uint32_t cnt = nd.y >> 3;
+    uint32_t first = nd.x, cnt = nd.y & 0xffu;
+    if (max_leaf >= PPE_LEAF_CNT_ESC && cnt == PPE_LEAF_CNT_ESC) cnt = lf[first++];  // long list: escaped count
     bool done = false;
 #pragma unroll 1
     for (uint32_t j = 0; j < max_leaf; ++j) {
         const bool live = !done && j < cnt;
-        const uint32_t e = lf[live ? nd.x + j : 0u];  // entry 0 exists whenever max_leaf > 0
+        const uint32_t e = lf[live ? first + j : 0u];  // entry 0 exists whenever max_leaf > 0
         const uint32_t slot = e & ~PPE_LEAF_CERTAIN;
         const uint4 *rp = (const uint4 *)(rules + 8u * slot);
         const uint4 a = rp[0], b = rp[1];
@@ -349,27 +369,29 @@ __device__ __forceinline__ void leaf_scan(uint2 nd, uint32_t max_leaf, const uin
 // struct to scratch.  Levels [0, lds_iters) read the staged top of the tree from LDS, the rest from global memory.
 template <int MODE, class Mac>
 __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ gimg, const uint32_t *__restrict__ limg,
-                                           const AclGeo &g, const uint32_t sip, const uint32_t dip,
-                                           const uint32_t sport, const uint32_t dport, const uint32_t proto,
-                                           const Mac &mac, const uint64_t *tsp, uint32_t p, uint64_t now,
-                                           int32_t &hit, uint32_t &action) {
+                                           const uint32_t *keys, const AclGeo &g, const uint32_t sip,
+                                           const uint32_t dip, const uint32_t sport, const uint32_t dport,
+                                           const uint32_t proto, const Mac &mac, const uint64_t *tsp, uint32_t p,
+                                           uint64_t now, int32_t &hit, uint32_t &action) {
     const uint2 *gn = (const uint2 *)(gimg + PPE_IMG_HDR_WORDS);
     const uint2 *ln = (const uint2 *)(limg + PPE_IMG_HDR_WORDS);
-    uint32_t node = 0, it = 0;
+    uint32_t it = 0;
     uint2 nd;
     if (MODE == IMG_GLOBAL) {
         nd = gn[0];
-    } else {
+    } else if (MODE == IMG_LDS) {
+        nd = ln[0];
+#pragma unroll 2
+        for (; it < g.max_depth; ++it) walk_level_lds(ln, keys, nd);
+    } else {  // IMG_SPLIT: the staged top of the tree, keys selected in registers
         nd = ln[0];
 #pragma unroll 1
-        for (; it < g.lds_iters; ++it) walk_level(ln, node, nd, sip, dip, sport, dport, proto);
+        for (; it < g.lds_iters; ++it) nd = ln[NODE_CHILD(nd, node_key(PPE_NODE_DIM(nd.y), sip, dip, sport, dport, proto))];
     }
     if (MODE != IMG_LDS) {  // below the staged top: per-lane exit (a finished lane must not keep reading L2/HBM)
 #pragma unroll 1
-        for (; it < g.max_depth && !NODE_IS_LEAF(nd); ++it) {
-            node = NODE_CHILD(nd, node_key(nd.y & 7u, sip, dip, sport, dport, proto));
-            nd = gn[node];
-        }
+        for (; it < g.max_depth && !NODE_IS_LEAF(nd); ++it)
+            nd = gn[NODE_CHILD(nd, node_key(PPE_NODE_DIM(nd.y), sip, dip, sport, dport, proto))];
     }
     hit = -1;
     action = g.default_action;
@@ -518,14 +540,23 @@ __device__ __forceinline__ void pipe_read(uint32_t slot, uint32_t lane, uint4 &q
     q2 = make_uint4(r2.x, r2.y, r2.z, r2.w);
 }
 
-template <int MODE, bool PIPE, int BLOCK>
+// PF: how the next tile's window is fetched while this one is classified
+#define PF_NONE 0  // loaded at the top of its own iteration
+#define PF_REG 1   // register double buffer: the next tile's loads are issued before this tile's compute
+#define PF_LDS 2   // LDS-DMA slot (PIPE, above)
+
+template <int MODE, int PF, int BLOCK>
 __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
+    constexpr bool PIPE = PF == PF_LDS;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     // a separate LDS object from the image: the compiler then knows the slot DMA never aliases image reads
     __shared__ __attribute__((aligned(16))) uint32_t ring[PIPE ? BLOCK / 64 : 1][PIPE ? PIPE_SLOT_BYTES / 4 : 1];
     uint32_t *bins = smem;                   // [PPE_NBINS] packets per (status, flags) bin of this workgroup
     uint32_t *lcnt = smem + PPE_NBINS;       // [32] per-reason counters of this workgroup
-    uint32_t *limg = smem + PPE_NBINS + 32;  // staged classifier image
+    // IMG_LDS: per-wave walk keys (KEY_WAVE_WORDS per wave), then the staged classifier image
+    constexpr uint32_t KEYW = MODE == IMG_LDS ? (BLOCK / 64) * KEY_WAVE_WORDS : 0u;
+    uint32_t *lkeys = smem + PPE_NBINS + 32;
+    uint32_t *limg = lkeys + KEYW;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -533,11 +564,17 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t stride_waves = gridDim.x * (BLOCK / 64);
     uint32_t tile = blockIdx.x * (BLOCK / 64) + wv;
     const uint32_t slot = PIPE ? (uint32_t)(uintptr_t)(lptr_t)&ring[wv][0] : 0u;
+    const uint32_t twave = blockIdx.x * (BLOCK / 64) + wv;
+    uint32_t titer = 0;
+    TRACE_AT(0);
     if (PIPE && tile < ntiles) pipe_issue(a, tile, slot, lane);  // in flight during the image staging
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) smem[i] = 0;
+    uint32_t *keys = lkeys + (MODE == IMG_LDS ? wv * KEY_WAVE_WORDS + lane : 0u);  // this lane's slot 0
+    if (MODE == IMG_LDS) keys[64u * PPE_NODE_LEAF] = 0u;                           // the leaves' zero key
     if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img, limg, a.lds_words, tid);
     __syncthreads();
+    TRACE_AT(1);
     const AclGeo geo = {a.lds_iters, a.max_depth, a.max_leaf, a.off_leaf, a.off_rules, a.off_resid, a.leaf_lds,
                         a.default_action};
 
@@ -556,28 +593,39 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     // current tile's window: bytes 0..51 (w[0..12]) and the wire length
     uint4 q0, q1, q2;
     uint32_t w12, qlen;
+    // clamped (unconditional) loads of tile t's window into q*: a past-the-end lane re-reads the last packet
+    auto load_tile = [&](uint32_t t) {
+        const uint32_t pc = min((t << 6) + lane, a.n - 1u);
+        const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)pc * a.stride);
+        q0 = r4[0]; q1 = r4[1]; q2 = r4[2];
+        w12 = ((const uint32_t *)r4)[12];
+        qlen = a.len[pc];
+    };
     if (PIPE && tile < ntiles) {
         pipe_read(slot, lane, q0, q1, q2, w12, qlen);
         if (tile + stride_waves < ntiles) pipe_issue(a, tile + stride_waves, slot, lane);
     }
+    if (PF == PF_REG && tile < ntiles) load_tile(tile);
     for (; tile < ntiles; tile += stride_waves) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < a.n;
-        if (!PIPE) {
-            const uint32_t pc = min(p, a.n - 1u);
-            const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)pc * a.stride);
-            q0 = r4[0]; q1 = r4[1]; q2 = r4[2];
-            w12 = ((const uint32_t *)r4)[12];
-            qlen = a.len[pc];
-        }
+        if (PPE_TRACE && titer < 4) TRACE_AT(2 + 5 * titer);
+        if (PF == PF_NONE) load_tile(tile);
+        if (PPE_TRACE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (PPE_TRACE && titer < 4) TRACE_AT(3 + 5 * titer);
         const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                                 q2.x, q2.y, q2.z, q2.w, w12, 0u, 0u, 0u};
         const uint32_t len = valid ? qlen : 0u;
+        if (PF == PF_REG && tile + stride_waves < ntiles) load_tile(tile + stride_waves);
         Dec k = decode(w, len, a.hdr, p, a.stride, a.syn_check);
 
         uint32_t fh = 0, act;
         int32_t hit = -1;
         if (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4)) fh = flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport);
+        if (PPE_TRACE && titer < 4) {
+            asm volatile("" ::"v"(fh), "v"(k.st));  // decoded + hashed before the stamp
+            TRACE_AT(4 + 5 * titer);
+        }
         if ((PPE_ABLATE & 1) && valid && k.st == ST_ACL) {
             k.st = PPE_ST_ACL_FW;
             k.flags |= PPE_F_ACL;
@@ -585,7 +633,14 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
         if (!(PPE_ABLATE & 1) && valid && k.st == ST_ACL) {
             uint32_t rule_act;
             const MacFromWindow mac = {a.hdr, p, a.stride};
-            acl_lookup<MODE>(a.img, limg, geo, k.sip, k.dip, k.sport, k.dport, k.proto, mac, a.ts, p, a.now, hit,
+            if (MODE == IMG_LDS) {
+                keys[0] = k.sip;
+                keys[64] = k.dip;
+                keys[128] = k.sport;
+                keys[192] = k.dport;
+                keys[256] = k.proto;
+            }
+            acl_lookup<MODE>(a.img, limg, keys, geo, k.sip, k.dip, k.sport, k.dport, k.proto, mac, a.ts, p, a.now, hit,
                              rule_act);
             const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
             k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
@@ -593,6 +648,10 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
         }
         const uint32_t st = k.st;
         act = (uint32_t)(act_table >> (2u * st)) & 3u;
+        if (PPE_TRACE && titer < 4) {
+            asm volatile("" ::"v"(hit), "v"(act));
+            TRACE_AT(5 + 5 * titer);
+        }
 
         // next tile: its DMA has had this whole tile's compute to land; take it into registers and start the one
         // after (the stores below are issued after this wait, so it never waits on this tile's own stores)
@@ -639,11 +698,15 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
             atomicAdd(&bins[st | ((k.flags & PPE_F_VLAN) ? 32u : 0u) | ((k.flags & PPE_F_TCP) ? 64u : 0u) |
                             ((k.flags & PPE_F_L4) ? 128u : 0u)],
                       1u);
+        if (PPE_TRACE && titer < 4) TRACE_AT(6 + 5 * titer);
+        ++titer;
         // the slot was emptied by pipe_read above; refill it with the tile after next (issued here, where little
         // is live, rather than right after the read)
         if (PIPE && tile + 2u * stride_waves < ntiles) pipe_issue(a, tile + 2u * stride_waves, slot, lane);
     }
 
+    TRACE_AT(22);
+    if (PPE_TRACE && lane == 0 && a.trace) a.trace[(size_t)twave * 32u + 31u] = titer;
     __syncthreads();
     for (uint32_t b = tid; b < PPE_NBINS; b += BLOCK) {  // expand the bins into counter increments
         const uint32_t c = bins[b];
@@ -661,8 +724,12 @@ template <bool LDS_IMG>
 __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t tid = threadIdx.x;
+    constexpr uint32_t KEYW = LDS_IMG ? (PPE_BLOCK / 64) * KEY_WAVE_WORDS : 0u;
+    uint32_t *keys = smem + (tid >> 6) * KEY_WAVE_WORDS + (tid & 63u);
+    uint32_t *limg = smem + KEYW;
     if (LDS_IMG) {
-        stage_image<PPE_BLOCK>(a.img, smem, a.img_words, tid);
+        keys[64u * PPE_NODE_LEAF] = 0u;
+        stage_image<PPE_BLOCK>(a.img, limg, a.img_words, tid);
         __syncthreads();
     }
     const uint32_t depth = a.img[PPE_IMG_W_MAXDEPTH];
@@ -675,11 +742,18 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
         int32_t hit;
         uint32_t act;
         const MacValues mac = {m.x, m.y, m.z, m.w};
+        if (LDS_IMG) {
+            keys[0] = t.x;
+            keys[64] = t.y;
+            keys[128] = t.z & 0xffffu;
+            keys[192] = t.z >> 16;
+            keys[256] = t.w & 0xffu;
+        }
         if (LDS_IMG)
-            acl_lookup<IMG_LDS>(a.img, smem, geo, t.x, t.y, t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i, a.now,
+            acl_lookup<IMG_LDS>(a.img, limg, keys, geo, t.x, t.y, t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i, a.now,
                                 hit, act);
         else
-            acl_lookup<IMG_GLOBAL>(a.img, smem, geo, t.x, t.y, t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i,
+            acl_lookup<IMG_GLOBAL>(a.img, limg, keys, geo, t.x, t.y, t.z & 0xffffu, t.z >> 16, t.w & 0xffu, mac, a.ts, i,
                                    a.now, hit, act);
         if (a.hit) a.hit[i] = hit;
         if (a.action) a.action[i] = act;
@@ -688,7 +762,7 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
 
 }  // namespace
 
-template <int M, bool P, int B>
+template <int M, int P, int B>
 static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     // hipExtLaunchKernelGGL's events are the dispatch packet's own start/end timestamps (what rocprofv3 reports),
     // unlike hipEventRecord markers around the launch
@@ -696,16 +770,18 @@ static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t
     return (int)hipGetLastError();
 }
 
-template <int M, bool P, int B>
+template <int M, int P, int B>
 static int occ_t(size_t shmem) {
     int nb = 0;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, P, B>, B, shmem) == hipSuccess
                ? nb : -1;
 }
 
-static size_t classify_shmem(uint32_t lds_words, int mode) {
+static size_t classify_shmem(uint32_t lds_words, int mode, int block) {
     const size_t base = (PPE_NBINS + 32u) * sizeof(uint32_t);  // counter bins + per-reason counters
-    return mode != IMG_GLOBAL ? base + (((size_t)lds_words * 4u + 1023u) & ~(size_t)1023u) : base;
+    if (mode == IMG_GLOBAL) return base;
+    const size_t keys = mode == IMG_LDS ? (size_t)(block / 64) * KEY_WAVE_WORDS * 4u : 0u;
+    return base + keys + (((size_t)lds_words * 4u + 1023u) & ~(size_t)1023u);
 }
 
 #define PPE_DISPATCH_B(FN, M, P, ...)                                \
@@ -716,21 +792,27 @@ static size_t classify_shmem(uint32_t lds_words, int mode) {
     } while (0)
 #define PPE_DISPATCH_P(FN, M, ...)                                   \
     do {                                                             \
-        if (pipe) PPE_DISPATCH_B(FN, M, true, __VA_ARGS__);          \
-        PPE_DISPATCH_B(FN, M, false, __VA_ARGS__);                   \
+        if (pipe == PF_LDS) PPE_DISPATCH_B(FN, M, PF_LDS, __VA_ARGS__); \
+        if (pipe == PF_REG) PPE_DISPATCH_B(FN, M, PF_REG, __VA_ARGS__); \
+        PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__);                 \
     } while (0)
-// the pipeline is built for the whole-image-in-LDS variant only: with tree nodes or rules read from global memory
-// every such load waits (in-order vmcnt) for the next tile's DMA, which defeats the overlap
+#define PPE_DISPATCH_Q(FN, M, ...)                                   \
+    do {                                                             \
+        if (pipe == PF_REG) PPE_DISPATCH_B(FN, M, PF_REG, __VA_ARGS__); \
+        PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__);                 \
+    } while (0)
+// the LDS-DMA pipeline is built for the whole-image-in-LDS variant only: with tree nodes or rules read from global
+// memory every such load waits (in-order vmcnt) for the next tile's DMA, which defeats the overlap
 #define PPE_DISPATCH(FN, ...)                                        \
     do {                                                             \
         if (mode == IMG_LDS) PPE_DISPATCH_P(FN, IMG_LDS, __VA_ARGS__);     \
-        if (mode == IMG_SPLIT) PPE_DISPATCH_B(FN, IMG_SPLIT, false, __VA_ARGS__); \
-        PPE_DISPATCH_B(FN, IMG_GLOBAL, false, __VA_ARGS__);          \
+        if (mode == IMG_SPLIT) PPE_DISPATCH_Q(FN, IMG_SPLIT, __VA_ARGS__); \
+        PPE_DISPATCH_Q(FN, IMG_GLOBAL, __VA_ARGS__);                 \
     } while (0)
 
 extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, void *stream,
                                    void *ev_start, void *ev_stop) {
-    const size_t shmem = classify_shmem(a->lds_words, mode);
+    const size_t shmem = classify_shmem(a->lds_words, mode, block);
     hipStream_t s = (hipStream_t)stream;
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     PPE_DISPATCH(launch_t, a, grid, shmem, s, e0, e1);
@@ -738,16 +820,19 @@ extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, 
 
 // resident workgroups per CU for the kernel variant (the persistent grid is sized to exactly fill the chip)
 extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block) {
-    const size_t shmem = classify_shmem(lds_words, mode);
+    const size_t shmem = classify_shmem(lds_words, mode, block);
     PPE_DISPATCH(occ_t, shmem);
 }
 
 // static LDS of the pipelined kernel (the per-wave DMA slots), for the engine's LDS budget
 extern "C" uint32_t ppe_classify_pipe_lds(int block) { return (uint32_t)(block / 64) * PIPE_SLOT_BYTES; }
+// dynamic LDS of the whole-image-in-LDS variant beyond counters + image (the per-wave walk keys)
+extern "C" uint32_t ppe_classify_keys_lds(int block) { return (uint32_t)(block / 64) * KEY_WAVE_WORDS * 4u; }
 
 extern "C" int ppe_launch_acl_tuples(const ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream) {
     if (lds_img) {
-        const size_t shmem = ((size_t)a->img_words * 4u + 1023u) & ~(size_t)1023u;
+        const size_t shmem = (size_t)(PPE_BLOCK / 64) * KEY_WAVE_WORDS * 4u +
+                             (((size_t)a->img_words * 4u + 1023u) & ~(size_t)1023u);
         hipLaunchKernelGGL(ppe_acl_tuple_kernel<true>, dim3(grid), dim3(PPE_BLOCK), shmem, (hipStream_t)stream, *a);
     } else {
         hipLaunchKernelGGL(ppe_acl_tuple_kernel<false>, dim3(grid), dim3(PPE_BLOCK), 0, (hipStream_t)stream, *a);

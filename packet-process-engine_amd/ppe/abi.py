@@ -98,7 +98,7 @@ EXPORTS = [
     "ppe_classify_host", "ppe_acl_lookup", "ppe_acl_lookup_host", "ppe_dev_alloc", "ppe_dev_free",
     "ppe_host_alloc", "ppe_host_free", "ppe_memcpy_h2d", "ppe_memcpy_d2h", "ppe_memset_d", "ppe_sync",
     "ppe_counters_read", "ppe_counters_clear", "ppe_timing_enable", "ppe_timing_read", "ppe_acl_image",
-    "ppe_launch_info", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
+    "ppe_launch_info", "ppe_debug_trace", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
     "ppe_get_tuning",
     # ppe_acl.h
     "ppe_rule_list_init", "ppe_rule_list_free", "Rule_add", "Rule_del_by_id", "Rule_del_all",
@@ -160,6 +160,7 @@ def _open(p: Path, mode) -> C.CDLL:
         "ppe_timing_read": ([vp, C.POINTER(C.c_double), C.POINTER(u32), C.c_int], C.c_int),
         "ppe_acl_image": ([vp, vp, C.POINTER(u32)], C.c_int),
         "ppe_launch_info": ([vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], C.c_int),
+        "ppe_debug_trace": ([vp, vp], C.c_int),
         "ppe_last_error": ([vp], C.c_char_p),
         "ppe_set_tuning": ([vp, C.POINTER(Tuning)], C.c_int),
         "ppe_get_tuning": ([vp, C.POINTER(Tuning)], C.c_int),

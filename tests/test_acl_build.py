@@ -95,9 +95,43 @@ def test_large_ruleset_builds_bounded():
 def test_image_layout():
     rules = synth.make_rules(64)
     img, st = abi.build_image(rules)
-    assert img[0] == 0x41455050 and img[1] == 1
+    assert img[0] == 0x41455050
     assert img[2] == st["n_nodes"] and img[4] == 64 and img[11] == len(img)
     assert img[7] % 8 == 0  # rules 32-B aligned
     nodes = img[16:16 + 2 * img[2]].reshape(-1, 2)
-    leaves = nodes[(nodes[:, 1] & 7) == 7]
-    assert img[10] >= 1 and img[12] == (leaves[:, 1] >> 3).max()  # max depth, max leaf entries
+    dim = (nodes[:, 1] >> 8) & 7
+    is_leaf = dim == 5
+    leaves = nodes[is_leaf]
+    assert img[10] >= 1 and img[12] == (leaves[:, 1] & 0xFF).max()  # max depth, max leaf entries
+    assert (dim[~is_leaf] <= 4).all()  # internal: a real dimension
+    assert ((leaves[:, 1] >> 11) == np.nonzero(is_leaf)[0]).all()  # a leaf's child is itself (walk fixed point)
+    assert img[1] == 2
+
+
+def test_long_leaf_list_escape():
+    """More than 254 candidates in one leaf (rules the 5-tuple cannot separate: same box, different MACs) use the
+    escaped count word; the walk must still find the lowest matching index."""
+    n = 600
+    rules = np.zeros(n, RULE_DTYPE)
+    rules["sip"] = 0x0A000000
+    rules["sip_mask"] = 8
+    rules["sport_end"] = rules["dport_end"] = 0xFFFF
+    rules["protocol_end"] = 0xFF
+    rules["action"] = np.arange(n) & 1
+    macs = np.arange(1, n + 1, dtype=np.uint64)
+    for b in range(6):
+        rules["dmac"][:, b] = (macs >> np.uint64(8 * b)) & np.uint64(0xFF)
+    img, st = abi.build_image(rules, default_action=1)
+    nodes = img[16:16 + 2 * img[2]].reshape(-1, 2)
+    assert ((nodes[:, 1] & 0xFF) == 255).any() and img[12] >= n
+    pk = synth.make_packets(4000, rules, seed=5, kind="udp64", stride=64)
+    # point some packets' dmac at late rules
+    idx = np.arange(0, 4000, 7)
+    want = (idx * 13) % n
+    for b in range(6):
+        pk["hdr"][idx, b] = ((want + 1) >> (8 * b)) & 0xFF
+    o = pyoracle.Oracle(rules, default_action=1, image=img)
+    tree = o.classify_batch(pk["hdr"], pk["len"], nthreads=8, use_tree=True)
+    lin = o.classify_batch(pk["hdr"], pk["len"], nthreads=8)
+    assert np.array_equal(tree["acl_hit"], lin["acl_hit"])
+    assert (lin["acl_hit"] >= 300).any()

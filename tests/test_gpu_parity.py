@@ -210,8 +210,9 @@ def test_argument_errors(eng):
 
 
 TUNINGS = [dict(lds_image=0), dict(block=512), dict(block=1024), dict(block=256), dict(pipeline=1),
-           dict(pipeline=2, block=256), dict(pipeline=2, block=512), dict(pipeline=2, lds_image=0),
-           dict(pipeline=1, lds_image=0), dict(blocks_per_cu=16), dict(blocks_per_cu=1)]
+           dict(pipeline=2), dict(pipeline=2, block=256), dict(pipeline=2, block=512), dict(pipeline=2, lds_image=0),
+           dict(pipeline=1, lds_image=0), dict(pipeline=3), dict(pipeline=3, lds_image=0), dict(pipeline=3, block=1024),
+           dict(blocks_per_cu=16), dict(blocks_per_cu=1)]
 
 
 @pytest.mark.parametrize("tune", TUNINGS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))

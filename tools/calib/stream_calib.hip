@@ -36,6 +36,30 @@ __global__ __launch_bounds__(256) void k_row(Args a) {
     }
 }
 
+// 1b. row per lane + K rounds of dummy VALU work per packet (8 independent chains, ~2 instr per chain per round):
+// how much per-tile compute the HBM stream hides
+template <int K>
+__global__ __launch_bounds__(256) void k_rowc(Args a) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ntiles = (a.n + 63) >> 6;
+    uint32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t step = gridDim.x * 4;
+    for (; tile < ntiles; tile += step) {
+        const uint32_t p = tile * 64 + lane;
+        if (p >= a.n) continue;
+        const uint4 *r = (const uint4 *)(a.hdr + (size_t)p * 64);
+        const uint4 q0 = r[0], q1 = r[1], q2 = r[2], q3 = r[3];
+        const uint32_t l = a.len[p];
+        uint32_t c[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) c[j] = (c[j] ^ (c[(j + 1) & 7] >> 3)) + 0x9e3779b9u;
+        const uint32_t x = c[0] ^ c[1] ^ c[2] ^ c[3] ^ c[4] ^ c[5] ^ c[6] ^ c[7] ^ q2.x ^ q3.y;
+        emit(a, p, x, l);
+    }
+}
+
 // 2. coalesced: each 16-B load instruction covers 1 KB contiguous; the packet's 64 B end up in 4 lanes, gathered
 // back with an LDS transpose (row-per-lane afterwards, like the classify kernel needs)
 template <bool PERSIST>
@@ -167,7 +191,9 @@ int main(int argc, char **argv) {
               {"flat persist 8/CU", 4, (uint32_t)ncu * 8}, {"flat 1 vec/thread", 4, (n * 4 + 255) / 256},
               {"soa  1tile/wave", 5, (tiles + 3) / 4}, {"soa  persist 8/CU", 6, (uint32_t)ncu * 8},
               {"dma2 persist 4/CU", 7, (uint32_t)ncu * 4}, {"dma2 persist 8/CU", 7, (uint32_t)ncu * 8},
-              {"dma3 persist 4/CU", 8, (uint32_t)ncu * 4}};
+              {"dma3 persist 4/CU", 8, (uint32_t)ncu * 4},
+              {"row+VALU x8 (~200/tile)", 9, (uint32_t)ncu * 8}, {"row+VALU x16 (~400/tile)", 10, (uint32_t)ncu * 8},
+              {"row+VALU x32 (~800/tile)", 11, (uint32_t)ncu * 8}, {"row+VALU x64 (~1600/tile)", 12, (uint32_t)ncu * 8}};
     const int iters = 200;
     for (const V &v : vs) {
         std::vector<float> t;
@@ -184,6 +210,10 @@ int main(int argc, char **argv) {
             case 6: hipExtLaunchKernelGGL(k_soa<true>, dim3(v.grid), dim3(256), 0, 0, s, f, 0, a); break;
             case 7: hipExtLaunchKernelGGL(k_dma<2>, dim3(v.grid), dim3(256), 0, 0, s, f, 0, a); break;
             case 8: hipExtLaunchKernelGGL(k_dma<3>, dim3(v.grid), dim3(256), 0, 0, s, f, 0, a); break;
+            case 9: hipExtLaunchKernelGGL(k_rowc<8>, dim3(v.grid), dim3(256), 0, 0, s, f, 0, a); break;
+            case 10: hipExtLaunchKernelGGL(k_rowc<16>, dim3(v.grid), dim3(256), 0, 0, s, f, 0, a); break;
+            case 11: hipExtLaunchKernelGGL(k_rowc<32>, dim3(v.grid), dim3(256), 0, 0, s, f, 0, a); break;
+            case 12: hipExtLaunchKernelGGL(k_rowc<64>, dim3(v.grid), dim3(256), 0, 0, s, f, 0, a); break;
             }
             if (it >= 20) { CK(hipEventSynchronize(e1)); float ms; CK(hipEventElapsedTime(&ms, e0, e1)); t.push_back(ms); }
         }
