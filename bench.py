@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (16 threads)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,19 +199,33 @@ def main():
         img = eng.image()
         o = pyoracle.Oracle(rules, default_action=1, image=img)
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        reps = 16
         o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=thr, use_tree=True)
+        # bounded sample: whole passes over the batch until ~10 s of wall time (x thr cores), then a ~2 s 1-thread run
+        reps = 0
         tc = time.perf_counter()
-        for _ in range(reps):
+        while time.perf_counter() - tc < args.cpu_seconds:
             o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=thr, use_tree=True)
+            reps += 1
         cpu_s = time.perf_counter() - tc
+        ones = 0
         t1 = time.perf_counter()
-        o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=1, use_tree=True)
-        one_s = time.perf_counter() - t1
+        while time.perf_counter() - t1 < args.cpu_seconds / 5:
+            o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=1, use_tree=True)
+            ones += 1
+        one_s = (time.perf_counter() - t1) / ones
         cpu = {"value": n * reps / cpu_s / 1e6, "unit": "Mpps", "cores": thr, "kind": "port",
-               "sample": f"{reps} passes over the {n}-packet {args.config} batch ({n * reps} packets), "
-                         f"{thr} pthreads run-to-completion shards; 1-thread rate {n / one_s / 1e6:.2f} Mpps",
+               "sample": f"{reps} passes over the {n}-packet {args.config} batch ({n * reps} packets, {cpu_s:.1f} s), "
+                         f"{thr} pthreads run-to-completion shards; 1-thread rate {n / one_s / 1e6:.2f} Mpps "
+                         f"({ones} passes)",
                "single_thread_mpps": n / one_s / 1e6}
+
+    # HBM bytes per launch from the committed rocprofv3 PMC profile of this config (tools/collect_traffic.py)
+    traffic = None
+    tfiles = sorted(Path(__file__).resolve().parent.glob(f"profiles/*traffic_{args.config}.json"))
+    if tfiles and n == cfgd["n"] and stride == 64:
+        tj = json.load(open(tfiles[-1]))
+        if tj.get("n_packets") == n:
+            traffic = round(tj["traffic_bytes"])
 
     if rank == 0:
         li = eng.launch_info()
@@ -223,7 +238,7 @@ def main():
                        "packets_per_gpu": n, "rules": cfgd["rules"], "window_bytes": stride, "resident_batches": nbufs,
                        "parallelism": f"batch-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": rd + wr,
                          "launches_timed": launches},
             "cpu_baseline": cpu,

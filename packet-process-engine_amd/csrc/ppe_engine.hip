@@ -26,8 +26,9 @@ namespace {
 constexpr int kSlotSets = 4;      // set 0: ppe_classify; 1..3: host pipeline streams
 constexpr int kHostStreams = 3;
 #ifndef PPE_PIPE_DEFAULT
-// next-tile fetch of the classify kernel (PF_* in ppe_kernels.hip): 0 none, 1 register double buffer, 2 LDS-DMA
-#define PPE_PF_DEFAULT 0  // none: register (28.3 us) and LDS-DMA (24.4) prefetch measured slower on C1 (22.2)
+// next-tile fetch of the classify kernel (PF_* in ppe_kernels.hip): 0 none, 1 register double buffer, 2 LDS-DMA,
+// 3 none with the first tile's loads before the image staging
+#define PPE_PF_DEFAULT 3  // hoisted first load: C1 21.7 us vs none 22.2; register (28.3) / LDS-DMA (24.4) prefetch slower
 #endif
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 
@@ -102,7 +103,7 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl >= 1 && pl <= 3 ? (uint32_t)pl : 0u;
+    t.pipeline = pl >= 1 && pl <= 4 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     return t;
 }
@@ -165,9 +166,9 @@ StagePlan stage_plan_for(const ppe_ctx *c, const std::vector<uint32_t> &img, int
 // The LDS-DMA pipeline runs only with the whole image in LDS (see PPE_DISPATCH); when the image with the pipeline's
 // slots does not fit, the plan falls back to the non-pipelined kernel.
 StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
-    // tuning.pipeline: 0 automatic, 1 none, 2 LDS-DMA, 3 register double buffer
-    static const int kPf[4] = {PPE_PF_DEFAULT, 0, 2, 1};
-    const int pf = kPf[c->tune.pipeline & 3u];
+    // tuning.pipeline: 0 automatic, 1 none, 2 LDS-DMA, 3 register double buffer, 4 first load before the staging
+    static const int kPf[5] = {PPE_PF_DEFAULT, 0, 2, 1, 3};
+    const int pf = kPf[std::min(c->tune.pipeline, 4u)];
     if (pf == 2 && c->tune.lds_image) {
         const StagePlan p = stage_plan_for(c, img, 2);
         if (p.mode == 1) return p;
@@ -622,8 +623,9 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline > 3)
-        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto), 1 (none), 2 (LDS-DMA) or 3 (register prefetch)");
+    if (t->pipeline > 4)
+        return fail(c, PPE_EINVAL,
+                    "pipeline must be 0 (auto), 1 (none), 2 (LDS-DMA), 3 (register prefetch) or 4 (hoisted first load)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     c->tune = *t;
     c->tune.pipeline = t->pipeline;

@@ -544,6 +544,7 @@ __device__ __forceinline__ void pipe_read(uint32_t slot, uint32_t lane, uint4 &q
 #define PF_NONE 0  // loaded at the top of its own iteration
 #define PF_REG 1   // register double buffer: the next tile's loads are issued before this tile's compute
 #define PF_LDS 2   // LDS-DMA slot (PIPE, above)
+#define PF_HOIST 3 // as PF_NONE, but the first tile's loads are issued before the image staging
 
 template <int MODE, int PF, int BLOCK>
 __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
@@ -566,8 +567,21 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t slot = PIPE ? (uint32_t)(uintptr_t)(lptr_t)&ring[wv][0] : 0u;
     const uint32_t twave = blockIdx.x * (BLOCK / 64) + wv;
     uint32_t titer = 0;
+    bool titer_any = false;  // a tile was processed already (PF_HOIST: the first one was loaded in the prologue)
     TRACE_AT(0);
     if (PIPE && tile < ntiles) pipe_issue(a, tile, slot, lane);  // in flight during the image staging
+    // current tile's window: bytes 0..51 (w[0..12]) and the wire length
+    uint4 q0, q1, q2;
+    uint32_t w12, qlen;
+    // clamped (unconditional) loads of tile t's window into q*: a past-the-end lane re-reads the last packet
+    auto load_tile = [&](uint32_t t) {
+        const uint32_t pc = min((t << 6) + lane, a.n - 1u);
+        const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)pc * a.stride);
+        q0 = r4[0]; q1 = r4[1]; q2 = r4[2];
+        w12 = ((const uint32_t *)r4)[12];
+        qlen = a.len[pc];
+    };
+    if (PF == PF_HOIST && tile < ntiles) load_tile(tile);  // first window in flight during the image staging
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) smem[i] = 0;
     uint32_t *keys = lkeys + (MODE == IMG_LDS ? wv * KEY_WAVE_WORDS + lane : 0u);  // this lane's slot 0
@@ -590,17 +604,6 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
         act_table |= ac << (2u * st);
     }
 
-    // current tile's window: bytes 0..51 (w[0..12]) and the wire length
-    uint4 q0, q1, q2;
-    uint32_t w12, qlen;
-    // clamped (unconditional) loads of tile t's window into q*: a past-the-end lane re-reads the last packet
-    auto load_tile = [&](uint32_t t) {
-        const uint32_t pc = min((t << 6) + lane, a.n - 1u);
-        const uint4 *r4 = (const uint4 *)(a.hdr + (size_t)pc * a.stride);
-        q0 = r4[0]; q1 = r4[1]; q2 = r4[2];
-        w12 = ((const uint32_t *)r4)[12];
-        qlen = a.len[pc];
-    };
     if (PIPE && tile < ntiles) {
         pipe_read(slot, lane, q0, q1, q2, w12, qlen);
         if (tile + stride_waves < ntiles) pipe_issue(a, tile + stride_waves, slot, lane);
@@ -610,7 +613,8 @@ __global__ __launch_bounds__(BLOCK, 8) void ppe_classify_kernel(ppe_kargs a) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < a.n;
         if (PPE_TRACE && titer < 4) TRACE_AT(2 + 5 * titer);
-        if (PF == PF_NONE) load_tile(tile);
+        if (PF == PF_NONE || (PF == PF_HOIST && titer_any)) load_tile(tile);
+        titer_any = true;
         if (PPE_TRACE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (PPE_TRACE && titer < 4) TRACE_AT(3 + 5 * titer);
         const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
@@ -794,11 +798,13 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int block) {
     do {                                                             \
         if (pipe == PF_LDS) PPE_DISPATCH_B(FN, M, PF_LDS, __VA_ARGS__); \
         if (pipe == PF_REG) PPE_DISPATCH_B(FN, M, PF_REG, __VA_ARGS__); \
+        if (pipe == PF_HOIST) PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__); \
         PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__);                 \
     } while (0)
 #define PPE_DISPATCH_Q(FN, M, ...)                                   \
     do {                                                             \
         if (pipe == PF_REG) PPE_DISPATCH_B(FN, M, PF_REG, __VA_ARGS__); \
+        if (pipe == PF_HOIST) PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__); \
         PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__);                 \
     } while (0)
 // the LDS-DMA pipeline is built for the whole-image-in-LDS variant only: with tree nodes or rules read from global

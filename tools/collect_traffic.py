@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the classify kernel from rocprofv3 PMC passes, calibrated on the memory-skeleton
+kernel of tools/calib/stream_calib.hip (same access pattern, known byte count), as MI355X_MICROARCH.md's HBM section
+prescribes (FETCH_SIZE is only calibrated for 16-B-per-lane coalesced reads; ours are row-per-lane).
+
+  python tools/collect_traffic.py --fetch <bench fetch csv> --write <bench write csv> \
+      --cal-fetch <calib fetch csv> --cal-write <calib write csv> --n 1048576 --out profiles/r1_traffic_C1.json
+"""
+import argparse
+import csv
+import json
+import statistics
+
+
+def per_dispatch(path, kernel, counter):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--cal-fetch", required=True)
+    ap.add_argument("--cal-write", required=True)
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--cal-kernel", default="k_row<true>")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    n = a.n
+    f = statistics.median(per_dispatch(a.fetch, "ppe_classify_kernel", "FETCH_SIZE"))
+    w = statistics.median(per_dispatch(a.write, "ppe_classify_kernel", "WRITE_SIZE"))
+    cf = statistics.median(per_dispatch(a.cal_fetch, a.cal_kernel, "FETCH_SIZE"))
+    cw = statistics.median(per_dispatch(a.cal_write, a.cal_kernel, "WRITE_SIZE"))
+    cal_rd, cal_wr = n * 68, n * 16  # skeleton: 64-B window + 4-B length read, 4 x 4-B results written
+    kr, kw = cal_rd / cf, cal_wr / cw  # bytes per counter unit for this access pattern
+    alg_rd, alg_wr = n * 68, n * 16 + ((n + 63) // 64) * 4
+    out = {"n_packets": n, "fetch_size_raw": f, "write_size_raw": w, "calib": {"fetch_raw": cf, "write_raw": cw,
+           "bytes_per_fetch_unit": kr, "bytes_per_write_unit": kw, "kernel": a.cal_kernel},
+           "read_bytes": f * kr, "write_bytes": w * kw, "traffic_bytes": f * kr + w * kw,
+           "algorithmic_bytes": alg_rd + alg_wr,
+           "traffic_over_algorithmic": (f * kr + w * kw) / (alg_rd + alg_wr)}
+    json.dump(out, open(a.out, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
