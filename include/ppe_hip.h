@@ -204,15 +204,15 @@ int  ppe_acl_image(ppe_ctx_t *ctx, uint32_t *words, uint32_t *n_words);
 typedef struct {
     uint32_t block;          /* workgroup size 256, 512 or 1024; 0 = chosen per classifier image   */
     uint32_t blocks_per_cu;  /* workgroups per CU (<= 32); 0 = resident count from the occupancy API */
-    uint32_t pipeline;       /* tile fetch: 0 auto, 1 none, 2 LDS-DMA slot, 3 register prefetch,
-                                4 first tile requested before the image staging                     */
+    uint32_t pipeline;       /* tile fetch: 0 auto (= 4), 1 first tile loaded at the loop top,
+                                4 first tile requested before the image staging; others PPE_EINVAL  */
     uint32_t lds_image;      /* 1 = stage the image (or its top) in LDS, 0 = read it from global   */
 } ppe_tuning_t;
 int  ppe_set_tuning(ppe_ctx_t *ctx, const ppe_tuning_t *t);
 int  ppe_get_tuning(ppe_ctx_t *ctx, ppe_tuning_t *t);
 
 /* Launch geometry in use (for profiling notes).  variant = image mode (0 global, 1 LDS, 2 split) | fetch << 4
- * (fetch 0 none, 1 register prefetch, 2 LDS-DMA, 3 hoisted first load). */
+ * (fetch 0 first tile at the loop top, 1 first tile requested before the image staging). */
 int  ppe_launch_info(ppe_ctx_t *ctx, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes, uint32_t *variant);
 
 /* Diagnostics: device buffer for per-wave phase timestamps written by a library built with -DPPE_TRACE (make

@@ -134,42 +134,56 @@ static uint32_t mac_lo(const uint8_t *m) {
 }
 static uint32_t mac_hi(const uint8_t *m) { return (uint32_t)m[4] | ((uint32_t)m[5] << 8); }
 
+/* Walk of the device classifier image (format v3, packet-process-engine_amd/csrc/ppe_image.h): the same tree the
+ * GPU walks, checked here against oracle_acl_linear (the definition).  Test infrastructure only. */
+static int oracle_rule_match(const uint32_t *im, uint32_t slot, uint32_t sip, uint32_t dip, uint32_t sport,
+                             uint32_t dport, uint32_t proto, const uint8_t *dmac, const uint8_t *smac, uint64_t ts) {
+    const uint32_t *r = im + im[PPE_IMG_W_OFFRULES] + 8u * slot;
+    int m = sip - r[0] <= r[1] && dip - r[2] <= r[3] && (uint16_t)(sport - (r[4] & 0xffffu)) <= (r[5] & 0xffffu) &&
+            (uint16_t)(dport - (r[4] >> 16)) <= (r[5] >> 16) && proto - (r[6] & 0xffu) <= ((r[6] >> 8) & 0xffu);
+    const uint32_t rs = r[7] >> 29;
+    const uint32_t *x8 = im + im[PPE_IMG_W_OFFRESID] + 8u * slot;
+    if (m && (rs & PPE_RESID_DMAC)) m = x8[0] == mac_lo(dmac) && x8[1] == mac_hi(dmac);
+    if (m && (rs & PPE_RESID_SMAC)) m = x8[2] == mac_lo(smac) && x8[3] == mac_hi(smac);
+    if (m && (rs & PPE_RESID_TIME)) {
+        const uint64_t t0 = x8[4] | ((uint64_t)x8[5] << 32), t1 = x8[6] | ((uint64_t)x8[7] << 32);
+        m = ts >= t0 && ts <= t1;
+    }
+    return m;
+}
+
 int32_t oracle_acl_tree(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
                         const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action) {
     const uint32_t *im = g_img;
-    const uint32_t key[5] = {sip, dip, sport, dport, proto};
-    uint32_t node = 0;
-    for (int it = 0; it <= PPE_MAX_DEPTH; it++) {
-        const uint32_t x = im[PPE_IMG_HDR_WORDS + 2 * node], y = im[PPE_IMG_HDR_WORDS + 2 * node + 1];
-        if (PPE_NODE_DIM(y) == PPE_NODE_LEAF) {
-            uint32_t first = x, cnt = y & 0xffu;
-            if (cnt == PPE_LEAF_CNT_ESC) cnt = im[im[PPE_IMG_W_OFFLEAF] + first++];
-            const uint32_t *lf = im + im[PPE_IMG_W_OFFLEAF] + first;
-            for (uint32_t j = 0; j < cnt; j++) {
-                const uint32_t slot = lf[j] & ~PPE_LEAF_CERTAIN;
-                const uint32_t *r = im + im[PPE_IMG_W_OFFRULES] + 8 * slot;
-                int m = (lf[j] & PPE_LEAF_CERTAIN) != 0;
-                if (!m) {
-                    m = sip >= r[0] && sip <= r[1] && dip >= r[2] && dip <= r[3] && sport >= (r[4] & 0xffffu) &&
-                        sport <= (r[4] >> 16) && dport >= (r[5] & 0xffffu) && dport <= (r[5] >> 16) &&
-                        proto >= (r[6] & 0xffu) && proto <= ((r[6] >> 8) & 0xffu);
-                    const uint32_t rs = r[7] >> 29;
-                    const uint32_t *x8 = im + im[PPE_IMG_W_OFFRESID] + 8 * slot;
-                    if (m && (rs & PPE_RESID_DMAC)) m = x8[0] == mac_lo(dmac) && x8[1] == mac_hi(dmac);
-                    if (m && (rs & PPE_RESID_SMAC)) m = x8[2] == mac_lo(smac) && x8[3] == mac_hi(smac);
-                    if (m && (rs & PPE_RESID_TIME)) {
-                        const uint64_t t0 = x8[4] | ((uint64_t)x8[5] << 32), t1 = x8[6] | ((uint64_t)x8[7] << 32);
-                        m = ts >= t0 && ts <= t1;
-                    }
-                }
-                if (m) {
-                    if (action) *action = r[6] >> 16;
-                    return (int32_t)(r[7] & 0x1fffffffu);
-                }
-            }
-            break;
+    const uint32_t key[6] = {sip, dip, sport, dport, proto, 0u};
+    uint32_t noff = 4u * PPE_IMG_HDR_WORDS, ks = im[PPE_IMG_W_ROOTKS] >> 8;
+    const uint32_t *nd = im + noff / 4u;
+    for (int it = 0; it <= PPE_MAX_DEPTH + 1; it++) {
+        nd = im + noff / 4u;
+        if (nd[0] == PPE_LEAF_THR) break;
+        const int gt = key[ks] > nd[0];
+        noff = gt ? nd[2] : nd[1];
+        ks = ((gt ? nd[3] >> 16 : nd[3]) >> 8) & 0xffu;
+    }
+    const uint32_t max_leaf = im[PPE_IMG_W_MAXLEAF];
+    uint32_t first = 0, cnt = 0;
+    const uint32_t *lf = im + im[PPE_IMG_W_OFFLEAF];
+    uint32_t one = nd[2];
+    if (max_leaf <= 1) {
+        lf = &one;  /* payload = the candidate slot, or the sentinel (n_rules: matches all, index -1, default) */
+        cnt = 1;
+    } else {
+        first = nd[2] & 0xffffffu;
+        cnt = nd[2] >> 24;
+        if (cnt == PPE_LEAF_CNT_ESC) cnt = lf[first++];
+    }
+    for (uint32_t j = 0; j < cnt; j++) {
+        const uint32_t slot = lf[first + j];
+        if (oracle_rule_match(im, slot, sip, dip, sport, dport, proto, dmac, smac, ts)) {
+            const uint32_t *r = im + im[PPE_IMG_W_OFFRULES] + 8u * slot;
+            if (action) *action = r[6] >> 16;
+            return (int32_t)(r[7] << 3) >> 3;
         }
-        node = (y >> PPE_NODE_CHILD_SHIFT) + (key[PPE_NODE_DIM(y)] > x ? 1u : 0u);
     }
     if (action) *action = im[PPE_IMG_W_DEFACT];
     return -1;

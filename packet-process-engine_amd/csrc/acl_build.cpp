@@ -114,7 +114,14 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     }
 
     // ---- recursive partitioning, BFS so that children are contiguous and numbered after their parent ----
-    std::vector<uint32_t> nodes;  // 2 words per node
+    struct TNode {
+        uint32_t thr;    // internal: split threshold
+        uint32_t left;   // internal: left child index (right = left + 1)
+        uint32_t dim;    // split dimension, PPE_NODE_LEAF for a leaf
+        uint32_t first;  // leaf: first entry in `leaf`
+        uint32_t cnt;    // leaf: number of candidates
+    };
+    std::vector<TNode> nodes;
     std::vector<uint32_t> leaf;
     const size_t node_budget = PPE_NODE_MAX - 2;
     uint32_t max_depth = 0, n_leaves = 0, max_leaf = 0;
@@ -132,7 +139,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         w.rules.resize(R.size());
         for (uint32_t s = 0; s < R.size(); ++s) w.rules[s] = s;
         q.push_back(std::move(w));
-        nodes.resize(2);
+        nodes.resize(1);
     }
 
     std::vector<uint32_t> clo, chi, cand;
@@ -151,16 +158,11 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         w.rules.shrink_to_fit();
 
         auto make_leaf = [&](const std::vector<uint32_t> &L) {
-            const uint32_t cnt = (uint32_t)L.size();
-            nodes[2 * w.node + 0] = (uint32_t)leaf.size();
-            nodes[2 * w.node + 1] =
-                (w.node << PPE_NODE_CHILD_SHIFT) | (PPE_NODE_LEAF << 8) | std::min(cnt, PPE_LEAF_CNT_ESC);
-            if (cnt >= PPE_LEAF_CNT_ESC) leaf.push_back(cnt);  // long list: its length leads the entries
-            for (uint32_t s : L) {
-                uint32_t e = s;
-                if (R[s].resid == 0 && covers(R[s], w.lo, w.hi)) e |= PPE_LEAF_CERTAIN;
-                leaf.push_back(e);
-            }
+            TNode &nd = nodes[w.node];
+            nd.dim = PPE_NODE_LEAF;
+            nd.first = (uint32_t)leaf.size();
+            nd.cnt = (uint32_t)L.size();
+            leaf.insert(leaf.end(), L.begin(), L.end());
             ++n_leaves;
             max_leaf = std::max(max_leaf, (uint32_t)L.size());
             depth_sum += w.depth;
@@ -169,7 +171,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
 
         const bool first_certain = !S.empty() && R[S[0]].resid == 0 && covers(R[S[0]], w.lo, w.hi);
         if (S.empty() || first_certain || S.size() <= binth || w.depth + 1 >= PPE_MAX_DEPTH ||
-            nodes.size() / 2 + 2 > node_budget) {
+            nodes.size() + 2 > node_budget) {
             if (first_certain) S.resize(1);
             make_leaf(S);
             continue;
@@ -213,10 +215,12 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
             continue;
         }
 
-        const uint32_t left_idx = (uint32_t)(nodes.size() / 2);
-        nodes.resize(nodes.size() + 4);
-        nodes[2 * w.node + 0] = best_t;
-        nodes[2 * w.node + 1] = (left_idx << PPE_NODE_CHILD_SHIFT) | ((uint32_t)best_d << 8);
+        // a threshold is l - 1 (l > region lo) or h (h < region hi): never 0xffffffff, the leaf marker
+        const uint32_t left_idx = (uint32_t)nodes.size();
+        nodes.resize(nodes.size() + 2);
+        nodes[w.node].thr = best_t;
+        nodes[w.node].left = left_idx;
+        nodes[w.node].dim = (uint32_t)best_d;
 
         Work L, Rt;
         L.node = left_idx;
@@ -237,24 +241,36 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     }
 
     // ---- assemble the image ----
-    const uint32_t n_nodes = (uint32_t)(nodes.size() / 2);
+    const uint32_t n_nodes = (uint32_t)nodes.size();
+    const uint32_t n_slots = (uint32_t)R.size();  // + the sentinel at slot n_slots
+    // leaf list section: only when some leaf holds more than one candidate (else the payload is the rule slot)
+    std::vector<uint32_t> lwords;
+    if (max_leaf > 1) {
+        for (TNode &nd : nodes) {
+            if (nd.dim != PPE_NODE_LEAF) continue;
+            const uint32_t first = (uint32_t)lwords.size();
+            if (nd.cnt >= PPE_LEAF_CNT_ESC) lwords.push_back(nd.cnt);  // long list: its length leads the entries
+            lwords.insert(lwords.end(), leaf.begin() + nd.first, leaf.begin() + nd.first + nd.cnt);
+            nd.first = first;
+        }
+    }
     const uint32_t off_nodes = PPE_IMG_HDR_WORDS;
-    const uint32_t off_leaf = off_nodes + 2 * n_nodes;
-    uint32_t off_rules = off_leaf + (uint32_t)leaf.size();
+    const uint32_t off_leaf = off_nodes + PPE_NODE_WORDS * n_nodes;
+    uint32_t off_rules = off_leaf + (uint32_t)lwords.size();
     off_rules = (off_rules + 7u) & ~7u;
     // residual (MAC / time) records only when some rule has one: the kernel reads them only for such rules
     bool any_resid = false;
     for (const Rule &r : R) any_resid |= r.resid != 0;
-    const uint32_t off_resid = off_rules + 8u * (uint32_t)R.size();
-    const uint32_t total = off_resid + (any_resid ? 8u * (uint32_t)R.size() : 0u);
+    const uint32_t off_resid = off_rules + 8u * (n_slots + 1u);
+    const uint32_t total = off_resid + (any_resid ? 8u * (n_slots + 1u) : 0u);
 
-    uint32_t *img = (uint32_t *)std::calloc(total ? total : 1, sizeof(uint32_t));
+    uint32_t *img = (uint32_t *)std::calloc(total, sizeof(uint32_t));
     if (!img) return PPE_ENOMEM;
     img[0] = PPE_IMG_MAGIC;
     img[1] = PPE_IMG_VERSION;
     img[PPE_IMG_W_NNODES] = n_nodes;
     img[PPE_IMG_W_NLEAF] = (uint32_t)leaf.size();
-    img[PPE_IMG_W_NRULES] = (uint32_t)R.size();
+    img[PPE_IMG_W_NRULES] = n_slots;
     img[PPE_IMG_W_OFFNODES] = off_nodes;
     img[PPE_IMG_W_OFFLEAF] = off_leaf;
     img[PPE_IMG_W_OFFRULES] = off_rules;
@@ -263,18 +279,48 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     img[PPE_IMG_W_MAXDEPTH] = max_depth;
     img[PPE_IMG_W_MAXLEAF] = max_leaf;
     img[PPE_IMG_W_TOTAL] = total;
-    std::memcpy(img + off_nodes, nodes.data(), nodes.size() * sizeof(uint32_t));
-    if (!leaf.empty()) std::memcpy(img + off_leaf, leaf.data(), leaf.size() * sizeof(uint32_t));
-    for (size_t s = 0; s < R.size(); ++s) {
-        const Rule &r = R[s];
+    img[PPE_IMG_W_ROOTKS] = nodes[0].dim << 8;
+    auto node_byte = [&](uint32_t k) { return 4u * off_nodes + 16u * k; };
+    for (uint32_t k = 0; k < n_nodes; ++k) {
+        const TNode &nd = nodes[k];
+        uint32_t *o = img + off_nodes + PPE_NODE_WORDS * k;
+        if (nd.dim == PPE_NODE_LEAF) {
+            o[0] = PPE_LEAF_THR;
+            o[1] = node_byte(k);
+            if (max_leaf > 1)
+                o[2] = nd.first | (std::min(nd.cnt, PPE_LEAF_CNT_ESC) << 24);
+            else
+                o[2] = nd.cnt ? leaf[nd.first] : n_slots;  // the sentinel slot for an empty leaf
+            o[3] = (PPE_NODE_LEAF << 8) | (PPE_NODE_LEAF << 24);
+        } else {
+            o[0] = nd.thr;
+            o[1] = node_byte(nd.left);
+            o[2] = node_byte(nd.left + 1);
+            o[3] = (nodes[nd.left].dim << 8) | (nodes[nd.left + 1].dim << 24);
+        }
+    }
+    if (!lwords.empty()) std::memcpy(img + off_leaf, lwords.data(), lwords.size() * sizeof(uint32_t));
+    for (uint32_t s = 0; s <= n_slots; ++s) {
         uint32_t *o = img + off_rules + 8 * s;
+        if (s == n_slots) {  // sentinel: matches every key, rule index -1, the default action
+            o[0] = 0;
+            o[1] = 0xffffffffu;
+            o[2] = 0;
+            o[3] = 0xffffffffu;
+            o[4] = 0;
+            o[5] = 0xffffffffu;
+            o[6] = 0xffu << 8 | ((default_action & 0xffffu) << 16);
+            o[7] = 0x1fffffffu;
+            continue;
+        }
+        const Rule &r = R[s];
         o[0] = r.lo[PPE_DIM_SIP];
-        o[1] = r.hi[PPE_DIM_SIP];
+        o[1] = r.hi[PPE_DIM_SIP] - r.lo[PPE_DIM_SIP];
         o[2] = r.lo[PPE_DIM_DIP];
-        o[3] = r.hi[PPE_DIM_DIP];
-        o[4] = r.lo[PPE_DIM_SPORT] | (r.hi[PPE_DIM_SPORT] << 16);
-        o[5] = r.lo[PPE_DIM_DPORT] | (r.hi[PPE_DIM_DPORT] << 16);
-        o[6] = r.lo[PPE_DIM_PROTO] | (r.hi[PPE_DIM_PROTO] << 8) | ((r.action & 0xffffu) << 16);
+        o[3] = r.hi[PPE_DIM_DIP] - r.lo[PPE_DIM_DIP];
+        o[4] = r.lo[PPE_DIM_SPORT] | (r.lo[PPE_DIM_DPORT] << 16);
+        o[5] = (r.hi[PPE_DIM_SPORT] - r.lo[PPE_DIM_SPORT]) | ((r.hi[PPE_DIM_DPORT] - r.lo[PPE_DIM_DPORT]) << 16);
+        o[6] = r.lo[PPE_DIM_PROTO] | ((r.hi[PPE_DIM_PROTO] - r.lo[PPE_DIM_PROTO]) << 8) | ((r.action & 0xffffu) << 16);
         o[7] = r.id | (r.resid << 29);
     }
     if (any_resid) std::memcpy(img + off_resid, resid_words.data(), resid_words.size() * sizeof(uint32_t));

@@ -25,11 +25,10 @@ namespace {
 
 constexpr int kSlotSets = 4;      // set 0: ppe_classify; 1..3: host pipeline streams
 constexpr int kHostStreams = 3;
-#ifndef PPE_PIPE_DEFAULT
-// next-tile fetch of the classify kernel (PF_* in ppe_kernels.hip): 0 none, 1 register double buffer, 2 LDS-DMA,
-// 3 none with the first tile's loads before the image staging
-#define PPE_PF_DEFAULT 3  // hoisted first load: C1 21.7 us vs none 22.2; register (28.3) / LDS-DMA (24.4) prefetch slower
-#endif
+// tile fetch of the classify kernel (PF_* in ppe_kernels.hip): 0 at the loop top, 1 the first tile's loads issued
+// before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering and an LDS-DMA next-tile
+// pipeline were measured slower (28.3 / 24.4 us) and are not built.
+constexpr int kPfNone = 0, kPfHoist = 1;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 
 struct HostStage {
@@ -103,77 +102,64 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl >= 1 && pl <= 4 ? (uint32_t)pl : 0u;
+    t.pipeline = pl == 1 || pl == 4 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     return t;
 }
 
-// How the classify kernel holds the classifier image (see IMG_* in ppe_kernels.hip) and whether it runs the LDS-DMA
-// packet pipeline.
+// How the classify kernel holds the classifier image (see IMG_* in ppe_kernels.hip) and how it fetches tiles.
 struct StagePlan {
     int mode;            // 0 global, 1 whole image in LDS, 2 prefix in LDS
-    int pipe;            // next-tile fetch: 0 none, 1 register double buffer, 2 LDS-DMA slot
+    int pipe;            // tile fetch (kPf*)
     uint32_t block;
-    uint32_t lds_words, lds_nodes, leaf_lds;
+    uint32_t lds_words, lds_nodes;
 };
 
 // LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves): 160 KiB shared, minus
-// the counter bins, the 1-KB rounding of the staged image, the pipeline's per-wave packet slots and (whole image in
-// LDS) the per-wave walk keys
-uint32_t image_budget(uint32_t block, bool pipe, bool keys) {
+// the per-wave walk keys and counter bins, and the 1-KB rounding of the staged image
+uint32_t image_budget(uint32_t block) {
     const uint32_t per_wg = (160u * 1024u) / (2048u / block);
-    const uint32_t fixed = PPE_LDS_FIXED + 1024u + (pipe ? ppe_classify_pipe_lds((int)block) : 0u) +
-                           (keys ? ppe_classify_keys_lds((int)block) : 0u);
-    return per_wg > fixed ? std::min<uint32_t>(PPE_LDS_IMG_MAX, per_wg - fixed) : 0u;
+    const uint32_t fixed = ppe_classify_fixed_lds((int)block) + 1024u;
+    return per_wg > fixed ? per_wg - fixed : 0u;
 }
 
-StagePlan stage_plan_for(const ppe_ctx *c, const std::vector<uint32_t> &img, int pf) {
-    const bool pipe = pf == 2;
+StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
+    const int pf = c->tune.pipeline == 1 ? kPfNone : kPfHoist;
     const uint32_t words = (uint32_t)img.size(), bytes = words * 4u;
-    StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0, 0};
+    StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0};
     if (!c->tune.lds_image) {
-        if (!c->tune.block && !pipe) p.block = 256;
+        if (!c->tune.block) p.block = 256;
         return p;
     }
     // the whole image in LDS: the smallest workgroup (most copies per CU) whose share holds it
     if (!c->tune.block) {
         for (uint32_t b : {256u, 512u, 1024u}) {
-            if (bytes <= image_budget(b, pipe, true)) {
+            if (bytes <= image_budget(b)) {
                 p.block = b;
                 break;
             }
         }
     }
-    const uint32_t off_rules = img[PPE_IMG_W_OFFRULES], n_nodes = img[PPE_IMG_W_NNODES];
-    const uint32_t budget = image_budget(p.block, pipe, false);
-    if (bytes <= image_budget(p.block, pipe, true)) {
+    const uint32_t budget = image_budget(p.block);
+    const uint32_t off_resid = img[PPE_IMG_W_OFFRESID], off_rules = img[PPE_IMG_W_OFFRULES];
+    const uint32_t n_nodes = img[PPE_IMG_W_NNODES];
+    if (bytes <= budget) {
         p.mode = 1;
         p.lds_words = words;
+    } else if (off_resid * 4u <= budget) {  // nodes, leaf lists and rule records; residual records from global
+        p.mode = 2;
+        p.lds_words = off_resid;
+        p.lds_nodes = n_nodes;
     } else if (off_rules * 4u <= budget) {  // every node and leaf list; rule records from global (L2)
         p.mode = 2;
         p.lds_words = off_rules;
         p.lds_nodes = n_nodes;
-        p.leaf_lds = 1;
-    } else if (budget >= 4u * (PPE_IMG_HDR_WORDS + 2u * 64u)) {  // the top of the tree (BFS order) fills the budget
+    } else if (budget >= 4u * (PPE_IMG_HDR_WORDS + PPE_NODE_WORDS * 64u)) {  // the top of the BFS tree
         p.mode = 2;
-        p.lds_nodes = std::min(n_nodes, (budget / 4u - PPE_IMG_HDR_WORDS) / 2u);
-        p.lds_words = PPE_IMG_HDR_WORDS + 2u * p.lds_nodes;
-        p.leaf_lds = 0;
+        p.lds_nodes = std::min(n_nodes, (budget / 4u - PPE_IMG_HDR_WORDS) / PPE_NODE_WORDS);
+        p.lds_words = PPE_IMG_HDR_WORDS + PPE_NODE_WORDS * p.lds_nodes;
     }
     return p;
-}
-
-// The LDS-DMA pipeline runs only with the whole image in LDS (see PPE_DISPATCH); when the image with the pipeline's
-// slots does not fit, the plan falls back to the non-pipelined kernel.
-StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
-    // tuning.pipeline: 0 automatic, 1 none, 2 LDS-DMA, 3 register double buffer, 4 first load before the staging
-    static const int kPf[5] = {PPE_PF_DEFAULT, 0, 2, 1, 3};
-    const int pf = kPf[std::min(c->tune.pipeline, 4u)];
-    if (pf == 2 && c->tune.lds_image) {
-        const StagePlan p = stage_plan_for(c, img, 2);
-        if (p.mode == 1) return p;
-    }
-    return stage_plan_for(c, img, pf == 2 ? 0 : pf);
 }
 
 // Resident workgroups per CU: the occupancy API's answer (register and LDS limits) unless the tuning fixes it.
@@ -206,9 +192,11 @@ int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const 
         const uint32_t nn = words[PPE_IMG_W_NNODES];
         std::vector<uint8_t> depth(nn, 0);
         for (uint32_t k = 0; k < nn; ++k) {
-            const uint32_t y = words[PPE_IMG_HDR_WORDS + 2u * k + 1u];
-            const uint32_t ch = y >> PPE_NODE_CHILD_SHIFT;
-            if (PPE_NODE_DIM(y) != PPE_NODE_LEAF) depth[ch] = depth[ch + 1u] = (uint8_t)(depth[k] + 1u);
+            const uint32_t *nd = words + PPE_IMG_HDR_WORDS + PPE_NODE_WORDS * k;
+            if (nd[0] != PPE_LEAF_THR) {  // children: byte offsets from the image start
+                depth[(nd[1] / 4u - PPE_IMG_HDR_WORDS) / PPE_NODE_WORDS] = (uint8_t)(depth[k] + 1u);
+                depth[(nd[2] / 4u - PPE_IMG_HDR_WORDS) / PPE_NODE_WORDS] = (uint8_t)(depth[k] + 1u);
+            }
             if (le.size() <= depth[k]) le.resize(depth[k] + 1u, 0u);
             le[depth[k]] = k + 1u;
         }
@@ -254,15 +242,15 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
     a.lds_words = plan.lds_words;
     a.max_depth = c->h_img[r][PPE_IMG_W_MAXDEPTH];
     a.max_leaf = c->h_img[r][PPE_IMG_W_MAXLEAF];
+    a.root_ks = c->h_img[r][PPE_IMG_W_ROOTKS];
     if (plan.mode == 1) {
-        a.lds_iters = a.max_depth;
-    } else if (plan.mode == 2) {  // levels 1..L all inside the staged prefix [0, lds_nodes)
+        a.lds_iters = a.max_depth + 1u;
+    } else if (plan.mode == 2) {  // node reads 0..L-1 only visit depths < L: all inside the staged prefix
         const std::vector<uint32_t> &le = c->level_end[r];
         uint32_t L = 0;
-        while (L + 1u < le.size() && le[L + 1u] <= plan.lds_nodes) ++L;
-        a.lds_iters = std::min(L, a.max_depth);
+        while (L < le.size() && le[L] <= plan.lds_nodes) ++L;
+        a.lds_iters = std::min(L, a.max_depth + 1u);
     }
-    a.leaf_lds = plan.leaf_lds;
     a.off_leaf = c->h_img[r][PPE_IMG_W_OFFLEAF];
     a.off_rules = c->h_img[r][PPE_IMG_W_OFFRULES];
     a.off_resid = c->h_img[r][PPE_IMG_W_OFFRESID];
@@ -477,7 +465,7 @@ int ppe_acl_lookup(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint32_t 
     HIPCHK(c, hipSetDevice(c->device));
     const int r = c->running;
     const uint32_t words = (uint32_t)c->h_img[r].size();
-    const bool lds = (size_t)words * 4u <= PPE_LDS_IMG_MAX;
+    const bool lds = (size_t)words * 4u + 1024u <= PPE_LDS_IMG_MAX;
     ppe_tuple_kargs a;
     std::memset(&a, 0, sizeof a);
     a.tuple = in->tuple;
@@ -623,9 +611,9 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline > 4)
-        return fail(c, PPE_EINVAL,
-                    "pipeline must be 0 (auto), 1 (none), 2 (LDS-DMA), 3 (register prefetch) or 4 (hoisted first load)");
+    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 4)
+        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top) or 4 (first tile's "
+                                   "loads before the image staging)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     c->tune = *t;
     c->tune.pipeline = t->pipeline;
@@ -659,9 +647,7 @@ int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds
     if (grid) *grid = std::min(c->n_cu * blocks_per_cu(c, plan), c->max_grid);
     if (block) *block = plan.block;
     if (lds_bytes)
-        *lds_bytes = PPE_LDS_FIXED + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u) +
-                     (plan.mode == 1 ? ppe_classify_keys_lds((int)plan.block) : 0u) +
-                     (plan.pipe == 2 ? ppe_classify_pipe_lds((int)plan.block) : 0u);
+        *lds_bytes = ppe_classify_fixed_lds((int)plan.block) + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u);
     if (variant) *variant = (uint32_t)plan.mode | ((uint32_t)plan.pipe << 4);
     return PPE_OK;
 }

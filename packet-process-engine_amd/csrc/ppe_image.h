@@ -1,34 +1,41 @@
 /*
- * ppe_image.h — layout of the device classifier image (one flat array of u32 words).
+ * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v3.
  *
  * The image is a HyperSplit-style binary decision tree over the five header dimensions, flattened in BFS order
- * (children of node k are 2 consecutive nodes with index > k, so a walk strictly increases the node index and
- * always terminates), followed by the leaf rule lists, the compact rule records and their residual (MAC / time)
- * records.  The reference's tree engine (dp_acl.c / acl64.c, built by dataplane/src/acl/acl.mk:13-15) is absent;
- * its statistics names (gWstDepth, gAvgDepth, gNumTreeNode, gNumLeafNode: dataplane/src/common/dp_cmd.c:2032-2036)
- * are reproduced from this structure.
+ * (children of node k are numbered after k, so a walk strictly descends and always terminates), followed by the
+ * leaf candidate lists, the compact rule records and their residual (MAC / time) records.  The reference's tree
+ * engine (dp_acl.c / acl64.c, built by dataplane/src/acl/acl.mk:13-15) is absent; its statistics names (gWstDepth,
+ * gAvgDepth, gNumTreeNode, gNumLeafNode: dataplane/src/common/dp_cmd.c:2032-2036) are reproduced from this structure.
  *
  *  word 0   PPE_IMG_MAGIC
  *  word 1   PPE_IMG_VERSION
- *  word 2   n_nodes           word 3  n_leaf_entries      word 4  n_rules (slots)
+ *  word 2   n_nodes           word 3  n_leaf_entries      word 4  n_rules (slots, excluding the sentinel)
  *  word 5   off_nodes         word 6  off_leaf            word 7  off_rules       word 8  off_resid   (word offsets)
  *  word 9   default_action    word 10 max_depth           word 11 total words     word 12 max leaf entries
- *  word 13..15 reserved
+ *  word 13  root key slot << 8 (the dimension the root splits on; PPE_NODE_LEAF when the root is a leaf)
+ *  word 14..15 reserved
  *
- *  node (2 words, 8-B aligned):  y = (child << 11) | (dim << 8) | count
- *      internal: x = threshold, child = left, dim 0 sip, 1 dip, 2 sport, 3 dport, 4 proto, count 0
- *                key <= threshold → left, key > threshold → left + 1
- *      leaf:     dim = PPE_NODE_LEAF (5): the walk's key slot 5 holds 0, so "key > x" is false and the walk stays
- *                at child = the leaf itself (a fixed point: every lane can walk max_depth levels without a per-lane
- *                exit).  x = first leaf entry; count = number of entries, or PPE_LEAF_CNT_ESC when the count is
- *                stored in leaf entry x and the entries start at x + 1.
- *      The field positions let the walk form the key's LDS offset as y & 0x700 (slot stride 256 B) and the child's
- *      byte offset as (y >> 8) & ~7.
- *  leaf entry (1 word): rule slot | (certain << 31)      certain: the rule's 5-tuple box covers the leaf's region
- *                                                          and it has no residual field, so it matches unchecked
- *  rule (8 words, 32-B aligned), slot order == ascending rule index:
- *      sip_lo, sip_hi, dip_lo, dip_hi, sport_lo | sport_hi << 16, dport_lo | dport_hi << 16,
- *      proto_lo | proto_hi << 8 | action << 16, rule_index | resid << 29
+ *  node (4 words, 16-B aligned; node k at byte 4 * off_nodes + 16 k of the image):
+ *      internal: { threshold, left child byte offset, right child byte offset, kslots }
+ *                key <= threshold → left, key > threshold → right.  Child byte offsets are from the image start, so
+ *                one offset addresses the node in LDS (staged image base + offset) and in global memory alike.
+ *                kslots = (left child's key slot << 8) | (right child's key slot << 24): the dimension the CHILD
+ *                splits on, known one level ahead, so a walk issues the key read and the node read of a level
+ *                together (one LDS round trip per level).  Key slot d = dimension d (0 sip, 1 dip, 2 sport,
+ *                3 dport, 4 proto); PPE_NODE_LEAF (5) for a leaf child: the walk's key slot 5 holds 0.
+ *      leaf:     { 0xffffffff, own byte offset, payload, PPE_NODE_LEAF << 8 | PPE_NODE_LEAF << 24 }
+ *                key 0 is never > 0xffffffff (no internal threshold is 0xffffffff), so a walk that reached a leaf
+ *                stays there: every lane can run max_depth + 1 levels without a per-lane exit.
+ *                payload, when max_leaf <= 1: the rule slot of the leaf's one candidate, or the sentinel slot
+ *                n_rules (an always-matching record with rule index -1 and the default action) for an empty leaf.
+ *                payload, when max_leaf > 1: first leaf entry | count << 24, count == PPE_LEAF_CNT_ESC meaning the
+ *                count is stored in leaf entry `first` and the entries start at first + 1.
+ *  leaf entry (1 word): rule slot, in ascending rule index (= priority) order
+ *  rule (8 words, 32-B aligned), slot order == ascending rule index, slot n_rules = the sentinel:
+ *      sip_lo, sip_hi - sip_lo, dip_lo, dip_hi - dip_lo, sport_lo | dport_lo << 16,
+ *      (sport_hi - sport_lo) | (dport_hi - dport_lo) << 16, proto_lo | (proto_hi - proto_lo) << 8 | action << 16,
+ *      rule_index (29-bit two's complement: the sentinel's is -1) | resid << 29
+ *      A field matches iff (key - lo) mod 2^w <= span (w = the field width), i.e. lo <= key <= hi.
  *  resid (8 words per slot; present only when at least one rule has a residual field, read only for those):
  *      dmac bytes 0-3 (LE), dmac bytes 4-5, smac bytes 0-3, smac bytes 4-5,
  *      time_start lo, hi, time_end lo, hi
@@ -38,7 +45,7 @@
 #define PPE_IMAGE_H
 
 #define PPE_IMG_MAGIC   0x41455050u /* "PPEA" */
-#define PPE_IMG_VERSION 2u
+#define PPE_IMG_VERSION 3u
 #define PPE_IMG_HDR_WORDS 16u
 
 #define PPE_IMG_W_NNODES   2
@@ -52,11 +59,12 @@
 #define PPE_IMG_W_MAXDEPTH 10
 #define PPE_IMG_W_TOTAL    11
 #define PPE_IMG_W_MAXLEAF  12
+#define PPE_IMG_W_ROOTKS   13
 
-#define PPE_NODE_LEAF 5u          /* leaf marker in the dim field; also the index of the walk's zero key slot */
-#define PPE_NODE_CHILD_SHIFT 11u
-#define PPE_NODE_DIM(y) (((y) >> 8) & 7u)
-#define PPE_NODE_MAX (1u << 21)   /* child index field: 21 bits */
+#define PPE_NODE_WORDS 4u
+#define PPE_NODE_LEAF 5u          /* key slot of a leaf: the walk's zero key */
+#define PPE_LEAF_THR 0xffffffffu  /* threshold word of a leaf */
+#define PPE_NODE_MAX (1u << 20)   /* node budget: child byte offsets stay below 16 MiB */
 #define PPE_LEAF_CNT_ESC 255u     /* count field value meaning "count stored in the first leaf word" */
 #define PPE_DIM_SIP   0u
 #define PPE_DIM_DIP   1u
@@ -69,9 +77,7 @@
 #define PPE_RESID_SMAC 2u
 #define PPE_RESID_TIME 4u
 
-#define PPE_LEAF_CERTAIN 0x80000000u
-
-/* hard bound on walk length, enforced by the builder (max_depth) and by the kernel loop */
+/* hard bound on walk length, enforced by the builder (max_depth) */
 #define PPE_MAX_DEPTH 60
 
 #endif

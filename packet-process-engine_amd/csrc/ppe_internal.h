@@ -26,12 +26,12 @@ struct ppe_kargs {
     uint64_t now;
     uint32_t idx_base;        /* added to the packet indices written to fw_idx / drop_idx */
     uint32_t lds_words;       /* image words staged in LDS (IMG_LDS: all; IMG_SPLIT: header + top nodes [+ leaves]) */
-    uint32_t lds_iters;       /* walk levels whose nodes are all in LDS (IMG_LDS: max_depth; IMG_SPLIT: BFS prefix)  */
-    uint32_t max_depth;       /* deepest leaf: uniform trip count of the tree walk                                    */
+    uint32_t lds_iters;       /* IMG_SPLIT: walk levels (node reads) whose nodes are all in the staged BFS prefix      */
+    uint32_t max_depth;       /* deepest leaf: the walk reads max_depth + 1 nodes                                     */
     uint32_t max_leaf;        /* longest leaf candidate list: uniform trip count of the leaf scan                     */
-    uint32_t leaf_lds;        /* IMG_SPLIT: the leaf lists are in LDS too                                             */
+    uint32_t root_ks;         /* the root node's key slot << 8 (image header word PPE_IMG_W_ROOTKS)                    */
     uint32_t off_leaf, off_rules, off_resid; /* image section offsets (words), from the image header: kernel arguments
-                                                so the loop holds no vector load the LDS-DMA pipeline would wait on */
+                                                (scalar registers, no load in the loop)                               */
     unsigned long long *cslots; /* [grid][PPE_CSLOT_WORDS] counter slots, one per workgroup */
     unsigned long long *trace;  /* diagnostic builds (PPE_TRACE) only: per-wave phase timestamps, else unused */
 };
@@ -50,23 +50,21 @@ struct ppe_tuple_kargs {
 };
 
 #define PPE_CSLOT_WORDS 32
-#define PPE_LDS_FIXED 1152u /* classify kernel LDS before the image: 256 counter bins + 32 counters (u32) */
+#define PPE_LDS_FIXED 1152u /* classify kernel LDS after the walk keys: 256 counter bins + 32 counters (u32) */
 #define PPE_BLOCK 256
-/* LDS available to the staged classifier image per workgroup: small images with 256-thread workgroups (8 per CU),
- * larger ones with 1024-thread workgroups (2 per CU, so 2 × (128 B + image) ≤ 160 KiB) */
-#define PPE_LDS_IMG_SMALL (20u * 1024u)
-#define PPE_LDS_IMG_MAX (78u * 1024u)
+/* largest staged classifier image per workgroup (1024-thread workgroups, 2 per CU, each with 25 KB of keys + bins) */
+#define PPE_LDS_IMG_MAX (54u * 1024u)
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 /* Launch the classify kernel. grid = workgroups (persistent), lds_img = stage image in LDS. Returns hipError_t. */
-/* mode: 0 image in global memory, 1 whole image in LDS, 2 prefix in LDS (see ppe_kernels.hip) */
+/* mode: 0 image in global memory, 1 whole image in LDS, 2 prefix in LDS; pipe: 0 first tile loaded at the loop top,
+ * 1 first tile's loads issued before the image staging (see ppe_kernels.hip) */
 int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, void *stream,
                         void *ev_start, void *ev_stop);
 int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block);
-uint32_t ppe_classify_pipe_lds(int block);
-uint32_t ppe_classify_keys_lds(int block);
+uint32_t ppe_classify_fixed_lds(int block);
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
 #ifdef __cplusplus
 }

@@ -93,19 +93,30 @@ def test_large_ruleset_builds_bounded():
 
 
 def test_image_layout():
+    """Image format v3 (csrc/ppe_image.h): 16-B nodes {threshold, left, right, child key slots}, leaves as walk
+    fixed points, the always-matching sentinel rule at slot n_rules."""
     rules = synth.make_rules(64)
     img, st = abi.build_image(rules)
-    assert img[0] == 0x41455050
+    assert img[0] == 0x41455050 and img[1] == 3
     assert img[2] == st["n_nodes"] and img[4] == 64 and img[11] == len(img)
     assert img[7] % 8 == 0  # rules 32-B aligned
-    nodes = img[16:16 + 2 * img[2]].reshape(-1, 2)
-    dim = (nodes[:, 1] >> 8) & 7
-    is_leaf = dim == 5
-    leaves = nodes[is_leaf]
-    assert img[10] >= 1 and img[12] == (leaves[:, 1] & 0xFF).max()  # max depth, max leaf entries
-    assert (dim[~is_leaf] <= 4).all()  # internal: a real dimension
-    assert ((leaves[:, 1] >> 11) == np.nonzero(is_leaf)[0]).all()  # a leaf's child is itself (walk fixed point)
-    assert img[1] == 2
+    nodes = img[16:16 + 4 * img[2]].reshape(-1, 4)
+    own = 64 + 16 * np.arange(len(nodes))
+    is_leaf = nodes[:, 0] == 0xFFFFFFFF
+    leaves, inner = nodes[is_leaf], nodes[~is_leaf]
+    assert img[10] >= 1 and img[12] == 1  # max depth; binth 1: one candidate per leaf
+    assert (leaves[:, 1] == own[is_leaf]).all()  # a leaf's left child is itself (walk fixed point)
+    assert (leaves[:, 3] == (5 << 8 | 5 << 24)).all()  # ... and its key slot is the zero key
+    assert (leaves[:, 2] <= 64).all()  # payload: a rule slot or the sentinel (64)
+    # internal: children are the two consecutive nodes after it (BFS), their key slots are theirs
+    li = (inner[:, 1] - 64) // 16
+    assert ((inner[:, 2] - 64) // 16 == li + 1).all() and (li > np.nonzero(~is_leaf)[0]).all()
+    # a child's key slot (carried by its parent) is 5 exactly for leaves
+    ks_l, ks_r = (inner[:, 3] >> 8) & 0xFF, (inner[:, 3] >> 24) & 0xFF
+    assert ((ks_l == 5) == is_leaf[li]).all() and ((ks_r == 5) == is_leaf[li + 1]).all()
+    assert (ks_l <= 5).all() and (ks_r <= 5).all() and (img[13] >> 8) <= 4
+    sent = img[img[7] + 8 * 64: img[7] + 8 * 65]
+    assert sent[1] == sent[3] == sent[5] == 0xFFFFFFFF and sent[7] == 0x1FFFFFFF
 
 
 def test_long_leaf_list_escape():
@@ -122,8 +133,9 @@ def test_long_leaf_list_escape():
     for b in range(6):
         rules["dmac"][:, b] = (macs >> np.uint64(8 * b)) & np.uint64(0xFF)
     img, st = abi.build_image(rules, default_action=1)
-    nodes = img[16:16 + 2 * img[2]].reshape(-1, 2)
-    assert ((nodes[:, 1] & 0xFF) == 255).any() and img[12] >= n
+    nodes = img[16:16 + 4 * img[2]].reshape(-1, 4)
+    leaves = nodes[nodes[:, 0] == 0xFFFFFFFF]
+    assert ((leaves[:, 2] >> 24) == 255).any() and img[12] >= n
     pk = synth.make_packets(4000, rules, seed=5, kind="udp64", stride=64)
     # point some packets' dmac at late rules
     idx = np.arange(0, 4000, 7)

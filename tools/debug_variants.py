@@ -20,7 +20,7 @@ for resid in (0.0, 0.2):
     o = pyoracle.Oracle(rules, default_action=1)
     for ts in (None, pk["ts"]):
         ref = o.classify_batch(pk["hdr"], pk["len"], ts=ts, cfg=o.cfg(0, 1, NOW))
-        for tune in (dict(pipeline=1), dict(pipeline=2), dict(pipeline=1, lds_image=0)):
+        for tune in (dict(pipeline=1), dict(pipeline=4), dict(pipeline=1, lds_image=0)):
             eng.tuning(block=0, blocks_per_cu=0, pipeline=0, lds_image=1)
             eng.tuning(**tune)
             got = eng.classify_host(pk["hdr"], pk["len"], ts=ts, cfg=eng.cfg(0, 1, NOW))

@@ -71,6 +71,9 @@ def main():
     end = us(t[:, 22]).max()
     print(f"span entry..last wave done: {end:.2f} us; entry spread {us(t[:, 0]).max():.2f} us; "
           f"staging {np.median(us(t[:, 1]) - us(t[:, 0])):.2f} us median")
+    ep = us(t[:, 23]) - us(t[:, 22])
+    print(f"epilogue (loop exit .. counters flushed): median {np.median(ep):.2f} p90 {np.percentile(ep, 90):.2f} us; "
+          f"last flush at {us(t[:, 23]).max():.2f} us; last loop exit at {end:.2f} us")
     names = ["wait window", "decode+hash", "ACL", "outputs+counters", "to next top"]
     for i in range(int(iters.max())):
         if i >= 4:
