@@ -35,9 +35,9 @@ NOW = 1_700_000_000
 
 def algorithmic_bytes(stride: int) -> tuple[float, float]:
     """(read, write) bytes per packet the kernel must move: the 64-B header window + 4-B length
-    read; verdict + flow hash + ACL hit (12 B) + one compacted index (4 B) + the tile count (4 B / 64 packets)
+    read; verdict + flow hash + ACL hit (12 B) + the packet's entry in its tile's FW/PUNT/DROP partition list (4 B)
     written.  Payload bytes past the window are never touched (IMIX included)."""
-    return float(min(stride, 64)) + 4.0, 12.0 + 4.0 + 4.0 / 64.0
+    return float(min(stride, 64)) + 4.0, 12.0 + 4.0
 
 
 def main():
@@ -90,9 +90,8 @@ def main():
         out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
                "flow_hash": torch.empty(n, dtype=torch.int32, device=dev),
                "acl_hit": torch.empty(n, dtype=torch.int32, device=dev),
-               "fw_idx": torch.empty(n, dtype=torch.int32, device=dev),
-               "drop_idx": torch.empty(n, dtype=torch.int32, device=dev),
-               "tile_cnt": torch.empty((n + 63) // 64, dtype=torch.int32, device=dev)}
+               # the ballot-compacted FW / DROP lists in the partition layout (one list, ppe_hip.h)
+               "part_idx": torch.empty(n, dtype=torch.int32, device=dev)}
         bufs.append((hdr, lens, out, pk if b == 0 else None))
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
@@ -103,8 +102,8 @@ def main():
     calls = []
     for hdr, lens, out, _ in bufs:
         b = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, stride)
-        r = abi.Result(*(out[k].data_ptr() for k in ("verdict", "flow_hash", "acl_hit", "fw_idx", "drop_idx",
-                                                      "tile_cnt")), None)
+        r = abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(),
+                       out["part_idx"].data_ptr(), out["part_idx"].data_ptr(), None, None)
         calls.append((C.byref(b), C.byref(r), b, r))
     cfg_ref = C.byref(cfg)
     sptr = C.c_void_p(stream.cuda_stream)
@@ -168,8 +167,14 @@ def main():
         # packets whose headers reach past the window must be WINDOW_PUNT; every other one bit-exact
         far = ref["reach"] > stride
         ok = ~far
+        # the partition list of those tiles: FW, PUNT, DROP per tile, each ascending, entry = index | action << 30
+        act = (got_v >> 8) & 0xFF
+        order = np.argsort((np.arange(m) // 64) * 4 + np.array([0, 2, 1], np.int64)[act], kind="stable")
+        want_part = (order.astype(np.uint32) | (act[order] << 30)).astype(np.uint32)
+        got_p = out["part_idx"][:m].cpu().numpy().view(np.uint32)
         parity = bool(np.array_equal(got_v[ok], ref["verdict"][ok]) and np.array_equal(got_h[ok], ref["flow_hash"][ok])
-                      and np.array_equal(got_a[ok], ref["acl_hit"][ok]) and ((got_v[far] & 0xFF) == 18).all())
+                      and np.array_equal(got_a[ok], ref["acl_hit"][ok]) and ((got_v[far] & 0xFF) == 18).all()
+                      and np.array_equal(got_p, want_part))
 
     # ---- host-inclusive rate (pinned host buffers, H2D + classify + D2H pipeline) ----
     host_mpps = None

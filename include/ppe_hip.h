@@ -78,6 +78,9 @@ enum ppe_action { PPE_ACT_FW = 0, PPE_ACT_DROP = 1, PPE_ACT_PUNT = 2 };
 #define PPE_F_ACL    0x0010u   /* ACL consulted (acl_hit is its result)               */
 #define PPE_F_FRAG   0x0020u   /* IPv4 fragment seen                                  */
 
+#define PPE_PART_INDEX(e)  ((e) & 0x3fffffffu)   /* partition-layout entry → packet index                */
+#define PPE_PART_ACTION(e) ((e) >> 30)           /* partition-layout entry → enum ppe_action             */
+
 #define PPE_VERDICT_STATUS(v) ((v) & 0xffu)
 #define PPE_VERDICT_ACTION(v) (((v) >> 8) & 0xffu)
 #define PPE_VERDICT_FLAGS(v)  ((v) >> 16)
@@ -116,6 +119,10 @@ typedef struct {
     int32_t  *acl_hit;         /* n × lowest matching rule index, -1 on no match / not consulted               */
     uint32_t *fw_idx;          /* n slots: per 64-packet tile t, the FW packet indices packed at [64t, 64t+k)  */
     uint32_t *drop_idx;        /* n slots: same for DROP                                                      */
+                               /* fw_idx == drop_idx selects the PARTITION layout: slots [64t, 64t+v) of tile t
+                                  (v = its packet count) hold all of its packet indices, FW ascending from the
+                                  front, DROP ascending at the back, PUNT ascending in between; each entry is
+                                  index | action << 30 (PPE_PART_*), so no tile_cnt is needed to split them     */
     uint32_t *tile_cnt;        /* ceil(n/64) × (nfw | ndrop << 8 | npunt << 16)                                */
     uint32_t *tuple;           /* optional n × 4 words: sip, dip, sport|dport<<16, proto|vlan<<8|payload_len<<16 */
 } ppe_result_t;

@@ -28,7 +28,7 @@ constexpr int kHostStreams = 3;
 // tile fetch of the classify kernel (PF_* in ppe_kernels.hip): 0 at the loop top, 1 the first tile's loads issued
 // before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering and an LDS-DMA next-tile
 // pipeline were measured slower (28.3 / 24.4 us) and are not built.
-constexpr int kPfNone = 0, kPfHoist = 1;
+constexpr int kPfNone = 0, kPfHoist = 1, kPfReg = 2;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 
 struct HostStage {
@@ -102,7 +102,7 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl == 1 || pl == 4 ? (uint32_t)pl : 0u;
+    t.pipeline = pl == 1 || pl == 2 || pl == 4 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     return t;
 }
@@ -124,7 +124,7 @@ uint32_t image_budget(uint32_t block) {
 }
 
 StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
-    const int pf = c->tune.pipeline == 1 ? kPfNone : kPfHoist;
+    const int pf = c->tune.pipeline == 1 ? kPfNone : (c->tune.pipeline == 2 ? kPfReg : kPfHoist);
     const uint32_t words = (uint32_t)img.size(), bytes = words * 4u;
     StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0};
     if (!c->tune.lds_image) {
@@ -288,6 +288,8 @@ int check_batch(ppe_ctx *c, const ppe_batch_t *in, const ppe_cfg_t *cfg) {
     if (in->n == 0) return PPE_OK;
     if (!in->hdr || !in->len) return fail(c, PPE_EINVAL, "hdr/len required");
     if (in->stride != 64 && in->stride != 128) return fail(c, PPE_EINVAL, "stride must be 64 or 128");
+    // byte offsets inside the kernel are 32-bit, and partition-list entries keep the action in bits 31:30
+    if ((uint64_t)in->n * in->stride >= (1ull << 31)) return fail(c, PPE_EINVAL, "batch too large (n * stride >= 2^31)");
     if (((uintptr_t)in->hdr & 15u) != 0) return fail(c, PPE_EINVAL, "hdr must be 16-byte aligned");
     if (cfg && cfg->unsupport_proto_action > 1) return fail(c, PPE_EINVAL, "unsupport_proto_action must be 0/1");
     if (cfg && cfg->syn_check > 1) return fail(c, PPE_EINVAL, "syn_check must be 0/1");
@@ -437,8 +439,9 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         r.verdict = out->verdict ? h.verdict : nullptr;
         r.flow_hash = out->flow_hash ? h.fhash : nullptr;
         r.acl_hit = out->acl_hit ? h.hit : nullptr;
+        const bool part = out->fw_idx && out->fw_idx == out->drop_idx;  // partition layout: one list
         r.fw_idx = out->fw_idx ? h.fw : nullptr;
-        r.drop_idx = out->drop_idx ? h.drop : nullptr;
+        r.drop_idx = part ? h.fw : (out->drop_idx ? h.drop : nullptr);
         r.tile_cnt = out->tile_cnt ? h.tcnt : nullptr;
         r.tuple = out->tuple ? h.tuple : nullptr;
         rc = launch(c, &b, &r, cfg, h.s, 1 + (int)(i % kHostStreams), base);
@@ -451,7 +454,8 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
             HIPCHK(c, hipMemcpyAsync(out->tile_cnt + base / 64, h.tcnt, (size_t)((m + 63) / 64) * 4, d2h, h.s));
         // compacted indices carry the batch index (idx_base); chunk is a multiple of 64, so tiles line up
         if (out->fw_idx) HIPCHK(c, hipMemcpyAsync(out->fw_idx + base, h.fw, (size_t)m * 4, d2h, h.s));
-        if (out->drop_idx) HIPCHK(c, hipMemcpyAsync(out->drop_idx + base, h.drop, (size_t)m * 4, d2h, h.s));
+        if (out->drop_idx && !part)
+            HIPCHK(c, hipMemcpyAsync(out->drop_idx + base, h.drop, (size_t)m * 4, d2h, h.s));
     }
     for (auto &h : c->hs) HIPCHK(c, hipStreamSynchronize(h.s));
     return PPE_OK;
@@ -611,9 +615,9 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 4)
-        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top) or 4 (first tile's "
-                                   "loads before the image staging)");
+    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 2 && t->pipeline != 4)
+        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top), 2 (next tile "
+                                   "prefetched into registers) or 4 (first tile's loads before the image staging)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     c->tune = *t;
     c->tune.pipeline = t->pipeline;

@@ -42,6 +42,10 @@
 #define PPE_TRACE 0
 #endif
 // minimum resident waves per SIMD the classify kernel is compiled for (VGPR budget 512 / this)
+// per-reason counter binning: 0 one LDS add per packet, 1 one LDS add per distinct bin key of the wave
+#ifndef PPE_CNT_LEADER
+#define PPE_CNT_LEADER 0
+#endif
 #ifndef PPE_WAVES_PER_EU
 #define PPE_WAVES_PER_EU 8
 #endif
@@ -505,9 +509,12 @@ __device__ __forceinline__ void stage_image(const uint32_t *img, uint32_t *lds, 
 // PF: when a tile's window is fetched
 #define PF_NONE 0   // at the top of its own iteration
 #define PF_HOIST 1  // as PF_NONE, but the first tile's loads are issued before the image staging
+#define PF_REG 2    // one tile ahead: the next tile's loads are issued before the current tile is processed (its
+                    // window waits in registers); compiled for half the waves per SIMD (twice the VGPR budget)
 
 template <int MODE, int PF, int BLOCK>
-__global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(ppe_kargs a) {
+__global__ __launch_bounds__(BLOCK, PF == PF_REG ? PPE_WAVES_PER_EU / 2 : PPE_WAVES_PER_EU)
+void ppe_classify_kernel(ppe_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     using L = Lds<BLOCK>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
@@ -534,7 +541,7 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
         w12 = gld<uint32_t>(a.hdr, ro + 48u);
         qlen = gld<uint32_t>(a.len, 4u * pc);
     };
-    if (PF == PF_HOIST && tile < ntiles) load_tile(tile);  // first window in flight during the image staging
+    if (PF != PF_NONE && tile < ntiles) load_tile(tile);  // first window in flight during the image staging
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
     const uint32_t lanebase = wv * KEY_WAVE_BYTES + 4u * lane;  // this lane's key slot 0 (LDS byte address)
@@ -557,17 +564,22 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
         act_table |= ac << (2u * st);
     }
 
+    uint32_t acc_n = 0, acc_fw = 0, acc_vl = 0, acc_tcp = 0;  // PPE_CNT_LEADER == 2: wave-uniform ACL-path counts
     bool first = true;
     for (; tile < ntiles; tile += stride_waves) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < a.n;
         if (PPE_TRACE && titer < 4) TRACE_AT(2 + 5 * titer);
-        if (PF == PF_NONE || !first) load_tile(tile);
+        if (PF == PF_NONE || (PF == PF_HOIST && !first)) load_tile(tile);
         first = false;
+        // PF_REG: this tile's window is in q*, requested one iteration ago; take it, then request the next tile's
+        const uint4 c0 = q0, c1 = q1, c2 = q2;
+        const uint32_t c12 = w12, clen = qlen;
+        if (PF == PF_REG && tile + stride_waves < ntiles) load_tile(tile + stride_waves);
         if (PPE_TRACE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (PPE_TRACE && titer < 4) TRACE_AT(3 + 5 * titer);
-        const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
-        Dec k = decode(w, qlen, a.hdr, p, a.stride, a.syn_check);
+        const uint32_t w[13] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w, c12};
+        Dec k = decode(w, clen, a.hdr, p, a.stride, a.syn_check);
 
         uint32_t fh = 0;
         int32_t hit = -1;
@@ -625,7 +637,15 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
             const uint32_t pfw = __builtin_amdgcn_mbcnt_hi((uint32_t)(bfw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bfw, 0u));
             const uint32_t pdr = __builtin_amdgcn_mbcnt_hi((uint32_t)(bdr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bdr, 0u));
             const uint32_t so = (tile << 8) + 4u * (is_fw ? pfw : pdr);  // byte offset in the tile's segment
-            if (a.fw_idx && a.drop_idx) {  // both lists: one store instruction
+            if (a.fw_idx == a.drop_idx && a.fw_idx) {
+                // partition layout (one shared list): the tile's segment holds every packet of the tile, FW from the
+                // front, DROP at the back, PUNT in between, each in ascending order, the action in bits 31:30 —
+                // every slot written by one store instruction (whole-line writes, no tile count needed)
+                const uint32_t nv = min(a.n - (tile << 6), 64u);
+                const uint32_t ndr = (uint32_t)__popcll(bdr), nfw = (uint32_t)__popcll(bfw);
+                const uint32_t slot = is_fw ? pfw : (is_drop ? nv - ndr + pdr : nfw + lane - pfw - pdr);
+                if (valid) gst<uint32_t>(a.fw_idx, (tile << 8) + 4u * slot, (p + a.idx_base) | (act << 30));
+            } else if (a.fw_idx && a.drop_idx) {  // both lists: one store instruction
                 if (is_fw || is_drop) gst<uint32_t>(is_fw ? a.fw_idx : a.drop_idx, so, p + a.idx_base);
             } else {
                 if (a.fw_idx && is_fw) gst<uint32_t>(a.fw_idx, so, p + a.idx_base);
@@ -639,14 +659,53 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
         }
 
         // ---- per-reason counters: one LDS add per packet into its (status, flags) bin ----
-        if (!(PPE_ABLATE & 2) && valid)
-            atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
+        if (!(PPE_ABLATE & 2)) {
+            const uint32_t key = st | ((k.flags & 7u) << 5);
+            if (PPE_CNT_LEADER == 2) {
+                // packets that reached the ACL (the common case) are counted with wave ballots into scalar
+                // accumulators; only the others take an LDS add into their bin
+                const bool acl = valid && st <= (uint32_t)PPE_ST_ACL_DROP;
+                if (valid && !acl) atomicAdd(&bins[key], 1u);
+                acc_n += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(acl));
+                acc_fw += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(acl && st == (uint32_t)PPE_ST_ACL_FW));
+                acc_vl += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(acl && (k.flags & PPE_F_VLAN)));
+                acc_tcp += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(acl && (k.flags & PPE_F_TCP)));
+            } else if (PPE_CNT_LEADER) {
+                // one LDS add per distinct bin key in the wave (typically 2-3), by the key's first lane
+                uint64_t rem = __builtin_amdgcn_ballot_w64(valid);
+                while (rem) {
+                    const uint32_t lead = (uint32_t)__builtin_ctzll(rem);
+                    const uint32_t kl = __builtin_amdgcn_readlane(key, lead);
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(key == kl) & rem;
+                    if (lane == lead) atomicAdd(&bins[kl], (uint32_t)__popcll(m));
+                    rem &= ~m;
+                }
+            } else if (valid) {
+                atomicAdd(&bins[key], 1u);
+            }
+        }
         if (PPE_TRACE && titer < 4) TRACE_AT(6 + 5 * titer);
         ++titer;
     }
 
     TRACE_AT(22);
     if (PPE_TRACE && lane == 0 && a.trace) a.trace[(size_t)twave * 32u + 31u] = titer;
+    if (PPE_CNT_LEADER == 2 && acc_n && lane < 12u) {
+        // the ACL-path packets' counter increments (bin_counters for status ACL_FW / ACL_DROP), one lane each
+        const uint32_t ndr = acc_n - acc_fw;
+        const uint32_t ci[12] = {PPE_C_PKTS, PPE_C_L2_RX_OK, PPE_C_IPV4_RX_OK, PPE_C_ACL_FW, PPE_C_FLOW_PROC_OK,
+                                 PPE_C_OUT_FW, PPE_C_ACL_DROP, PPE_C_FLOW_PROC_FAIL, PPE_C_OUT_DROP, PPE_C_VLAN_RX_OK,
+                                 PPE_C_TCP_RX_OK, PPE_C_UDP_RX_OK};
+        const uint32_t cv[12] = {acc_n, acc_n, acc_n, acc_fw, acc_fw, acc_fw, ndr, ndr, ndr, acc_vl, acc_tcp,
+                                 acc_n - acc_tcp};
+        uint32_t idx = 0, val = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 12u; ++j) {
+            idx = lane == j ? ci[j] : idx;
+            val = lane == j ? cv[j] : val;
+        }
+        if (val) atomicAdd(&lcnt[idx], val);
+    }
     __syncthreads();
     for (uint32_t b = tid; b < PPE_NBINS; b += BLOCK) {  // expand the bins into counter increments
         const uint32_t c = bins[b];
@@ -729,6 +788,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int block) {
 #define PPE_DISPATCH_P(FN, M, ...)                                   \
     do {                                                             \
         if (pipe == PF_NONE) PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__); \
+        if (pipe == PF_REG) PPE_DISPATCH_B(FN, M, PF_REG, __VA_ARGS__); \
         PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__);                \
     } while (0)
 #define PPE_DISPATCH(FN, ...)                                        \

@@ -78,6 +78,8 @@ class Engine:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         stride = hdr.shape[1]
         ptrs = {k: (v.data_ptr() if v is not None else None) for k, v in out.items()}
+        if ptrs.get("part_idx"):  # partition layout: one list passed as both fw_idx and drop_idx
+            ptrs["fw_idx"] = ptrs["drop_idx"] = ptrs.pop("part_idx")
         self.classify_ptrs(hdr.data_ptr(), lens.data_ptr(), lens.numel(), stride, ptrs, cfg,
                            ts.data_ptr() if ts is not None else None, s.cuda_stream)
 
@@ -101,14 +103,16 @@ class Engine:
             res["drop_idx"] = np.zeros(n, np.uint32)
         if "tile_cnt" in outputs:
             res["tile_cnt"] = np.zeros((n + 63) // 64, np.uint32)
+        if "part_idx" in outputs:  # partition layout: one list passed as both fw_idx and drop_idx
+            res["part_idx"] = np.zeros(n, np.uint32)
         if "tuple" in outputs:
             res["tuple"] = np.zeros((n, 4), np.uint32)
         if ts is not None:
             ts = np.ascontiguousarray(ts, dtype=np.uint64)
         b = abi.Batch(hdr.ctypes.data, lens.ctypes.data, ts.ctypes.data if ts is not None else None, n, stride)
         g = lambda k: res[k].ctypes.data if k in res else None  # noqa: E731
-        r = abi.Result(g("verdict"), g("flow_hash"), g("acl_hit"), g("fw_idx"), g("drop_idx"), g("tile_cnt"),
-                       g("tuple"))
+        fw, dr = (g("part_idx"), g("part_idx")) if "part_idx" in res else (g("fw_idx"), g("drop_idx"))
+        r = abi.Result(g("verdict"), g("flow_hash"), g("acl_hit"), fw, dr, g("tile_cnt"), g("tuple"))
         rc = self.lib.ppe_classify_host(self.ctx, C.byref(b), C.byref(r), C.byref(cfg or self.cfg()), int(chunk))
         self._check(rc, "ppe_classify_host")
         return res

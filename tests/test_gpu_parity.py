@@ -17,6 +17,7 @@ from ppe.abi import ST  # noqa: E402
 NOW = 1_700_000_000
 DEV = torch.device("cuda:0")
 OUTS = ("verdict", "flow_hash", "acl_hit", "fw_idx", "drop_idx", "tile_cnt", "tuple")
+PART_OUTS = ("verdict", "flow_hash", "acl_hit", "part_idx", "tuple")
 
 
 @pytest.fixture(scope="module")
@@ -34,7 +35,7 @@ def gpu_classify(eng, hdr, lens, ts=None, cfg=None, outs=OUTS):
     tt = torch.from_numpy(np.ascontiguousarray(ts, np.uint64).view(np.int64)).to(DEV) if ts is not None else None
     shapes = {"tile_cnt": ((n + 63) // 64,), "tuple": (n, 4)}
     out = {k: torch.full(shapes.get(k, (n,)), -7, dtype=torch.int32, device=DEV) if k in outs else None
-           for k in OUTS}
+           for k in OUTS + ("part_idx",)}
     eng.classify_torch(th, tl, out, cfg=cfg or eng.cfg(now_seconds=NOW), ts=tt)
     torch.cuda.synchronize()
     res = {}
@@ -69,6 +70,20 @@ def check_compaction(res, n):
         assert np.array_equal(res["drop_idx"][lo:lo + len(dr)], dr), t
 
 
+def check_partition(res, n):
+    """Partition layout (fw_idx == drop_idx): each tile's slots hold all of its packets, FW ascending from the front,
+    DROP ascending at the back, PUNT ascending in between, each entry index | action << 30."""
+    act = (res["verdict"] >> 8) & 0xFF
+    part = res["part_idx"]
+    for t in range((n + 63) // 64):
+        lo, hi = 64 * t, min(n, 64 * t + 64)
+        fw = np.nonzero(act[lo:hi] == 0)[0] + lo
+        dr = np.nonzero(act[lo:hi] == 1)[0] + lo
+        pu = np.nonzero(act[lo:hi] == 2)[0] + lo
+        want = np.concatenate([fw, pu | (2 << 30), dr | (1 << 30)]).astype(np.uint32)
+        assert np.array_equal(part[lo:hi], want), t
+
+
 # ---------------------------------------------------------------- fixtures frozen in tests/golden
 @pytest.mark.parametrize("tag,cfg", [("a", (0, 1)), ("b", (1, 0))])
 def test_golden_fixture_device_path(eng, golden, tag, cfg):
@@ -80,6 +95,20 @@ def test_golden_fixture_device_path(eng, golden, tag, cfg):
     check_compaction(res, len(g["len"]))
     cnt = eng.counters()
     assert [cnt[n] for n in abi.COUNTERS] == g[f"{tag}_counters"][:30].tolist()
+
+
+@pytest.mark.parametrize("tag,cfg", [("a", (0, 1)), ("b", (1, 0))])
+def test_golden_fixture_partition_layout(eng, golden, tag, cfg):
+    g = golden
+    eng.commit(g["rules"], g["used"], default_action=1)
+    res = gpu_classify(eng, g["hdr"], g["len"], g["ts"], eng.cfg(cfg[0], cfg[1], int(g["now"])), outs=PART_OUTS)
+    assert_same(res, {k: g[f"{tag}_{k}"] for k in ("verdict", "flow_hash", "acl_hit", "tuple")})
+    check_partition(res, len(g["len"]))
+    for chunk in (64, 1000):  # host pipeline, chunked: entries carry the batch index
+        res = eng.classify_host(g["hdr"], g["len"], ts=g["ts"], cfg=eng.cfg(cfg[0], cfg[1], int(g["now"])),
+                                chunk=chunk, outputs=PART_OUTS)
+        assert_same(res, {k: g[f"{tag}_{k}"] for k in ("verdict", "flow_hash", "acl_hit", "tuple")})
+        check_partition(res, len(g["len"]))
 
 
 def test_golden_fixture_host_pipeline(eng, golden):
@@ -186,8 +215,12 @@ def test_ragged_sizes(eng, n):
     eng.commit(rules, default_action=1)
     res = gpu_classify(eng, pk["hdr"], pk["len"])
     o = pyoracle.Oracle(rules, default_action=1)
-    assert_same(res, o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW)))
+    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW))
+    assert_same(res, ref)
     check_compaction(res, n)
+    part = gpu_classify(eng, pk["hdr"], pk["len"], outs=PART_OUTS)
+    assert_same(part, ref)
+    check_partition(part, n)
 
 
 def test_argument_errors(eng):
@@ -207,14 +240,15 @@ def test_argument_errors(eng):
     assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == 0
     t = abi.Tuning(block=300)
     assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
-    for pl in (2, 3, 5):  # the register / LDS-DMA prefetch variants are not built
+    for pl in (3, 5):  # the LDS-DMA prefetch variant is not built
         t = abi.Tuning(pipeline=pl)
         assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
 
 
 TUNINGS = [dict(lds_image=0), dict(block=512), dict(block=1024), dict(block=256), dict(pipeline=1),
            dict(pipeline=4), dict(pipeline=1, block=256), dict(pipeline=1, block=512), dict(pipeline=1, lds_image=0),
-           dict(pipeline=4, lds_image=0), dict(pipeline=4, block=1024), dict(blocks_per_cu=16), dict(blocks_per_cu=1)]
+           dict(pipeline=4, lds_image=0), dict(pipeline=4, block=1024), dict(blocks_per_cu=16), dict(blocks_per_cu=1),
+           dict(pipeline=2), dict(pipeline=2, block=256, blocks_per_cu=4), dict(pipeline=2, lds_image=0)]
 
 
 @pytest.mark.parametrize("tune", TUNINGS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))

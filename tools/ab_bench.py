@@ -62,12 +62,18 @@ def main():
             libs[path] = abi.load_variant(path)
         eng = Engine(0, lib=libs[path])
         eng.commit(rules, default_action=1)
-        if kv:
-            eng.tuning(**{k: int(v) for k, v in (x.split("=") for x in kv.split(","))})
+        kvs = dict(x.split("=") for x in kv.split(",")) if kv else {}
+        # outs=sep (default): separate FW / DROP lists + tile counts; outs=part: one partition list, no tile counts
+        mode = kvs.pop("outs", "sep")
+        if kvs:
+            eng.tuning(**{k: int(v) for k, v in kvs.items()})
         calls = []
         for hdr, lens, outs in bufs:
             bb = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, args.stride)
-            rr = abi.Result(*(o.data_ptr() for o in outs), None)
+            ptrs = [o.data_ptr() for o in outs]
+            if mode == "part":
+                ptrs[4], ptrs[5] = ptrs[3], None
+            rr = abi.Result(*ptrs, None)
             calls.append((bb, rr))
         variants.append(dict(name=name, eng=eng, calls=calls, kern=[], step=[]))
     cfg = Engine.cfg(now_seconds=NOW)
