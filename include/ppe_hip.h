@@ -163,6 +163,13 @@ int  ppe_rules_commit(ppe_ctx_t *ctx, const RCP_BLOCK_ACL_RULE_TUPLE *rules, con
 int  ppe_classify(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
                   void *stream);
 
+/* Several device-resident batches (in[i] → out[i]), pipelined: consecutive batches alternate over two internal
+ * streams so that one batch's launch ramp-up overlaps the previous batch's tail.  Stream-ordered like
+ * ppe_classify: the batches run after the work already queued on `stream`, and work queued on `stream` after this
+ * call runs after all of them.  The batches' output buffers must not overlap (two may be written at once). */
+int  ppe_classify_batches(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, uint32_t nbatch,
+                          const ppe_cfg_t *cfg, void *stream);
+
 /* Host-resident batch: pipelined H2D → classify → D2H over `chunk`-packet slices on internal streams.
  * Output pointers are host pointers (NULL to skip).  Blocks until done. */
 int  ppe_classify_host(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,

@@ -21,6 +21,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <vector>
@@ -67,81 +68,90 @@ inline uint32_t mac_lo(const uint8_t *m) {
 }
 inline uint32_t mac_hi(const uint8_t *m) { return (uint32_t)m[4] | ((uint32_t)m[5] << 8); }
 
-}  // namespace
+struct TNode {
+    uint32_t thr;    // internal: split threshold
+    uint32_t left;   // internal: left child index (right = left + 1)
+    uint32_t dim;    // split dimension, PPE_NODE_LEAF for a leaf
+    uint32_t first;  // leaf: first entry in `leaf`
+    uint32_t cnt;    // leaf: number of candidates
+};
 
-extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
-                                   uint32_t default_action, uint32_t binth, uint32_t **words_out,
-                                   uint32_t *n_words_out, ppe_acl_stats_t *st) {
-    if (!words_out || !n_words_out) return PPE_EINVAL;
-    if (n && !rules) return PPE_EINVAL;
-    if (n > (1u << 24)) return PPE_EINVAL;
-    if (binth == 0) binth = 1;  // one candidate per leaf: deepest tree, shortest scan (fastest measured, DESIGN.md)
-    auto t0 = std::chrono::steady_clock::now();
-
-    // ---- compile eligible rules to boxes (slot order = ascending rule index) ----
-    std::vector<Rule> R;
-    std::vector<uint32_t> resid_words;
-    R.reserve(n);
-    for (uint32_t i = 0; i < n; ++i) {
-        if (used && used[i] != RULE_ENTRY_STATUS_USED) continue;
-        const RCP_BLOCK_ACL_RULE_TUPLE &t = rules[i];
-        if (t.sip_mask > 32 || t.dip_mask > 32) return PPE_EINVAL;  // parsers reject these (rule/rule.c:63-73)
-        if (t.sport_start > t.sport_end || t.dport_start > t.dport_end || t.protocol_start > t.protocol_end)
-            continue;  // empty range: can never match
-        Rule r;
-        r.lo[PPE_DIM_SIP] = prefix_lo(t.sip, t.sip_mask);
-        r.hi[PPE_DIM_SIP] = prefix_hi(t.sip, t.sip_mask);
-        r.lo[PPE_DIM_DIP] = prefix_lo(t.dip, t.dip_mask);
-        r.hi[PPE_DIM_DIP] = prefix_hi(t.dip, t.dip_mask);
-        r.lo[PPE_DIM_SPORT] = t.sport_start;
-        r.hi[PPE_DIM_SPORT] = t.sport_end;
-        r.lo[PPE_DIM_DPORT] = t.dport_start;
-        r.hi[PPE_DIM_DPORT] = t.dport_end;
-        r.lo[PPE_DIM_PROTO] = t.protocol_start;
-        r.hi[PPE_DIM_PROTO] = t.protocol_end;
-        r.id = i;
-        r.action = t.action;
-        r.resid = 0;
-        if (mac_nonzero(t.dmac)) r.resid |= PPE_RESID_DMAC;
-        if (mac_nonzero(t.smac)) r.resid |= PPE_RESID_SMAC;
-        if (t.time_start != 0 || t.time_end != 0) r.resid |= PPE_RESID_TIME;
-        r.slot = (uint32_t)R.size();
-        R.push_back(r);
-        uint32_t rw[8] = {mac_lo(t.dmac), mac_hi(t.dmac), mac_lo(t.smac), mac_hi(t.smac),
-                          (uint32_t)t.time_start, (uint32_t)(t.time_start >> 32),
-                          (uint32_t)t.time_end, (uint32_t)(t.time_end >> 32)};
-        resid_words.insert(resid_words.end(), rw, rw + 8);
-    }
-
-    // ---- recursive partitioning, BFS so that children are contiguous and numbered after their parent ----
-    struct TNode {
-        uint32_t thr;    // internal: split threshold
-        uint32_t left;   // internal: left child index (right = left + 1)
-        uint32_t dim;    // split dimension, PPE_NODE_LEAF for a leaf
-        uint32_t first;  // leaf: first entry in `leaf`
-        uint32_t cnt;    // leaf: number of candidates
-    };
-    std::vector<TNode> nodes;
+struct Forest {
+    std::vector<TNode> nodes;  // BFS over every root: roots first, children contiguous and after their parent
     std::vector<uint32_t> leaf;
-    const size_t node_budget = PPE_NODE_MAX - 2;
-    uint32_t max_depth = 0, n_leaves = 0, max_leaf = 0;
+    uint32_t max_depth = 0, n_leaves = 0, max_leaf = 0, n_roots = 0;
     double depth_sum = 0;
+    std::vector<uint32_t> runs;  // jump root: buckets per root, in bucket order
+    double avg_depth() const { return n_leaves ? depth_sum / n_leaves : 0.0; }
+};
 
-    std::deque<Work> q;
-    {
-        Work w;
-        w.node = 0;
-        w.depth = 0;
-        w.lo[0] = w.lo[1] = w.lo[2] = w.lo[3] = w.lo[4] = 0;
-        w.hi[0] = w.hi[1] = 0xffffffffu;
-        w.hi[2] = w.hi[3] = 0xffffu;
-        w.hi[4] = 0xffu;
-        w.rules.resize(R.size());
-        for (uint32_t s = 0; s < R.size(); ++s) w.rules[s] = s;
-        q.push_back(std::move(w));
-        nodes.resize(1);
+// Jump (cut) root: bucket b = key[dim] >> shift, 2^bits buckets, each the root of its own subtree
+struct Jump {
+    uint32_t dim = 0, shift = 0, bits = 0;
+};
+
+Work full_box(const std::vector<Rule> &R) {
+    Work w;
+    w.node = 0;
+    w.depth = 0;
+    w.lo[0] = w.lo[1] = w.lo[2] = w.lo[3] = w.lo[4] = 0;
+    w.hi[0] = w.hi[1] = 0xffffffffu;
+    w.hi[2] = w.hi[3] = 0xffffu;
+    w.hi[4] = 0xffu;
+    w.rules.resize(R.size());
+    for (uint32_t s = 0; s < R.size(); ++s) w.rules[s] = s;
+    return w;
+}
+
+// The cut's buckets as subtree roots: every bucket gets the rules whose box meets it (ascending, closed after the
+// first unconditional cover); a run of consecutive buckets with the same rule list shares one subtree, built over
+// the run's union box (a classifier correct for the union is correct for each bucket in it).
+// Returns one Work per run, and each run's bucket count in `runs`.
+std::vector<Work> cut_roots(const std::vector<Rule> &R, const Jump &j, std::vector<uint32_t> &runs) {
+    const uint32_t nb = 1u << j.bits;
+    std::vector<std::vector<uint32_t>> lists(nb);
+    std::vector<uint8_t> closed(nb, 0);
+    Work box = full_box({});
+    for (uint32_t s = 0; s < R.size(); ++s) {
+        const Rule &r = R[s];
+        const uint32_t b0 = r.lo[j.dim] >> j.shift, b1 = r.hi[j.dim] >> j.shift;
+        for (uint32_t b = b0; b <= b1; ++b) {
+            if (closed[b]) continue;
+            lists[b].push_back(s);
+            box.lo[j.dim] = b << j.shift;
+            box.hi[j.dim] = box.lo[j.dim] | ((1u << j.shift) - 1u);
+            if (r.resid == 0 && covers(r, box.lo, box.hi)) closed[b] = 1;
+        }
     }
+    std::vector<Work> roots;
+    for (uint32_t b = 0; b < nb;) {
+        uint32_t e = b + 1;
+        while (e < nb && lists[e] == lists[b]) ++e;
+        Work w = full_box({});
+        w.lo[j.dim] = b << j.shift;
+        w.hi[j.dim] = ((e - 1u) << j.shift) | ((1u << j.shift) - 1u);
+        w.rules = std::move(lists[b]);
+        runs.push_back(e - b);
+        roots.push_back(std::move(w));
+        b = e;
+    }
+    return roots;
+}
 
+// HyperSplit partitioning of every root box, breadth-first over the whole forest (so the nodes of depth < L are a
+// prefix of the node array for every L: the LDS-staged top of the image is whole levels)
+Forest build_forest(const std::vector<Rule> &R, std::vector<Work> roots, uint32_t binth) {
+    Forest f;
+    std::vector<TNode> &nodes = f.nodes;
+    const size_t node_budget = PPE_NODE_MAX - 2;
+    std::deque<Work> q;
+    f.n_roots = (uint32_t)roots.size();
+    nodes.resize(roots.size());
+    for (uint32_t i = 0; i < roots.size(); ++i) {
+        roots[i].node = i;
+        roots[i].depth = 0;
+        q.push_back(std::move(roots[i]));
+    }
     std::vector<uint32_t> clo, chi, cand;
     while (!q.empty()) {
         Work w = std::move(q.front());
@@ -160,13 +170,13 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         auto make_leaf = [&](const std::vector<uint32_t> &L) {
             TNode &nd = nodes[w.node];
             nd.dim = PPE_NODE_LEAF;
-            nd.first = (uint32_t)leaf.size();
+            nd.first = (uint32_t)f.leaf.size();
             nd.cnt = (uint32_t)L.size();
-            leaf.insert(leaf.end(), L.begin(), L.end());
-            ++n_leaves;
-            max_leaf = std::max(max_leaf, (uint32_t)L.size());
-            depth_sum += w.depth;
-            if (w.depth > max_depth) max_depth = w.depth;
+            f.leaf.insert(f.leaf.end(), L.begin(), L.end());
+            ++f.n_leaves;
+            f.max_leaf = std::max(f.max_leaf, (uint32_t)L.size());
+            f.depth_sum += w.depth;
+            if (w.depth > f.max_depth) f.max_depth = w.depth;
         };
 
         const bool first_certain = !S.empty() && R[S[0]].resid == 0 && covers(R[S[0]], w.lo, w.hi);
@@ -239,6 +249,101 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         q.push_back(std::move(L));
         q.push_back(std::move(Rt));
     }
+    return f;
+}
+
+}  // namespace
+
+extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                                   uint32_t default_action, uint32_t binth, uint32_t **words_out,
+                                   uint32_t *n_words_out, ppe_acl_stats_t *st) {
+    if (!words_out || !n_words_out) return PPE_EINVAL;
+    if (n && !rules) return PPE_EINVAL;
+    if (n > (1u << 24)) return PPE_EINVAL;
+    if (binth == 0) binth = 1;  // one candidate per leaf: deepest tree, shortest scan (fastest measured, DESIGN.md)
+    auto t0 = std::chrono::steady_clock::now();
+
+    // ---- compile eligible rules to boxes (slot order = ascending rule index) ----
+    std::vector<Rule> R;
+    std::vector<uint32_t> resid_words;
+    R.reserve(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (used && used[i] != RULE_ENTRY_STATUS_USED) continue;
+        const RCP_BLOCK_ACL_RULE_TUPLE &t = rules[i];
+        if (t.sip_mask > 32 || t.dip_mask > 32) return PPE_EINVAL;  // parsers reject these (rule/rule.c:63-73)
+        if (t.sport_start > t.sport_end || t.dport_start > t.dport_end || t.protocol_start > t.protocol_end)
+            continue;  // empty range: can never match
+        Rule r;
+        r.lo[PPE_DIM_SIP] = prefix_lo(t.sip, t.sip_mask);
+        r.hi[PPE_DIM_SIP] = prefix_hi(t.sip, t.sip_mask);
+        r.lo[PPE_DIM_DIP] = prefix_lo(t.dip, t.dip_mask);
+        r.hi[PPE_DIM_DIP] = prefix_hi(t.dip, t.dip_mask);
+        r.lo[PPE_DIM_SPORT] = t.sport_start;
+        r.hi[PPE_DIM_SPORT] = t.sport_end;
+        r.lo[PPE_DIM_DPORT] = t.dport_start;
+        r.hi[PPE_DIM_DPORT] = t.dport_end;
+        r.lo[PPE_DIM_PROTO] = t.protocol_start;
+        r.hi[PPE_DIM_PROTO] = t.protocol_end;
+        r.id = i;
+        r.action = t.action;
+        r.resid = 0;
+        if (mac_nonzero(t.dmac)) r.resid |= PPE_RESID_DMAC;
+        if (mac_nonzero(t.smac)) r.resid |= PPE_RESID_SMAC;
+        if (t.time_start != 0 || t.time_end != 0) r.resid |= PPE_RESID_TIME;
+        r.slot = (uint32_t)R.size();
+        R.push_back(r);
+        uint32_t rw[8] = {mac_lo(t.dmac), mac_hi(t.dmac), mac_lo(t.smac), mac_hi(t.smac),
+                          (uint32_t)t.time_start, (uint32_t)(t.time_start >> 32),
+                          (uint32_t)t.time_end, (uint32_t)(t.time_end >> 32)};
+        resid_words.insert(resid_words.end(), rw, rw + 8);
+    }
+
+    // ---- the root: a cut on the top bits of one dimension (jump table) or a single split tree ----
+    const Forest base = build_forest(R, {full_box(R)}, binth);
+    Forest best = base;
+    Jump jbest;  // bits == 0: no jump table
+    if (!base.nodes.empty() && base.nodes[0].dim != PPE_NODE_LEAF) {
+        // cut the dimension the plain tree splits first; try a few widths, keep the cheapest: walk levels (the
+        // fixed-trip LDS walk pays the deepest leaf, the per-lane global walk the average; the table read counts
+        // as a level) plus one level per 16 KB of nodes and table (LDS footprint: fewer image copies per CU).
+        // Measured on MI355X (C1 / C4, two-stream pipeline): 10 bits beat 0, 8 and 12.
+        const uint32_t jd = base.nodes[0].dim;
+        const uint32_t width = jd <= PPE_DIM_DIP ? 32u : (jd <= PPE_DIM_DPORT ? 16u : 8u);
+        auto cost = [](const Forest &f, uint32_t bits) {
+            const double bytes = 16.0 * f.nodes.size() + (bits ? 4.0 * (1u << bits) : 0.0);
+            return 0.5 * (f.max_depth + 1) + 0.5 * (f.avg_depth() + 1) + (bits ? 1.0 : 0.0) + bytes / 16384.0;
+        };
+        double cbest = cost(base, 0);
+        // PPE_JUMP_BITS (tuning / experiments): 0 = never cut, k = cut exactly k bits
+        const char *fj = std::getenv("PPE_JUMP_BITS");
+        const int force = fj && *fj ? std::atoi(fj) : -1;
+        if (force >= 0) cbest = 1e30;
+        for (uint32_t bits : {4u, 6u, 8u, 10u, 12u}) {
+            if (bits >= width || force == 0) break;
+            if (force > 0 && (int)bits != force) continue;
+            if (force < 0 && bits > 8 && base.nodes.size() > 65536) break;  // large sets: wide cuts only replicate
+            Jump j = {jd, width - bits, bits};
+            std::vector<uint32_t> runs;
+            std::vector<Work> roots = cut_roots(R, j, runs);
+            Forest f = build_forest(R, std::move(roots), binth);
+            f.runs = std::move(runs);
+            if (force < 0 && f.nodes.size() > 2 * base.nodes.size() + (1u << bits) + 64u) continue;  // blow-up
+            const double c = cost(f, bits);
+            if (std::getenv("PPE_ACL_DEBUG"))
+                std::fprintf(stderr, "acl_build: jump dim %u bits %u: nodes %zu max_depth %u avg %.2f cost %.2f\n",
+                             jd, bits, f.nodes.size(), f.max_depth, f.avg_depth(), c);
+            if (c < cbest - 1e-9) {
+                cbest = c;
+                best = std::move(f);
+                jbest = j;
+            }
+        }
+    }
+    if (best.nodes.size() > PPE_NODE_MAX - 2) return PPE_ENOMEM;
+    std::vector<TNode> &nodes = best.nodes;
+    std::vector<uint32_t> &leaf = best.leaf;
+    const uint32_t max_depth = best.max_depth, n_leaves = best.n_leaves, max_leaf = best.max_leaf;
+    const double depth_sum = best.depth_sum;
 
     // ---- assemble the image ----
     const uint32_t n_nodes = (uint32_t)nodes.size();
@@ -254,7 +359,8 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
             nd.first = first;
         }
     }
-    const uint32_t off_nodes = PPE_IMG_HDR_WORDS;
+    const uint32_t n_jump = jbest.bits ? 1u << jbest.bits : 0u;
+    const uint32_t off_nodes = PPE_IMG_HDR_WORDS + n_jump;  // the jump table (if any) sits between header and nodes
     const uint32_t off_leaf = off_nodes + PPE_NODE_WORDS * n_nodes;
     uint32_t off_rules = off_leaf + (uint32_t)lwords.size();
     off_rules = (off_rules + 7u) & ~7u;
@@ -280,6 +386,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     img[PPE_IMG_W_MAXLEAF] = max_leaf;
     img[PPE_IMG_W_TOTAL] = total;
     img[PPE_IMG_W_ROOTKS] = nodes[0].dim << 8;
+    img[PPE_IMG_W_JUMP] = jbest.bits ? (jbest.dim | (jbest.shift << 8) | (jbest.bits << 16)) : 0u;
     auto node_byte = [&](uint32_t k) { return 4u * off_nodes + 16u * k; };
     for (uint32_t k = 0; k < n_nodes; ++k) {
         const TNode &nd = nodes[k];
@@ -298,6 +405,12 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
             o[2] = node_byte(nd.left + 1);
             o[3] = (nodes[nd.left].dim << 8) | (nodes[nd.left + 1].dim << 24);
         }
+    }
+    if (n_jump) {  // bucket → its subtree root: node byte offset | the root's key slot << 24
+        uint32_t b = 0;
+        for (uint32_t r = 0; r < best.n_roots; ++r)
+            for (uint32_t i = 0; i < best.runs[r]; ++i, ++b)
+                img[PPE_IMG_HDR_WORDS + b] = node_byte(r) | (nodes[r].dim << 24);
     }
     if (!lwords.empty()) std::memcpy(img + off_leaf, lwords.data(), lwords.size() * sizeof(uint32_t));
     for (uint32_t s = 0; s <= n_slots; ++s) {

@@ -25,10 +25,13 @@ namespace {
 
 constexpr int kSlotSets = 4;      // set 0: ppe_classify; 1..3: host pipeline streams
 constexpr int kHostStreams = 3;
+// ppe_classify_batches: two streams, so a batch's launch ramp-up overlaps the previous batch's tail (C1: 20.6 ->
+// 16.5 us per batch; three streams measured 17.0)
+constexpr int kPipeStreams = 2;
 // tile fetch of the classify kernel (PF_* in ppe_kernels.hip): 0 at the loop top, 1 the first tile's loads issued
 // before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering and an LDS-DMA next-tile
 // pipeline were measured slower (28.3 / 24.4 us) and are not built.
-constexpr int kPfNone = 0, kPfHoist = 1, kPfReg = 2;
+constexpr int kPfNone = 0, kPfHoist = 1, kPfReg = 2, kPfHead = 3;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 
 struct HostStage {
@@ -65,6 +68,9 @@ struct ppe_ctx {
     size_t ev_used = 0;
     // host pipeline
     HostStage hs[kHostStreams];
+    // device-batch pipeline (ppe_classify_batches): consecutive batches alternate over these streams
+    hipStream_t pipe[kPipeStreams] = {};
+    hipEvent_t pipe_ev[kPipeStreams + 1] = {};
     ppe_tuning_t tune;
     unsigned long long *trace = nullptr;  // ppe_debug_trace
     char err[256] = {0};
@@ -102,7 +108,7 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl == 1 || pl == 2 || pl == 4 ? (uint32_t)pl : 0u;
+    t.pipeline = pl >= 1 && pl <= 4 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     return t;
 }
@@ -124,7 +130,9 @@ uint32_t image_budget(uint32_t block) {
 }
 
 StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
-    const int pf = c->tune.pipeline == 1 ? kPfNone : (c->tune.pipeline == 2 ? kPfReg : kPfHoist);
+    const int pf = c->tune.pipeline == 1 ? kPfNone
+                 : c->tune.pipeline == 2 ? kPfReg
+                 : c->tune.pipeline == 3 ? kPfHead : kPfHoist;
     const uint32_t words = (uint32_t)img.size(), bytes = words * 4u;
     StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0};
     if (!c->tune.lds_image) {
@@ -142,7 +150,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
     }
     const uint32_t budget = image_budget(p.block);
     const uint32_t off_resid = img[PPE_IMG_W_OFFRESID], off_rules = img[PPE_IMG_W_OFFRULES];
-    const uint32_t n_nodes = img[PPE_IMG_W_NNODES];
+    const uint32_t n_nodes = img[PPE_IMG_W_NNODES], off_nodes = img[PPE_IMG_W_OFFNODES];
     if (bytes <= budget) {
         p.mode = 1;
         p.lds_words = words;
@@ -154,10 +162,10 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
         p.mode = 2;
         p.lds_words = off_rules;
         p.lds_nodes = n_nodes;
-    } else if (budget >= 4u * (PPE_IMG_HDR_WORDS + PPE_NODE_WORDS * 64u)) {  // the top of the BFS tree
+    } else if (budget >= 4u * (off_nodes + PPE_NODE_WORDS * 64u)) {  // header, jump table, top of the BFS forest
         p.mode = 2;
-        p.lds_nodes = std::min(n_nodes, (budget / 4u - PPE_IMG_HDR_WORDS) / PPE_NODE_WORDS);
-        p.lds_words = PPE_IMG_HDR_WORDS + PPE_NODE_WORDS * p.lds_nodes;
+        p.lds_nodes = std::min(n_nodes, (budget / 4u - off_nodes) / PPE_NODE_WORDS);
+        p.lds_words = off_nodes + PPE_NODE_WORDS * p.lds_nodes;
     }
     return p;
 }
@@ -189,13 +197,13 @@ int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const 
     {
         std::vector<uint32_t> &le = c->level_end[slot];
         le.clear();
-        const uint32_t nn = words[PPE_IMG_W_NNODES];
-        std::vector<uint8_t> depth(nn, 0);
+        const uint32_t nn = words[PPE_IMG_W_NNODES], on = words[PPE_IMG_W_OFFNODES];
+        std::vector<uint8_t> depth(nn, 0);  // every root of the forest (jump root: several) has depth 0
         for (uint32_t k = 0; k < nn; ++k) {
-            const uint32_t *nd = words + PPE_IMG_HDR_WORDS + PPE_NODE_WORDS * k;
+            const uint32_t *nd = words + on + PPE_NODE_WORDS * k;
             if (nd[0] != PPE_LEAF_THR) {  // children: byte offsets from the image start
-                depth[(nd[1] / 4u - PPE_IMG_HDR_WORDS) / PPE_NODE_WORDS] = (uint8_t)(depth[k] + 1u);
-                depth[(nd[2] / 4u - PPE_IMG_HDR_WORDS) / PPE_NODE_WORDS] = (uint8_t)(depth[k] + 1u);
+                depth[(nd[1] / 4u - on) / PPE_NODE_WORDS] = (uint8_t)(depth[k] + 1u);
+                depth[(nd[2] / 4u - on) / PPE_NODE_WORDS] = (uint8_t)(depth[k] + 1u);
             }
             if (le.size() <= depth[k]) le.resize(depth[k] + 1u, 0u);
             le[depth[k]] = k + 1u;
@@ -243,6 +251,8 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe
     a.max_depth = c->h_img[r][PPE_IMG_W_MAXDEPTH];
     a.max_leaf = c->h_img[r][PPE_IMG_W_MAXLEAF];
     a.root_ks = c->h_img[r][PPE_IMG_W_ROOTKS];
+    a.jump = c->h_img[r][PPE_IMG_W_JUMP];
+    a.off_nodes = c->h_img[r][PPE_IMG_W_OFFNODES];
     if (plan.mode == 1) {
         a.lds_iters = a.max_depth + 1u;
     } else if (plan.mode == 2) {  // node reads 0..L-1 only visit depths < L: all inside the staged prefix
@@ -350,6 +360,10 @@ int ppe_ctx_destroy(ppe_ctx_t *c) {
     }
     if (c->d_cslots) (void)hipFree(c->d_cslots);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    for (hipStream_t s : c->pipe)
+        if (s) (void)hipStreamDestroy(s);
+    for (hipEvent_t e : c->pipe_ev)
+        if (e) (void)hipEventDestroy(e);
     for (auto &h : c->hs) {
         if (h.s) (void)hipStreamDestroy(h.s);
         (void)hipFree(h.hdr);
@@ -396,6 +410,36 @@ int ppe_classify(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, c
     if (rc != PPE_OK || in->n == 0) return rc;
     HIPCHK(c, use_device(c));
     return launch(c, in, out, cfg, (hipStream_t)stream, 0);
+}
+
+int ppe_classify_batches(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t nbatch,
+                         const ppe_cfg_t *cfg, void *stream) {
+    if (!c || (nbatch && (!in || !out))) return PPE_EINVAL;
+    for (uint32_t i = 0; i < nbatch; ++i) {
+        const int rc = check_batch(c, &in[i], cfg);
+        if (rc != PPE_OK) return rc;
+    }
+    if (nbatch == 0) return PPE_OK;
+    HIPCHK(c, use_device(c));
+    const hipStream_t s = (hipStream_t)stream;
+    if (!c->pipe[0]) {
+        for (int k = 0; k < kPipeStreams; ++k) HIPCHK(c, hipStreamCreateWithFlags(&c->pipe[k], hipStreamNonBlocking));
+        for (hipEvent_t &e : c->pipe_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    // fork: the pipeline streams start after the work already queued on `stream`
+    HIPCHK(c, hipEventRecord(c->pipe_ev[kPipeStreams], s));
+    for (int k = 0; k < kPipeStreams; ++k) HIPCHK(c, hipStreamWaitEvent(c->pipe[k], c->pipe_ev[kPipeStreams], 0));
+    for (uint32_t i = 0; i < nbatch; ++i) {
+        if (in[i].n == 0) continue;
+        const int rc = launch(c, &in[i], &out[i], cfg, c->pipe[i % kPipeStreams], 0);
+        if (rc != PPE_OK) return rc;
+    }
+    // join: `stream` continues after every batch
+    for (int k = 0; k < kPipeStreams; ++k) {
+        HIPCHK(c, hipEventRecord(c->pipe_ev[k], c->pipe[k]));
+        HIPCHK(c, hipStreamWaitEvent(s, c->pipe_ev[k], 0));
+    }
+    return PPE_OK;
 }
 
 int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
@@ -615,9 +659,10 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 2 && t->pipeline != 4)
+    if (t->pipeline > 4)
         return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top), 2 (next tile "
-                                   "prefetched into registers) or 4 (first tile's loads before the image staging)");
+                                   "prefetched into registers), 3 (next tile's head prefetched) or 4 (first tile's "
+                                   "loads before the image staging)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     c->tune = *t;
     c->tune.pipeline = t->pipeline;

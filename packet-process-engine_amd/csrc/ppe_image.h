@@ -1,5 +1,5 @@
 /*
- * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v3.
+ * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v4.
  *
  * The image is a HyperSplit-style binary decision tree over the five header dimensions, flattened in BFS order
  * (children of node k are numbered after k, so a walk strictly descends and always terminates), followed by the
@@ -13,7 +13,14 @@
  *  word 5   off_nodes         word 6  off_leaf            word 7  off_rules       word 8  off_resid   (word offsets)
  *  word 9   default_action    word 10 max_depth           word 11 total words     word 12 max leaf entries
  *  word 13  root key slot << 8 (the dimension the root splits on; PPE_NODE_LEAF when the root is a leaf)
- *  word 14..15 reserved
+ *  word 14  jump root: dim | shift << 8 | bits << 16, or 0 for a single tree rooted at node 0
+ *  word 15  reserved
+ *
+ *  jump table (format v4; present iff word 14 != 0): 2^bits words right after the header.  A walk starts at
+ *      bucket b = key[dim] >> shift: word b = the byte offset of that bucket's subtree root | its key slot << 24.
+ *      The subtrees (a HyperCuts-style cut of the top bits of one dimension, each bucket then split HyperSplit-
+ *      style) are laid out breadth-first as one forest, roots first, so whole levels of every subtree form a prefix
+ *      of the node array (the LDS-staged top of the image).
  *
  *  node (4 words, 16-B aligned; node k at byte 4 * off_nodes + 16 k of the image):
  *      internal: { threshold, left child byte offset, right child byte offset, kslots }
@@ -45,7 +52,7 @@
 #define PPE_IMAGE_H
 
 #define PPE_IMG_MAGIC   0x41455050u /* "PPEA" */
-#define PPE_IMG_VERSION 3u
+#define PPE_IMG_VERSION 4u
 #define PPE_IMG_HDR_WORDS 16u
 
 #define PPE_IMG_W_NNODES   2
@@ -60,6 +67,7 @@
 #define PPE_IMG_W_TOTAL    11
 #define PPE_IMG_W_MAXLEAF  12
 #define PPE_IMG_W_ROOTKS   13
+#define PPE_IMG_W_JUMP     14
 
 #define PPE_NODE_WORDS 4u
 #define PPE_NODE_LEAF 5u          /* key slot of a leaf: the walk's zero key */

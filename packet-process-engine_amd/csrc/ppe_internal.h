@@ -30,6 +30,8 @@ struct ppe_kargs {
     uint32_t max_depth;       /* deepest leaf: the walk reads max_depth + 1 nodes                                     */
     uint32_t max_leaf;        /* longest leaf candidate list: uniform trip count of the leaf scan                     */
     uint32_t root_ks;         /* the root node's key slot << 8 (image header word PPE_IMG_W_ROOTKS)                    */
+    uint32_t jump;            /* jump root descriptor (image header word PPE_IMG_W_JUMP), 0 = none                    */
+    uint32_t off_nodes;       /* image word offset of the nodes (after the jump table)                                */
     uint32_t off_leaf, off_rules, off_resid; /* image section offsets (words), from the image header: kernel arguments
                                                 (scalar registers, no load in the loop)                               */
     unsigned long long *cslots; /* [grid][PPE_CSLOT_WORDS] counter slots, one per workgroup */

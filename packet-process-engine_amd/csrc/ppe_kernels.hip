@@ -42,10 +42,6 @@
 #define PPE_TRACE 0
 #endif
 // minimum resident waves per SIMD the classify kernel is compiled for (VGPR budget 512 / this)
-// per-reason counter binning: 0 one LDS add per packet, 1 one LDS add per distinct bin key of the wave
-#ifndef PPE_CNT_LEADER
-#define PPE_CNT_LEADER 0
-#endif
 #ifndef PPE_WAVES_PER_EU
 #define PPE_WAVES_PER_EU 8
 #endif
@@ -86,11 +82,17 @@ __device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) {
     *(__attribute__((address_space(3))) uint32_t *)(uintptr_t)addr = v;
 }
 // global accesses by 32-bit byte offset from a uniform base (the saddr form: no 64-bit address math per lane)
+// (explicitly global: a select between two output pointers must not degrade to a flat store, whose out-of-order
+// completion makes the compiler wait for vmcnt(0) at the next use of any load)
+template <class T> struct GType { typedef T type; };
+template <> struct GType<uint4> { typedef uint32_t __attribute__((ext_vector_type(4))) type; };
 template <class T> __device__ __forceinline__ T gld(const void *base, uint32_t off) {
-    return *(const T *)((const char *)base + off);
+    typedef typename GType<T>::type G;
+    return __builtin_bit_cast(T, *(const __attribute__((address_space(1))) G *)((const char *)base + off));
 }
 template <class T> __device__ __forceinline__ void gst(void *base, uint32_t off, T v) {
-    *(T *)((char *)base + off) = v;
+    typedef typename GType<T>::type G;
+    *(__attribute__((address_space(1))) G *)((char *)base + off) = __builtin_bit_cast(G, v);
 }
 
 __device__ __forceinline__ uint32_t be16_lo(uint32_t w) { return ((w & 0xffu) << 8) | ((w >> 8) & 0xffu); }
@@ -342,6 +344,8 @@ struct AclGeo {
     uint32_t off_leaf, off_rules, off_resid;  // words
     uint32_t lds_words;   // staged prefix (words)
     uint32_t default_action;
+    uint32_t jump;        // jump root (image word PPE_IMG_W_JUMP): dim | shift << 8 | bits << 16, 0 = none
+    uint32_t off_nodes;   // words (the jump table is [PPE_IMG_HDR_WORDS, off_nodes))
 };
 
 // One level of the walk, node and key both in flight: the node's child pointer carries the child's key slot, so
@@ -358,6 +362,14 @@ __device__ __forceinline__ void walk_step(uint4 nd, uint32_t key, uint32_t laneb
 template <int MODE, int IMGB>
 __device__ __forceinline__ uint4 acl_walk(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t lanebase) {
     uint32_t noff = 4u * PPE_IMG_HDR_WORDS, kaddr = lanebase + g.root_ks;
+    if (g.jump) {
+        // jump root (image v4): bucket = key[dim] >> shift picks this lane's subtree root and its key slot
+        const uint32_t key = lds_u32(lanebase + ((g.jump & 0xffu) << 8));
+        const uint32_t jo = 4u * PPE_IMG_HDR_WORDS + 4u * (key >> ((g.jump >> 8) & 0xffu));
+        const uint32_t e = (MODE != IMG_GLOBAL && g.lds_words >= g.off_nodes) ? lds_u32(IMGB + jo) : gld<uint32_t>(gimg, jo);
+        noff = e & 0xffffffu;
+        kaddr = lanebase + ((e >> 16) & 0xff00u);
+    }
     uint4 nd = make_uint4(0u, 0u, 0u, 0u);
     uint32_t it = 0;
     if (MODE != IMG_GLOBAL) {
@@ -506,11 +518,24 @@ __device__ __forceinline__ void stage_image(const uint32_t *img, uint32_t *lds, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// An empty asm that takes a loaded window as its operands: the window's vmcnt wait lands here, and no computation
+// on it can be hoisted above this point (towards the loads)
+__device__ __forceinline__ void pin_window(uint4 &x0, uint4 &x1, uint4 &x2, uint32_t &x12, uint32_t &xlen) {
+    u32x4 v0 = {x0.x, x0.y, x0.z, x0.w}, v1 = {x1.x, x1.y, x1.z, x1.w}, v2 = {x2.x, x2.y, x2.z, x2.w};
+    asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(x12), "+v"(xlen));
+    x0 = make_uint4(v0.x, v0.y, v0.z, v0.w);
+    x1 = make_uint4(v1.x, v1.y, v1.z, v1.w);
+    x2 = make_uint4(v2.x, v2.y, v2.z, v2.w);
+}
+
 // PF: when a tile's window is fetched
 #define PF_NONE 0   // at the top of its own iteration
 #define PF_HOIST 1  // as PF_NONE, but the first tile's loads are issued before the image staging
 #define PF_REG 2    // one tile ahead: the next tile's loads are issued before the current tile is processed (its
                     // window waits in registers); compiled for half the waves per SIMD (twice the VGPR budget)
+#define PF_HEAD 3   // one tile ahead, head only: the next tile's first 16 B and length are requested before the
+                    // current tile is processed (bringing its header lines on chip); the rest of its window is
+                    // loaded at its own iteration (on-chip hits).  Fits the full-occupancy VGPR budget.
 
 template <int MODE, int PF, int BLOCK>
 __global__ __launch_bounds__(BLOCK, PF == PF_REG ? PPE_WAVES_PER_EU / 2 : PPE_WAVES_PER_EU)
@@ -531,17 +556,18 @@ void ppe_classify_kernel(ppe_kargs a) {
     // current tile's window: bytes 0..51 (w[0..12]) and the wire length.  Clamped (unconditional) loads: a lane past
     // the end of the batch re-reads the last packet.  Byte offsets are 32-bit (the engine keeps n * stride < 2^31).
     uint4 q0, q1, q2;
-    uint32_t w12, qlen;
-    auto load_tile = [&](uint32_t t) {
+    uint32_t w12 = 0, qlen = 0;
+    auto load_tile = [&](uint32_t t, uint4 &x0, uint4 &x1, uint4 &x2, uint32_t &x12, uint32_t &xlen) {
         const uint32_t pc = min((t << 6) + lane, a.n - 1u);
         const uint32_t ro = pc * a.stride;
-        q0 = gld<uint4>(a.hdr, ro);
-        q1 = gld<uint4>(a.hdr, ro + 16u);
-        q2 = gld<uint4>(a.hdr, ro + 32u);
-        w12 = gld<uint32_t>(a.hdr, ro + 48u);
-        qlen = gld<uint32_t>(a.len, 4u * pc);
+        x0 = gld<uint4>(a.hdr, ro);
+        x1 = gld<uint4>(a.hdr, ro + 16u);
+        x2 = gld<uint4>(a.hdr, ro + 32u);
+        x12 = gld<uint32_t>(a.hdr, ro + 48u);
+        xlen = gld<uint32_t>(a.len, 4u * pc);
     };
-    if (PF != PF_NONE && tile < ntiles) load_tile(tile);  // first window in flight during the image staging
+    // first window in flight during the image staging
+    if (PF != PF_NONE && tile < ntiles) load_tile(tile, q0, q1, q2, w12, qlen);
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
     const uint32_t lanebase = wv * KEY_WAVE_BYTES + 4u * lane;  // this lane's key slot 0 (LDS byte address)
@@ -550,7 +576,7 @@ void ppe_classify_kernel(ppe_kargs a) {
     __syncthreads();
     TRACE_AT(1);
     const AclGeo geo = {a.lds_iters, a.max_depth, a.max_leaf, a.root_ks, a.off_leaf, a.off_rules, a.off_resid,
-                        a.lds_words, a.default_action};
+                        a.lds_words, a.default_action, a.jump, a.off_nodes};
 
     // action of each terminal status, 2 bits per status: FW for ACL_FW, PUNT for fragments / short windows, the
     // configured action for unsupported protocols (Decode_unsupport_proto_handle, decode.c:31-45), else DROP
@@ -564,22 +590,11 @@ void ppe_classify_kernel(ppe_kargs a) {
         act_table |= ac << (2u * st);
     }
 
-    uint32_t acc_n = 0, acc_fw = 0, acc_vl = 0, acc_tcp = 0;  // PPE_CNT_LEADER == 2: wave-uniform ACL-path counts
-    bool first = true;
-    for (; tile < ntiles; tile += stride_waves) {
+    // one tile: decode, hash, ACL, stores, compaction, counters.  w = the window's first 52 bytes, wlen = wire length
+    auto process = [&](uint32_t tile, const uint32_t (&w)[13], uint32_t wlen) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < a.n;
-        if (PPE_TRACE && titer < 4) TRACE_AT(2 + 5 * titer);
-        if (PF == PF_NONE || (PF == PF_HOIST && !first)) load_tile(tile);
-        first = false;
-        // PF_REG: this tile's window is in q*, requested one iteration ago; take it, then request the next tile's
-        const uint4 c0 = q0, c1 = q1, c2 = q2;
-        const uint32_t c12 = w12, clen = qlen;
-        if (PF == PF_REG && tile + stride_waves < ntiles) load_tile(tile + stride_waves);
-        if (PPE_TRACE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (PPE_TRACE && titer < 4) TRACE_AT(3 + 5 * titer);
-        const uint32_t w[13] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w, c12};
-        Dec k = decode(w, clen, a.hdr, p, a.stride, a.syn_check);
+        Dec k = decode(w, wlen, a.hdr, p, a.stride, a.syn_check);
 
         uint32_t fh = 0;
         int32_t hit = -1;
@@ -659,53 +674,93 @@ void ppe_classify_kernel(ppe_kargs a) {
         }
 
         // ---- per-reason counters: one LDS add per packet into its (status, flags) bin ----
-        if (!(PPE_ABLATE & 2)) {
-            const uint32_t key = st | ((k.flags & 7u) << 5);
-            if (PPE_CNT_LEADER == 2) {
-                // packets that reached the ACL (the common case) are counted with wave ballots into scalar
-                // accumulators; only the others take an LDS add into their bin
-                const bool acl = valid && st <= (uint32_t)PPE_ST_ACL_DROP;
-                if (valid && !acl) atomicAdd(&bins[key], 1u);
-                acc_n += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(acl));
-                acc_fw += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(acl && st == (uint32_t)PPE_ST_ACL_FW));
-                acc_vl += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(acl && (k.flags & PPE_F_VLAN)));
-                acc_tcp += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(acl && (k.flags & PPE_F_TCP)));
-            } else if (PPE_CNT_LEADER) {
-                // one LDS add per distinct bin key in the wave (typically 2-3), by the key's first lane
-                uint64_t rem = __builtin_amdgcn_ballot_w64(valid);
-                while (rem) {
-                    const uint32_t lead = (uint32_t)__builtin_ctzll(rem);
-                    const uint32_t kl = __builtin_amdgcn_readlane(key, lead);
-                    const uint64_t m = __builtin_amdgcn_ballot_w64(key == kl) & rem;
-                    if (lane == lead) atomicAdd(&bins[kl], (uint32_t)__popcll(m));
-                    rem &= ~m;
-                }
-            } else if (valid) {
-                atomicAdd(&bins[key], 1u);
-            }
-        }
+        if (!(PPE_ABLATE & 2) && valid) atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
         if (PPE_TRACE && titer < 4) TRACE_AT(6 + 5 * titer);
         ++titer;
+    };
+
+    if (PF == PF_HEAD) {
+        // window head (first 16 B + length) of the current (A) and next (B) tile, used in turn (unrolled twice)
+        uint4 b0;
+        uint32_t blen = 0;
+        auto load_head = [&](uint32_t t, uint4 &x0, uint32_t &xlen) {
+            const uint32_t pc = min((t << 6) + lane, a.n - 1u);
+            x0 = gld<uint4>(a.hdr, pc * a.stride);
+            xlen = gld<uint32_t>(a.len, 4u * pc);
+        };
+        auto load_rest = [&](uint32_t t, uint4 &x1, uint4 &x2, uint32_t &x12) {
+            const uint32_t pc = min((t << 6) + lane, a.n - 1u);
+            const uint32_t ro = pc * a.stride;
+            x1 = gld<uint4>(a.hdr, ro + 16u);
+            x2 = gld<uint4>(a.hdr, ro + 32u);
+            x12 = gld<uint32_t>(a.hdr, ro + 48u);
+        };
+        // (the hoisted first load fetched the whole first window into q*: no rest load for it)
+        bool first = true;
+        for (;;) {
+            if (tile >= ntiles) break;
+            uint32_t nt = tile + stride_waves;
+            if (!first) load_rest(tile, q1, q2, w12);
+            first = false;
+            load_head(nt < ntiles ? nt : tile, b0, blen);  // unconditional: static vmcnt accounting
+            pin_window(q0, q1, q2, w12, qlen);
+            {
+                const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
+                process(tile, w, qlen);
+            }
+            tile = nt;
+            if (tile >= ntiles) break;
+            nt = tile + stride_waves;
+            load_rest(tile, q1, q2, w12);
+            load_head(nt < ntiles ? nt : tile, q0, qlen);
+            pin_window(b0, q1, q2, w12, blen);
+            {
+                const uint32_t w[13] = {b0.x, b0.y, b0.z, b0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
+                process(tile, w, blen);
+            }
+            tile = nt;
+        }
+    } else if (PF != PF_REG) {
+        bool first = true;
+        for (; tile < ntiles; tile += stride_waves) {
+            if (PPE_TRACE && titer < 4) TRACE_AT(2 + 5 * titer);
+            if (PF == PF_NONE || !first) load_tile(tile, q0, q1, q2, w12, qlen);
+            first = false;
+            if (PPE_TRACE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (PPE_TRACE && titer < 4) TRACE_AT(3 + 5 * titer);
+            const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
+            process(tile, w, qlen);
+        }
+    } else {
+        // two register windows used in turn (the loop body is unrolled twice, so no copy between them makes the
+        // compiler wait for an in-flight window): the next tile's loads are issued before this tile is processed.
+        // The empty asm pins each window's first use (and so its vmcnt wait) to the start of its own processing.
+        uint4 r0, r1, r2;
+        uint32_t r12 = 0, rlen = 0;
+        for (;;) {
+            if (tile >= ntiles) break;
+            uint32_t nt = tile + stride_waves;
+            load_tile(nt < ntiles ? nt : tile, r0, r1, r2, r12, rlen);  // unconditional: static vmcnt accounting
+            pin_window(q0, q1, q2, w12, qlen);
+            {
+                const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
+                process(tile, w, qlen);
+            }
+            tile = nt;
+            if (tile >= ntiles) break;
+            nt = tile + stride_waves;
+            load_tile(nt < ntiles ? nt : tile, q0, q1, q2, w12, qlen);
+            pin_window(r0, r1, r2, r12, rlen);
+            {
+                const uint32_t w[13] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, r12};
+                process(tile, w, rlen);
+            }
+            tile = nt;
+        }
     }
 
     TRACE_AT(22);
     if (PPE_TRACE && lane == 0 && a.trace) a.trace[(size_t)twave * 32u + 31u] = titer;
-    if (PPE_CNT_LEADER == 2 && acc_n && lane < 12u) {
-        // the ACL-path packets' counter increments (bin_counters for status ACL_FW / ACL_DROP), one lane each
-        const uint32_t ndr = acc_n - acc_fw;
-        const uint32_t ci[12] = {PPE_C_PKTS, PPE_C_L2_RX_OK, PPE_C_IPV4_RX_OK, PPE_C_ACL_FW, PPE_C_FLOW_PROC_OK,
-                                 PPE_C_OUT_FW, PPE_C_ACL_DROP, PPE_C_FLOW_PROC_FAIL, PPE_C_OUT_DROP, PPE_C_VLAN_RX_OK,
-                                 PPE_C_TCP_RX_OK, PPE_C_UDP_RX_OK};
-        const uint32_t cv[12] = {acc_n, acc_n, acc_n, acc_fw, acc_fw, acc_fw, ndr, ndr, ndr, acc_vl, acc_tcp,
-                                 acc_n - acc_tcp};
-        uint32_t idx = 0, val = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 12u; ++j) {
-            idx = lane == j ? ci[j] : idx;
-            val = lane == j ? cv[j] : val;
-        }
-        if (val) atomicAdd(&lcnt[idx], val);
-    }
     __syncthreads();
     for (uint32_t b = tid; b < PPE_NBINS; b += BLOCK) {  // expand the bins into counter increments
         const uint32_t c = bins[b];
@@ -736,7 +791,7 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
     const uint32_t depth = a.img[PPE_IMG_W_MAXDEPTH];
     const AclGeo geo = {0u, depth, a.img[PPE_IMG_W_MAXLEAF], a.img[PPE_IMG_W_ROOTKS], a.img[PPE_IMG_W_OFFLEAF],
                         a.img[PPE_IMG_W_OFFRULES], a.img[PPE_IMG_W_OFFRESID], MODE == IMG_LDS ? a.img_words : 0u,
-                        a.default_action};
+                        a.default_action, a.img[PPE_IMG_W_JUMP], a.img[PPE_IMG_W_OFFNODES]};
     for (uint32_t i = blockIdx.x * PPE_BLOCK + tid; i < a.n; i += gridDim.x * PPE_BLOCK) {
         const uint4 t = ((const uint4 *)a.tuple)[i];
         uint4 m = make_uint4(0, 0, 0, 0);
@@ -789,6 +844,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int block) {
     do {                                                             \
         if (pipe == PF_NONE) PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__); \
         if (pipe == PF_REG) PPE_DISPATCH_B(FN, M, PF_REG, __VA_ARGS__); \
+        if (pipe == PF_HEAD) PPE_DISPATCH_B(FN, M, PF_HEAD, __VA_ARGS__); \
         PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__);                \
     } while (0)
 #define PPE_DISPATCH(FN, ...)                                        \

@@ -95,7 +95,7 @@ class Tuples(C.Structure):
 EXPORTS = [
     # ppe_hip.h
     "ppe_abi_version", "ppe_ctx_create", "ppe_ctx_destroy", "ppe_ctx_device", "ppe_rules_commit", "ppe_classify",
-    "ppe_classify_host", "ppe_acl_lookup", "ppe_acl_lookup_host", "ppe_dev_alloc", "ppe_dev_free",
+    "ppe_classify_batches", "ppe_classify_host", "ppe_acl_lookup", "ppe_acl_lookup_host", "ppe_dev_alloc", "ppe_dev_free",
     "ppe_host_alloc", "ppe_host_free", "ppe_memcpy_h2d", "ppe_memcpy_d2h", "ppe_memset_d", "ppe_sync",
     "ppe_counters_read", "ppe_counters_clear", "ppe_timing_enable", "ppe_timing_read", "ppe_acl_image",
     "ppe_launch_info", "ppe_debug_trace", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
@@ -144,6 +144,7 @@ def _open(p: Path, mode) -> C.CDLL:
         "ppe_rules_commit": ([vp, vp, vp, u32, u32, C.POINTER(AclStats)], C.c_int),
         "ppe_classify": ([vp, C.POINTER(Batch), C.POINTER(Result), C.POINTER(Cfg), vp], C.c_int),
         "ppe_classify_host": ([vp, C.POINTER(Batch), C.POINTER(Result), C.POINTER(Cfg), u32], C.c_int),
+        "ppe_classify_batches": ([vp, C.POINTER(Batch), C.POINTER(Result), u32, C.POINTER(Cfg), vp], C.c_int),
         "ppe_acl_lookup": ([vp, C.POINTER(Tuples), vp, vp, u64, vp], C.c_int),
         "ppe_acl_lookup_host": ([vp, C.POINTER(Tuples), vp, vp, u64], C.c_int),
         "ppe_dev_alloc": ([vp, C.c_size_t], vp),

@@ -93,30 +93,47 @@ def test_large_ruleset_builds_bounded():
 
 
 def test_image_layout():
-    """Image format v3 (csrc/ppe_image.h): 16-B nodes {threshold, left, right, child key slots}, leaves as walk
-    fixed points, the always-matching sentinel rule at slot n_rules."""
-    rules = synth.make_rules(64)
-    img, st = abi.build_image(rules)
-    assert img[0] == 0x41455050 and img[1] == 3
-    assert img[2] == st["n_nodes"] and img[4] == 64 and img[11] == len(img)
-    assert img[7] % 8 == 0  # rules 32-B aligned
-    nodes = img[16:16 + 4 * img[2]].reshape(-1, 4)
-    own = 64 + 16 * np.arange(len(nodes))
-    is_leaf = nodes[:, 0] == 0xFFFFFFFF
-    leaves, inner = nodes[is_leaf], nodes[~is_leaf]
-    assert img[10] >= 1 and img[12] == 1  # max depth; binth 1: one candidate per leaf
-    assert (leaves[:, 1] == own[is_leaf]).all()  # a leaf's left child is itself (walk fixed point)
-    assert (leaves[:, 3] == (5 << 8 | 5 << 24)).all()  # ... and its key slot is the zero key
-    assert (leaves[:, 2] <= 64).all()  # payload: a rule slot or the sentinel (64)
-    # internal: children are the two consecutive nodes after it (BFS), their key slots are theirs
-    li = (inner[:, 1] - 64) // 16
-    assert ((inner[:, 2] - 64) // 16 == li + 1).all() and (li > np.nonzero(~is_leaf)[0]).all()
-    # a child's key slot (carried by its parent) is 5 exactly for leaves
-    ks_l, ks_r = (inner[:, 3] >> 8) & 0xFF, (inner[:, 3] >> 24) & 0xFF
-    assert ((ks_l == 5) == is_leaf[li]).all() and ((ks_r == 5) == is_leaf[li + 1]).all()
-    assert (ks_l <= 5).all() and (ks_r <= 5).all() and (img[13] >> 8) <= 4
-    sent = img[img[7] + 8 * 64: img[7] + 8 * 65]
-    assert sent[1] == sent[3] == sent[5] == 0xFFFFFFFF and sent[7] == 0x1FFFFFFF
+    """Image format v4 (csrc/ppe_image.h): optional jump table after the header, 16-B nodes {threshold, left, right,
+    child key slots}, leaves as walk fixed points, the always-matching sentinel rule at slot n_rules."""
+    for nrules in (64, 256):
+        rules = synth.make_rules(nrules)
+        img, st = abi.build_image(rules)
+        assert img[0] == 0x41455050 and img[1] == 4
+        assert img[2] == st["n_nodes"] and img[4] == nrules and img[11] == len(img)
+        assert img[7] % 8 == 0  # rules 32-B aligned
+        off = int(img[5])
+        jw = int(img[14])
+        nroots = 1
+        if jw:  # jump root: 2^bits bucket entries -> subtree roots (the first nodes), with their key slots
+            dim, shift, bits = jw & 0xFF, (jw >> 8) & 0xFF, (jw >> 16) & 0xFF
+            assert dim <= 4 and 1 <= bits <= 16 and off == 16 + (1 << bits)
+            width = 32 if dim <= 1 else (16 if dim <= 3 else 8)
+            assert shift == width - bits
+            jt = img[16:off]
+            roots = (jt & 0xFFFFFF).astype(np.int64)
+            assert (np.diff(roots) >= 0).all() and roots[0] == 4 * off  # runs of buckets, in order
+            nroots = len(np.unique(roots))
+            assert roots[-1] == 4 * off + 16 * (nroots - 1)
+        nodes = img[off:off + 4 * img[2]].reshape(-1, 4)
+        own = 4 * off + 16 * np.arange(len(nodes))
+        is_leaf = nodes[:, 0] == 0xFFFFFFFF
+        leaves, inner = nodes[is_leaf], nodes[~is_leaf]
+        if jw:
+            assert ((jt >> 24) == np.where(is_leaf[(roots - 4 * off) // 16], 5, (jt >> 24))).all()
+        assert img[12] == 1  # binth 1: one candidate per leaf
+        assert (leaves[:, 1] == own[is_leaf]).all()  # a leaf's left child is itself (walk fixed point)
+        assert (leaves[:, 3] == (5 << 8 | 5 << 24)).all()  # ... and its key slot is the zero key
+        assert (leaves[:, 2] <= nrules).all()  # payload: a rule slot or the sentinel (n_rules)
+        # internal: children are the two consecutive nodes after it (BFS), after every root
+        li = (inner[:, 1] - 4 * off) // 16
+        assert ((inner[:, 2] - 4 * off) // 16 == li + 1).all() and (li > np.nonzero(~is_leaf)[0]).all()
+        assert (li >= nroots).all()
+        # a child's key slot (carried by its parent) is 5 exactly for leaves
+        ks_l, ks_r = (inner[:, 3] >> 8) & 0xFF, (inner[:, 3] >> 24) & 0xFF
+        assert ((ks_l == 5) == is_leaf[li]).all() and ((ks_r == 5) == is_leaf[li + 1]).all()
+        assert (ks_l <= 5).all() and (ks_r <= 5).all() and (img[13] >> 8) <= 5
+        sent = img[img[7] + 8 * nrules: img[7] + 8 * (nrules + 1)]
+        assert sent[1] == sent[3] == sent[5] == 0xFFFFFFFF and sent[7] == 0x1FFFFFFF
 
 
 def test_long_leaf_list_escape():
@@ -133,7 +150,7 @@ def test_long_leaf_list_escape():
     for b in range(6):
         rules["dmac"][:, b] = (macs >> np.uint64(8 * b)) & np.uint64(0xFF)
     img, st = abi.build_image(rules, default_action=1)
-    nodes = img[16:16 + 4 * img[2]].reshape(-1, 4)
+    nodes = img[img[5]:img[5] + 4 * img[2]].reshape(-1, 4)
     leaves = nodes[nodes[:, 0] == 0xFFFFFFFF]
     assert ((leaves[:, 2] >> 24) == 255).any() and img[12] >= n
     pk = synth.make_packets(4000, rules, seed=5, kind="udp64", stride=64)
@@ -147,3 +164,18 @@ def test_long_leaf_list_escape():
     lin = o.classify_batch(pk["hdr"], pk["len"], nthreads=8)
     assert np.array_equal(tree["acl_hit"], lin["acl_hit"])
     assert (lin["acl_hit"] >= 300).any()
+
+
+@pytest.mark.parametrize("jump", ["0", "4", "8", "12"])
+@pytest.mark.parametrize("nrules,resid,any_ip", [(256, 0.0, 0.0), (300, 0.3, 0.2), (2048, 0.05, 0.1)])
+def test_jump_root_equals_linear(monkeypatch, jump, nrules, resid, any_ip):
+    """Image v4 jump root (a cut of the top bits of one dimension, one subtree per run of buckets): forced to each
+    width, the walk still gives exactly the linear first match — wildcard rules replicated into every bucket,
+    residual MAC / time rules, prefixes shorter than the cut."""
+    monkeypatch.setenv("PPE_JUMP_BITS", jump)
+    rules = synth.make_rules(nrules, seed=nrules + int(jump), resid_frac=resid, any_ip_frac=any_ip)
+    pk = synth.make_packets(6000, rules, seed=11, kind="imix", stride=128, malformed_frac=0.02, with_ts=True)
+    img, st, lin = compare(rules, None, pk)
+    jw = int(img[14])
+    assert (jw >> 16) & 0xFF == int(jump) and (jump == "0") == (jw == 0)
+    assert (lin["acl_hit"] >= 0).sum() > 500

@@ -240,7 +240,7 @@ def test_argument_errors(eng):
     assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == 0
     t = abi.Tuning(block=300)
     assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
-    for pl in (3, 5):  # the LDS-DMA prefetch variant is not built
+    for pl in (5, 7):  # not a fetch variant
         t = abi.Tuning(pipeline=pl)
         assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
 
@@ -353,3 +353,49 @@ def test_full_size_properties_c1(eng):
     ref = o.classify_batch(pk["hdr"][idx], pk["len"][idx], cfg=o.cfg(0, 1, NOW), nthreads=16)
     for k in ("verdict", "flow_hash", "acl_hit"):
         assert np.array_equal(whole[k][idx], ref[k]), k
+
+
+def test_classify_batches_pipelined(eng):
+    """ppe_classify_batches: several batches (ragged sizes, an empty one, both window strides) pipelined over the
+    engine's two streams, stream-ordered on the caller's stream — every batch bit-exact against the oracle, the
+    partition lists per batch, and the counters equal to the sum over batches."""
+    rules = synth.make_rules(256, seed=90)
+    eng.commit(rules, default_action=1)
+    o = pyoracle.Oracle(rules, default_action=1)
+    sizes = [100_000, 0, 65, 70_001, 1, 64 * 1000]
+    bats, ress, keep, refs = [], [], [], []
+    for j, n in enumerate(sizes):
+        stride = 64 if j % 2 == 0 else 128
+        pk = synth.make_packets(max(n, 1), rules, seed=91 + j, kind="imix", stride=stride, malformed_frac=0.05)
+        th = torch.from_numpy(pk["hdr"][:n].copy()).to(DEV) if n else torch.zeros((1, stride), dtype=torch.uint8, device=DEV)
+        tl = torch.from_numpy(pk["len"][:n].view(np.int32).copy()).to(DEV) if n else torch.zeros(1, dtype=torch.int32, device=DEV)
+        out = {k: torch.full((max(n, 1),), -7, dtype=torch.int32, device=DEV) for k in ("verdict", "flow_hash", "acl_hit", "part")}
+        bats.append(abi.Batch(th.data_ptr(), tl.data_ptr(), None, n, stride))
+        ress.append(abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(),
+                               out["part"].data_ptr(), out["part"].data_ptr(), None, None))
+        keep.append((th, tl, out))
+        refs.append(o.classify_batch(pk["hdr"][:n], pk["len"][:n], cfg=o.cfg(0, 1, NOW)) if n else None)
+    ins, outs = (abi.Batch * len(bats))(*bats), (abi.Result * len(ress))(*ress)
+    eng.clear_counters()
+    s = torch.cuda.current_stream(DEV)
+    cfg = eng.cfg(now_seconds=NOW)
+    assert eng.lib.ppe_classify_batches(eng.ctx, ins, outs, len(bats), C.byref(cfg), C.c_void_p(s.cuda_stream)) == 0
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    total = 0
+    for (th, tl, out), ref, n in zip(keep, refs, sizes):
+        if not n:
+            assert (out["verdict"].cpu().numpy() == -7).all()  # empty batch: nothing written
+            continue
+        got = {k: out[k].cpu().numpy() for k in out}
+        got = {k: (v if k == "acl_hit" else v.view(np.uint32)) for k, v in got.items()}
+        far = ref["reach"] > th.shape[1]
+        ok = ~far
+        for k in ("verdict", "flow_hash", "acl_hit"):
+            assert np.array_equal(got[k][ok], ref[k][ok]), (n, k)
+        assert ((got["verdict"][far] & 0xFF) == ST["WINDOW_PUNT"]).all()
+        check_partition({"verdict": got["verdict"], "part_idx": got["part"]}, n)
+        total += n
+    assert cnt["pkts"] == total
+    # stream order: work queued on the caller's stream after the call sees every batch's outputs
+    assert eng.lib.ppe_classify_batches(eng.ctx, ins, outs, 0, C.byref(cfg), C.c_void_p(s.cuda_stream)) == 0

@@ -61,10 +61,21 @@ def main():
         if path not in libs:
             libs[path] = abi.load_variant(path)
         eng = Engine(0, lib=libs[path])
-        eng.commit(rules, default_action=1)
         kvs = dict(x.split("=") for x in kv.split(",")) if kv else {}
         # outs=sep (default): separate FW / DROP lists + tile counts; outs=part: one partition list, no tile counts
         mode = kvs.pop("outs", "sep")
+        # streams=N: consecutive launches round-robin over N streams (batch pipelining: a launch's ramp-up overlaps
+        # the previous one's tail); each stream needs its own output buffers, so --nbufs must be a multiple of N
+        nstr = int(kvs.pop("streams", "1"))
+        # api=batches: the step loop is one ppe_classify_batches call (the engine's own two-stream pipeline)
+        api = kvs.pop("api", "classify")
+        # jump=N: classifier built with exactly N jump bits (0 = single tree); default: the builder's choice
+        import os
+        os.environ.pop("PPE_JUMP_BITS", None)
+        if "jump" in kvs:
+            os.environ["PPE_JUMP_BITS"] = kvs.pop("jump")
+        eng.commit(rules, default_action=1)
+        os.environ.pop("PPE_JUMP_BITS", None)
         if kvs:
             eng.tuning(**{k: int(v) for k, v in kvs.items()})
         calls = []
@@ -75,28 +86,47 @@ def main():
                 ptrs[4], ptrs[5] = ptrs[3], None
             rr = abi.Result(*ptrs, None)
             calls.append((bb, rr))
-        variants.append(dict(name=name, eng=eng, calls=calls, kern=[], step=[]))
+        strs = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nstr - 1)]
+        variants.append(dict(name=name, eng=eng, calls=calls, kern=[], step=[], streams=strs, api=api))
     cfg = Engine.cfg(now_seconds=NOW)
     stream = torch.cuda.current_stream(dev)
     sp = C.c_void_p(stream.cuda_stream)
 
     def run(v, steps, timed):
         fn, ctx = v["eng"].lib.ppe_classify, v["eng"].ctx
-        if timed:
+        if timed:  # kernel durations (dispatch timestamps), one stream
             v["eng"].timing(True)
             v["eng"].timing_read(reset=True)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        e0.record(stream)
-        for i in range(steps):
-            bb, rr = v["calls"][i % len(v["calls"])]
-            assert fn(ctx, C.byref(bb), C.byref(rr), C.byref(cfg), sp) == 0
-        e1.record(stream)
-        torch.cuda.synchronize()
-        if timed:
+            torch.cuda.synchronize()
+            for i in range(steps):
+                bb, rr = v["calls"][i % len(v["calls"])]
+                assert fn(ctx, C.byref(bb), C.byref(rr), C.byref(cfg), sp) == 0
             kms, nl = v["eng"].timing_read(reset=True)
             v["eng"].timing(False)
             v["kern"].append(kms / nl * 1e3)
+        # step time: back-to-back launches without per-launch events, round-robin over the variant's streams
+        strs = v["streams"]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for st in strs[1:]:
+            st.wait_event(e0)
+        if v["api"] == "batches":
+            ins = (abi.Batch * steps)(*(v["calls"][i % len(v["calls"])][0] for i in range(steps)))
+            outs = (abi.Result * steps)(*(v["calls"][i % len(v["calls"])][1] for i in range(steps)))
+            assert v["eng"].lib.ppe_classify_batches(ctx, ins, outs, steps, C.byref(cfg), sp) == 0
+        else:
+            for i in range(steps):
+                bb, rr = v["calls"][i % len(v["calls"])]
+                st = strs[i % len(strs)]
+                assert fn(ctx, C.byref(bb), C.byref(rr), C.byref(cfg), C.c_void_p(st.cuda_stream)) == 0
+        for st in strs[1:]:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            stream.wait_event(ev)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if timed:
             v["step"].append(e0.elapsed_time(e1) / steps * 1e3)
 
     ref = None
