@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: > 256 MiB total)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
+                    help="2: the K batches go through ppe_classify_batches (two-stream pipeline); 1: one ppe_classify "
+                         "per batch on one stream, launches never overlap (profiling: kernel durations = step times)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (16 threads)")
     args = ap.parse_args()
@@ -137,13 +140,20 @@ def main():
         torch.cuda.synchronize()
 
     warm, timed = batch_arrays(max(args.warmup, 1)), batch_arrays(args.steps)
-    if args.warmup:
+    if args.warmup and args.streams == 2:
         steps_pipelined(warm)
+    else:
+        for i in range(args.warmup):
+            step(i)
     # timed region 1 (value): K batches, barrier + synchronize on both sides, no per-launch events
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     ev0.record(stream)
-    steps_pipelined(timed)
+    if args.streams == 2:
+        steps_pipelined(timed)
+    else:
+        for i in range(args.steps):
+            step(i)
     ev1.record(stream)
     barrier()
     elapsed_ms = ev0.elapsed_time(ev1)
@@ -257,7 +267,7 @@ def main():
             "config": {"workload": f"{args.config}: {n} x {'64B IPv4/UDP' if cfgd['kind'] == 'udp64' else 'IMIX'}"
                                    f" packets per GPU, {cfgd['rules']} five-tuple ACL rules",
                        "packets_per_gpu": n, "rules": cfgd["rules"], "window_bytes": stride, "resident_batches": nbufs,
-                       "streams": 2,
+                       "streams": args.streams,
                        "parallelism": f"batch-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,

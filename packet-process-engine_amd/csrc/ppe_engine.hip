@@ -29,9 +29,10 @@ constexpr int kHostStreams = 3;
 // 16.5 us per batch; three streams measured 17.0)
 constexpr int kPipeStreams = 2;
 // tile fetch of the classify kernel (PF_* in ppe_kernels.hip): 0 at the loop top, 1 the first tile's loads issued
-// before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering and an LDS-DMA next-tile
-// pipeline were measured slower (28.3 / 24.4 us) and are not built.
-constexpr int kPfNone = 0, kPfHoist = 1, kPfReg = 2, kPfHead = 3;
+// before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering (next tile's window, or
+// only its first 16 B, requested before the current tile is processed) and an LDS-DMA next-tile pipeline were
+// measured slower and are not built.
+constexpr int kPfNone = 0, kPfHoist = 1;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 
 struct HostStage {
@@ -71,6 +72,8 @@ struct ppe_ctx {
     // device-batch pipeline (ppe_classify_batches): consecutive batches alternate over these streams
     hipStream_t pipe[kPipeStreams] = {};
     hipEvent_t pipe_ev[kPipeStreams + 1] = {};
+    int pipe_mode = 1;  // PPE_PIPE_MODE at context creation (see ppe_classify_batches)
+    uint32_t batches_per_launch = PPE_MAX_BATCH;  // PPE_BATCHES_PER_LAUNCH at context creation
     ppe_tuning_t tune;
     unsigned long long *trace = nullptr;  // ppe_debug_trace
     char err[256] = {0};
@@ -108,7 +111,7 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl >= 1 && pl <= 4 ? (uint32_t)pl : 0u;
+    t.pipeline = pl == 1 || pl == 4 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     return t;
 }
@@ -130,9 +133,7 @@ uint32_t image_budget(uint32_t block) {
 }
 
 StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
-    const int pf = c->tune.pipeline == 1 ? kPfNone
-                 : c->tune.pipeline == 2 ? kPfReg
-                 : c->tune.pipeline == 3 ? kPfHead : kPfHoist;
+    const int pf = c->tune.pipeline == 1 ? kPfNone : kPfHoist;
     const uint32_t words = (uint32_t)img.size(), bytes = words * 4u;
     StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0};
     if (!c->tune.lds_image) {
@@ -215,38 +216,45 @@ int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const 
     return PPE_OK;
 }
 
-int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg, hipStream_t s,
-           int slot_set, uint32_t idx_base = 0) {
+// One launch over batches in[0..nb) (nb <= PPE_MAX_BATCH, each n > 0): every wave takes its tiles of batch 0, then
+// of batch 1, ... (no barrier between batches, one image staging for all of them).
+int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t nb, const ppe_cfg_t *cfg,
+           hipStream_t s, int slot_set, uint32_t idx_base = 0) {
     const int r = c->running;
     const uint32_t words = (uint32_t)c->h_img[r].size();
     const StagePlan plan = stage_plan(c, c->h_img[r]);
     const uint32_t wpb = plan.block / 64u;
-    const uint32_t tiles = (in->n + 63u) / 64u;
+    ppe_kargs a;
+    std::memset(&a, 0, sizeof a);
+    uint32_t tiles = 0;
+    for (uint32_t i = 0; i < nb; ++i) {
+        ppe_bdesc &d = a.batch[i];
+        d.hdr = in[i].hdr;
+        d.len = in[i].len;
+        d.ts = in[i].ts;
+        d.n = in[i].n;
+        d.stride = in[i].stride;
+        d.verdict = out[i].verdict;
+        d.fhash = out[i].flow_hash;
+        d.hit = out[i].acl_hit;
+        d.fw_idx = out[i].fw_idx;
+        d.drop_idx = out[i].drop_idx;
+        d.tile_cnt = out[i].tile_cnt;
+        d.tuple = out[i].tuple;
+        d.idx_base = idx_base;
+        tiles = std::max(tiles, (in[i].n + 63u) / 64u);
+    }
+    a.nbatch = nb;
+    a.max_tiles = tiles;
     const uint32_t want = (tiles + wpb - 1) / wpb;
     const uint32_t maxg = c->n_cu * blocks_per_cu(c, plan);
     const uint32_t grid = std::max(1u, std::min(want, std::min(maxg, c->max_grid)));
-
-    ppe_kargs a;
-    std::memset(&a, 0, sizeof a);
-    a.hdr = in->hdr;
-    a.len = in->len;
-    a.ts = in->ts;
-    a.n = in->n;
-    a.stride = in->stride;
-    a.verdict = out->verdict;
-    a.fhash = out->flow_hash;
-    a.hit = out->acl_hit;
-    a.fw_idx = out->fw_idx;
-    a.drop_idx = out->drop_idx;
-    a.tile_cnt = out->tile_cnt;
-    a.tuple = out->tuple;
     a.img = c->d_img[r];
     a.img_words = words;
     a.unsup_fw = cfg ? cfg->unsupport_proto_action : 0u;
     a.syn_check = cfg ? cfg->syn_check : 1u;
     a.now = cfg ? cfg->now_seconds : 0u;
     a.default_action = c->h_img[r][PPE_IMG_W_DEFACT];
-    a.idx_base = idx_base;
     a.lds_words = plan.lds_words;
     a.max_depth = c->h_img[r][PPE_IMG_W_MAXDEPTH];
     a.max_leaf = c->h_img[r][PPE_IMG_W_MAXLEAF];
@@ -332,6 +340,9 @@ int ppe_ctx_create(int device, ppe_ctx_t **out) {
         c->n_cu = (uint32_t)prop.multiProcessorCount;
     c->max_grid = c->n_cu * kMaxBlocksPerCU;
     c->tune = default_tuning();
+    c->pipe_mode = env_int("PPE_PIPE_MODE", 1);
+    c->batches_per_launch = (uint32_t)std::max(1, std::min(env_int("PPE_BATCHES_PER_LAUNCH", PPE_MAX_BATCH),
+                                                           PPE_MAX_BATCH));
     const size_t cs_bytes = (size_t)kSlotSets * c->max_grid * PPE_CSLOT_WORDS * sizeof(unsigned long long);
     int rc = PPE_OK;
     if (hipMalloc(&c->d_cslots, cs_bytes) != hipSuccess || hipMemset(c->d_cslots, 0, cs_bytes) != hipSuccess)
@@ -409,7 +420,7 @@ int ppe_classify(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, c
     int rc = check_batch(c, in, cfg);
     if (rc != PPE_OK || in->n == 0) return rc;
     HIPCHK(c, use_device(c));
-    return launch(c, in, out, cfg, (hipStream_t)stream, 0);
+    return launch(c, in, out, 1, cfg, (hipStream_t)stream, 0);
 }
 
 int ppe_classify_batches(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t nbatch,
@@ -422,21 +433,42 @@ int ppe_classify_batches(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t
     if (nbatch == 0) return PPE_OK;
     HIPCHK(c, use_device(c));
     const hipStream_t s = (hipStream_t)stream;
+    const int mode = c->pipe_mode;
     if (!c->pipe[0]) {
-        for (int k = 0; k < kPipeStreams; ++k) HIPCHK(c, hipStreamCreateWithFlags(&c->pipe[k], hipStreamNonBlocking));
+        for (int k = 0; k < kPipeStreams; ++k)
+            HIPCHK(c, hipStreamCreateWithFlags(&c->pipe[k], mode == 2 ? hipStreamDefault : hipStreamNonBlocking));
         for (hipEvent_t &e : c->pipe_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    // fork: the pipeline streams start after the work already queued on `stream`
+    // mode 1: the caller's stream carries the even batches and one engine stream the odd ones; else two engine
+    // streams.  fork: the engine streams start after the work already queued on `stream`
+    hipStream_t q[kPipeStreams];
+    for (int k = 0; k < kPipeStreams; ++k) q[k] = (mode == 1 && k == 0) ? s : c->pipe[k];
     HIPCHK(c, hipEventRecord(c->pipe_ev[kPipeStreams], s));
-    for (int k = 0; k < kPipeStreams; ++k) HIPCHK(c, hipStreamWaitEvent(c->pipe[k], c->pipe_ev[kPipeStreams], 0));
-    for (uint32_t i = 0; i < nbatch; ++i) {
-        if (in[i].n == 0) continue;
-        const int rc = launch(c, &in[i], &out[i], cfg, c->pipe[i % kPipeStreams], 0);
-        if (rc != PPE_OK) return rc;
+    for (int k = 0; k < kPipeStreams; ++k)
+        if (q[k] != s) HIPCHK(c, hipStreamWaitEvent(q[k], c->pipe_ev[kPipeStreams], 0));
+    // groups of up to PPE_MAX_BATCH non-empty batches per launch, launches alternating over the streams
+    ppe_batch_t gin[PPE_MAX_BATCH];
+    ppe_result_t gout[PPE_MAX_BATCH];
+    uint32_t ng = 0, nl = 0;
+    const uint32_t per = std::max(1u, std::min<uint32_t>(c->batches_per_launch, PPE_MAX_BATCH));
+    for (uint32_t i = 0; i <= nbatch; ++i) {
+        if (i < nbatch && in[i].n == 0) continue;
+        if (i < nbatch) {
+            gin[ng] = in[i];
+            gout[ng] = out[i];
+            ++ng;
+        }
+        if (ng == per || (i == nbatch && ng)) {
+            const int rc = launch(c, gin, gout, ng, cfg, q[nl % kPipeStreams], 0);
+            if (rc != PPE_OK) return rc;
+            ng = 0;
+            ++nl;
+        }
     }
     // join: `stream` continues after every batch
     for (int k = 0; k < kPipeStreams; ++k) {
-        HIPCHK(c, hipEventRecord(c->pipe_ev[k], c->pipe[k]));
+        if (q[k] == s) continue;
+        HIPCHK(c, hipEventRecord(c->pipe_ev[k], q[k]));
         HIPCHK(c, hipStreamWaitEvent(s, c->pipe_ev[k], 0));
     }
     return PPE_OK;
@@ -488,7 +520,7 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         r.drop_idx = part ? h.fw : (out->drop_idx ? h.drop : nullptr);
         r.tile_cnt = out->tile_cnt ? h.tcnt : nullptr;
         r.tuple = out->tuple ? h.tuple : nullptr;
-        rc = launch(c, &b, &r, cfg, h.s, 1 + (int)(i % kHostStreams), base);
+        rc = launch(c, &b, &r, 1, cfg, h.s, 1 + (int)(i % kHostStreams), base);
         if (rc != PPE_OK) return rc;
         if (out->verdict) HIPCHK(c, hipMemcpyAsync(out->verdict + base, h.verdict, (size_t)m * 4, d2h, h.s));
         if (out->flow_hash) HIPCHK(c, hipMemcpyAsync(out->flow_hash + base, h.fhash, (size_t)m * 4, d2h, h.s));
@@ -659,9 +691,8 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline > 4)
-        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top), 2 (next tile "
-                                   "prefetched into registers), 3 (next tile's head prefetched) or 4 (first tile's "
+    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 4)
+        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top) or 4 (first tile's "
                                    "loads before the image staging)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     c->tune = *t;

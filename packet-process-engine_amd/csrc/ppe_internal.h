@@ -4,13 +4,11 @@
 
 #include <stdint.h>
 
-/* Kernel launch parameters, passed by value. */
-struct ppe_kargs {
+/* One batch of a launch: inputs, outputs (NULL = skipped) and sizes, as in ppe_batch_t / ppe_result_t. */
+struct ppe_bdesc {
     const uint8_t *hdr;
     const uint32_t *len;
     const uint64_t *ts;
-    uint32_t n;
-    uint32_t stride;
     uint32_t *verdict;
     uint32_t *fhash;
     int32_t *hit;
@@ -18,13 +16,26 @@ struct ppe_kargs {
     uint32_t *drop_idx;
     uint32_t *tile_cnt;
     uint32_t *tuple;
+    uint32_t n;
+    uint32_t stride;
+    uint32_t idx_base;        /* added to the packet indices written to fw_idx / drop_idx */
+    uint32_t pad;
+};
+
+/* batches per launch: the descriptors travel in the kernel arguments (8 × 96 B) */
+#define PPE_MAX_BATCH 8
+
+/* Kernel launch parameters, passed by value. */
+struct ppe_kargs {
+    struct ppe_bdesc batch[PPE_MAX_BATCH];  /* [0, nbatch): processed in order by every wave, no barrier between */
+    uint32_t nbatch;
+    uint32_t max_tiles;       /* largest batch's tile count */
     const uint32_t *img;      /* device classifier image (ppe_image.h) */
     uint32_t img_words;
     uint32_t unsup_fw;        /* 1: unsupported protocols are forwarded */
     uint32_t syn_check;
     uint32_t default_action;
     uint64_t now;
-    uint32_t idx_base;        /* added to the packet indices written to fw_idx / drop_idx */
     uint32_t lds_words;       /* image words staged in LDS (IMG_LDS: all; IMG_SPLIT: header + top nodes [+ leaves]) */
     uint32_t lds_iters;       /* IMG_SPLIT: walk levels (node reads) whose nodes are all in the staged BFS prefix      */
     uint32_t max_depth;       /* deepest leaf: the walk reads max_depth + 1 nodes                                     */

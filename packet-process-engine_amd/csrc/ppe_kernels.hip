@@ -518,28 +518,12 @@ __device__ __forceinline__ void stage_image(const uint32_t *img, uint32_t *lds, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// An empty asm that takes a loaded window as its operands: the window's vmcnt wait lands here, and no computation
-// on it can be hoisted above this point (towards the loads)
-__device__ __forceinline__ void pin_window(uint4 &x0, uint4 &x1, uint4 &x2, uint32_t &x12, uint32_t &xlen) {
-    u32x4 v0 = {x0.x, x0.y, x0.z, x0.w}, v1 = {x1.x, x1.y, x1.z, x1.w}, v2 = {x2.x, x2.y, x2.z, x2.w};
-    asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(x12), "+v"(xlen));
-    x0 = make_uint4(v0.x, v0.y, v0.z, v0.w);
-    x1 = make_uint4(v1.x, v1.y, v1.z, v1.w);
-    x2 = make_uint4(v2.x, v2.y, v2.z, v2.w);
-}
-
 // PF: when a tile's window is fetched
 #define PF_NONE 0   // at the top of its own iteration
 #define PF_HOIST 1  // as PF_NONE, but the first tile's loads are issued before the image staging
-#define PF_REG 2    // one tile ahead: the next tile's loads are issued before the current tile is processed (its
-                    // window waits in registers); compiled for half the waves per SIMD (twice the VGPR budget)
-#define PF_HEAD 3   // one tile ahead, head only: the next tile's first 16 B and length are requested before the
-                    // current tile is processed (bringing its header lines on chip); the rest of its window is
-                    // loaded at its own iteration (on-chip hits).  Fits the full-occupancy VGPR budget.
 
 template <int MODE, int PF, int BLOCK>
-__global__ __launch_bounds__(BLOCK, PF == PF_REG ? PPE_WAVES_PER_EU / 2 : PPE_WAVES_PER_EU)
-void ppe_classify_kernel(ppe_kargs a) {
+__global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(ppe_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     using L = Lds<BLOCK>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
@@ -547,27 +531,28 @@ void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t ntiles = (a.n + 63u) >> 6;
     const uint32_t stride_waves = gridDim.x * (BLOCK / 64);
-    uint32_t tile = blockIdx.x * (BLOCK / 64) + wv;
-    const uint32_t twave = blockIdx.x * (BLOCK / 64) + wv;
+    const uint32_t twave = blockIdx.x * (BLOCK / 64) + wv;  // this wave's first tile of every batch
     uint32_t titer = 0;
     TRACE_AT(0);
+    // the batch being processed (kernel-argument descriptor: scalar loads)
+    ppe_bdesc B = a.batch[0];
     // current tile's window: bytes 0..51 (w[0..12]) and the wire length.  Clamped (unconditional) loads: a lane past
     // the end of the batch re-reads the last packet.  Byte offsets are 32-bit (the engine keeps n * stride < 2^31).
     uint4 q0, q1, q2;
     uint32_t w12 = 0, qlen = 0;
-    auto load_tile = [&](uint32_t t, uint4 &x0, uint4 &x1, uint4 &x2, uint32_t &x12, uint32_t &xlen) {
-        const uint32_t pc = min((t << 6) + lane, a.n - 1u);
-        const uint32_t ro = pc * a.stride;
-        x0 = gld<uint4>(a.hdr, ro);
-        x1 = gld<uint4>(a.hdr, ro + 16u);
-        x2 = gld<uint4>(a.hdr, ro + 32u);
-        x12 = gld<uint32_t>(a.hdr, ro + 48u);
-        xlen = gld<uint32_t>(a.len, 4u * pc);
+    auto load_tile = [&](uint32_t t) {
+        const uint32_t pc = min((t << 6) + lane, B.n - 1u);
+        const uint32_t ro = pc * B.stride;
+        q0 = gld<uint4>(B.hdr, ro);
+        q1 = gld<uint4>(B.hdr, ro + 16u);
+        q2 = gld<uint4>(B.hdr, ro + 32u);
+        w12 = gld<uint32_t>(B.hdr, ro + 48u);
+        qlen = gld<uint32_t>(B.len, 4u * pc);
     };
     // first window in flight during the image staging
-    if (PF != PF_NONE && tile < ntiles) load_tile(tile, q0, q1, q2, w12, qlen);
+    bool have = PF == PF_HOIST && twave < ((B.n + 63u) >> 6);
+    if (have) load_tile(twave);
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
     const uint32_t lanebase = wv * KEY_WAVE_BYTES + 4u * lane;  // this lane's key slot 0 (LDS byte address)
@@ -593,8 +578,8 @@ void ppe_classify_kernel(ppe_kargs a) {
     // one tile: decode, hash, ACL, stores, compaction, counters.  w = the window's first 52 bytes, wlen = wire length
     auto process = [&](uint32_t tile, const uint32_t (&w)[13], uint32_t wlen) {
         const uint32_t p = (tile << 6) + lane;
-        const bool valid = p < a.n;
-        Dec k = decode(w, wlen, a.hdr, p, a.stride, a.syn_check);
+        const bool valid = p < B.n;
+        Dec k = decode(w, wlen, B.hdr, p, B.stride, a.syn_check);
 
         uint32_t fh = 0;
         int32_t hit = -1;
@@ -609,13 +594,13 @@ void ppe_classify_kernel(ppe_kargs a) {
         }
         if (!(PPE_ABLATE & 1) && k.st == ST_ACL) {
             uint32_t rule_act;
-            const MacFromWindow mac = {a.hdr, p, a.stride};
+            const MacFromWindow mac = {B.hdr, p, B.stride};
             lds_st32(lanebase + 256u * PPE_DIM_SIP, k.sip);
             lds_st32(lanebase + 256u * PPE_DIM_DIP, k.dip);
             lds_st32(lanebase + 256u * PPE_DIM_SPORT, k.sport);
             lds_st32(lanebase + 256u * PPE_DIM_DPORT, k.dport);
             lds_st32(lanebase + 256u * PPE_DIM_PROTO, k.proto);
-            acl_lookup<MODE, L::IMGB>(a.img, geo, lanebase, k.sip, k.dip, k.sport, k.dport, k.proto, mac, a.ts, p,
+            acl_lookup<MODE, L::IMGB>(a.img, geo, lanebase, k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts, p,
                                       a.now, hit, rule_act);
             const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
             k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
@@ -630,16 +615,16 @@ void ppe_classify_kernel(ppe_kargs a) {
 
         const uint32_t po = 4u * p;  // byte offset of this packet's SoA output words
         if (valid) {
-            if (a.verdict) gst<uint32_t>(a.verdict, po, st | (act << 8) | (k.flags << 16));
-            if (a.fhash) gst<uint32_t>(a.fhash, po, fh);
-            if (a.hit) gst<int32_t>(a.hit, po, hit);
-            if (a.tuple) {
+            if (B.verdict) gst<uint32_t>(B.verdict, po, st | (act << 8) | (k.flags << 16));
+            if (B.fhash) gst<uint32_t>(B.fhash, po, fh);
+            if (B.hit) gst<int32_t>(B.hit, po, hit);
+            if (B.tuple) {
                 uint4 t;
                 t.x = k.sip;
                 t.y = k.dip;
                 t.z = k.sport | (k.dport << 16);
                 t.w = k.proto | (((k.flags & PPE_F_VLAN) ? 1u : 0u) << 8) | (k.paylen << 16);
-                gst<uint4>(a.tuple, 4u * po, t);
+                gst<uint4>(B.tuple, 4u * po, t);
             }
         }
 
@@ -652,24 +637,24 @@ void ppe_classify_kernel(ppe_kargs a) {
             const uint32_t pfw = __builtin_amdgcn_mbcnt_hi((uint32_t)(bfw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bfw, 0u));
             const uint32_t pdr = __builtin_amdgcn_mbcnt_hi((uint32_t)(bdr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bdr, 0u));
             const uint32_t so = (tile << 8) + 4u * (is_fw ? pfw : pdr);  // byte offset in the tile's segment
-            if (a.fw_idx == a.drop_idx && a.fw_idx) {
+            if (B.fw_idx == B.drop_idx && B.fw_idx) {
                 // partition layout (one shared list): the tile's segment holds every packet of the tile, FW from the
                 // front, DROP at the back, PUNT in between, each in ascending order, the action in bits 31:30 —
                 // every slot written by one store instruction (whole-line writes, no tile count needed)
-                const uint32_t nv = min(a.n - (tile << 6), 64u);
+                const uint32_t nv = min(B.n - (tile << 6), 64u);
                 const uint32_t ndr = (uint32_t)__popcll(bdr), nfw = (uint32_t)__popcll(bfw);
                 const uint32_t slot = is_fw ? pfw : (is_drop ? nv - ndr + pdr : nfw + lane - pfw - pdr);
-                if (valid) gst<uint32_t>(a.fw_idx, (tile << 8) + 4u * slot, (p + a.idx_base) | (act << 30));
-            } else if (a.fw_idx && a.drop_idx) {  // both lists: one store instruction
-                if (is_fw || is_drop) gst<uint32_t>(is_fw ? a.fw_idx : a.drop_idx, so, p + a.idx_base);
+                if (valid) gst<uint32_t>(B.fw_idx, (tile << 8) + 4u * slot, (p + B.idx_base) | (act << 30));
+            } else if (B.fw_idx && B.drop_idx) {  // both lists: one store instruction
+                if (is_fw || is_drop) gst<uint32_t>(is_fw ? B.fw_idx : B.drop_idx, so, p + B.idx_base);
             } else {
-                if (a.fw_idx && is_fw) gst<uint32_t>(a.fw_idx, so, p + a.idx_base);
-                if (a.drop_idx && is_drop) gst<uint32_t>(a.drop_idx, so, p + a.idx_base);
+                if (B.fw_idx && is_fw) gst<uint32_t>(B.fw_idx, so, p + B.idx_base);
+                if (B.drop_idx && is_drop) gst<uint32_t>(B.drop_idx, so, p + B.idx_base);
             }
-            if (a.tile_cnt && lane == 0) {
-                const uint32_t nv = min(a.n - (tile << 6), 64u);
+            if (B.tile_cnt && lane == 0) {
+                const uint32_t nv = min(B.n - (tile << 6), 64u);
                 const uint32_t nfw = (uint32_t)__popcll(bfw), ndr = (uint32_t)__popcll(bdr);
-                gst<uint32_t>(a.tile_cnt, 4u * tile, nfw | (ndr << 8) | ((nv - nfw - ndr) << 16));
+                gst<uint32_t>(B.tile_cnt, 4u * tile, nfw | (ndr << 8) | ((nv - nfw - ndr) << 16));
             }
         }
 
@@ -679,83 +664,17 @@ void ppe_classify_kernel(ppe_kargs a) {
         ++titer;
     };
 
-    if (PF == PF_HEAD) {
-        // window head (first 16 B + length) of the current (A) and next (B) tile, used in turn (unrolled twice)
-        uint4 b0;
-        uint32_t blen = 0;
-        auto load_head = [&](uint32_t t, uint4 &x0, uint32_t &xlen) {
-            const uint32_t pc = min((t << 6) + lane, a.n - 1u);
-            x0 = gld<uint4>(a.hdr, pc * a.stride);
-            xlen = gld<uint32_t>(a.len, 4u * pc);
-        };
-        auto load_rest = [&](uint32_t t, uint4 &x1, uint4 &x2, uint32_t &x12) {
-            const uint32_t pc = min((t << 6) + lane, a.n - 1u);
-            const uint32_t ro = pc * a.stride;
-            x1 = gld<uint4>(a.hdr, ro + 16u);
-            x2 = gld<uint4>(a.hdr, ro + 32u);
-            x12 = gld<uint32_t>(a.hdr, ro + 48u);
-        };
-        // (the hoisted first load fetched the whole first window into q*: no rest load for it)
-        bool first = true;
-        for (;;) {
-            if (tile >= ntiles) break;
-            uint32_t nt = tile + stride_waves;
-            if (!first) load_rest(tile, q1, q2, w12);
-            first = false;
-            load_head(nt < ntiles ? nt : tile, b0, blen);  // unconditional: static vmcnt accounting
-            pin_window(q0, q1, q2, w12, qlen);
-            {
-                const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
-                process(tile, w, qlen);
-            }
-            tile = nt;
-            if (tile >= ntiles) break;
-            nt = tile + stride_waves;
-            load_rest(tile, q1, q2, w12);
-            load_head(nt < ntiles ? nt : tile, q0, qlen);
-            pin_window(b0, q1, q2, w12, blen);
-            {
-                const uint32_t w[13] = {b0.x, b0.y, b0.z, b0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
-                process(tile, w, blen);
-            }
-            tile = nt;
-        }
-    } else if (PF != PF_REG) {
-        bool first = true;
-        for (; tile < ntiles; tile += stride_waves) {
+    for (uint32_t bi = 0; bi < a.nbatch; ++bi) {
+        if (bi) B = a.batch[bi];
+        const uint32_t ntiles = (B.n + 63u) >> 6;
+        for (uint32_t tile = twave; tile < ntiles; tile += stride_waves) {
             if (PPE_TRACE && titer < 4) TRACE_AT(2 + 5 * titer);
-            if (PF == PF_NONE || !first) load_tile(tile, q0, q1, q2, w12, qlen);
-            first = false;
+            if (!have) load_tile(tile);
+            have = false;
             if (PPE_TRACE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (PPE_TRACE && titer < 4) TRACE_AT(3 + 5 * titer);
             const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
             process(tile, w, qlen);
-        }
-    } else {
-        // two register windows used in turn (the loop body is unrolled twice, so no copy between them makes the
-        // compiler wait for an in-flight window): the next tile's loads are issued before this tile is processed.
-        // The empty asm pins each window's first use (and so its vmcnt wait) to the start of its own processing.
-        uint4 r0, r1, r2;
-        uint32_t r12 = 0, rlen = 0;
-        for (;;) {
-            if (tile >= ntiles) break;
-            uint32_t nt = tile + stride_waves;
-            load_tile(nt < ntiles ? nt : tile, r0, r1, r2, r12, rlen);  // unconditional: static vmcnt accounting
-            pin_window(q0, q1, q2, w12, qlen);
-            {
-                const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
-                process(tile, w, qlen);
-            }
-            tile = nt;
-            if (tile >= ntiles) break;
-            nt = tile + stride_waves;
-            load_tile(nt < ntiles ? nt : tile, q0, q1, q2, w12, qlen);
-            pin_window(r0, r1, r2, r12, rlen);
-            {
-                const uint32_t w[13] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w, r12};
-                process(tile, w, rlen);
-            }
-            tile = nt;
         }
     }
 
@@ -843,8 +762,6 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int block) {
 #define PPE_DISPATCH_P(FN, M, ...)                                   \
     do {                                                             \
         if (pipe == PF_NONE) PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__); \
-        if (pipe == PF_REG) PPE_DISPATCH_B(FN, M, PF_REG, __VA_ARGS__); \
-        if (pipe == PF_HEAD) PPE_DISPATCH_B(FN, M, PF_HEAD, __VA_ARGS__); \
         PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__);                \
     } while (0)
 #define PPE_DISPATCH(FN, ...)                                        \

@@ -240,15 +240,14 @@ def test_argument_errors(eng):
     assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == 0
     t = abi.Tuning(block=300)
     assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
-    for pl in (5, 7):  # not a fetch variant
+    for pl in (2, 3, 5):  # the register / LDS-DMA prefetch variants are not built
         t = abi.Tuning(pipeline=pl)
         assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
 
 
 TUNINGS = [dict(lds_image=0), dict(block=512), dict(block=1024), dict(block=256), dict(pipeline=1),
            dict(pipeline=4), dict(pipeline=1, block=256), dict(pipeline=1, block=512), dict(pipeline=1, lds_image=0),
-           dict(pipeline=4, lds_image=0), dict(pipeline=4, block=1024), dict(blocks_per_cu=16), dict(blocks_per_cu=1),
-           dict(pipeline=2), dict(pipeline=2, block=256, blocks_per_cu=4), dict(pipeline=2, lds_image=0)]
+           dict(pipeline=4, lds_image=0), dict(pipeline=4, block=1024), dict(blocks_per_cu=16), dict(blocks_per_cu=1)]
 
 
 @pytest.mark.parametrize("tune", TUNINGS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
@@ -355,10 +354,21 @@ def test_full_size_properties_c1(eng):
         assert np.array_equal(whole[k][idx], ref[k]), k
 
 
-def test_classify_batches_pipelined(eng):
-    """ppe_classify_batches: several batches (ragged sizes, an empty one, both window strides) pipelined over the
-    engine's two streams, stream-ordered on the caller's stream — every batch bit-exact against the oracle, the
-    partition lists per batch, and the counters equal to the sum over batches."""
+@pytest.mark.parametrize("per_launch", ["8", "2", "1"])
+def test_classify_batches_pipelined(monkeypatch, per_launch):
+    """ppe_classify_batches: several batches (ragged sizes, an empty one, both window strides) grouped per launch
+    (every wave walks its tiles of each batch in turn) and pipelined over two streams, stream-ordered on the caller's
+    stream — every batch bit-exact against the oracle, the partition lists per batch, and the counters equal to the
+    sum over batches."""
+    monkeypatch.setenv("PPE_BATCHES_PER_LAUNCH", per_launch)
+    eng = Engine(0)
+    try:
+        _classify_batches_case(eng)
+    finally:
+        eng.close()
+
+
+def _classify_batches_case(eng):
     rules = synth.make_rules(256, seed=90)
     eng.commit(rules, default_action=1)
     o = pyoracle.Oracle(rules, default_action=1)

@@ -60,8 +60,13 @@ def main():
         path = str(Path(path).resolve())
         if path not in libs:
             libs[path] = abi.load_variant(path)
-        eng = Engine(0, lib=libs[path])
         kvs = dict(x.split("=") for x in kv.split(",")) if kv else {}
+        import os
+        if "pipemode" in kvs:  # ppe_classify_batches stream arrangement (PPE_PIPE_MODE, read at context creation)
+            os.environ["PPE_PIPE_MODE"] = kvs.pop("pipemode")
+        if "bpl" in kvs:  # ppe_classify_batches: batches per launch (PPE_BATCHES_PER_LAUNCH)
+            os.environ["PPE_BATCHES_PER_LAUNCH"] = kvs.pop("bpl")
+        eng = Engine(0, lib=libs[path])
         # outs=sep (default): separate FW / DROP lists + tile counts; outs=part: one partition list, no tile counts
         mode = kvs.pop("outs", "sep")
         # streams=N: consecutive launches round-robin over N streams (batch pipelining: a launch's ramp-up overlaps
@@ -111,10 +116,13 @@ def main():
         e0.record(stream)
         for st in strs[1:]:
             st.wait_event(e0)
-        if v["api"] == "batches":
-            ins = (abi.Batch * steps)(*(v["calls"][i % len(v["calls"])][0] for i in range(steps)))
-            outs = (abi.Result * steps)(*(v["calls"][i % len(v["calls"])][1] for i in range(steps)))
-            assert v["eng"].lib.ppe_classify_batches(ctx, ins, outs, steps, C.byref(cfg), sp) == 0
+        if v["api"].startswith("batches"):
+            ch = int(v["api"][7:] or steps)  # api=batchesK: K batches per ppe_classify_batches call
+            for j in range(0, steps, ch):
+                m = min(ch, steps - j)
+                ins = (abi.Batch * m)(*(v["calls"][i % len(v["calls"])][0] for i in range(j, j + m)))
+                outs = (abi.Result * m)(*(v["calls"][i % len(v["calls"])][1] for i in range(j, j + m)))
+                assert v["eng"].lib.ppe_classify_batches(ctx, ins, outs, m, C.byref(cfg), sp) == 0
         else:
             for i in range(steps):
                 bb, rr = v["calls"][i % len(v["calls"])]

@@ -231,5 +231,29 @@ int main(int argc, char **argv) {
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         printf("back-to-back %s: %.2f us/launch  %.1f GB/s\n", w ? "flat" : "row persist", ms * 1e3 / iters, bytes * iters / (ms * 1e-3) / 1e9);
     }
+    // the same launches alternating over two streams (consecutive launches overlap, like ppe_classify_batches)
+    {
+        hipStream_t s2[2];
+        hipEvent_t ej[2];
+        for (int k = 0; k < 2; ++k) {
+            CK(hipStreamCreateWithFlags(&s2[k], hipStreamNonBlocking));
+            CK(hipEventCreate(&ej[k]));
+        }
+        for (int w = 0; w < 2; ++w) {
+            const uint32_t grid = (uint32_t)ncu * 8;
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, 0));
+            for (int k = 0; k < 2; ++k) CK(hipStreamWaitEvent(s2[k], e0, 0));
+            for (int it = 0; it < iters; ++it)
+                hipLaunchKernelGGL(w ? k_flat : k_row<true>, dim3(grid), dim3(256), 0, s2[it & 1], A[it % nb]);
+            for (int k = 0; k < 2; ++k) {
+                CK(hipEventRecord(ej[k], s2[k]));
+                CK(hipStreamWaitEvent(0, ej[k], 0));
+            }
+            CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("two-stream %s: %.2f us/launch  %.1f GB/s\n", w ? "flat" : "row persist", ms * 1e3 / iters, bytes * iters / (ms * 1e-3) / 1e9);
+        }
+    }
     return 0;
 }

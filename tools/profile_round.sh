@@ -11,6 +11,8 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 B="bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-host-inclusive"
 P="bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-host-inclusive"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o c1 -- python3 $B > $O/kt.log 2>&1
+# the same bench with every launch on one stream (no overlap): kernel durations comparable with roofline.kernel_avg_us
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt1 -o c1 -- python3 $B --streams 1 > $O/kt1.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch -o c1 -- python3 $P > $O/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write -o c1 -- python3 $P > $O/write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/cal_fetch -o cal -- tools/calib/stream_calib 1048576 4 > $O/cal_fetch.log 2>&1
