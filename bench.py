@@ -45,17 +45,18 @@ def algorithmic_bytes(stride: int) -> tuple[float, float]:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="C1", choices=sorted(synth.CONFIGS))
     ap.add_argument("--n", type=int, default=0, help="packets per GPU (default: the config's)")
     ap.add_argument("--stride", type=int, default=64)
-    ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: > 256 MiB total)")
+    ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: >= 8 and > 600 MB total)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
-                    help="2: the K batches go through ppe_classify_batches (two-stream pipeline); 1: one ppe_classify "
-                         "per batch on one stream, launches never overlap (profiling: kernel durations = step times)")
+                    help="2: the K batches go through one ppe_classify_batches call (launches of up to 8 batches "
+                         "alternating over two streams); 1: launches of 8 batches serialized on one stream, no "
+                         "overlap (profiling: kernel durations = step times)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (16 threads)")
     args = ap.parse_args()
@@ -77,7 +78,9 @@ def main():
     stride = args.stride
     rules = synth.make_rules(cfgd["rules"])
     per_buf = n * (stride + 4 + 16)
-    nbufs = args.nbufs or max(2, int(np.ceil(300e6 / per_buf)))
+    # distinct resident batches: at least PPE_MAX_BATCH (a ppe_classify_batches launch groups up to 8 batches, and no
+    # batch may repeat inside one launch) and > 2x the 256 MiB MALL, so every timed read is served by HBM
+    nbufs = args.nbufs or max(8, int(np.ceil(600e6 / per_buf)))
 
     eng = Engine(local)
     acl = eng.commit(rules, default_action=1)
@@ -134,6 +137,19 @@ def main():
         if rc:
             raise RuntimeError(f"ppe_classify_batches failed: {rc}")
 
+    # the same batches as launches of GROUP batches each, serialized on `stream` (one ppe_classify_batches call per
+    # group: its single launch goes on the caller's stream), so launch durations do not overlap
+    GROUP = 8
+
+    def steps_grouped(k):
+        for g0 in range(0, k, GROUP):
+            m = min(GROUP, k - g0)
+            ins = (abi.Batch * m)(*(calls[(g0 + i) % nbufs][2] for i in range(m)))
+            outs = (abi.Result * m)(*(calls[(g0 + i) % nbufs][3] for i in range(m)))
+            rc = eng.lib.ppe_classify_batches(ctx, ins, outs, m, cfg_ref, sptr)
+            if rc:
+                raise RuntimeError(f"ppe_classify_batches failed: {rc}")
+
     def barrier():
         if dist is not None:
             dist.barrier()
@@ -142,9 +158,8 @@ def main():
     warm, timed = batch_arrays(max(args.warmup, 1)), batch_arrays(args.steps)
     if args.warmup and args.streams == 2:
         steps_pipelined(warm)
-    else:
-        for i in range(args.warmup):
-            step(i)
+    elif args.warmup:
+        steps_grouped(args.warmup)
     # timed region 1 (value): K batches, barrier + synchronize on both sides, no per-launch events
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
@@ -152,18 +167,16 @@ def main():
     if args.streams == 2:
         steps_pipelined(timed)
     else:
-        for i in range(args.steps):
-            step(i)
+        steps_grouped(args.steps)
     ev1.record(stream)
     barrier()
     elapsed_ms = ev0.elapsed_time(ev1)
-    # timed region 2 (roofline): the same K launches one at a time on `stream` (no overlap between launches), with
-    # the dispatch's own start / end timestamps (hipExtLaunchKernelGGL events) around each
+    # timed region 2 (roofline): the same K batches as launches of 8 batches serialized on `stream` (no overlap
+    # between launches), with the dispatch's own start / end timestamps (hipExtLaunchKernelGGL events) around each
     eng.timing(True)
     eng.timing_read(reset=True)
     barrier()
-    for i in range(args.steps):
-        step(i)
+    steps_grouped(args.steps)
     barrier()
     kern_ms, launches = eng.timing_read(reset=True)
     eng.timing(False)
@@ -177,7 +190,7 @@ def main():
     mpps = total_pkts / (my_ms / 1e3) / 1e6
     rd, wr = algorithmic_bytes(stride)
     kern_avg_ms = kern_ms / max(launches, 1)
-    achieved = (rd + wr) * n / (kern_avg_ms / 1e3) / 1e9
+    achieved = (rd + wr) * n * args.steps / (kern_ms / 1e3) / 1e9
 
     # ---- parity spot check of the timed buffers (batch 0) against the oracle, 1/16 sample ----
     parity = None
@@ -272,7 +285,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": rd + wr,
-                         "launches_timed": launches,
+                         "launches_timed": launches, "packets_per_launch": n * GROUP if args.steps % GROUP == 0 else None,
                          # the value's own rate in the same bytes: consecutive batches overlap on two streams
                          "pipelined_GBps": round(mpps * 1e6 / world * (rd + wr) / 1e9, 1)},
             "cpu_baseline": cpu,

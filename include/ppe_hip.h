@@ -66,7 +66,8 @@ enum ppe_status {
     PPE_ST_TCP_LEN_ERR = 16,      /* l4len<hlen or (u8)(hlen-20)>40                        decode-tcp.c:148-160         */
     PPE_ST_FLOW_TCP_NO_SYN_FIRST = 17, /* flow miss, TCP without SYN, syn_check on        flow.c:204-214               */
     PPE_ST_WINDOW_PUNT = 18,      /* needed header bytes lie beyond the header window (engine-specific PUNT)          */
-    PPE_ST__COUNT = 19
+    PPE_ST_FLOW_NOMEM = 19,       /* flow table: ACL passed but the flow pool is exhausted  STAT_FLOW_NODE_NOMEM flow.c:127 */
+    PPE_ST__COUNT = 20
 };
 
 enum ppe_action { PPE_ACT_FW = 0, PPE_ACT_DROP = 1, PPE_ACT_PUNT = 2 };
@@ -77,6 +78,9 @@ enum ppe_action { PPE_ACT_FW = 0, PPE_ACT_DROP = 1, PPE_ACT_PUNT = 2 };
 #define PPE_F_SYN    0x0008u   /* TCP SYN flag set                                    */
 #define PPE_F_ACL    0x0010u   /* ACL consulted (acl_hit is its result)               */
 #define PPE_F_FRAG   0x0020u   /* IPv4 fragment seen                                  */
+#define PPE_F_FLOW   0x0040u   /* flow table: the packet has a flow (PKT_HAS_FLOW, flow.c:307)              */
+#define PPE_F_TOCLIENT 0x0080u /* flow table: PKT_TO_CLIENT (clear with PPE_F_FLOW: PKT_TO_SERVER, flow.c:248-301) */
+#define PPE_F_NEWFLOW 0x0100u  /* flow table: this packet created its flow (FlowAdd, flow.c:120-158)             */
 
 #define PPE_PART_INDEX(e)  ((e) & 0x3fffffffu)   /* partition-layout entry → packet index                */
 #define PPE_PART_ACTION(e) ((e) >> 30)           /* partition-layout entry → enum ppe_action             */
@@ -96,7 +100,8 @@ enum ppe_counter {
     PPE_C_ACL_DROP, PPE_C_ACL_FW,
     PPE_C_FLOW_PROC_OK, PPE_C_FLOW_PROC_FAIL, PPE_C_FLOW_TCP_NO_SYN_FIRST,
     PPE_C_OUT_FW, PPE_C_OUT_DROP, PPE_C_OUT_PUNT, PPE_C_WINDOW_PUNT, PPE_C_PKTS,
-    PPE_C__COUNT /* 30 */
+    PPE_C_FLOW_NODE_NOMEM,     /* flow table only: FlowAdd found the pool empty (decode-statistic.h:304) */
+    PPE_C__COUNT /* 31 */
 };
 
 typedef struct {
@@ -232,6 +237,54 @@ int  ppe_launch_info(ppe_ctx_t *ctx, uint32_t *grid, uint32_t *block, uint32_t *
 /* Diagnostics: device buffer for per-wave phase timestamps written by a library built with -DPPE_TRACE (make
  * variant NAME=trace VFLAGS=-DPPE_TRACE=1); the product build ignores it.  Layout: tools/trace_analyze.py. */
 int  ppe_debug_trace(ppe_ctx_t *ctx, void *dev_buf);
+
+/* ---- Stateful flow table (dataplane/src/flow/flow.c) ----
+ * One table per context (the reference keeps one per core, flow_table[LOCAL_CPU_ID]; across GPUs, shard packets by
+ * flow hash so each flow lives on one device).  ppe_classify_flow() runs the reference's FlowHandlePacket for a whole
+ * batch with exactly the sequential semantics of one core processing the batch in index order:
+ *   - a packet whose flow exists (FlowFind: 5-tuple match in either direction, flow.c:81-115) is forwarded without
+ *     an ACL lookup, counted ACL_FW / FLOW_PROC_OK, and updates the flow's per-direction packet / byte counters
+ *     (FlowUpdate, flow.c:163-178, bytes = pkt_totallen) and last-seen time (FLOW_UPDATE_TIMESTAMP = cfg->now_seconds);
+ *   - otherwise syn_check and the ACL decide as in the stateless path; an ACL FW creates the flow (FlowAdd, oriented
+ *     as that packet), or fails with PPE_ST_FLOW_NOMEM when `capacity` flows are live (flow.c:124-129);
+ *   - later packets of the same batch see flows created by earlier ones (in index order).
+ * acl_hit is -1 and PPE_F_ACL clear for packets that found their flow.  Aging (FlowTimeOut / FlowAgeTimeoutCB, flow.c:391-467) is
+ * explicit: ppe_flow_age() removes flows idle for more than `timeout_seconds` (reference: FLOW_MAX_TIMEOUT = 20 s).
+ * Batches go through one stream in order; out->verdict is required; n <= max_batch. */
+typedef struct {
+    uint32_t sip, dip;            /* flow_item_t.ipv4 of the creating packet (flow.h:57)                        */
+    uint16_t sport, dport;
+    uint8_t  protocol, pad[3];
+    uint32_t flowflags;           /* FLOW_FLAG_* (always 0: nothing sets PERSISTENT in the reference)            */
+    uint32_t slot;                /* device table slot (diagnostic)                                              */
+    uint64_t pktcnts2d, pktcntd2s, bytecnts2d, bytecntd2s;   /* flow.h:66-69                                       */
+    uint64_t last_seen;           /* `cycle`: cfg->now_seconds of the last packet of the flow                    */
+} ppe_flow_entry_t;
+
+typedef struct {
+    uint64_t live;                /* flows in the table                                                          */
+    uint64_t new_flow, del_flow;  /* FlowAdd / aging totals since create or ppe_flow_clear_stat (dp_cmd.c:2327)  */
+    uint32_t capacity;            /* flow pool size (reference MEM_POOL_FLOW_NODE_NUM = 100000)                  */
+    uint32_t max_batch;
+    uint32_t slots;               /* open-addressing slots (power of two >= 2 x (capacity + max_batch))          */
+    uint32_t tombstones;          /* deleted slots not yet reclaimed by a rehash                                 */
+    uint32_t rehashes;
+    uint32_t pad;
+} ppe_flow_info_t;
+
+/* FlowInit (flow.c:471-516): create / replace the context's table.  capacity 0 = 100000, max_batch 0 = 1<<20. */
+int  ppe_flow_create(ppe_ctx_t *ctx, uint32_t capacity, uint32_t max_batch);
+int  ppe_flow_destroy(ppe_ctx_t *ctx);                                /* FlowRelease (flow.c:519-530) */
+/* FlowHandlePacket for a device-resident batch (same buffers as ppe_classify), stream-ordered on `stream`. */
+int  ppe_classify_flow(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
+                       void *stream);
+/* FlowAgeTimeoutCB: delete flows with now > last_seen && now - last_seen > timeout_seconds; *deleted = count
+ * (may be NULL).  Synchronises. */
+int  ppe_flow_age(ppe_ctx_t *ctx, uint64_t now_seconds, uint64_t timeout_seconds, uint64_t *deleted);
+int  ppe_flow_info(ppe_ctx_t *ctx, ppe_flow_info_t *info);         /* dp_show_flow_stat (dp_cmd.c:2346); syncs */
+int  ppe_flow_clear_stat(ppe_ctx_t *ctx);                           /* dp_clear_flow_stat (dp_cmd.c:2327) */
+/* Copy up to `max` live flows to host (table order); *n = live flows.  Synchronises. */
+int  ppe_flow_dump(ppe_ctx_t *ctx, ppe_flow_entry_t *entries, uint32_t max, uint32_t *n);
 
 /* Human-readable last error of this context (static storage of the ctx). */
 const char *ppe_last_error(ppe_ctx_t *ctx);

@@ -25,6 +25,7 @@ typedef struct {
     int vlan_idx;
     uint8_t smac[6], dmac[6];
     int decided;
+    uint32_t totallen;  /* mbuf->pkt_totallen (FlowUpdate byte counts) */
 } omb_t;
 
 static const RCP_BLOCK_ACL_RULE_TUPLE *g_rules;
@@ -195,39 +196,188 @@ int32_t oracle_acl_tree(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dpo
     return -1;
 }
 
-/* ---- flow: dataplane/src/flow/flow.c:181-245 (miss path), 271-292 ---- */
+/* ---- flow table: one core's flow_table[LOCAL_CPU_ID] (dataplane/src/flow/flow.c, flow.h) ----
+ * FLOW_BUCKET_NUM chained buckets indexed by flow_hashfn & FLOW_BUCKET_MASK (flow.c:76-79, flow.h:87-88), items from
+ * a fixed pool of `capacity` (the FPA flow-node pool, mem_pool.h:72), head insertion (FlowInsert, flow.c:69-72). */
+#define OFLOW_BUCKETS 65536u
+typedef struct oflow_item {
+    struct oflow_item *next;
+    uint64_t cycle;                               /* FLOW_UPDATE_TIMESTAMP: the batch time */
+    uint32_t sip, dip;
+    uint16_t sport, dport, protocol;
+    uint64_t pkts2d, pktd2s, bytes2d, byted2s;    /* flow.h:66-69 */
+} oflow_item_t;
+
+struct oracle_flow {
+    oflow_item_t *bucket[OFLOW_BUCKETS];
+    oflow_item_t *pool, *free_list;
+    uint32_t capacity;
+    uint64_t live, new_flow, del_flow;
+};
+
+oracle_flow_t *oracle_flow_create(uint32_t capacity) {
+    oracle_flow_t *f = (oracle_flow_t *)calloc(1, sizeof *f);
+    if (!f) return NULL;
+    f->capacity = capacity;
+    f->pool = (oflow_item_t *)calloc(capacity ? capacity : 1, sizeof(oflow_item_t));
+    if (!f->pool) {
+        free(f);
+        return NULL;
+    }
+    for (uint32_t i = 0; i < capacity; i++) {
+        f->pool[i].next = f->free_list;
+        f->free_list = &f->pool[i];
+    }
+    return f;
+}
+
+void oracle_flow_destroy(oracle_flow_t *f) {
+    if (!f) return;
+    free(f->pool);
+    free(f);
+}
+
+/* FlowMatch, flow.c:81-94: the 5-tuple in either direction */
+static int flow_match(const oflow_item_t *f, const oracle_result_t *r) {
+    return (f->sip == r->sip && f->dip == r->dip && f->sport == r->sport && f->dport == r->dport &&
+            f->protocol == r->proto) ||
+           (f->sip == r->dip && f->dip == r->sip && f->sport == r->dport && f->dport == r->sport &&
+            f->protocol == r->proto);
+}
+
+static __thread oracle_flow_t *t_flow;  /* table of the current batch (NULL: stateless, every packet a miss) */
+static __thread uint64_t t_now;
+
+static void flow_miss_drop(omb_t *m, uint32_t st, int c) {
+    cnt(m, c);
+    set_status(m, st);
+    out_drop(m);  /* FlowHandlePacket: f == NULL → output_drop_proc, STAT_FLOW_PROC_FAIL, flow.c:278-284 */
+    cnt(m, PPE_C_FLOW_PROC_FAIL);
+}
+
+/* ---- FlowHandlePacket, dataplane/src/flow/flow.c:271-310 with FlowGetFlowFromHash :181-245 ---- */
 static __thread int t_use_tree;  /* per shard: 1 = walk the image, 0 = linear first match */
 
 static void flow_handle_packet(omb_t *m) {
     oracle_result_t *r = m->r;
     r->flags |= PPE_F_L4;
     r->flow_hash = oracle_flow_hashfn(r->proto, r->sip, r->dip, r->sport, r->dport);  /* flow.c:189 */
-    /* every packet is a flow-table miss (stateless path) */
-    if (m->cfg->syn_check && r->proto == 6 && !(r->flags & PPE_F_SYN)) {  /* flow.c:204-214 */
-        cnt(m, PPE_C_FLOW_TCP_NO_SYN_FIRST);
-        set_status(m, PPE_ST_FLOW_TCP_NO_SYN_FIRST);
-        out_drop(m);  /* FlowHandlePacket :278-284 */
-        cnt(m, PPE_C_FLOW_PROC_FAIL);
-        return;
+    oracle_flow_t *ft = t_flow;
+    oflow_item_t *f = NULL;
+    uint32_t b = r->flow_hash & (OFLOW_BUCKETS - 1u);
+    if (ft) {  /* FlowFind, flow.c:96-115 */
+        for (f = ft->bucket[b]; f; f = f->next)
+            if (flow_match(f, r)) break;
     }
-    /* PortScan_Detect disabled (portscan_able = 0) */
-    uint32_t act;
-    r->flags |= PPE_F_ACL;
-    r->acl_hit = t_use_tree ? oracle_acl_tree(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
-                                              m->ts, &act)
-                            : oracle_acl_linear(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
-                                                m->ts, &act);
-    if (act == ACL_RULE_ACTION_DROP) {  /* flow.c:232-237 */
-        cnt(m, PPE_C_ACL_DROP);
-        set_status(m, PPE_ST_ACL_DROP);
-        out_drop(m);
-        cnt(m, PPE_C_FLOW_PROC_FAIL);
-        return;
+    if (f) {
+        f->cycle = t_now;       /* flow.c:110 */
+        cnt(m, PPE_C_ACL_FW);   /* flow.c:197-201 */
+        set_status(m, PPE_ST_ACL_FW);
+    } else {
+        if (m->cfg->syn_check && r->proto == 6 && !(r->flags & PPE_F_SYN)) {  /* flow.c:204-214 */
+            flow_miss_drop(m, PPE_ST_FLOW_TCP_NO_SYN_FIRST, PPE_C_FLOW_TCP_NO_SYN_FIRST);
+            return;
+        }
+        /* PortScan_Detect disabled (portscan_able = 0) */
+        uint32_t act;
+        r->flags |= PPE_F_ACL;
+        r->acl_hit = t_use_tree ? oracle_acl_tree(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
+                                                  m->ts, &act)
+                                : oracle_acl_linear(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
+                                                    m->ts, &act);
+        if (act == ACL_RULE_ACTION_DROP) {  /* flow.c:232-237 */
+            flow_miss_drop(m, PPE_ST_ACL_DROP, PPE_C_ACL_DROP);
+            return;
+        }
+        cnt(m, PPE_C_ACL_FW);  /* flow.c:240 */
+        set_status(m, PPE_ST_ACL_FW);
+        if (ft) {  /* FlowAdd, flow.c:120-158 */
+            f = ft->free_list;
+            if (!f) {  /* flow.c:124-129 */
+                cnt(m, PPE_C_FLOW_NODE_NOMEM);
+                r->status = PPE_ST_FLOW_NOMEM;
+                out_drop(m);
+                cnt(m, PPE_C_FLOW_PROC_FAIL);
+                return;
+            }
+            ft->free_list = f->next;
+            memset(f, 0, sizeof *f);
+            f->sip = r->sip;
+            f->dip = r->dip;
+            f->sport = (uint16_t)r->sport;
+            f->dport = (uint16_t)r->dport;
+            f->protocol = (uint16_t)r->proto;
+            f->cycle = t_now;
+            f->next = ft->bucket[b];  /* FlowInsert: hlist_add_head */
+            ft->bucket[b] = f;
+            ft->live++;
+            ft->new_flow++;
+            r->flags |= PPE_F_NEWFLOW;
+        }
     }
-    cnt(m, PPE_C_ACL_FW);  /* flow.c:240 */
-    set_status(m, PPE_ST_ACL_FW);
+    if (f) {
+        /* FlowGetPacketDirection, flow.c:248-269 (TCP/UDP only reach here) */
+        const int to_server = r->sport != r->dport ? f->sport == r->sport : f->sip == r->sip;
+        r->flags |= PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
+        if (r->sport == f->sport) {  /* FlowUpdate, flow.c:163-178 */
+            f->pkts2d++;
+            f->bytes2d += m->totallen;
+        } else {
+            f->pktd2s++;
+            f->byted2s += m->totallen;
+        }
+    }
     cnt(m, PPE_C_FLOW_PROC_OK);  /* flow.c:309 */
     out_fw(m);                   /* SELF_TEST, flow.c:376-377 */
+}
+
+/* FlowTimeOut + FlowAgeTimeoutCB, flow.c:391-467 (no flow is ever PERSISTENT) */
+uint64_t oracle_flow_age(oracle_flow_t *ft, uint64_t now, uint64_t timeout) {
+    uint64_t n = 0;
+    for (uint32_t b = 0; b < OFLOW_BUCKETS; b++) {
+        oflow_item_t **pp = &ft->bucket[b];
+        while (*pp) {
+            oflow_item_t *f = *pp;
+            if (now > f->cycle && now - f->cycle > timeout) {
+                *pp = f->next;
+                f->next = ft->free_list;
+                ft->free_list = f;
+                ft->live--;
+                ft->del_flow++;
+                n++;
+            } else {
+                pp = &f->next;
+            }
+        }
+    }
+    return n;
+}
+
+uint32_t oracle_flow_dump(const oracle_flow_t *ft, ppe_flow_entry_t *out, uint32_t max) {
+    uint32_t k = 0;
+    for (uint32_t b = 0; b < OFLOW_BUCKETS; b++)
+        for (const oflow_item_t *f = ft->bucket[b]; f; f = f->next, k++) {
+            if (k >= max) continue;
+            ppe_flow_entry_t *e = &out[k];
+            memset(e, 0, sizeof *e);
+            e->sip = f->sip;
+            e->dip = f->dip;
+            e->sport = f->sport;
+            e->dport = f->dport;
+            e->protocol = (uint8_t)f->protocol;
+            e->pktcnts2d = f->pkts2d;
+            e->pktcntd2s = f->pktd2s;
+            e->bytecnts2d = f->bytes2d;
+            e->bytecntd2s = f->byted2s;
+            e->last_seen = f->cycle;
+        }
+    return k;
+}
+
+void oracle_flow_stats(const oracle_flow_t *ft, uint64_t *live, uint64_t *new_flow, uint64_t *del_flow) {
+    if (live) *live = ft->live;
+    if (new_flow) *new_flow = ft->new_flow;
+    if (del_flow) *del_flow = ft->del_flow;
 }
 
 /* ---- UDP: dataplane/src/decode/decode-udp.c:16-71 ---- */
@@ -442,6 +592,7 @@ void oracle_classify(const uint8_t *pkt, uint32_t avail, uint32_t len, uint64_t 
     m.ts = ts;
     m.cfg = cfg;
     m.r = out;
+    m.totallen = len;
     out->counters |= 1u << PPE_C_PKTS;
     /* Decode(): dataplane/src/decode/decode.c:19-28, len = (uint16_t)pkt_totallen */
     if (decode_ethernet(&m, pkt, (uint16_t)len) != DEC_OK) out_drop(&m);
@@ -461,6 +612,7 @@ typedef struct {
     uint32_t lo, hi;
     const oracle_cfg_t *cfg;
     int use_tree;
+    oracle_flow_t *flow;
     uint32_t *verdict, *flow_hash, *tuple, *reach;
     int32_t *acl_hit;
     uint64_t counters[32];
@@ -469,6 +621,8 @@ typedef struct {
 static void *run_shard(void *arg) {
     shard_t *s = (shard_t *)arg;
     t_use_tree = s->use_tree;
+    t_flow = s->flow;
+    t_now = s->cfg->now_seconds;
     memset(s->counters, 0, sizeof s->counters);
     for (uint32_t i = s->lo; i < s->hi; i++) {
         oracle_result_t r;
@@ -533,5 +687,31 @@ int oracle_classify_batch(const uint8_t *hdr, uint32_t stride, const uint32_t *l
     }
     free(sh);
     free(th);
+    return 0;
+}
+
+/* The batch through one core's flow table, in index order (one shard: the table is per core). */
+int oracle_flow_classify_batch(oracle_flow_t *ft, const uint8_t *hdr, uint32_t stride, const uint32_t *len,
+                               const uint64_t *ts, uint32_t n, const oracle_cfg_t *cfg, int use_tree,
+                               uint32_t *verdict, uint32_t *flow_hash, int32_t *acl_hit, uint32_t *tuple,
+                               uint64_t *counters) {
+    shard_t s;
+    memset(&s, 0, sizeof s);
+    s.hdr = hdr;
+    s.stride = stride;
+    s.len = len;
+    s.ts = ts;
+    s.lo = 0;
+    s.hi = n;
+    s.cfg = cfg;
+    s.use_tree = use_tree;
+    s.flow = ft;
+    s.verdict = verdict;
+    s.flow_hash = flow_hash;
+    s.acl_hit = acl_hit;
+    s.tuple = tuple;
+    run_shard(&s);
+    t_flow = NULL;
+    if (counters) memcpy(counters, s.counters, sizeof s.counters);
     return 0;
 }

@@ -18,6 +18,7 @@
 
 #include <stdint.h>
 #include "ppe_acl.h"
+#include "ppe_hip.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -68,6 +69,22 @@ int oracle_classify_batch(const uint8_t *hdr, uint32_t stride, const uint32_t *l
                           const oracle_cfg_t *cfg, int nthreads, int use_tree, uint32_t *verdict,
                           uint32_t *flow_hash, int32_t *acl_hit, uint32_t *tuple, uint32_t *reach,
                           uint64_t *counters /* [32] */);
+
+/* ---- flow table (dataplane/src/flow/flow.c): one core's chained table over a pool of `capacity` items ---- */
+typedef struct oracle_flow oracle_flow_t;
+oracle_flow_t *oracle_flow_create(uint32_t capacity);
+void oracle_flow_destroy(oracle_flow_t *f);
+/* FlowHandlePacket with the table for packets 0..n-1 in order; cfg->now_seconds is the batch time (the flows'
+ * last-seen `cycle`).  Same outputs as oracle_classify_batch (tuple optional). */
+int oracle_flow_classify_batch(oracle_flow_t *f, const uint8_t *hdr, uint32_t stride, const uint32_t *len,
+                               const uint64_t *ts, uint32_t n, const oracle_cfg_t *cfg, int use_tree,
+                               uint32_t *verdict, uint32_t *flow_hash, int32_t *acl_hit, uint32_t *tuple,
+                               uint64_t *counters /* [32] */);
+/* FlowAgeTimeoutCB: removes flows with now > cycle && now - cycle > timeout; returns the count */
+uint64_t oracle_flow_age(oracle_flow_t *f, uint64_t now, uint64_t timeout);
+/* live flows in bucket order (first `max` copied); returns the live count */
+uint32_t oracle_flow_dump(const oracle_flow_t *f, ppe_flow_entry_t *out, uint32_t max);
+void oracle_flow_stats(const oracle_flow_t *f, uint64_t *live, uint64_t *new_flow, uint64_t *del_flow);
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,17 @@ def load():
         lib.oracle_acl_linear.restype = C.c_int32
         lib.oracle_acl_tree.argtypes = [u32, u32, u32, u32, u32, vp, vp, u64, C.POINTER(u32)]
         lib.oracle_acl_tree.restype = C.c_int32
+        lib.oracle_flow_create.argtypes = [u32]
+        lib.oracle_flow_create.restype = vp
+        lib.oracle_flow_destroy.argtypes = [vp]
+        lib.oracle_flow_classify_batch.argtypes = [vp, vp, u32, vp, vp, u32, C.POINTER(OCfg), C.c_int, vp, vp, vp,
+                                                   vp, vp]
+        lib.oracle_flow_classify_batch.restype = C.c_int
+        lib.oracle_flow_age.argtypes = [vp, u64, u64]
+        lib.oracle_flow_age.restype = u64
+        lib.oracle_flow_dump.argtypes = [vp, vp, u32]
+        lib.oracle_flow_dump.restype = u32
+        lib.oracle_flow_stats.argtypes = [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]
         _lib = lib
     return _lib
 
@@ -103,6 +114,58 @@ class Oracle:
                                        out["tuple"].ctypes.data, out["reach"].ctypes.data,
                                        out["counters"].ctypes.data)
         return out
+
+
+
+
+class OracleFlow:
+    """One core's flow table (dataplane/src/flow/flow.c) driven by the oracle's FlowHandlePacket, batch by batch in
+    packet order; `oracle` supplies the rule set (and image for use_tree)."""
+
+    def __init__(self, oracle: Oracle, capacity=100000):
+        self.o = oracle
+        self.lib = oracle.lib
+        self.h = self.lib.oracle_flow_create(int(capacity))
+        if not self.h:
+            raise MemoryError("oracle_flow_create")
+
+    def close(self):
+        if self.h:
+            self.lib.oracle_flow_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def classify_batch(self, hdr, lens, ts=None, cfg=None, use_tree=False):
+        hdr = np.ascontiguousarray(hdr, np.uint8)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        n, stride = hdr.shape
+        out = dict(verdict=np.zeros(n, np.uint32), flow_hash=np.zeros(n, np.uint32), acl_hit=np.zeros(n, np.int32),
+                   tuple=np.zeros((n, 4), np.uint32), counters=np.zeros(32, np.uint64))
+        if ts is not None:
+            ts = np.ascontiguousarray(ts, np.uint64)
+        self.lib.oracle_flow_classify_batch(self.h, hdr.ctypes.data, stride, lens.ctypes.data,
+                                            ts.ctypes.data if ts is not None else None, n,
+                                            C.byref(cfg or self.o.cfg()), 1 if use_tree else 0,
+                                            out["verdict"].ctypes.data, out["flow_hash"].ctypes.data,
+                                            out["acl_hit"].ctypes.data, out["tuple"].ctypes.data,
+                                            out["counters"].ctypes.data)
+        return out
+
+    def age(self, now, timeout=20):
+        return int(self.lib.oracle_flow_age(self.h, int(now), int(timeout)))
+
+    def dump(self) -> np.ndarray:
+        from ppe.abi import FLOW_ENTRY_DTYPE
+        n = self.lib.oracle_flow_dump(self.h, None, 0)
+        out = np.zeros(n, FLOW_ENTRY_DTYPE)
+        self.lib.oracle_flow_dump(self.h, out.ctypes.data if n else None, n)
+        return out
+
+    def stats(self) -> dict:
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self.lib.oracle_flow_stats(self.h, C.byref(a), C.byref(b), C.byref(c))
+        return dict(live=a.value, new_flow=b.value, del_flow=c.value)
 
 
 def ref_hash_lib():

@@ -46,6 +46,29 @@ struct HostStage {
     uint32_t cap = 0, stride = 0;
 };
 
+// Device flow table (ppe_classify_flow) and what the host knows about it without synchronising.
+struct FlowArrays {
+    uint32_t *keys = nullptr, *creator = nullptr;
+    unsigned long long *stats = nullptr, *last = nullptr;
+};
+struct FlowTable {
+    uint32_t capacity = 0, max_batch = 0, nslots = 0;
+    FlowArrays arr[2];  // arr[cur] in use; the other is the rehash target (allocated on first rehash)
+    int cur = 0;
+    unsigned long long *ctl = nullptr;
+    uint32_t *rec = nullptr, *rslot = nullptr;
+    unsigned long long *tile_miss = nullptr, *tile_new = nullptr;
+    uint64_t live_ub = 0;   // upper bound of live flows: a snapshot's count + n per batch since
+    uint64_t tomb_ub = 0;   // upper bound of tombstones: a snapshot's count + n per batch that could revoke
+    uint32_t rehashes = 0;
+    // asynchronous snapshot of ctl (pinned copy + event), taken when the bounds get close to a limit, so the host
+    // refreshes them without synchronising
+    unsigned long long *ctl_h = nullptr;
+    hipEvent_t snap_ev = nullptr;
+    bool snap_inflight = false;
+    uint64_t snap_n = 0, snap_n_rev = 0;  // packets (of batches that may revoke) submitted after the snapshot
+};
+
 }  // namespace
 
 struct ppe_ctx {
@@ -75,6 +98,7 @@ struct ppe_ctx {
     int pipe_mode = 1;  // PPE_PIPE_MODE at context creation (see ppe_classify_batches)
     uint32_t batches_per_launch = PPE_MAX_BATCH;  // PPE_BATCHES_PER_LAUNCH at context creation
     ppe_tuning_t tune;
+    FlowTable *flow = nullptr;  // ppe_flow_create
     unsigned long long *trace = nullptr;  // ppe_debug_trace
     char err[256] = {0};
 };
@@ -219,7 +243,8 @@ int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const 
 // One launch over batches in[0..nb) (nb <= PPE_MAX_BATCH, each n > 0): every wave takes its tiles of batch 0, then
 // of batch 1, ... (no barrier between batches, one image staging for all of them).
 int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t nb, const ppe_cfg_t *cfg,
-           hipStream_t s, int slot_set, uint32_t idx_base = 0) {
+           hipStream_t s, int slot_set, uint32_t idx_base = 0, const ppe_flowdev *fl = nullptr,
+           uint32_t *grid_out = nullptr) {
     const int r = c->running;
     const uint32_t words = (uint32_t)c->h_img[r].size();
     const StagePlan plan = stage_plan(c, c->h_img[r]);
@@ -274,6 +299,8 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     a.off_resid = c->h_img[r][PPE_IMG_W_OFFRESID];
     a.cslots = c->d_cslots + (size_t)slot_set * c->max_grid * PPE_CSLOT_WORDS;
     a.trace = c->trace;
+    if (fl) a.flow = *fl;
+    if (grid_out) *grid_out = grid;
 
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
@@ -289,7 +316,8 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         c->ev_used += 2;
     }
     const int rc =
-        ppe_launch_classify(&a, grid, plan.mode, plan.pipe, (int)plan.block, (void *)s, (void *)e0, (void *)e1);
+        ppe_launch_classify(&a, grid, plan.mode, plan.pipe, (int)plan.block, fl != nullptr, (void *)s, (void *)e0,
+                            (void *)e1);
     if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
     c->img_used[r] = true;
     return PPE_OK;
@@ -375,6 +403,7 @@ int ppe_ctx_destroy(ppe_ctx_t *c) {
         if (s) (void)hipStreamDestroy(s);
     for (hipEvent_t e : c->pipe_ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->flow) ppe_flow_destroy(c);
     for (auto &h : c->hs) {
         if (h.s) (void)hipStreamDestroy(h.s);
         (void)hipFree(h.hdr);
@@ -729,6 +758,298 @@ int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds
     if (lds_bytes)
         *lds_bytes = ppe_classify_fixed_lds((int)plan.block) + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u);
     if (variant) *variant = (uint32_t)plan.mode | ((uint32_t)plan.pipe << 4);
+    return PPE_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Flow table (FlowInit / FlowHandlePacket / FlowAgeTimeoutCB / FlowRelease, dataplane/src/flow/flow.c)
+
+static void flow_free_arrays(FlowArrays &a) {
+    (void)hipFree(a.keys);
+    (void)hipFree(a.creator);
+    (void)hipFree(a.stats);
+    (void)hipFree(a.last);
+    a = FlowArrays();
+}
+
+// allocate (if needed) and clear one slot-array set: every slot EMPTY with zero counters, no creator
+static int flow_clear_arrays(ppe_ctx *c, FlowArrays &a, uint32_t nslots, hipStream_t s) {
+    if (!a.keys) {
+        if (hipMalloc(&a.keys, (size_t)nslots * 16u) != hipSuccess ||
+            hipMalloc(&a.creator, (size_t)nslots * 4u) != hipSuccess ||
+            hipMalloc(&a.stats, (size_t)nslots * 32u) != hipSuccess ||
+            hipMalloc(&a.last, (size_t)nslots * 8u) != hipSuccess) {
+            flow_free_arrays(a);
+            return fail(c, PPE_ENOMEM, "flow table: out of device memory (%u slots)", nslots);
+        }
+    }
+    HIPCHK(c, hipMemsetAsync(a.keys, 0, (size_t)nslots * 16u, s));
+    HIPCHK(c, hipMemsetAsync(a.creator, 0xff, (size_t)nslots * 4u, s));
+    HIPCHK(c, hipMemsetAsync(a.stats, 0, (size_t)nslots * 32u, s));
+    HIPCHK(c, hipMemsetAsync(a.last, 0, (size_t)nslots * 8u, s));
+    return PPE_OK;
+}
+
+static ppe_flowdev flow_dev(const FlowTable &t, int which) {
+    ppe_flowdev d;
+    std::memset(&d, 0, sizeof d);
+    const FlowArrays &a = t.arr[which];
+    d.keys = a.keys;
+    d.stats = a.stats;
+    d.last = a.last;
+    d.creator = a.creator;
+    d.ctl = t.ctl;
+    d.rec = t.rec;
+    d.tile_miss = t.tile_miss;
+    d.tile_new = t.tile_new;
+    d.rslot = t.rslot;
+    d.gmask = t.nslots / 4u - 1u;
+    d.capacity = t.capacity;
+    return d;
+}
+
+static uint32_t flow_grid(const ppe_ctx *c, uint64_t items, uint32_t per_wg) {
+    const uint64_t want = (items + per_wg - 1u) / per_wg;
+    return (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>(want, (uint64_t)c->n_cu * 8u));
+}
+
+// exact live / tombstone counts (synchronises)
+static int flow_sync_counts(ppe_ctx *c, unsigned long long *ctl_out) {
+    FlowTable &t = *c->flow;
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(ctl_out, t.ctl, PPE_FCTL_WORDS * 8u, hipMemcpyDeviceToHost));
+    t.live_ub = ctl_out[PPE_FCTL_LIVE];
+    t.tomb_ub = ctl_out[PPE_FCTL_TOMBS];
+    t.snap_inflight = false;  // (the device is idle: any snapshot has landed and is superseded)
+    return PPE_OK;
+}
+
+// Rebuild the table without tombstones when they exceed a quarter of the slots (keeps every probe sequence short
+// and an EMPTY slot on each).  Synchronises when the host bound says it may be needed.
+static int flow_maybe_rehash(ppe_ctx *c) {
+    FlowTable &t = *c->flow;
+    if (t.tomb_ub <= t.nslots / 4u) return PPE_OK;
+    unsigned long long ctl[PPE_FCTL_WORDS];
+    int rc = flow_sync_counts(c, ctl);
+    if (rc != PPE_OK || t.tomb_ub <= t.nslots / 4u) return rc;
+    const int dst = 1 - t.cur;
+    rc = flow_clear_arrays(c, t.arr[dst], t.nslots, nullptr);
+    if (rc != PPE_OK) return rc;
+    ppe_flow_kargs k;
+    std::memset(&k, 0, sizeof k);
+    k.f = flow_dev(t, t.cur);
+    k.dst = flow_dev(t, dst);
+    k.nslots = t.nslots;
+    rc = ppe_launch_flow(PPE_FLOW_K_REHASH, &k, flow_grid(c, t.nslots, 256u), nullptr);
+    if (rc != 0) return fail(c, PPE_EIO, "flow rehash launch failed: %s", hipGetErrorString((hipError_t)rc));
+    HIPCHK(c, hipMemset(t.ctl + PPE_FCTL_TOMBS, 0, 8u));
+    HIPCHK(c, hipDeviceSynchronize());
+    t.cur = dst;
+    t.tomb_ub = 0;
+    ++t.rehashes;
+    return PPE_OK;
+}
+
+int ppe_flow_destroy(ppe_ctx_t *c) {
+    if (!c) return PPE_EINVAL;
+    if (!c->flow) return PPE_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    FlowTable *t = c->flow;
+    for (FlowArrays &a : t->arr) flow_free_arrays(a);
+    if (t->ctl_h) (void)hipHostFree(t->ctl_h);
+    if (t->snap_ev) (void)hipEventDestroy(t->snap_ev);
+    (void)hipFree(t->ctl);
+    (void)hipFree(t->rec);
+    (void)hipFree(t->rslot);
+    (void)hipFree(t->tile_miss);
+    (void)hipFree(t->tile_new);
+    delete t;
+    c->flow = nullptr;
+    return PPE_OK;
+}
+
+int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
+    if (!c) return PPE_EINVAL;
+    if (capacity == 0) capacity = 100000u;  // MEM_POOL_FLOW_NODE_NUM, dataplane/src/platform/mem_pool.h:72
+    if (max_batch == 0) max_batch = 1u << 20;
+    if (capacity > (1u << 26) || max_batch > (1u << 26))
+        return fail(c, PPE_EINVAL, "flow table: capacity and max_batch must be <= 2^26");
+    HIPCHK(c, hipSetDevice(c->device));
+    ppe_flow_destroy(c);
+    FlowTable *t = new (std::nothrow) FlowTable();
+    if (!t) return PPE_ENOMEM;
+    c->flow = t;
+    t->capacity = capacity;
+    t->max_batch = max_batch;
+    // load <= 1/2 with the pool full and a whole batch of claims pending; tombstones are rehashed away at 1/4
+    uint32_t ns = 64;
+    while ((uint64_t)ns < 2ull * ((uint64_t)capacity + max_batch)) ns <<= 1;
+    t->nslots = ns;
+    const uint32_t tiles = (max_batch + 63u) / 64u;
+    int rc = PPE_OK;
+    if (hipMalloc(&t->ctl, PPE_FCTL_WORDS * 8u) != hipSuccess || hipMalloc(&t->rec, (size_t)max_batch * 16u) != hipSuccess ||
+        hipMalloc(&t->rslot, (size_t)max_batch * 4u) != hipSuccess ||
+        hipMalloc(&t->tile_miss, (size_t)tiles * 8u) != hipSuccess ||
+        hipMalloc(&t->tile_new, (size_t)tiles * 8u) != hipSuccess)
+        rc = fail(c, PPE_ENOMEM, "flow table: out of device memory");
+    if (rc == PPE_OK && hipMemset(t->ctl, 0, PPE_FCTL_WORDS * 8u) != hipSuccess) rc = fail(c, PPE_EIO, "memset");
+    if (rc == PPE_OK && (hipHostMalloc(&t->ctl_h, PPE_FCTL_WORDS * 8u, hipHostMallocDefault) != hipSuccess ||
+                         hipEventCreateWithFlags(&t->snap_ev, hipEventDisableTiming) != hipSuccess))
+        rc = fail(c, PPE_ENOMEM, "flow table: pinned snapshot buffer");
+    if (rc == PPE_OK) rc = flow_clear_arrays(c, t->arr[0], ns, nullptr);
+    if (rc == PPE_OK && hipDeviceSynchronize() != hipSuccess) rc = fail(c, PPE_EIO, "flow table init failed");
+    if (rc != PPE_OK) ppe_flow_destroy(c);
+    return rc;
+}
+
+int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
+                      void *stream) {
+    if (!c || !out) return PPE_EINVAL;
+    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    if (!out->verdict) return fail(c, PPE_EINVAL, "ppe_classify_flow needs the verdict output");
+    int rc = check_batch(c, in, cfg);
+    if (rc != PPE_OK || in->n == 0) return rc;
+    FlowTable &t = *c->flow;
+    if (in->n > t.max_batch) return fail(c, PPE_EINVAL, "batch larger than the flow table's max_batch");
+    HIPCHK(c, use_device(c));
+    if (t.snap_inflight && hipEventQuery(t.snap_ev) == hipSuccess) {  // a finished snapshot tightens the bounds
+        t.snap_inflight = false;
+        t.live_ub = std::min<uint64_t>(t.ctl_h[PPE_FCTL_LIVE] + t.snap_n, t.capacity);
+        t.tomb_ub = t.ctl_h[PPE_FCTL_TOMBS] + t.snap_n_rev;
+    }
+    rc = flow_maybe_rehash(c);
+    if (rc != PPE_OK) return rc;
+    const hipStream_t s = (hipStream_t)stream;
+    const ppe_flowdev d = flow_dev(t, t.cur);
+    // 1. decode, hash, FlowFind; found flows are accounted and forwarded, the rest get syn_check + ACL
+    rc = launch(c, in, out, 1, cfg, s, 0, 0, &d);
+    if (rc != PPE_OK) return rc;
+    ppe_flow_kargs k;
+    std::memset(&k, 0, sizeof k);
+    k.f = d;
+    k.len = in->len;
+    k.verdict = out->verdict;
+    k.hit = out->acl_hit;
+    k.fw_idx = out->fw_idx;
+    k.drop_idx = out->drop_idx;
+    k.tile_cnt = out->tile_cnt;
+    k.n = in->n;
+    k.unsup_fw = cfg ? cfg->unsupport_proto_action : 0u;
+    k.now = cfg ? cfg->now_seconds : 0u;
+    k.nslots = t.nslots;
+    k.cslots = c->d_cslots;
+    const uint32_t fg = flow_grid(c, (in->n + 63u) / 64u, PPE_FLOW_BLOCK_WAVES);
+    // 2-5. claim, resolve, [revoke: only when the pool may overflow], finalize
+    const bool may_overflow = t.live_ub + in->n > t.capacity;
+    for (int kind : {PPE_FLOW_K_CLAIM, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_REVOKE, PPE_FLOW_K_FINALIZE}) {
+        if (kind == PPE_FLOW_K_REVOKE && !may_overflow) continue;
+        const int e = ppe_launch_flow(kind, &k, kind == PPE_FLOW_K_REVOKE ? 1u : fg, (void *)s);
+        if (e != 0) return fail(c, PPE_EIO, "flow kernel %d launch failed: %s", kind, hipGetErrorString((hipError_t)e));
+    }
+    t.live_ub = std::min<uint64_t>(t.live_ub + in->n, t.capacity);
+    if (may_overflow) t.tomb_ub += in->n;  // revoked claims leave tombstones
+    if (t.snap_inflight) {
+        t.snap_n += in->n;
+        if (may_overflow) t.snap_n_rev += in->n;
+    } else if (may_overflow || t.tomb_ub > t.nslots / 8u) {  // bounds near a limit: refresh them asynchronously
+        HIPCHK(c, hipMemcpyAsync(t.ctl_h, t.ctl, PPE_FCTL_WORDS * 8u, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipEventRecord(t.snap_ev, s));
+        t.snap_inflight = true;
+        t.snap_n = t.snap_n_rev = 0;
+    }
+    return PPE_OK;
+}
+
+int ppe_flow_age(ppe_ctx_t *c, uint64_t now_seconds, uint64_t timeout_seconds, uint64_t *deleted) {
+    if (!c) return PPE_EINVAL;
+    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    HIPCHK(c, use_device(c));
+    FlowTable &t = *c->flow;
+    unsigned long long before[PPE_FCTL_WORDS], after[PPE_FCTL_WORDS];
+    int rc = flow_sync_counts(c, before);
+    if (rc != PPE_OK) return rc;
+    ppe_flow_kargs k;
+    std::memset(&k, 0, sizeof k);
+    k.f = flow_dev(t, t.cur);
+    k.now = now_seconds;
+    k.timeout = timeout_seconds;
+    k.nslots = t.nslots;
+    rc = ppe_launch_flow(PPE_FLOW_K_AGE, &k, flow_grid(c, t.nslots, 256u), nullptr);
+    if (rc != 0) return fail(c, PPE_EIO, "flow age launch failed: %s", hipGetErrorString((hipError_t)rc));
+    rc = flow_sync_counts(c, after);
+    if (rc != PPE_OK) return rc;
+    if (deleted) *deleted = after[PPE_FCTL_DEL_FLOW] - before[PPE_FCTL_DEL_FLOW];
+    return flow_maybe_rehash(c);
+}
+
+int ppe_flow_info(ppe_ctx_t *c, ppe_flow_info_t *info) {
+    if (!c || !info) return PPE_EINVAL;
+    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    HIPCHK(c, use_device(c));
+    unsigned long long ctl[PPE_FCTL_WORDS];
+    const int rc = flow_sync_counts(c, ctl);
+    if (rc != PPE_OK) return rc;
+    std::memset(info, 0, sizeof *info);
+    const FlowTable &t = *c->flow;
+    info->live = ctl[PPE_FCTL_LIVE];
+    info->new_flow = ctl[PPE_FCTL_NEW_FLOW];
+    info->del_flow = ctl[PPE_FCTL_DEL_FLOW];
+    info->capacity = t.capacity;
+    info->max_batch = t.max_batch;
+    info->slots = t.nslots;
+    info->tombstones = (uint32_t)ctl[PPE_FCTL_TOMBS];
+    info->rehashes = t.rehashes;
+    return PPE_OK;
+}
+
+int ppe_flow_clear_stat(ppe_ctx_t *c) {
+    if (!c) return PPE_EINVAL;
+    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    HIPCHK(c, use_device(c));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemset(c->flow->ctl + PPE_FCTL_NEW_FLOW, 0, 16u));  // new_flow, del_flow
+    return PPE_OK;
+}
+
+int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_t *n) {
+    if (!c || !n) return PPE_EINVAL;
+    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    HIPCHK(c, use_device(c));
+    HIPCHK(c, hipDeviceSynchronize());
+    const FlowTable &t = *c->flow;
+    const FlowArrays &a = t.arr[t.cur];
+    std::vector<uint32_t> keys((size_t)t.nslots * 4u);
+    HIPCHK(c, hipMemcpy(keys.data(), a.keys, keys.size() * 4u, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> stats, last;
+    if (entries && max) {
+        stats.resize((size_t)t.nslots * 4u);
+        last.resize(t.nslots);
+        HIPCHK(c, hipMemcpy(stats.data(), a.stats, stats.size() * 8u, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(last.data(), a.last, last.size() * 8u, hipMemcpyDeviceToHost));
+    }
+    uint32_t k = 0;
+    for (uint32_t s = 0; s < t.nslots; ++s) {
+        const uint32_t st = keys[4u * s + 3u];
+        if ((st & (PPE_FS_PEND | 0xffu)) != PPE_FS_LIVE(0u)) continue;
+        if (entries && k < max) {
+            ppe_flow_entry_t &e = entries[k];
+            std::memset(&e, 0, sizeof e);
+            e.sip = keys[4u * s];
+            e.dip = keys[4u * s + 1u];
+            e.sport = (uint16_t)(keys[4u * s + 2u] & 0xffffu);
+            e.dport = (uint16_t)(keys[4u * s + 2u] >> 16);
+            e.protocol = (uint8_t)(st >> 8);
+            e.slot = s;
+            e.pktcnts2d = stats[4u * s];
+            e.bytecnts2d = stats[4u * s + 1u];
+            e.pktcntd2s = stats[4u * s + 2u];
+            e.bytecntd2s = stats[4u * s + 3u];
+            e.last_seen = last[s];
+        }
+        ++k;
+    }
+    *n = k;
     return PPE_OK;
 }
 

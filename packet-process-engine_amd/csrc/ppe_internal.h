@@ -22,6 +22,48 @@ struct ppe_bdesc {
     uint32_t pad;
 };
 
+/* Device flow table (ppe_classify_flow; ppe_kernels.hip "flow table").  Open addressing over groups of 4 slots
+ * (64 B of keys), linear probing from group flow_hash & gmask; a key lies before the first EMPTY slot of its probe
+ * sequence (slots never return to EMPTY: deletions leave TOMBs, reclaimed by a rehash). */
+#define PPE_FS_EMPTY 0u
+#define PPE_FS_TOMB 1u
+#define PPE_FS_LIVE(proto) (2u | ((proto) << 8))  /* key words valid */
+#define PPE_FS_PEND 0x80000000u                   /* | packet index: claimed by this batch, key = rec[index] */
+#define PPE_FLOW_NONE 0xffffffffu
+#define PPE_FLOW_REVOKED 0x80000000u              /* creator word: pool exhausted, the claim is withdrawn */
+enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_NEW, PPE_FCTL_TOMBS,
+       PPE_FCTL_WORDS = 8 };
+struct ppe_flowdev {
+    uint32_t *keys;               /* nslots × {sip, dip, sport | dport << 16, state}, the creating packet's orientation */
+    unsigned long long *stats;    /* nslots × {pkts s2d, bytes s2d, pkts d2s, bytes d2s}                               */
+    unsigned long long *last;     /* nslots × last-seen time                                                          */
+    uint32_t *creator;            /* nslots: lowest index of the packets claiming the slot in this batch (| REVOKED)   */
+    unsigned long long *ctl;      /* PPE_FCTL_* device counters                                                        */
+    uint32_t *rec;                /* max_batch × {sip, dip, ports, proto | provisional status << 8} of pending packets */
+    unsigned long long *tile_miss;  /* per tile: lanes whose flow was not found (pending resolution)                   */
+    unsigned long long *tile_new;   /* per tile: lanes that create their flow                                          */
+    uint32_t *rslot;              /* max_batch: the slot a pending packet's flow was claimed in, or PPE_FLOW_NONE       */
+    uint32_t gmask;               /* slot groups - 1                                                                   */
+    uint32_t capacity;            /* flow pool size                                                                     */
+};
+
+/* flow-table kernels after the classify kernel (one batch) */
+struct ppe_flow_kargs {
+    struct ppe_flowdev f;
+    const uint32_t *len;          /* the batch's wire lengths (byte counters) */
+    uint32_t *verdict;
+    int32_t *hit;
+    uint32_t *fw_idx, *drop_idx, *tile_cnt;
+    uint32_t n;
+    uint32_t unsup_fw;
+    uint64_t now;
+    uint64_t timeout;             /* aging */
+    uint32_t nslots;
+    uint32_t pad;
+    unsigned long long *cslots;   /* counter slots (one per workgroup) */
+    struct ppe_flowdev dst;       /* rehash target */
+};
+
 /* batches per launch: the descriptors travel in the kernel arguments (8 × 96 B) */
 #define PPE_MAX_BATCH 8
 
@@ -47,6 +89,7 @@ struct ppe_kargs {
                                                 (scalar registers, no load in the loop)                               */
     unsigned long long *cslots; /* [grid][PPE_CSLOT_WORDS] counter slots, one per workgroup */
     unsigned long long *trace;  /* diagnostic builds (PPE_TRACE) only: per-wave phase timestamps, else unused */
+    struct ppe_flowdev flow;    /* flow-table launches (ppe_classify_flow, one batch) */
 };
 
 struct ppe_tuple_kargs {
@@ -74,8 +117,14 @@ extern "C" {
 /* Launch the classify kernel. grid = workgroups (persistent), lds_img = stage image in LDS. Returns hipError_t. */
 /* mode: 0 image in global memory, 1 whole image in LDS, 2 prefix in LDS; pipe: 0 first tile loaded at the loop top,
  * 1 first tile's loads issued before the image staging (see ppe_kernels.hip) */
-int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, void *stream,
-                        void *ev_start, void *ev_stop);
+int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, int flow,
+                        void *stream, void *ev_start, void *ev_stop);
+/* flow-table phases after a flow-mode classify launch (stream order): claim, resolve, [revoke], finalize */
+enum { PPE_FLOW_K_CLAIM = 0, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_REVOKE, PPE_FLOW_K_FINALIZE, PPE_FLOW_K_AGE,
+       PPE_FLOW_K_REHASH };
+int ppe_launch_flow(int kind, const struct ppe_flow_kargs *a, uint32_t grid, void *stream);
+#define PPE_FLOW_BLOCK 256      /* flow kernels' workgroup size */
+#define PPE_FLOW_BLOCK_WAVES 4u /* waves (tiles in flight) per flow-kernel workgroup */
 int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block);
 uint32_t ppe_classify_fixed_lds(int block);
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);

@@ -135,11 +135,11 @@ __device__ __forceinline__ uint32_t reason_counter(uint32_t st) {
         ((uint64_t)PPE_C_IPV4_HEADERLEN_ERR << 35) | ((uint64_t)PPE_C_IPV4_VERSION_ERR << 40) |
         ((uint64_t)PPE_C_IPV4_PKTLEN_ERR << 45) | ((uint64_t)PPE_C_FRAG_FRAGLEN_ERR << 50) |
         ((uint64_t)PPE_C_FRAG_PUNT << 55);
-    constexpr uint64_t K1 =  // st 12..18
+    constexpr uint64_t K1 =  // st 12..19
         ((uint64_t)PPE_C_IPV4_UNSUPPORT << 0) | ((uint64_t)PPE_C_UDP_HEADERLEN_ERR << 5) |
         ((uint64_t)PPE_C_UDP_PKTLEN_ERR << 10) | ((uint64_t)PPE_C_TCP_HEADERLEN_ERR << 15) |
         ((uint64_t)PPE_C_TCP_PKTLEN_ERR << 20) | ((uint64_t)PPE_C_FLOW_TCP_NO_SYN_FIRST << 25) |
-        ((uint64_t)PPE_C_WINDOW_PUNT << 30);
+        ((uint64_t)PPE_C_WINDOW_PUNT << 30) | ((uint64_t)PPE_C_FLOW_NODE_NOMEM << 35);
     const bool lo = st < 12u;
     return (uint32_t)(((lo ? K0 : K1) >> (5u * (lo ? st : st - 12u))) & 31u);
 }
@@ -213,11 +213,13 @@ __device__ __forceinline__ uint32_t bin_counters(uint32_t key, uint64_t act_tabl
     if (vl && st != PPE_ST_VLAN_UNSUPPORT) cb |= CB(PPE_C_VLAN_RX_OK);
     const bool l4_in = st == PPE_ST_ACL_FW || st == PPE_ST_ACL_DROP || st == PPE_ST_UDP_HEADER_ERR ||
                        st == PPE_ST_UDP_LEN_ERR || st == PPE_ST_TCP_HEADER_ERR || st == PPE_ST_TCP_LEN_ERR ||
-                       st == PPE_ST_FLOW_TCP_NO_SYN_FIRST || st == PPE_ST_WINDOW_PUNT;
+                       st == PPE_ST_FLOW_TCP_NO_SYN_FIRST || st == PPE_ST_WINDOW_PUNT || st == PPE_ST_FLOW_NOMEM;
     if (l4_in) cb |= CB(PPE_C_IPV4_RX_OK);
     if (l4 && !tcp) cb |= CB(PPE_C_UDP_RX_OK);
     if (tcp) cb |= CB(PPE_C_TCP_RX_OK);
-    if (st == PPE_ST_FLOW_TCP_NO_SYN_FIRST || st == PPE_ST_ACL_DROP) cb |= CB(PPE_C_FLOW_PROC_FAIL);
+    if (st == PPE_ST_FLOW_TCP_NO_SYN_FIRST || st == PPE_ST_ACL_DROP || st == PPE_ST_FLOW_NOMEM)
+        cb |= CB(PPE_C_FLOW_PROC_FAIL);
+    if (st == PPE_ST_FLOW_NOMEM) cb |= CB(PPE_C_ACL_FW);  // counted before FlowAdd failed (flow.c:240)
     if (st == PPE_ST_ACL_FW) cb |= CB(PPE_C_FLOW_PROC_OK);
     const uint32_t act = (uint32_t)(act_table >> (2u * st)) & 3u;
     cb |= act == PPE_ACT_FW ? CB(PPE_C_OUT_FW) : (act == PPE_ACT_DROP ? CB(PPE_C_OUT_DROP) : CB(PPE_C_OUT_PUNT));
@@ -518,11 +520,115 @@ __device__ __forceinline__ void stage_image(const uint32_t *img, uint32_t *lds, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// action of each terminal status, 2 bits per status: FW for ACL_FW, PUNT for fragments / short windows, the
+// configured action for unsupported protocols (Decode_unsupport_proto_handle, decode.c:31-45), else DROP
+__device__ __forceinline__ uint64_t make_act_table(uint32_t unsup_fw) {
+    uint64_t t = 0;
+#pragma unroll
+    for (uint32_t st = 0; st < PPE_ST__COUNT; ++st) {
+        const uint64_t ac = st == PPE_ST_ACL_FW ? PPE_ACT_FW
+                          : (st == PPE_ST_L2_UNSUPPORT || st == PPE_ST_VLAN_UNSUPPORT || st == PPE_ST_IPV4_UNSUPPORT)
+                              ? (unsup_fw ? PPE_ACT_FW : PPE_ACT_DROP)
+                          : (st == PPE_ST_FRAG || st == PPE_ST_WINDOW_PUNT) ? PPE_ACT_PUNT : PPE_ACT_DROP;
+        t |= ac << (2u * st);
+    }
+    return t;
+}
+
+// Wave-ballot compaction of a 64-packet tile's FW / DROP indices into the tile's 64-slot segment of each list (or
+// the partition layout when fw_idx == drop_idx), plus the tile count.  Every lane of the wave calls it.
+__device__ __forceinline__ void compact_tile(uint32_t *fw_idx, uint32_t *drop_idx, uint32_t *tile_cnt, uint32_t n,
+                                             uint32_t idx_base, uint32_t tile, uint32_t lane, bool valid, uint32_t act) {
+    const uint32_t p = (tile << 6) + lane;
+    const bool is_fw = valid && act == PPE_ACT_FW;
+    const bool is_drop = valid && act == PPE_ACT_DROP;
+    const uint64_t bfw = __builtin_amdgcn_ballot_w64(is_fw);
+    const uint64_t bdr = __builtin_amdgcn_ballot_w64(is_drop);
+    const uint32_t pfw = __builtin_amdgcn_mbcnt_hi((uint32_t)(bfw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bfw, 0u));
+    const uint32_t pdr = __builtin_amdgcn_mbcnt_hi((uint32_t)(bdr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bdr, 0u));
+    const uint32_t so = (tile << 8) + 4u * (is_fw ? pfw : pdr);  // byte offset in the tile's segment
+    if (fw_idx == drop_idx && fw_idx) {
+        // partition layout (one shared list): the tile's segment holds every packet of the tile, FW from the
+        // front, DROP at the back, PUNT in between, each in ascending order, the action in bits 31:30 —
+        // every slot written by one store instruction (whole-line writes, no tile count needed)
+        const uint32_t nv = min(n - (tile << 6), 64u);
+        const uint32_t ndr = (uint32_t)__popcll(bdr), nfw = (uint32_t)__popcll(bfw);
+        const uint32_t slot = is_fw ? pfw : (is_drop ? nv - ndr + pdr : nfw + lane - pfw - pdr);
+        if (valid) gst<uint32_t>(fw_idx, (tile << 8) + 4u * slot, (p + idx_base) | (act << 30));
+    } else if (fw_idx && drop_idx) {  // both lists: one store instruction
+        if (is_fw || is_drop) gst<uint32_t>(is_fw ? fw_idx : drop_idx, so, p + idx_base);
+    } else {
+        if (fw_idx && is_fw) gst<uint32_t>(fw_idx, so, p + idx_base);
+        if (drop_idx && is_drop) gst<uint32_t>(drop_idx, so, p + idx_base);
+    }
+    if (tile_cnt && lane == 0) {
+        const uint32_t nv = min(n - (tile << 6), 64u);
+        const uint32_t nfw = (uint32_t)__popcll(bfw), ndr = (uint32_t)__popcll(bdr);
+        gst<uint32_t>(tile_cnt, 4u * tile, nfw | (ndr << 8) | ((nv - nfw - ndr) << 16));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Flow table (dataplane/src/flow/flow.c; layout in ppe_internal.h).  Slot state word: EMPTY, TOMB, LIVE | proto,
+// or PEND | packet index (claimed during the current batch, key in rec[index]).
+
+__device__ __forceinline__ uint32_t swap_ports(uint32_t ports) { return (ports >> 16) | (ports << 16); }
+
+// FlowMatch (flow.c:81-94) of two keys {sip, dip, ports}: the same 5-tuple in either direction (protocol compared
+// by the caller)
+__device__ __forceinline__ bool key_match(uint32_t ax, uint32_t ay, uint32_t az, uint32_t bx, uint32_t by,
+                                          uint32_t bz) {
+    return (ax == bx && ay == by && az == bz) || (ax == by && ay == bx && az == swap_ports(bz));
+}
+
+// FlowFind (flow.c:96-115) over the table as it stood at the start of the batch: the slot of the live flow of
+// this 5-tuple, or -1.  One 64-B group (4 slots) per probe step; stops at the first EMPTY slot.
+__device__ __forceinline__ int32_t flow_find(const ppe_flowdev &f, uint32_t fh, uint32_t sip, uint32_t dip,
+                                             uint32_t ports, uint32_t proto, uint32_t &fsip, uint32_t &fports) {
+    const uint32_t live = PPE_FS_LIVE(proto);
+    const uint4 *keys = (const uint4 *)f.keys;
+    uint32_t g = fh & f.gmask;
+#pragma unroll 1
+    for (uint32_t it = 0; it <= f.gmask; ++it) {
+        uint4 e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[j] = keys[4u * g + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (e[j].w == live && key_match(e[j].x, e[j].y, e[j].z, sip, dip, ports)) {
+                fsip = e[j].x;
+                fports = e[j].z;
+                return (int32_t)(4u * g + j);
+            }
+            if (e[j].w == PPE_FS_EMPTY) return -1;
+        }
+        g = (g + 1u) & f.gmask;
+    }
+    return -1;
+}
+
+// FlowGetPacketDirection (flow.c:248-269) + FlowUpdate (flow.c:163-178) + FLOW_UPDATE_TIMESTAMP: the packet's
+// direction flag; per-direction packet / byte counters by returnless atomics, last-seen time.
+__device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t s, uint32_t fsip, uint32_t fports,
+                                                 uint32_t sip, uint32_t ports, uint32_t wire_len, uint64_t now) {
+    const uint32_t sport = ports & 0xffffu, dport = ports >> 16, fsport = fports & 0xffffu;
+    const bool to_server = sport != dport ? fsport == sport : fsip == sip;
+    const uint32_t d = sport == fsport ? 0u : 2u;
+    unsigned long long *st = f.stats + 4ull * s + d;
+    __hip_atomic_fetch_add(st, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(st + 1, (unsigned long long)wire_len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    f.last[s] = now;  // every packet of the batch stores the same batch time
+    return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
+}
+
 // PF: when a tile's window is fetched
 #define PF_NONE 0   // at the top of its own iteration
 #define PF_HOIST 1  // as PF_NONE, but the first tile's loads are issued before the image staging
 
-template <int MODE, int PF, int BLOCK>
+// FLOW: stateful flow-table mode (ppe_classify_flow, one batch): packets whose flow exists are accounted and
+// forwarded here; the rest are recorded for the claim / resolve / finalize kernels below, which complete their
+// tiles (verdict, compaction, counters).
+template <int MODE, int PF, int BLOCK, bool FLOW>
 __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(ppe_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     using L = Lds<BLOCK>;
@@ -563,17 +669,9 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
     const AclGeo geo = {a.lds_iters, a.max_depth, a.max_leaf, a.root_ks, a.off_leaf, a.off_rules, a.off_resid,
                         a.lds_words, a.default_action, a.jump, a.off_nodes};
 
-    // action of each terminal status, 2 bits per status: FW for ACL_FW, PUNT for fragments / short windows, the
-    // configured action for unsupported protocols (Decode_unsupport_proto_handle, decode.c:31-45), else DROP
-    uint64_t act_table = 0;
-#pragma unroll
-    for (uint32_t st = 0; st < PPE_ST__COUNT; ++st) {
-        const uint64_t ac = st == PPE_ST_ACL_FW ? PPE_ACT_FW
-                          : (st == PPE_ST_L2_UNSUPPORT || st == PPE_ST_VLAN_UNSUPPORT || st == PPE_ST_IPV4_UNSUPPORT)
-                              ? (a.unsup_fw ? PPE_ACT_FW : PPE_ACT_DROP)
-                          : (st == PPE_ST_FRAG || st == PPE_ST_WINDOW_PUNT) ? PPE_ACT_PUNT : PPE_ACT_DROP;
-        act_table |= ac << (2u * st);
-    }
+    const uint64_t act_table = make_act_table(a.unsup_fw);
+    // this batch's creator count, summed by the resolve kernel (which runs after this one)
+    if (FLOW && blockIdx.x == 0 && tid == 0) a.flow.ctl[PPE_FCTL_BATCH_NEW] = 0;
 
     // one tile: decode, hash, ACL, stores, compaction, counters.  w = the window's first 52 bytes, wlen = wire length
     auto process = [&](uint32_t tile, const uint32_t (&w)[13], uint32_t wlen) {
@@ -587,6 +685,18 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
         if (PPE_TRACE && titer < 4) {
             asm volatile("" ::"v"(fh), "v"(k.st));  // decoded + hashed before the stamp
             TRACE_AT(4 + 5 * titer);
+        }
+        bool pend = false;  // FLOW: flow not in the table; resolved by the kernels after this one
+        if (FLOW && (k.flags & PPE_F_L4)) {  // FlowGetFlowFromHash, flow.c:181-201
+            const uint32_t ports = k.sport | (k.dport << 16);
+            uint32_t fsip = 0, fports = 0;
+            const int32_t s = flow_find(a.flow, fh, k.sip, k.dip, ports, k.proto, fsip, fports);
+            if (s >= 0) {  // found: STAT_ACL_FW without an ACL lookup, then FlowHandlePacket's accounting
+                if (valid) k.flags |= flow_account(a.flow, (uint32_t)s, fsip, fports, k.sip, ports, wlen, a.now);
+                k.st = PPE_ST_ACL_FW;
+            } else {
+                pend = valid;
+            }
         }
         if ((PPE_ABLATE & 1) && k.st == ST_ACL) {
             k.st = PPE_ST_ACL_FW;
@@ -628,35 +738,19 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
             }
         }
 
-        // ---- wave-ballot compaction of FW / DROP indices into this tile's 64-slot segment of each list ----
-        if (!(PPE_ABLATE & 4)) {
-            const bool is_fw = valid && act == PPE_ACT_FW;
-            const bool is_drop = valid && act == PPE_ACT_DROP;
-            const uint64_t bfw = __builtin_amdgcn_ballot_w64(is_fw);
-            const uint64_t bdr = __builtin_amdgcn_ballot_w64(is_drop);
-            const uint32_t pfw = __builtin_amdgcn_mbcnt_hi((uint32_t)(bfw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bfw, 0u));
-            const uint32_t pdr = __builtin_amdgcn_mbcnt_hi((uint32_t)(bdr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bdr, 0u));
-            const uint32_t so = (tile << 8) + 4u * (is_fw ? pfw : pdr);  // byte offset in the tile's segment
-            if (B.fw_idx == B.drop_idx && B.fw_idx) {
-                // partition layout (one shared list): the tile's segment holds every packet of the tile, FW from the
-                // front, DROP at the back, PUNT in between, each in ascending order, the action in bits 31:30 —
-                // every slot written by one store instruction (whole-line writes, no tile count needed)
-                const uint32_t nv = min(B.n - (tile << 6), 64u);
-                const uint32_t ndr = (uint32_t)__popcll(bdr), nfw = (uint32_t)__popcll(bfw);
-                const uint32_t slot = is_fw ? pfw : (is_drop ? nv - ndr + pdr : nfw + lane - pfw - pdr);
-                if (valid) gst<uint32_t>(B.fw_idx, (tile << 8) + 4u * slot, (p + B.idx_base) | (act << 30));
-            } else if (B.fw_idx && B.drop_idx) {  // both lists: one store instruction
-                if (is_fw || is_drop) gst<uint32_t>(is_fw ? B.fw_idx : B.drop_idx, so, p + B.idx_base);
-            } else {
-                if (B.fw_idx && is_fw) gst<uint32_t>(B.fw_idx, so, p + B.idx_base);
-                if (B.drop_idx && is_drop) gst<uint32_t>(B.drop_idx, so, p + B.idx_base);
-            }
-            if (B.tile_cnt && lane == 0) {
-                const uint32_t nv = min(B.n - (tile << 6), 64u);
-                const uint32_t nfw = (uint32_t)__popcll(bfw), ndr = (uint32_t)__popcll(bdr);
-                gst<uint32_t>(B.tile_cnt, 4u * tile, nfw | (ndr << 8) | ((nv - nfw - ndr) << 16));
+        if (FLOW) {
+            // pending packets: key + provisional status (NO_SYN / ACL_DROP / ACL_FW = would create the flow)
+            if (pend) gst<uint4>(a.flow.rec, 16u * p, make_uint4(k.sip, k.dip, k.sport | (k.dport << 16), k.proto | (st << 8)));
+            const uint64_t pm = __builtin_amdgcn_ballot_w64(pend);
+            if (lane == 0) a.flow.tile_miss[tile] = pm;
+            if (pm != 0) {  // the finalize kernel completes this tile (compaction, pending lanes' counters)
+                if (!(PPE_ABLATE & 2) && valid && !pend) atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
+                ++titer;
+                return;
             }
         }
+        // ---- wave-ballot compaction of FW / DROP indices into this tile's 64-slot segment of each list ----
+        if (!(PPE_ABLATE & 4)) compact_tile(B.fw_idx, B.drop_idx, B.tile_cnt, B.n, B.idx_base, tile, lane, valid, act);
 
         // ---- per-reason counters: one LDS add per packet into its (status, flags) bin ----
         if (!(PPE_ABLATE & 2) && valid) atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
@@ -696,6 +790,294 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
     TRACE_AT(23);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Flow-table kernels after a FLOW classify launch.  Exact sequential semantics of one core running the batch in
+// packet order (flow.c:181-245): among the pending packets of one 5-tuple, the lowest-index packet that passes
+// syn_check and the ACL (provisional status ACL_FW) creates the flow; the packets before it keep their own miss
+// verdict, the packets after it find the flow.  When the pool runs out, creators beyond the free count (in packet
+// order) fail with FLOW_NOMEM, and so do the later would-be creators of their flows.
+//   claim     pending would-be creators claim one slot per 5-tuple (CAS EMPTY → PEND | index, or join the claim of
+//             an equal key found on the probe path) and lower the slot's creator index (atomicMin);
+//   resolve   every pending packet finds its flow's claimed slot (rslot) and whether it is the creator;
+//   revoke    (only when the pool may overflow) ranks the creators in packet order and revokes those past the
+//             free count;
+//   finalize  final verdicts of the pending packets, flow creation and accounting, the tile's compaction and the
+//             pending packets' counters.
+
+__device__ __forceinline__ bool rec_match(const uint4 &q, const uint4 &r) {
+    return ((q.w ^ r.w) & 0xffu) == 0u && key_match(q.x, q.y, q.z, r.x, r.y, r.z);
+}
+// flow_hashfn of a record / key (TCP or UDP only reach the flow table); symmetric, so either orientation
+__device__ __forceinline__ uint32_t key_hash(uint32_t sip, uint32_t dip, uint32_t ports, uint32_t proto) {
+    return flow_hashfn_l4(proto == 6u, sip, dip, ports & 0xffffu, ports >> 16);
+}
+
+struct TileWalk {  // persistent grid: wave gw of W takes tiles gw, gw + W, ...
+    uint32_t lane, gw, W, ntiles;
+    template <int BLOCK> __device__ __forceinline__ static TileWalk make(uint32_t n) {
+        TileWalk t;
+        t.lane = threadIdx.x & 63u;
+        t.gw = blockIdx.x * (BLOCK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        t.W = gridDim.x * (BLOCK / 64);
+        t.ntiles = (n + 63u) >> 6;
+        return t;
+    }
+};
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ppe_flow_claim_kernel(ppe_flow_kargs a) {
+    const TileWalk w = TileWalk::make<BLOCK>(a.n);
+    const uint4 *rec = (const uint4 *)a.f.rec;
+    for (uint32_t t = w.gw; t < w.ntiles; t += w.W) {
+        const uint64_t mask = a.f.tile_miss[t];
+        if (!((mask >> w.lane) & 1ull)) continue;
+        const uint32_t p = (t << 6) + w.lane;
+        const uint4 r = rec[p];
+        if (((r.w >> 8) & 0xffu) != PPE_ST_ACL_FW) continue;  // only a packet that would create its flow claims
+        uint32_t g = key_hash(r.x, r.y, r.z, r.w & 0xffu) & a.f.gmask;
+        bool done = false;
+#pragma unroll 1
+        for (uint32_t it = 0; it <= a.f.gmask && !done; ++it) {
+#pragma unroll 1
+            for (uint32_t j = 0; j < 4u && !done; ++j) {
+                const uint32_t s = 4u * g + j;
+                uint32_t *sw = a.f.keys + 4ull * s + 3u;
+                uint32_t st = __hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (st == PPE_FS_EMPTY) {
+                    uint32_t expect = PPE_FS_EMPTY;
+                    if (__hip_atomic_compare_exchange_strong(sw, &expect, PPE_FS_PEND | p, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        atomicMin(&a.f.creator[s], p);
+                        done = true;
+                        break;
+                    }
+                    st = expect;  // claimed meanwhile (by this flow or another)
+                }
+                if ((st & PPE_FS_PEND) && rec_match(rec[st & ~PPE_FS_PEND], r)) {
+                    atomicMin(&a.f.creator[s], p);
+                    done = true;
+                }
+            }
+            g = (g + 1u) & a.f.gmask;
+        }
+    }
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ppe_flow_resolve_kernel(ppe_flow_kargs a) {
+    const TileWalk w = TileWalk::make<BLOCK>(a.n);
+    const uint4 *rec = (const uint4 *)a.f.rec;
+    uint32_t creators = 0;
+    for (uint32_t t = w.gw; t < w.ntiles; t += w.W) {
+        const uint64_t mask = a.f.tile_miss[t];
+        if (!mask) continue;
+        const uint32_t p = (t << 6) + w.lane;
+        bool is_new = false;
+        if ((mask >> w.lane) & 1ull) {
+            const uint4 r = rec[p];
+            uint32_t g = key_hash(r.x, r.y, r.z, r.w & 0xffu) & a.f.gmask, found = PPE_FLOW_NONE;
+            bool stop = false;
+#pragma unroll 1
+            for (uint32_t it = 0; it <= a.f.gmask && !stop; ++it) {
+#pragma unroll 1
+                for (uint32_t j = 0; j < 4u && !stop; ++j) {
+                    const uint32_t s = 4u * g + j;
+                    const uint32_t st = a.f.keys[4ull * s + 3u];
+                    if (st == PPE_FS_EMPTY) stop = true;
+                    else if ((st & PPE_FS_PEND) && rec_match(rec[st & ~PPE_FS_PEND], r)) {
+                        found = s;
+                        stop = true;
+                    }
+                }
+                g = (g + 1u) & a.f.gmask;
+            }
+            a.f.rslot[p] = found;
+            is_new = found != PPE_FLOW_NONE && a.f.creator[found] == p;
+        }
+        const uint64_t bn = __builtin_amdgcn_ballot_w64(is_new);
+        if (w.lane == 0) a.f.tile_new[t] = bn;
+        creators += (uint32_t)__popcll(bn);
+    }
+    if (w.lane == 0 && creators)
+        __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_BATCH_NEW], (unsigned long long)creators, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One workgroup: if the batch's creators overflow the pool, rank them in packet order (tile counts, block scan)
+// and mark the ones past the free count revoked.
+__global__ __launch_bounds__(1024) void ppe_flow_revoke_kernel(ppe_flow_kargs a) {
+    __shared__ uint32_t part[1024];
+    const unsigned long long live = a.f.ctl[PPE_FCTL_LIVE], created = a.f.ctl[PPE_FCTL_BATCH_NEW];
+    if (live + created <= a.f.capacity) return;
+    const unsigned long long room = a.f.capacity > live ? a.f.capacity - live : 0ull;
+    const uint32_t tid = threadIdx.x, ntiles = (a.n + 63u) >> 6;
+    const uint32_t chunk = (ntiles + 1023u) / 1024u, lo = min(tid * chunk, ntiles), hi = min(lo + chunk, ntiles);
+    uint32_t cnt = 0;
+    for (uint32_t t = lo; t < hi; ++t)
+        if (a.f.tile_miss[t]) cnt += (uint32_t)__popcll(a.f.tile_new[t]);
+    part[tid] = cnt;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024u; o <<= 1) {  // inclusive scan
+        const uint32_t v = tid >= o ? part[tid - o] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    unsigned long long rank = part[tid] - cnt;
+    for (uint32_t t = lo; t < hi; ++t) {
+        uint64_t m = a.f.tile_miss[t] ? a.f.tile_new[t] : 0ull;
+        for (; m; m &= m - 1ull, ++rank) {
+            if (rank < room) continue;
+            const uint32_t p = (t << 6) + (uint32_t)__builtin_ctzll(m);
+            a.f.creator[a.f.rslot[p]] = p | PPE_FLOW_REVOKED;
+        }
+    }
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs a) {
+    __shared__ uint32_t bins[PPE_NBINS];
+    __shared__ uint32_t lcnt[32];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < PPE_NBINS; i += BLOCK) bins[i] = 0;
+    if (tid < 32u) lcnt[tid] = 0;
+    __syncthreads();
+    const TileWalk w = TileWalk::make<BLOCK>(a.n);
+    const uint4 *rec = (const uint4 *)a.f.rec;
+    const uint64_t act_table = make_act_table(a.unsup_fw);
+    uint32_t created = 0, revoked = 0;
+    for (uint32_t t = w.gw; t < w.ntiles; t += w.W) {
+        const uint64_t mask = a.f.tile_miss[t];
+        if (!mask) continue;
+        const uint32_t p = (t << 6) + w.lane;
+        const bool valid = p < a.n;
+        const uint32_t v = valid ? a.verdict[p] : 0u;
+        uint32_t act = (v >> 8) & 0xffu;
+        bool is_new = false, is_rev = false;
+        if ((mask >> w.lane) & 1ull) {
+            const uint4 r = rec[p];
+            const uint32_t prov = (r.w >> 8) & 0xffu;
+            uint32_t st = prov, flags = v >> 16;
+            const uint32_t s = a.f.rslot[p];
+            if (s != PPE_FLOW_NONE) {
+                const uint32_t cw = a.f.creator[s];
+                const bool rev = (cw & PPE_FLOW_REVOKED) != 0u;
+                const uint32_t c = cw & ~PPE_FLOW_REVOKED;
+                if (p == c) {
+                    if (rev) {  // FlowAdd: pool empty (flow.c:124-129); the claimed slot becomes a tombstone
+                        st = PPE_ST_FLOW_NOMEM;
+                        is_rev = true;
+                        a.f.keys[4ull * s + 3u] = PPE_FS_TOMB;
+                    } else {    // FlowAdd (flow.c:120-158), oriented as this packet, then FlowUpdate
+                        st = PPE_ST_ACL_FW;
+                        is_new = true;
+                        flags |= PPE_F_NEWFLOW | flow_account(a.f, s, r.x, r.z, r.x, r.z, a.len[p], a.now);
+                        ((uint4 *)a.f.keys)[s] = make_uint4(r.x, r.y, r.z, PPE_FS_LIVE(r.w & 0xffu));
+                    }
+                } else if (p > c) {
+                    if (rev) {
+                        if (prov == PPE_ST_ACL_FW) st = PPE_ST_FLOW_NOMEM;  // FlowAdd fails again, pool still empty
+                    } else {  // the flow was created earlier in this batch: found, no ACL lookup (flow.c:197-201)
+                        const uint4 rc = rec[c];
+                        st = PPE_ST_ACL_FW;
+                        flags = (flags & ~PPE_F_ACL) | flow_account(a.f, s, rc.x, rc.z, r.x, r.z, a.len[p], a.now);
+                        if (a.hit) a.hit[p] = -1;
+                    }
+                }
+            }
+            act = (uint32_t)(act_table >> (2u * st)) & 3u;
+            a.verdict[p] = st | (act << 8) | (flags << 16);
+            atomicAdd(&bins[st | ((flags & 7u) << 5)], 1u);
+        }
+        compact_tile(a.fw_idx, a.drop_idx, a.tile_cnt, a.n, 0u, t, w.lane, valid, act);
+        created += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(is_new));
+        revoked += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(is_rev));
+    }
+    if (w.lane == 0 && created) {
+        __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_LIVE], (unsigned long long)created, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_NEW_FLOW], (unsigned long long)created, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (w.lane == 0 && revoked)
+        __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_TOMBS], (unsigned long long)revoked, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    for (uint32_t b = tid; b < PPE_NBINS; b += BLOCK) {
+        const uint32_t c = bins[b];
+        if (c) {
+            for (uint32_t cb = bin_counters(b, act_table); cb; cb &= cb - 1u) atomicAdd(&lcnt[__builtin_ctz(cb)], c);
+        }
+    }
+    __syncthreads();
+    if (tid < PPE_C__COUNT && lcnt[tid])
+        __hip_atomic_fetch_add(&a.cslots[(size_t)blockIdx.x * PPE_CSLOT_WORDS + tid], (unsigned long long)lcnt[tid],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// FlowTimeOut + FlowAgeTimeoutCB (flow.c:391-467): live flows idle for more than `timeout` become tombstones.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ppe_flow_age_kernel(ppe_flow_kargs a) {
+    uint32_t del = 0;
+    for (uint32_t s = blockIdx.x * BLOCK + threadIdx.x; s < a.nslots; s += gridDim.x * BLOCK) {
+        const uint32_t st = a.f.keys[4ull * s + 3u];
+        if ((st & (PPE_FS_PEND | 0xffu)) != PPE_FS_LIVE(0u)) continue;
+        const uint64_t l = a.f.last[s];
+        if (a.now > l && a.now - l > a.timeout) {
+            a.f.keys[4ull * s + 3u] = PPE_FS_TOMB;
+            ((uint4 *)a.f.stats)[2ull * s] = make_uint4(0u, 0u, 0u, 0u);
+            ((uint4 *)a.f.stats)[2ull * s + 1u] = make_uint4(0u, 0u, 0u, 0u);
+            a.f.last[s] = 0;
+            ++del;
+        }
+    }
+    del = wave_sum(del);
+    if ((threadIdx.x & 63u) == 0 && del) {
+        __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_LIVE], 0ull - del, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_DEL_FLOW], (unsigned long long)del, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_TOMBS], (unsigned long long)del, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Rehash: every live flow of a.f into the empty table a.dst (tombstones dropped).  Inserters only look at slot
+// states (keys are distinct), so the state is claimed first and the rest of the slot written after.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ppe_flow_rehash_kernel(ppe_flow_kargs a) {
+    for (uint32_t s = blockIdx.x * BLOCK + threadIdx.x; s < a.nslots; s += gridDim.x * BLOCK) {
+        const uint4 k = ((const uint4 *)a.f.keys)[s];
+        if ((k.w & (PPE_FS_PEND | 0xffu)) != PPE_FS_LIVE(0u)) continue;
+        uint32_t g = key_hash(k.x, k.y, k.z, (k.w >> 8) & 0xffu) & a.dst.gmask;
+        bool done = false;
+#pragma unroll 1
+        for (uint32_t it = 0; it <= a.dst.gmask && !done; ++it) {
+#pragma unroll 1
+            for (uint32_t j = 0; j < 4u && !done; ++j) {
+                const uint32_t d = 4u * g + j;
+                uint32_t expect = PPE_FS_EMPTY;
+                if (__hip_atomic_compare_exchange_strong(a.dst.keys + 4ull * d + 3u, &expect, k.w, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    a.dst.keys[4ull * d] = k.x;
+                    a.dst.keys[4ull * d + 1u] = k.y;
+                    a.dst.keys[4ull * d + 2u] = k.z;
+                    ((uint4 *)a.dst.stats)[2ull * d] = ((const uint4 *)a.f.stats)[2ull * s];
+                    ((uint4 *)a.dst.stats)[2ull * d + 1u] = ((const uint4 *)a.f.stats)[2ull * s + 1u];
+                    a.dst.last[d] = a.f.last[s];
+                    done = true;
+                }
+            }
+            g = (g + 1u) & a.dst.gmask;
+        }
+    }
+}
+
 // ACL-only lookup over pre-decoded tuples (the DP_Acl_Lookup(mbuf) entry, dataplane/src/flow/flow.c:232):
 // tuple = {sip, dip, sport | dport << 16, proto}, macs = {dmac lo, dmac hi, smac lo, smac hi} (optional).
 template <int MODE>
@@ -733,17 +1115,24 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
 }  // namespace
 
 template <int M, int P, int B>
-static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                    int flow) {
     // hipExtLaunchKernelGGL's events are the dispatch packet's own start/end timestamps (what rocprofv3 reports),
     // unlike hipEventRecord markers around the launch
-    hipExtLaunchKernelGGL((ppe_classify_kernel<M, P, B>), dim3(grid), dim3(B), shmem, s, e0, e1, 0, *a);
+    if (flow) {  // the flow-table variant is built for the default tile fetch only
+        hipExtLaunchKernelGGL((ppe_classify_kernel<M, PF_HOIST, B, true>), dim3(grid), dim3(B), shmem, s, e0, e1, 0,
+                              *a);
+    } else {
+        hipExtLaunchKernelGGL((ppe_classify_kernel<M, P, B, false>), dim3(grid), dim3(B), shmem, s, e0, e1, 0, *a);
+    }
     return (int)hipGetLastError();
 }
 
 template <int M, int P, int B>
 static int occ_t(size_t shmem) {
     int nb = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, P, B>, B, shmem) == hipSuccess
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, P, B, false>, B, shmem) ==
+                   hipSuccess
                ? nb : -1;
 }
 
@@ -771,12 +1160,27 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int block) {
         PPE_DISPATCH_P(FN, IMG_GLOBAL, __VA_ARGS__);                 \
     } while (0)
 
-extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, void *stream,
-                                   void *ev_start, void *ev_stop) {
+extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, int flow,
+                                   void *stream, void *ev_start, void *ev_stop) {
     const size_t shmem = classify_shmem(a->lds_words, mode, block);
     hipStream_t s = (hipStream_t)stream;
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
-    PPE_DISPATCH(launch_t, a, grid, shmem, s, e0, e1);
+    PPE_DISPATCH(launch_t, a, grid, shmem, s, e0, e1, flow);
+}
+
+extern "C" int ppe_launch_flow(int kind, const ppe_flow_kargs *a, uint32_t grid, void *stream) {
+    const hipStream_t s = (hipStream_t)stream;
+    const dim3 g(grid), b(PPE_FLOW_BLOCK);
+    switch (kind) {
+        case PPE_FLOW_K_CLAIM: hipLaunchKernelGGL(ppe_flow_claim_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
+        case PPE_FLOW_K_RESOLVE: hipLaunchKernelGGL(ppe_flow_resolve_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
+        case PPE_FLOW_K_REVOKE: hipLaunchKernelGGL(ppe_flow_revoke_kernel, dim3(1), dim3(1024), 0, s, *a); break;
+        case PPE_FLOW_K_FINALIZE: hipLaunchKernelGGL(ppe_flow_finalize_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
+        case PPE_FLOW_K_AGE: hipLaunchKernelGGL(ppe_flow_age_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
+        case PPE_FLOW_K_REHASH: hipLaunchKernelGGL(ppe_flow_rehash_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
 }
 
 // resident workgroups per CU for the kernel variant (the persistent grid is sized to exactly fill the chip)

@@ -20,10 +20,11 @@ PPE_OK = 0
 ST = dict(ACL_FW=0, ACL_DROP=1, L2_HEADER_ERR=2, L2_UNSUPPORT=3, VLAN_HEADER_ERR=4, VLAN_LAYER_EXCEED=5,
           VLAN_UNSUPPORT=6, IPV4_HEADER_ERR=7, IPV4_VERSION_ERR=8, IPV4_LEN_ERR=9, FRAG_LEN_ERR=10, FRAG=11,
           IPV4_UNSUPPORT=12, UDP_HEADER_ERR=13, UDP_LEN_ERR=14, TCP_HEADER_ERR=15, TCP_LEN_ERR=16,
-          FLOW_TCP_NO_SYN_FIRST=17, WINDOW_PUNT=18)
+          FLOW_TCP_NO_SYN_FIRST=17, WINDOW_PUNT=18, FLOW_NOMEM=19)
 ST_NAME = {v: k for k, v in ST.items()}
 ACT_FW, ACT_DROP, ACT_PUNT = 0, 1, 2
 F_VLAN, F_L4, F_TCP, F_SYN, F_ACL, F_FRAG = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
+F_FLOW, F_TOCLIENT, F_NEWFLOW = 0x40, 0x80, 0x100
 COUNTERS = ["l2_headerlen_err", "l2_unsupport", "l2_rx_ok",
             "vlan_headerlen_err", "vlan_layer_exceed", "vlan_unsupport", "vlan_rx_ok",
             "ipv4_headerlen_err", "ipv4_version_err", "ipv4_pktlen_err", "ipv4_unsupport", "ipv4_rx_ok",
@@ -32,7 +33,7 @@ COUNTERS = ["l2_headerlen_err", "l2_unsupport", "l2_rx_ok",
             "tcp_headerlen_err", "tcp_pktlen_err", "tcp_rx_ok",
             "acl_drop", "acl_fw",
             "flow_proc_ok", "flow_proc_fail", "flow_tcp_no_syn_first",
-            "out_fw", "out_drop", "out_punt", "window_punt", "pkts"]
+            "out_fw", "out_drop", "out_punt", "window_punt", "pkts", "flow_node_nomem"]
 ACL_RULE_ACTION_FW, ACL_RULE_ACTION_DROP = 0, 1
 RULE_ENTRY_MAX = 10000
 
@@ -87,6 +88,23 @@ class Tuning(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class FlowInfo(C.Structure):
+    _fields_ = [("live", C.c_uint64), ("new_flow", C.c_uint64), ("del_flow", C.c_uint64), ("capacity", C.c_uint32),
+                ("max_batch", C.c_uint32), ("slots", C.c_uint32), ("tombstones", C.c_uint32), ("rehashes", C.c_uint32),
+                ("pad", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
+# ppe_flow_entry_t (include/ppe_hip.h), 64 bytes
+FLOW_ENTRY_DTYPE = np.dtype([("sip", "<u4"), ("dip", "<u4"), ("sport", "<u2"), ("dport", "<u2"), ("protocol", "u1"),
+                             ("pad", "u1", 3), ("flowflags", "<u4"), ("slot", "<u4"), ("pktcnts2d", "<u8"),
+                             ("pktcntd2s", "<u8"), ("bytecnts2d", "<u8"), ("bytecntd2s", "<u8"),
+                             ("last_seen", "<u8")])
+assert FLOW_ENTRY_DTYPE.itemsize == 64
+
+
 class Tuples(C.Structure):
     _fields_ = [("tuple", C.c_void_p), ("macs", C.c_void_p), ("ts", C.c_void_p), ("n", C.c_uint32)]
 
@@ -99,7 +117,8 @@ EXPORTS = [
     "ppe_host_alloc", "ppe_host_free", "ppe_memcpy_h2d", "ppe_memcpy_d2h", "ppe_memset_d", "ppe_sync",
     "ppe_counters_read", "ppe_counters_clear", "ppe_timing_enable", "ppe_timing_read", "ppe_acl_image",
     "ppe_launch_info", "ppe_debug_trace", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
-    "ppe_get_tuning",
+    "ppe_get_tuning", "ppe_flow_create", "ppe_flow_destroy", "ppe_classify_flow", "ppe_flow_age", "ppe_flow_info",
+    "ppe_flow_clear_stat", "ppe_flow_dump",
     # ppe_acl.h
     "ppe_rule_list_init", "ppe_rule_list_free", "Rule_add", "Rule_del_by_id", "Rule_del_all",
     "Rule_duplicate_check", "Rule_Load_Line", "ppe_rule_load_file", "DP_Acl_Rule_Init", "DP_Acl_Load_Rule",
@@ -168,6 +187,13 @@ def _open(p: Path, mode) -> C.CDLL:
         "ppe_acl_build_image": ([vp, vp, u32, u32, u32, C.POINTER(C.POINTER(u32)), C.POINTER(u32),
                                  C.POINTER(AclStats)], C.c_int),
         "ppe_acl_free_image": ([C.POINTER(u32)], None),
+        "ppe_flow_create": ([vp, u32, u32], C.c_int),
+        "ppe_flow_destroy": ([vp], C.c_int),
+        "ppe_classify_flow": ([vp, C.POINTER(Batch), C.POINTER(Result), C.POINTER(Cfg), vp], C.c_int),
+        "ppe_flow_age": ([vp, u64, u64, C.POINTER(u64)], C.c_int),
+        "ppe_flow_info": ([vp, C.POINTER(FlowInfo)], C.c_int),
+        "ppe_flow_clear_stat": ([vp], C.c_int),
+        "ppe_flow_dump": ([vp, vp, u32, C.POINTER(u32)], C.c_int),
         "ppe_rule_list_init": ([], C.c_int),
         "ppe_rule_list_free": ([], None),
         "Rule_add": ([vp, C.POINTER(u32)], C.c_int),

@@ -117,6 +117,48 @@ class Engine:
         self._check(rc, "ppe_classify_host")
         return res
 
+    # ---- flow table (ppe_flow_*, dataplane/src/flow/flow.c) ----
+    def flow_create(self, capacity: int = 0, max_batch: int = 0):
+        self._check(self.lib.ppe_flow_create(self.ctx, int(capacity), int(max_batch)), "ppe_flow_create")
+
+    def flow_destroy(self):
+        self._check(self.lib.ppe_flow_destroy(self.ctx), "ppe_flow_destroy")
+
+    def classify_flow_torch(self, hdr, lens, out: dict, cfg: abi.Cfg | None = None, ts=None, stream=None):
+        """ppe_classify_flow on tensors of this engine's GPU (same `out` convention as classify_torch)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        ptrs = {k: (v.data_ptr() if v is not None else None) for k, v in out.items()}
+        if ptrs.get("part_idx"):
+            ptrs["fw_idx"] = ptrs["drop_idx"] = ptrs.pop("part_idx")
+        b = abi.Batch(hdr.data_ptr(), lens.data_ptr(), ts.data_ptr() if ts is not None else None, lens.numel(),
+                      hdr.shape[1])
+        r = abi.Result(ptrs.get("verdict"), ptrs.get("flow_hash"), ptrs.get("acl_hit"), ptrs.get("fw_idx"),
+                       ptrs.get("drop_idx"), ptrs.get("tile_cnt"), ptrs.get("tuple"))
+        self._check(self.lib.ppe_classify_flow(self.ctx, C.byref(b), C.byref(r), C.byref(cfg or self.cfg()),
+                                               s.cuda_stream), "ppe_classify_flow")
+
+    def flow_age(self, now: int, timeout: int = 20) -> int:
+        d = C.c_uint64(0)
+        self._check(self.lib.ppe_flow_age(self.ctx, int(now), int(timeout), C.byref(d)), "ppe_flow_age")
+        return d.value
+
+    def flow_info(self) -> dict:
+        fi = abi.FlowInfo()
+        self._check(self.lib.ppe_flow_info(self.ctx, C.byref(fi)), "ppe_flow_info")
+        return fi.as_dict()
+
+    def flow_clear_stat(self):
+        self._check(self.lib.ppe_flow_clear_stat(self.ctx), "ppe_flow_clear_stat")
+
+    def flow_dump(self) -> np.ndarray:
+        n = C.c_uint32(0)
+        self._check(self.lib.ppe_flow_dump(self.ctx, None, 0, C.byref(n)), "ppe_flow_dump")
+        out = np.zeros(n.value, abi.FLOW_ENTRY_DTYPE)
+        if n.value:
+            self._check(self.lib.ppe_flow_dump(self.ctx, out.ctypes.data, n.value, C.byref(n)), "ppe_flow_dump")
+        return out
+
     def acl_lookup_host(self, tuple_: np.ndarray, macs: np.ndarray | None = None, ts: np.ndarray | None = None,
                         now_seconds: int = 0):
         tuple_ = np.ascontiguousarray(tuple_, dtype=np.uint32)

@@ -184,6 +184,38 @@ def make_packets(n: int, rules: np.ndarray, seed: int = SEED + 1, kind: str = "u
     return dict(hdr=hdr, len=lens, ts=ts, kinds=kinds)
 
 
+def make_flow_packets(n: int, rules: np.ndarray, n_flows: int, seed: int = SEED + 3, kind: str = "udp64",
+                      stride: int = 64, rev_frac: float = 0.4, syn_frac: float = 0.3, tcp_frac: float | None = None,
+                      malformed_frac: float = 0.0):
+    """Stateful traffic for the flow table: n packets drawn uniformly from n_flows flow templates (make_packets
+    tuples), each sent in the reverse direction (addresses and ports swapped) with probability rev_frac; TCP packets
+    carry SYN with probability syn_frac, else ACK (so syn_check drops some first packets).  Same dict as
+    make_packets, plus flow=(n,) template index."""
+    base = make_packets(n_flows, rules, seed=seed, kind=kind, stride=stride, malformed_frac=0.0, tcp_frac=tcp_frac)
+    rng = np.random.default_rng(seed ^ 0xF10)
+    idx = rng.integers(0, n_flows, n)
+    hdr = base["hdr"][idx].copy()
+    lens = base["len"][idx].copy()
+    rows = np.arange(n)
+    l3 = np.where(hdr[:, 12] == 0x81, 18, 14)
+    l4 = l3 + 20
+    rev = rows[rng.random(n) < rev_frac]
+    for a, b, w in ((12, 16, 4), (20, 22, 2)):  # sip <-> dip, sport <-> dport (offsets from L3)
+        for k in range(w):
+            x = hdr[rev, l3[rev] + a + k].copy()
+            hdr[rev, l3[rev] + a + k] = hdr[rev, l3[rev] + b + k]
+            hdr[rev, l3[rev] + b + k] = x
+    t = rows[hdr[rows, l3 + 9] == 6]
+    hdr[t, l4[t] + 13] = np.where(rng.random(len(t)) < syn_frac, 0x02, 0x10)
+    kinds = np.full(n, -1, np.int16)
+    if malformed_frac > 0:
+        bad = np.nonzero(rng.random(n) < malformed_frac)[0]
+        kinds[bad] = rng.integers(0, N_MALFORMED_KINDS, len(bad))
+        for i in bad:
+            _malform(hdr, lens, int(i), int(kinds[i]), rng, stride)
+    return dict(hdr=hdr, len=lens, ts=None, kinds=kinds, flow=idx)
+
+
 def _set16(h, off, v):
     h[off] = (v >> 8) & 0xFF
     h[off + 1] = v & 0xFF

@@ -1,0 +1,181 @@
+"""GPU parity of the stateful flow table (ppe_classify_flow / ppe_flow_age / ppe_flow_dump) against the oracle's
+sequential FlowHandlePacket (tests/test_oracle_flow.py pins the oracle to dataplane/src/flow/flow.c).
+
+Bar: bit-exact per-packet verdict, flow hash, ACL hit, compacted lists and counters, and the same table (key,
+per-direction packet / byte counters, last-seen time) after every batch and aging step."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import torch  # noqa: E402
+
+import pyoracle  # noqa: E402
+from ppe import Engine, abi, synth  # noqa: E402
+from test_gpu_parity import check_compaction, check_partition  # noqa: E402
+
+DEV = torch.device("cuda:0")
+NOW = 1_000_000
+
+
+def gpu_flow(eng, hdr, lens, now, syn_check=1, part=False):
+    n = len(lens)
+    th = torch.from_numpy(np.ascontiguousarray(hdr)).to(DEV)
+    tl = torch.from_numpy(np.ascontiguousarray(lens, np.uint32).view(np.int32)).to(DEV)
+    names = ("verdict", "flow_hash", "acl_hit") + (("part_idx",) if part else ("fw_idx", "drop_idx", "tile_cnt"))
+    out = {k: torch.full(((n + 63) // 64,) if k == "tile_cnt" else (n,), -7, dtype=torch.int32, device=DEV)
+           for k in names}
+    eng.classify_flow_torch(th, tl, out, cfg=eng.cfg(0, syn_check, now))
+    torch.cuda.synchronize()
+    return {k: (v.cpu().numpy() if k == "acl_hit" else v.cpu().numpy().view(np.uint32)) for k, v in out.items()}
+
+
+def table(d):
+    """order-independent view of a flow dump"""
+    cols = ("sip", "dip", "sport", "dport", "protocol", "pktcnts2d", "pktcntd2s", "bytecnts2d", "bytecntd2s",
+            "last_seen")
+    rows = sorted(tuple(int(x) for x in r) for r in zip(*(d[c] for c in cols)))
+    return rows
+
+
+class Pair:
+    """The HIP flow table and the oracle's, fed the same batches."""
+
+    def __init__(self, eng, rules, capacity, max_batch, default_action=0):
+        self.eng = eng
+        eng.commit(rules, default_action=default_action)
+        eng.flow_create(capacity, max_batch)
+        eng.clear_counters()
+        self.o = pyoracle.Oracle(rules, default_action=default_action)
+        self.ft = pyoracle.OracleFlow(self.o, capacity=capacity)
+        self.counters = np.zeros(32, np.uint64)
+
+    def batch(self, hdr, lens, now, syn_check=1, part=False):
+        got = gpu_flow(self.eng, hdr, lens, now, syn_check, part)
+        ref = self.ft.classify_batch(hdr, lens, cfg=self.o.cfg(0, syn_check, now))
+        for k in ("verdict", "flow_hash", "acl_hit"):
+            if not np.array_equal(got[k], ref[k]):
+                bad = np.nonzero(got[k] != ref[k])[0]
+                raise AssertionError(f"{k}: {len(bad)} mismatches, first {bad[:5].tolist()}: "
+                                     f"gpu={got[k][bad[:5]].tolist()} ref={ref[k][bad[:5]].tolist()}")
+        if part:
+            check_partition(got, len(lens))
+        else:
+            check_compaction(got, len(lens))
+        self.counters += ref["counters"]
+        cnt = self.eng.counters()
+        assert [cnt[c] for c in abi.COUNTERS] == self.counters[:len(abi.COUNTERS)].tolist()
+        return got, ref
+
+    def same_table(self):
+        assert table(self.eng.flow_dump()) == table(self.ft.dump())
+        info, st = self.eng.flow_info(), self.ft.stats()
+        assert (info["live"], info["new_flow"], info["del_flow"]) == (st["live"], st["new_flow"], st["del_flow"])
+        return info
+
+    def close(self):
+        self.eng.flow_destroy()
+        self.ft.close()
+
+
+@pytest.fixture(scope="module")
+def eng():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("kind,stride", [("udp64", 64), ("imix", 128)])
+def test_flow_batches_parity(eng, kind, stride):
+    """Several batches over a shared flow population: misses, in-batch creation, hits in both directions, syn_check,
+    ACL drops, malformed packets; the table is compared after every batch."""
+    rules = synth.make_rules(256, seed=21)
+    p = Pair(eng, rules, capacity=100000, max_batch=1 << 16, default_action=0)
+    try:
+        for b in range(4):
+            pk = synth.make_flow_packets(40000, rules, n_flows=6000, seed=100 + b if b < 2 else 100, kind=kind,
+                                         stride=stride, malformed_frac=0.01)
+            # batches 0 and 2 share the template seed, so batch 2 revisits batch 0's flows
+            got, _ = p.batch(pk["hdr"], pk["len"], NOW + b, part=(b % 2 == 1))
+            p.same_table()
+        v = got["verdict"]
+        assert ((v >> 16) & abi.F_FLOW).any() and ((v >> 16) & abi.F_TOCLIENT).any()
+    finally:
+        p.close()
+
+
+def test_flow_pool_exhaustion(eng):
+    """More new flows than the pool holds, within one batch and across batches: the creators past the free count
+    (in packet order) fail with FLOW_NOMEM, exactly as one core running the batch in order."""
+    rules = synth.make_rules(64, seed=22)
+    p = Pair(eng, rules, capacity=700, max_batch=1 << 14, default_action=0)
+    try:
+        for b in range(3):
+            pk = synth.make_flow_packets(12000, rules, n_flows=2000, seed=200 + b, syn_frac=0.8)
+            got, ref = p.batch(pk["hdr"], pk["len"], NOW + b)
+            p.same_table()
+        assert ((ref["verdict"] & 0xFF) == abi.ST["FLOW_NOMEM"]).any()
+        assert p.eng.counters()["flow_node_nomem"] > 0
+    finally:
+        p.close()
+
+
+def test_flow_aging_and_rehash(eng):
+    """Age flows out batch after batch (ppe_flow_age vs FlowAgeTimeoutCB) until the tombstones force rehashes; the
+    table stays equal to the oracle's throughout."""
+    rules = synth.make_rules(32, seed=23)
+    p = Pair(eng, rules, capacity=2000, max_batch=4096, default_action=0)
+    try:
+        now = NOW
+        for b in range(12):
+            pk = synth.make_flow_packets(4096, rules, n_flows=1500, seed=300 + b, syn_frac=0.9)
+            p.batch(pk["hdr"], pk["len"], now)
+            now += 15
+            d_gpu = p.eng.flow_age(now, 20)
+            d_ref = p.ft.age(now, 20)
+            assert d_gpu == d_ref
+            info = p.same_table()
+        assert info["del_flow"] > 0 and info["rehashes"] >= 1
+    finally:
+        p.close()
+
+
+def test_flow_known_answers(eng):
+    """The oracle's known-answer sequences (test_oracle_flow.py) through the HIP path."""
+    from pktbuild import tcp_packet, udp_packet
+    from test_oracle_flow import batch, rule
+    A, B = 0x0A000001, 0x0A000002
+    rules = rule(action=1, sip=B, sip_mask=32, dip=A, dip_mask=32)
+    p = Pair(eng, rules, capacity=2, max_batch=64, default_action=0)
+    try:
+        fwd = udp_packet(sip=A, dip=B, sport=1234, dport=80)
+        rev = udp_packet(sip=B, dip=A, sport=80, dport=1234)
+        seqs = [[rev, rev, fwd, rev, fwd], [tcp_packet(flags=0x10), tcp_packet(flags=0x02), tcp_packet(flags=0x10)],
+                [udp_packet(sport=7, dport=7), udp_packet(sport=8), udp_packet(sport=9)]]
+        for i, s in enumerate(seqs):
+            h, l = batch(s)
+            p.batch(h, l, NOW + i)
+            p.same_table()
+    finally:
+        p.close()
+
+
+def test_flow_argument_errors(eng):
+    import ctypes as C
+    lib = eng.lib
+    b = abi.Batch(None, None, None, 0, 64)
+    r = abi.Result(None, None, None, None, None, None, None)
+    eng.flow_destroy()
+    assert lib.ppe_classify_flow(eng.ctx, C.byref(b), C.byref(r), C.byref(eng.cfg()), None) == -22  # no table
+    eng.flow_create(100, 128)
+    th = torch.zeros((256, 64), dtype=torch.uint8, device=DEV)
+    tl = torch.full((256,), 64, dtype=torch.int32, device=DEV)
+    v = torch.zeros(256, dtype=torch.int32, device=DEV)
+    b = abi.Batch(th.data_ptr(), tl.data_ptr(), None, 256, 64)
+    r = abi.Result(v.data_ptr(), None, None, None, None, None, None)
+    assert lib.ppe_classify_flow(eng.ctx, C.byref(b), C.byref(r), C.byref(eng.cfg()), None) == -22  # n > max_batch
+    r = abi.Result(None, None, None, None, None, None, None)
+    b.n = 64
+    assert lib.ppe_classify_flow(eng.ctx, C.byref(b), C.byref(r), C.byref(eng.cfg()), None) == -22  # no verdict
+    eng.flow_destroy()

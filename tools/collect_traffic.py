@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--cal-fetch", required=True)
     ap.add_argument("--cal-write", required=True)
-    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--n", type=int, default=1 << 20, help="packets per classify dispatch")
+    ap.add_argument("--cal-n", type=int, default=1 << 20, help="packets per calibration-kernel dispatch")
     ap.add_argument("--cal-kernel", default="k_row<true>")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
@@ -35,9 +36,9 @@ def main():
     w = statistics.median(per_dispatch(a.write, "ppe_classify_kernel", "WRITE_SIZE"))
     cf = statistics.median(per_dispatch(a.cal_fetch, a.cal_kernel, "FETCH_SIZE"))
     cw = statistics.median(per_dispatch(a.cal_write, a.cal_kernel, "WRITE_SIZE"))
-    cal_rd, cal_wr = n * 68, n * 16  # skeleton: 64-B window + 4-B length read, 4 x 4-B results written
+    cal_rd, cal_wr = a.cal_n * 68, a.cal_n * 16  # skeleton: 64-B window + 4-B length read, 4 x 4-B results written
     kr, kw = cal_rd / cf, cal_wr / cw  # bytes per counter unit for this access pattern
-    alg_rd, alg_wr = n * 68, n * 16 + ((n + 63) // 64) * 4
+    alg_rd, alg_wr = n * 68, n * 16  # partition-layout list: no tile counts
     out = {"n_packets": n, "fetch_size_raw": f, "write_size_raw": w, "calib": {"fetch_raw": cf, "write_raw": cw,
            "bytes_per_fetch_unit": kr, "bytes_per_write_unit": kw, "kernel": a.cal_kernel},
            "read_bytes": f * kr, "write_bytes": w * kw, "traffic_bytes": f * kr + w * kw,
