@@ -74,6 +74,8 @@ def main():
     torch.cuda.set_device(dev)
 
     cfgd = synth.CONFIGS[args.config]
+    if "flows" in cfgd:
+        return run_flow(args, cfgd, dev, world, rank, dist)
     n = args.n or cfgd["n"]
     stride = args.stride
     rules = synth.make_rules(cfgd["rules"])
@@ -268,7 +270,7 @@ def main():
     tfiles = sorted(Path(__file__).resolve().parent.glob(f"profiles/*traffic_{args.config}.json"))
     if tfiles and n == cfgd["n"] and stride == 64:
         tj = json.load(open(tfiles[-1]))
-        if tj.get("n_packets") == n:
+        if tj.get("n_packets") == n * GROUP:  # per launch of GROUP batches
             traffic = round(tj["traffic_bytes"])
 
     if rank == 0:
@@ -293,6 +295,164 @@ def main():
             "parity_sample_ok": parity,
             "acl": {k: acl[k] for k in ("n_rules", "n_nodes", "max_depth", "blob_bytes", "lds_resident")},
             "launch": li,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+FLOW_METRIC = "Mpps device-resident decode+flow-table+ACL classify (stateful FlowHandlePacket)"
+
+
+def flow_bytes(stride: int) -> float:
+    """Algorithmic bytes per packet of the flow-mode classify kernel on the hit path: the stateless kernel's 84 B
+    (window + length read; verdict, hash, hit, partition entry written) plus the flow slot's 16-B key read, its
+    16-B direction counters read and written (two 8-B atomics) and the 8-B last-seen store, and the 8-B tile mask
+    per 64 packets."""
+    rd, wr = algorithmic_bytes(stride)
+    return rd + wr + 16.0 + 32.0 + 8.0 + 8.0 / 64.0
+
+
+def run_flow(args, cfgd, dev, world, rank, dist):
+    """--config F1: ppe_classify_flow batch after batch (one stream: each batch sees the table the previous ones
+    left) over a fixed population of bidirectional flows established during the warmup."""
+    import ctypes as C
+    from ppe import abi
+    n = args.n or cfgd["n"]
+    stride = args.stride
+    rules = synth.make_rules(cfgd["rules"])
+    flows = cfgd["flows"]
+    nbufs = args.nbufs or 8
+    eng = Engine(int(os.environ.get("LOCAL_RANK", "0")))
+    acl = eng.commit(rules, default_action=abi.ACL_RULE_ACTION_FW)
+    tseed = synth.SEED + 977 * (rank + 1)  # this rank's flow population (flow-hash sharding: disjoint per GPU)
+
+    # parity sample first: a fresh table, four 64k batches, against the oracle's sequential flow table
+    parity = None
+    if rank == 0:
+        import pyoracle
+        m = 1 << 16
+        eng.flow_create(2 * flows, m)
+        o = pyoracle.Oracle(rules, default_action=abi.ACL_RULE_ACTION_FW)
+        ft = pyoracle.OracleFlow(o, capacity=2 * flows)
+        ok = True
+        for b in range(4):
+            pk = synth.make_flow_packets(m, rules, flows // 16, seed=tseed + 31 * b, template_seed=tseed, stride=stride)
+            th = torch.from_numpy(pk["hdr"]).to(dev)
+            tl = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
+            out = {k: torch.empty(m, dtype=torch.int32, device=dev) for k in ("verdict", "flow_hash", "acl_hit")}
+            eng.classify_flow_torch(th, tl, out, cfg=eng.cfg(now_seconds=NOW + b))
+            ref = ft.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW + b))
+            torch.cuda.synchronize()
+            for k in ("verdict", "flow_hash", "acl_hit"):
+                g = out[k].cpu().numpy()
+                ok = ok and np.array_equal(g if k == "acl_hit" else g.view(np.uint32), ref[k])
+        parity = bool(ok and len(eng.flow_dump()) == ft.stats()["live"])
+        ft.close()
+
+    eng.flow_create(2 * flows, n)
+    bufs = []
+    for b in range(nbufs):
+        pk = synth.make_flow_packets(n, rules, flows, seed=tseed + 7919 * (b + 1), template_seed=tseed, stride=stride)
+        hdr = torch.from_numpy(pk["hdr"]).to(dev)
+        lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
+        out = torch.empty((3, n), dtype=torch.int32, device=dev)
+        part = torch.empty(n, dtype=torch.int32, device=dev)
+        bufs.append((hdr, lens, out, part, pk if b == 0 else None))
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    sptr = C.c_void_p(stream.cuda_stream)
+    calls = []
+    for hdr, lens, out, part, _ in bufs:
+        bb = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, stride)
+        rr = abi.Result(out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), part.data_ptr(), part.data_ptr(),
+                        None, None)
+        calls.append((bb, rr))
+    cfgs = [eng.cfg(now_seconds=NOW + i) for i in range(args.warmup + 2 * args.steps + 1)]
+    fn = eng.lib.ppe_classify_flow
+
+    def step(i):
+        bb, rr = calls[i % nbufs]
+        rc = fn(eng.ctx, C.byref(bb), C.byref(rr), C.byref(cfgs[i]), sptr)
+        if rc:
+            raise RuntimeError(f"ppe_classify_flow failed: {rc}")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(max(args.warmup, 1)):
+        step(i)
+    eng.clear_counters()
+    new0 = eng.flow_info()["new_flow"]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(args.warmup + i)
+    ev1.record(stream)
+    barrier()
+    my_ms = max(ev0.elapsed_time(ev1), 1e-9)
+    cnt = eng.counters()
+    new_timed = eng.flow_info()["new_flow"] - new0
+    # the classify (FlowFind) kernel alone: HIP-event dispatch timestamps of the same launches
+    eng.timing(True)
+    eng.timing_read(reset=True)
+    for i in range(args.steps):
+        step(args.warmup + args.steps + i)
+    kern_ms, launches = eng.timing_read(reset=True)
+    eng.timing(False)
+    info = eng.flow_info()
+    if dist is not None:
+        t = torch.tensor([my_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        my_ms = float(t.item())
+    mpps = n * args.steps * world / (my_ms / 1e3) / 1e6
+    kern_avg_ms = kern_ms / max(launches, 1)
+    bpp = flow_bytes(stride)
+    achieved = bpp * n / (kern_avg_ms / 1e3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import pyoracle
+        pk = bufs[0][4]
+        o = pyoracle.Oracle(rules, default_action=abi.ACL_RULE_ACTION_FW, image=eng.image())
+        ft = pyoracle.OracleFlow(o, capacity=2 * flows)
+        ft.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), use_tree=True)  # establish the flows
+        reps, tc = 0, time.perf_counter()
+        while time.perf_counter() - tc < args.cpu_seconds:
+            ft.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW + 1 + reps), use_tree=True)
+            reps += 1
+        cpu_s = time.perf_counter() - tc
+        ft.close()
+        cpu = {"value": n * reps / cpu_s / 1e6, "unit": "Mpps", "cores": 1, "kind": "port",
+               "sample": f"{reps} passes of one core's flow table (oracle FlowHandlePacket, tree-walk ACL) over the "
+                         f"{n}-packet batch after the flows were established ({n * reps} packets, {cpu_s:.1f} s); the "
+                         f"reference keeps one table per core, so cores scale it by flow-hash sharding"}
+
+    if rank == 0:
+        line = {
+            "metric": FLOW_METRIC, "value": round(mpps, 2), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(my_ms / args.steps, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"{args.config}: {n} x 64B IPv4/UDP packets per GPU per batch over {flows} "
+                                   f"bidirectional flows, {cfgd['rules']} five-tuple ACL rules, default FW",
+                       "packets_per_gpu": n, "flows": flows, "rules": cfgd["rules"], "resident_batches": nbufs,
+                       "parallelism": f"flow-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "ppe_classify_kernel<FLOW> (FlowFind + accounting; misses resolved by the flow "
+                                   "kernels)",
+                         "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": bpp,
+                         "batch_avg_us": round(my_ms / args.steps * 1e3, 3)},
+            "cpu_baseline": cpu,
+            "parity_sample_ok": parity,
+            "flow_table": info,
+            "new_flows_in_timed_region": new_timed,
+            "counters": {k: cnt[k] for k in ("pkts", "acl_fw", "acl_drop", "flow_proc_ok", "flow_proc_fail",
+                                             "flow_node_nomem")},
         }
         print(json.dumps(line), flush=True)
     eng.close()

@@ -49,15 +49,17 @@ struct HostStage {
 // Device flow table (ppe_classify_flow) and what the host knows about it without synchronising.
 struct FlowArrays {
     uint32_t *keys = nullptr, *creator = nullptr;
-    unsigned long long *stats = nullptr, *last = nullptr;
+    unsigned long long *stats = nullptr, *packed = nullptr, *last = nullptr;
 };
 struct FlowTable {
     uint32_t capacity = 0, max_batch = 0, nslots = 0;
     FlowArrays arr[2];  // arr[cur] in use; the other is the rehash target (allocated on first rehash)
     int cur = 0;
     unsigned long long *ctl = nullptr;
-    uint32_t *rec = nullptr, *rslot = nullptr;
+    uint32_t *rec = nullptr, *rslot = nullptr, *miss_tiles = nullptr;
     unsigned long long *tile_miss = nullptr, *tile_new = nullptr;
+    uint64_t batches = 0;   // ppe_classify_flow calls (the parity selects the miss-tile counter)
+    unsigned long long fold_pkts = PPE_PK_FOLD_PKTS, fold_bytes = PPE_PK_FOLD_BYTES;
     uint64_t live_ub = 0;   // upper bound of live flows: a snapshot's count + n per batch since
     uint64_t tomb_ub = 0;   // upper bound of tombstones: a snapshot's count + n per batch that could revoke
     uint32_t rehashes = 0;
@@ -768,6 +770,7 @@ static void flow_free_arrays(FlowArrays &a) {
     (void)hipFree(a.keys);
     (void)hipFree(a.creator);
     (void)hipFree(a.stats);
+    (void)hipFree(a.packed);
     (void)hipFree(a.last);
     a = FlowArrays();
 }
@@ -778,6 +781,7 @@ static int flow_clear_arrays(ppe_ctx *c, FlowArrays &a, uint32_t nslots, hipStre
         if (hipMalloc(&a.keys, (size_t)nslots * 16u) != hipSuccess ||
             hipMalloc(&a.creator, (size_t)nslots * 4u) != hipSuccess ||
             hipMalloc(&a.stats, (size_t)nslots * 32u) != hipSuccess ||
+            hipMalloc(&a.packed, (size_t)nslots * 16u) != hipSuccess ||
             hipMalloc(&a.last, (size_t)nslots * 8u) != hipSuccess) {
             flow_free_arrays(a);
             return fail(c, PPE_ENOMEM, "flow table: out of device memory (%u slots)", nslots);
@@ -786,6 +790,7 @@ static int flow_clear_arrays(ppe_ctx *c, FlowArrays &a, uint32_t nslots, hipStre
     HIPCHK(c, hipMemsetAsync(a.keys, 0, (size_t)nslots * 16u, s));
     HIPCHK(c, hipMemsetAsync(a.creator, 0xff, (size_t)nslots * 4u, s));
     HIPCHK(c, hipMemsetAsync(a.stats, 0, (size_t)nslots * 32u, s));
+    HIPCHK(c, hipMemsetAsync(a.packed, 0, (size_t)nslots * 16u, s));
     HIPCHK(c, hipMemsetAsync(a.last, 0, (size_t)nslots * 8u, s));
     return PPE_OK;
 }
@@ -796,6 +801,11 @@ static ppe_flowdev flow_dev(const FlowTable &t, int which) {
     const FlowArrays &a = t.arr[which];
     d.keys = a.keys;
     d.stats = a.stats;
+    d.packed = a.packed;
+    d.miss_tiles = t.miss_tiles;
+    d.parity = (uint32_t)(t.batches & 1u);
+    d.fold_pkts = t.fold_pkts;
+    d.fold_bytes = t.fold_bytes;
     d.last = a.last;
     d.creator = a.creator;
     d.ctl = t.ctl;
@@ -862,6 +872,7 @@ int ppe_flow_destroy(ppe_ctx_t *c) {
     (void)hipFree(t->ctl);
     (void)hipFree(t->rec);
     (void)hipFree(t->rslot);
+    (void)hipFree(t->miss_tiles);
     (void)hipFree(t->tile_miss);
     (void)hipFree(t->tile_new);
     delete t;
@@ -882,6 +893,10 @@ int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
     c->flow = t;
     t->capacity = capacity;
     t->max_batch = max_batch;
+    // test hook: lower fold thresholds so the fold path runs on small inputs (values <= the defaults only)
+    const int fp = env_int("PPE_FLOW_FOLD_PKTS", 0), fb = env_int("PPE_FLOW_FOLD_BYTES", 0);
+    if (fp > 0 && (unsigned long long)fp < t->fold_pkts) t->fold_pkts = (unsigned long long)fp;
+    if (fb > 0 && (unsigned long long)fb < t->fold_bytes) t->fold_bytes = (unsigned long long)fb;
     // load <= 1/2 with the pool full and a whole batch of claims pending; tombstones are rehashed away at 1/4
     uint32_t ns = 64;
     while ((uint64_t)ns < 2ull * ((uint64_t)capacity + max_batch)) ns <<= 1;
@@ -890,6 +905,7 @@ int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
     int rc = PPE_OK;
     if (hipMalloc(&t->ctl, PPE_FCTL_WORDS * 8u) != hipSuccess || hipMalloc(&t->rec, (size_t)max_batch * 16u) != hipSuccess ||
         hipMalloc(&t->rslot, (size_t)max_batch * 4u) != hipSuccess ||
+        hipMalloc(&t->miss_tiles, (size_t)tiles * 4u) != hipSuccess ||
         hipMalloc(&t->tile_miss, (size_t)tiles * 8u) != hipSuccess ||
         hipMalloc(&t->tile_new, (size_t)tiles * 8u) != hipSuccess)
         rc = fail(c, PPE_ENOMEM, "flow table: out of device memory");
@@ -947,6 +963,7 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         const int e = ppe_launch_flow(kind, &k, kind == PPE_FLOW_K_REVOKE ? 1u : fg, (void *)s);
         if (e != 0) return fail(c, PPE_EIO, "flow kernel %d launch failed: %s", kind, hipGetErrorString((hipError_t)e));
     }
+    ++t.batches;
     t.live_ub = std::min<uint64_t>(t.live_ub + in->n, t.capacity);
     if (may_overflow) t.tomb_ub += in->n;  // revoked claims leave tombstones
     if (t.snap_inflight) {
@@ -1021,11 +1038,13 @@ int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_
     const FlowArrays &a = t.arr[t.cur];
     std::vector<uint32_t> keys((size_t)t.nslots * 4u);
     HIPCHK(c, hipMemcpy(keys.data(), a.keys, keys.size() * 4u, hipMemcpyDeviceToHost));
-    std::vector<unsigned long long> stats, last;
+    std::vector<unsigned long long> stats, packed, last;
     if (entries && max) {
         stats.resize((size_t)t.nslots * 4u);
+        packed.resize((size_t)t.nslots * 2u);
         last.resize(t.nslots);
         HIPCHK(c, hipMemcpy(stats.data(), a.stats, stats.size() * 8u, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(packed.data(), a.packed, packed.size() * 8u, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(last.data(), a.last, last.size() * 8u, hipMemcpyDeviceToHost));
     }
     uint32_t k = 0;
@@ -1041,10 +1060,11 @@ int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_
             e.dport = (uint16_t)(keys[4u * s + 2u] >> 16);
             e.protocol = (uint8_t)(st >> 8);
             e.slot = s;
-            e.pktcnts2d = stats[4u * s];
-            e.bytecnts2d = stats[4u * s + 1u];
-            e.pktcntd2s = stats[4u * s + 2u];
-            e.bytecntd2s = stats[4u * s + 3u];
+            const unsigned long long bmask = (1ull << PPE_PK_SHIFT) - 1u, p0 = packed[2u * s], p1 = packed[2u * s + 1u];
+            e.pktcnts2d = stats[4u * s] + (p0 >> PPE_PK_SHIFT);
+            e.bytecnts2d = stats[4u * s + 1u] + (p0 & bmask);
+            e.pktcntd2s = stats[4u * s + 2u] + (p1 >> PPE_PK_SHIFT);
+            e.bytecntd2s = stats[4u * s + 3u] + (p1 & bmask);
             e.last_seen = last[s];
         }
         ++k;

@@ -32,10 +32,15 @@ struct ppe_bdesc {
 #define PPE_FLOW_NONE 0xffffffffu
 #define PPE_FLOW_REVOKED 0x80000000u              /* creator word: pool exhausted, the claim is withdrawn */
 enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_NEW, PPE_FCTL_TOMBS,
-       PPE_FCTL_WORDS = 8 };
+       PPE_FCTL_MISS0, PPE_FCTL_MISS1, /* tiles with pending packets, by batch parity */ PPE_FCTL_WORDS = 8 };
+#define PPE_PK_SHIFT 40u                       /* packed counter: packets in bits 63:40, bytes in 39:0 */
+#define PPE_PK_FOLD_PKTS (1ull << 23)          /* fold into `stats` once either field reaches half its range */
+#define PPE_PK_FOLD_BYTES (1ull << 39)
 struct ppe_flowdev {
     uint32_t *keys;               /* nslots × {sip, dip, sport | dport << 16, state}, the creating packet's orientation */
-    unsigned long long *stats;    /* nslots × {pkts s2d, bytes s2d, pkts d2s, bytes d2s}                               */
+    unsigned long long *packed;   /* nslots × {s2d, d2s}: packets << 40 | bytes, one atomic per packet (FlowUpdate)    */
+    unsigned long long *stats;    /* nslots × {pkts s2d, bytes s2d, pkts d2s, bytes d2s}: folded from `packed` before a
+                                     field can overflow; a flow's counters = stats + the packed fields               */
     unsigned long long *last;     /* nslots × last-seen time                                                          */
     uint32_t *creator;            /* nslots: lowest index of the packets claiming the slot in this batch (| REVOKED)   */
     unsigned long long *ctl;      /* PPE_FCTL_* device counters                                                        */
@@ -43,6 +48,9 @@ struct ppe_flowdev {
     unsigned long long *tile_miss;  /* per tile: lanes whose flow was not found (pending resolution)                   */
     unsigned long long *tile_new;   /* per tile: lanes that create their flow                                          */
     uint32_t *rslot;              /* max_batch: the slot a pending packet's flow was claimed in, or PPE_FLOW_NONE       */
+    uint32_t *miss_tiles;         /* tiles with pending packets (unordered), count in ctl[PPE_FCTL_MISS0 + parity]      */
+    uint32_t parity;              /* batch sequence number & 1                                                         */
+    unsigned long long fold_pkts, fold_bytes;  /* packed-counter fold thresholds (PPE_PK_FOLD_*; lowered by tests)   */
     uint32_t gmask;               /* slot groups - 1                                                                   */
     uint32_t capacity;            /* flow pool size                                                                     */
 };

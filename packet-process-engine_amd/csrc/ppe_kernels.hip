@@ -29,7 +29,8 @@
 #include "ppe_internal.h"
 
 // Diagnostic ablation builds only (make ablate): bit 0 skip the ACL walk, bit 1 skip counters, bit 2 skip the
-// compaction, bit 3 skip the flow hash.  The product build has PPE_ABLATE == 0.
+// compaction, bit 3 skip the flow hash, bit 4 skip the flow-counter atomics, bit 5 skip the flow last-seen stores.
+// The product build has PPE_ABLATE == 0.
 #ifndef PPE_ABLATE
 #define PPE_ABLATE 0
 #endif
@@ -614,10 +615,23 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
     const uint32_t sport = ports & 0xffffu, dport = ports >> 16, fsport = fports & 0xffffu;
     const bool to_server = sport != dport ? fsport == sport : fsip == sip;
     const uint32_t d = sport == fsport ? 0u : 2u;
-    unsigned long long *st = f.stats + 4ull * s + d;
-    __hip_atomic_fetch_add(st, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(st + 1, (unsigned long long)wire_len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    f.last[s] = now;  // every packet of the batch stores the same batch time
+    if (!(PPE_ABLATE & 16)) {
+        // one memory-side atomic per packet: packets and bytes packed in one word.  The lane whose add takes a field
+        // past half its range moves the whole word into the wide counters (exchange with 0, then add), so a field
+        // never wraps and concurrent folds never count twice.
+        unsigned long long *pk = f.packed + 2ull * s + (d >> 1);
+        const unsigned long long inc = (1ull << PPE_PK_SHIFT) | (unsigned long long)wire_len;
+        const unsigned long long nv =
+            __hip_atomic_fetch_add(pk, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + inc;
+        if ((nv >> PPE_PK_SHIFT) >= f.fold_pkts || (nv & ((1ull << PPE_PK_SHIFT) - 1u)) >= f.fold_bytes) {
+            const unsigned long long x = __hip_atomic_exchange(pk, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned long long *w = f.stats + 4ull * s + d;
+            __hip_atomic_fetch_add(w, x >> PPE_PK_SHIFT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(w + 1, x & ((1ull << PPE_PK_SHIFT) - 1u), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (!(PPE_ABLATE & 32)) f.last[s] = now;  // every packet of the batch stores the same batch time
     return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
 }
 
@@ -742,7 +756,14 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
             // pending packets: key + provisional status (NO_SYN / ACL_DROP / ACL_FW = would create the flow)
             if (pend) gst<uint4>(a.flow.rec, 16u * p, make_uint4(k.sip, k.dip, k.sport | (k.dport << 16), k.proto | (st << 8)));
             const uint64_t pm = __builtin_amdgcn_ballot_w64(pend);
-            if (lane == 0) a.flow.tile_miss[tile] = pm;
+            if (lane == 0) {
+                a.flow.tile_miss[tile] = pm;
+                if (pm) {
+                    const unsigned long long i = __hip_atomic_fetch_add(&a.flow.ctl[PPE_FCTL_MISS0 + a.flow.parity],
+                                                                        1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    a.flow.miss_tiles[i] = tile;
+                }
+            }
             if (pm != 0) {  // the finalize kernel completes this tile (compaction, pending lanes' counters)
                 if (!(PPE_ABLATE & 2) && valid && !pend) atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
                 ++titer;
@@ -812,14 +833,15 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t sip, uint32_t dip, uint32_
     return flow_hashfn_l4(proto == 6u, sip, dip, ports & 0xffffu, ports >> 16);
 }
 
-struct TileWalk {  // persistent grid: wave gw of W takes tiles gw, gw + W, ...
-    uint32_t lane, gw, W, ntiles;
-    template <int BLOCK> __device__ __forceinline__ static TileWalk make(uint32_t n) {
+struct TileWalk {  // persistent grid: wave gw of W takes the listed tiles gw, gw + W, ... (tiles with pending packets)
+    uint32_t lane, gw, W, count;
+    template <int BLOCK> __device__ __forceinline__ static TileWalk make(const ppe_flowdev &f) {
         TileWalk t;
         t.lane = threadIdx.x & 63u;
         t.gw = blockIdx.x * (BLOCK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         t.W = gridDim.x * (BLOCK / 64);
-        t.ntiles = (n + 63u) >> 6;
+        t.count = (uint32_t)__hip_atomic_load(&f.ctl[PPE_FCTL_MISS0 + f.parity], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
         return t;
     }
 };
@@ -832,9 +854,10 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ppe_flow_claim_kernel(ppe_flow_kargs a) {
-    const TileWalk w = TileWalk::make<BLOCK>(a.n);
+    const TileWalk w = TileWalk::make<BLOCK>(a.f);
     const uint4 *rec = (const uint4 *)a.f.rec;
-    for (uint32_t t = w.gw; t < w.ntiles; t += w.W) {
+    for (uint32_t i = w.gw; i < w.count; i += w.W) {
+        const uint32_t t = a.f.miss_tiles[i];
         const uint64_t mask = a.f.tile_miss[t];
         if (!((mask >> w.lane) & 1ull)) continue;
         const uint32_t p = (t << 6) + w.lane;
@@ -871,12 +894,12 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_claim_kernel(ppe_flow_kargs a)
 
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ppe_flow_resolve_kernel(ppe_flow_kargs a) {
-    const TileWalk w = TileWalk::make<BLOCK>(a.n);
+    const TileWalk w = TileWalk::make<BLOCK>(a.f);
     const uint4 *rec = (const uint4 *)a.f.rec;
     uint32_t creators = 0;
-    for (uint32_t t = w.gw; t < w.ntiles; t += w.W) {
+    for (uint32_t i = w.gw; i < w.count; i += w.W) {
+        const uint32_t t = a.f.miss_tiles[i];
         const uint64_t mask = a.f.tile_miss[t];
-        if (!mask) continue;
         const uint32_t p = (t << 6) + w.lane;
         bool is_new = false;
         if ((mask >> w.lane) & 1ull) {
@@ -948,13 +971,15 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
     for (uint32_t i = tid; i < PPE_NBINS; i += BLOCK) bins[i] = 0;
     if (tid < 32u) lcnt[tid] = 0;
     __syncthreads();
-    const TileWalk w = TileWalk::make<BLOCK>(a.n);
+    const TileWalk w = TileWalk::make<BLOCK>(a.f);
     const uint4 *rec = (const uint4 *)a.f.rec;
     const uint64_t act_table = make_act_table(a.unsup_fw);
     uint32_t created = 0, revoked = 0;
-    for (uint32_t t = w.gw; t < w.ntiles; t += w.W) {
+    // the next batch's miss-tile counter (last used by the previous batch, whose kernels have all completed)
+    if (blockIdx.x == 0 && tid == 0) a.f.ctl[PPE_FCTL_MISS0 + (a.f.parity ^ 1u)] = 0;
+    for (uint32_t i = w.gw; i < w.count; i += w.W) {
+        const uint32_t t = a.f.miss_tiles[i];
         const uint64_t mask = a.f.tile_miss[t];
-        if (!mask) continue;
         const uint32_t p = (t << 6) + w.lane;
         const bool valid = p < a.n;
         const uint32_t v = valid ? a.verdict[p] : 0u;
@@ -1033,6 +1058,7 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_age_kernel(ppe_flow_kargs a) {
             a.f.keys[4ull * s + 3u] = PPE_FS_TOMB;
             ((uint4 *)a.f.stats)[2ull * s] = make_uint4(0u, 0u, 0u, 0u);
             ((uint4 *)a.f.stats)[2ull * s + 1u] = make_uint4(0u, 0u, 0u, 0u);
+            ((uint4 *)a.f.packed)[s] = make_uint4(0u, 0u, 0u, 0u);
             a.f.last[s] = 0;
             ++del;
         }
@@ -1069,6 +1095,7 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_rehash_kernel(ppe_flow_kargs a
                     a.dst.keys[4ull * d + 2u] = k.z;
                     ((uint4 *)a.dst.stats)[2ull * d] = ((const uint4 *)a.f.stats)[2ull * s];
                     ((uint4 *)a.dst.stats)[2ull * d + 1u] = ((const uint4 *)a.f.stats)[2ull * s + 1u];
+                    ((uint4 *)a.dst.packed)[d] = ((const uint4 *)a.f.packed)[s];
                     a.dst.last[d] = a.f.last[s];
                     done = true;
                 }

@@ -22,6 +22,8 @@ CONFIGS = {
     "C2": dict(n=1 << 20, rules=4096, kind="imix"),
     "C3": dict(n=1 << 20, rules=65536, kind="udp64"),
     "C4": dict(n=1 << 20, rules=4096, kind="udp64"),
+    # stateful flow table: 1M-packet batches over 256k bidirectional UDP flows, default FW
+    "F1": dict(n=1 << 20, rules=256, kind="udp64", flows=1 << 18),
 }
 
 MAC_POOL = 16
@@ -186,12 +188,14 @@ def make_packets(n: int, rules: np.ndarray, seed: int = SEED + 1, kind: str = "u
 
 def make_flow_packets(n: int, rules: np.ndarray, n_flows: int, seed: int = SEED + 3, kind: str = "udp64",
                       stride: int = 64, rev_frac: float = 0.4, syn_frac: float = 0.3, tcp_frac: float | None = None,
-                      malformed_frac: float = 0.0):
+                      malformed_frac: float = 0.0, template_seed: int | None = None):
     """Stateful traffic for the flow table: n packets drawn uniformly from n_flows flow templates (make_packets
     tuples), each sent in the reverse direction (addresses and ports swapped) with probability rev_frac; TCP packets
     carry SYN with probability syn_frac, else ACK (so syn_check drops some first packets).  Same dict as
-    make_packets, plus flow=(n,) template index."""
-    base = make_packets(n_flows, rules, seed=seed, kind=kind, stride=stride, malformed_frac=0.0, tcp_frac=tcp_frac)
+    make_packets, plus flow=(n,) template index.  template_seed (default: seed) fixes the flow population, so
+    batches drawn with different seeds revisit the same flows."""
+    base = make_packets(n_flows, rules, seed=seed if template_seed is None else template_seed, kind=kind,
+                        stride=stride, malformed_frac=0.0, tcp_frac=tcp_frac)
     rng = np.random.default_rng(seed ^ 0xF10)
     idx = rng.integers(0, n_flows, n)
     hdr = base["hdr"][idx].copy()

@@ -141,6 +141,24 @@ def test_flow_aging_and_rehash(eng):
         p.close()
 
 
+def test_flow_counter_folding(monkeypatch):
+    """The packed per-flow counters fold into the wide ones when a field passes its threshold (lowered here to a few
+    packets / bytes so every flow folds many times); totals stay exact under concurrent folds."""
+    monkeypatch.setenv("PPE_FLOW_FOLD_PKTS", "3")
+    monkeypatch.setenv("PPE_FLOW_FOLD_BYTES", "500")
+    e = Engine(0)
+    rules = synth.make_rules(16, seed=24)
+    p = Pair(e, rules, capacity=10000, max_batch=1 << 15, default_action=0)
+    try:
+        for b in range(3):
+            pk = synth.make_flow_packets(30000, rules, n_flows=300, seed=400 + b, template_seed=400, syn_frac=0.9)
+            p.batch(pk["hdr"], pk["len"], NOW + b)
+            p.same_table()
+    finally:
+        p.close()
+        e.close()
+
+
 def test_flow_known_answers(eng):
     """The oracle's known-answer sequences (test_oracle_flow.py) through the HIP path."""
     from pktbuild import tcp_packet, udp_packet
