@@ -101,7 +101,8 @@ enum ppe_counter {
     PPE_C_FLOW_PROC_OK, PPE_C_FLOW_PROC_FAIL, PPE_C_FLOW_TCP_NO_SYN_FIRST,
     PPE_C_OUT_FW, PPE_C_OUT_DROP, PPE_C_OUT_PUNT, PPE_C_WINDOW_PUNT, PPE_C_PKTS,
     PPE_C_FLOW_NODE_NOMEM,     /* flow table only: FlowAdd found the pool empty (decode-statistic.h:304) */
-    PPE_C__COUNT /* 31 */
+    PPE_C_RX_BYTES,            /* sum of pkt_totallen (STAT_RECV_PB_ADD, oct-rxtx.c:213)                 */
+    PPE_C__COUNT /* 32 */
 };
 
 typedef struct {
@@ -285,6 +286,14 @@ int  ppe_flow_info(ppe_ctx_t *ctx, ppe_flow_info_t *info);         /* dp_show_fl
 int  ppe_flow_clear_stat(ppe_ctx_t *ctx);                           /* dp_clear_flow_stat (dp_cmd.c:2327) */
 /* Copy up to `max` live flows to host (table order); *n = live flows.  Synchronises. */
 int  ppe_flow_dump(ppe_ctx_t *ctx, ppe_flow_entry_t *entries, uint32_t max, uint32_t *n);
+
+/* Operator text of the reference's `show` commands, from counters / flow info read with ppe_counters_read /
+ * ppe_flow_info: dp_show_pkt_stat (dataplane/src/common/dp_cmd.c:844-1818; same sections, names and order; the
+ * reference's SELF_TEST build (flow.c:21) never counts output_*, and the I/O, ARP/ICMP/OSPF, defrag, TX and attack
+ * counters have no source on this path: those lines print 0) and dp_show_flow_stat (dp_cmd.c:2346-2392).
+ * snprintf semantics: returns the full length, writes at most cap bytes including the NUL. */
+int  ppe_format_pkt_stat(const ppe_counters_t *c, char *buf, size_t cap);
+int  ppe_format_flow_stat(const ppe_flow_info_t *f, char *buf, size_t cap);
 
 /* Human-readable last error of this context (static storage of the ctx). */
 const char *ppe_last_error(ppe_ctx_t *ctx);

@@ -642,6 +642,7 @@ static void *run_shard(void *arg) {
         }
         for (int c = 0; c < 32; c++)
             if (r.counters & (1u << c)) s->counters[c]++;
+        s->counters[PPE_C_RX_BYTES] += len;  /* STAT_RECV_PB_ADD(m->pkt_totallen), oct-rxtx.c:213 */
     }
     return NULL;
 }

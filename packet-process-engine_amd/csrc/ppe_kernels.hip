@@ -687,10 +687,13 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
     // this batch's creator count, summed by the resolve kernel (which runs after this one)
     if (FLOW && blockIdx.x == 0 && tid == 0) a.flow.ctl[PPE_FCTL_BATCH_NEW] = 0;
 
+    unsigned long long rx_bytes = 0;  // STAT_RECV_PB_ADD (oct-rxtx.c:213) of this lane's packets
+
     // one tile: decode, hash, ACL, stores, compaction, counters.  w = the window's first 52 bytes, wlen = wire length
     auto process = [&](uint32_t tile, const uint32_t (&w)[13], uint32_t wlen) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < B.n;
+        if (!(PPE_ABLATE & 2) && valid) rx_bytes += wlen;
         Dec k = decode(w, wlen, B.hdr, p, B.stride, a.syn_check);
 
         uint32_t fh = 0;
@@ -795,6 +798,11 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
 
     TRACE_AT(22);
     if (PPE_TRACE && lane == 0 && a.trace) a.trace[(size_t)twave * 32u + 31u] = titer;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) rx_bytes += __shfl_xor(rx_bytes, o, 64);
+    if (lane == 0 && rx_bytes)
+        __hip_atomic_fetch_add(&a.cslots[(size_t)blockIdx.x * PPE_CSLOT_WORDS + PPE_C_RX_BYTES], rx_bytes,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     for (uint32_t b = tid; b < PPE_NBINS; b += BLOCK) {  // expand the bins into counter increments
         const uint32_t c = bins[b];

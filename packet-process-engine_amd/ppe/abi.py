@@ -33,7 +33,7 @@ COUNTERS = ["l2_headerlen_err", "l2_unsupport", "l2_rx_ok",
             "tcp_headerlen_err", "tcp_pktlen_err", "tcp_rx_ok",
             "acl_drop", "acl_fw",
             "flow_proc_ok", "flow_proc_fail", "flow_tcp_no_syn_first",
-            "out_fw", "out_drop", "out_punt", "window_punt", "pkts", "flow_node_nomem"]
+            "out_fw", "out_drop", "out_punt", "window_punt", "pkts", "flow_node_nomem", "rx_bytes"]
 ACL_RULE_ACTION_FW, ACL_RULE_ACTION_DROP = 0, 1
 RULE_ENTRY_MAX = 10000
 
@@ -118,7 +118,7 @@ EXPORTS = [
     "ppe_counters_read", "ppe_counters_clear", "ppe_timing_enable", "ppe_timing_read", "ppe_acl_image",
     "ppe_launch_info", "ppe_debug_trace", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
     "ppe_get_tuning", "ppe_flow_create", "ppe_flow_destroy", "ppe_classify_flow", "ppe_flow_age", "ppe_flow_info",
-    "ppe_flow_clear_stat", "ppe_flow_dump",
+    "ppe_flow_clear_stat", "ppe_flow_dump", "ppe_format_pkt_stat", "ppe_format_flow_stat",
     # ppe_acl.h
     "ppe_rule_list_init", "ppe_rule_list_free", "Rule_add", "Rule_del_by_id", "Rule_del_all",
     "Rule_duplicate_check", "Rule_Load_Line", "ppe_rule_load_file", "DP_Acl_Rule_Init", "DP_Acl_Load_Rule",
@@ -194,6 +194,8 @@ def _open(p: Path, mode) -> C.CDLL:
         "ppe_flow_info": ([vp, C.POINTER(FlowInfo)], C.c_int),
         "ppe_flow_clear_stat": ([vp], C.c_int),
         "ppe_flow_dump": ([vp, vp, u32, C.POINTER(u32)], C.c_int),
+        "ppe_format_pkt_stat": ([C.POINTER(Counters), C.c_char_p, C.c_size_t], C.c_int),
+        "ppe_format_flow_stat": ([C.POINTER(FlowInfo), C.c_char_p, C.c_size_t], C.c_int),
         "ppe_rule_list_init": ([], C.c_int),
         "ppe_rule_list_free": ([], None),
         "Rule_add": ([vp, C.POINTER(u32)], C.c_int),

@@ -9,8 +9,11 @@ def test_oracle_vs_golden(golden):
     o = pyoracle.Oracle(g["rules"], g["used"], default_action=1)
     for tag, cfg in (("a", o.cfg(0, 1, int(g["now"]))), ("b", o.cfg(1, 0, int(g["now"])))):
         r = o.classify_batch(g["hdr"], g["len"], ts=g["ts"], cfg=cfg)
-        for k in ("verdict", "flow_hash", "acl_hit", "tuple", "reach", "counters"):
+        for k in ("verdict", "flow_hash", "acl_hit", "tuple", "reach"):
             assert np.array_equal(r[k], g[f"{tag}_{k}"]), (tag, k)
+        # per-reason counters as frozen; slot 31 (rx_bytes, added after the fixtures) is the sum of wire lengths
+        assert np.array_equal(r["counters"][:31], g[f"{tag}_counters"][:31]), tag
+        assert int(r["counters"][31]) == int(g["len"].astype(np.uint64).sum())
 
 
 def test_golden_covers_every_decode_reason(golden):

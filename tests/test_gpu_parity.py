@@ -96,6 +96,7 @@ def test_golden_fixture_device_path(eng, golden, tag, cfg):
     cnt = eng.counters()
     assert [cnt[n] for n in abi.COUNTERS[:30]] == g[f"{tag}_counters"][:30].tolist()
     assert cnt["flow_node_nomem"] == 0
+    assert cnt["rx_bytes"] == int(g["len"].astype(np.uint64).sum())
 
 
 @pytest.mark.parametrize("tag,cfg", [("a", (0, 1)), ("b", (1, 0))])

@@ -21,5 +21,5 @@ timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_IN
 python3 tools/collect_traffic.py --fetch $O/fetch/c1_counter_collection.csv --write $O/write/c1_counter_collection.csv \
   --cal-fetch $O/cal_fetch/cal_counter_collection.csv --cal-write $O/cal_write/cal_counter_collection.csv \
   --n $((8 * 1048576)) --out $O/${R}_traffic_C1.json > $O/traffic.log 2>&1
-python3 tools/pmc_summary.py $O/sq/c1_counter_collection.csv > $O/sq_summary.txt 2>&1
+python3 tools/pmc_summary.py $O/sq/c1_counter_collection.csv --tiles $((8 * 16384)) > $O/sq_summary.txt 2>&1
 echo profile done
