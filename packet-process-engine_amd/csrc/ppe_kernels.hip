@@ -369,7 +369,9 @@ __device__ __forceinline__ uint4 acl_walk(const uint32_t *__restrict__ gimg, con
         // jump root (image v4): bucket = key[dim] >> shift picks this lane's subtree root and its key slot
         const uint32_t key = lds_u32(lanebase + ((g.jump & 0xffu) << 8));
         const uint32_t jo = 4u * PPE_IMG_HDR_WORDS + 4u * (key >> ((g.jump >> 8) & 0xffu));
-        const uint32_t e = (MODE != IMG_GLOBAL && g.lds_words >= g.off_nodes) ? lds_u32(IMGB + jo) : gld<uint32_t>(gimg, jo);
+        // (IMG_LDS: always staged — no global-load path, whose merge would wait on every outstanding load)
+        const uint32_t e = (MODE == IMG_LDS || (MODE == IMG_SPLIT && g.lds_words >= g.off_nodes))
+                               ? lds_u32(IMGB + jo) : gld<uint32_t>(gimg, jo);
         noff = e & 0xffffffu;
         kaddr = lanebase + ((e >> 16) & 0xff00u);
     }
