@@ -183,6 +183,28 @@ def main():
     kern_ms, launches = eng.timing_read(reset=True)
     eng.timing(False)
     my_ms = max(elapsed_ms, 1e-9)
+    # N > 1: the consumer-side verdict gather, timed apart from `value` (the classify path itself
+    # exchanges nothing): all_gather over RCCL of one batch's verdict + flow hash + ACL hit (12 B per packet per rank)
+    gather = None
+    if dist is not None:
+        try:
+            _, _, out0, _ = bufs[0]
+            src = torch.stack([out0["verdict"], out0["flow_hash"], out0["acl_hit"]])
+            dst = torch.empty((world,) + tuple(src.shape), dtype=src.dtype, device=dev)
+            ts = []
+            for _ in range(6):
+                barrier()
+                t0 = time.perf_counter()
+                dist.all_gather_into_tensor(dst, src)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            g_ms = float(np.median(ts[1:])) * 1e3
+            gt = torch.tensor([g_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+            g_ms = float(gt.item())
+            gather = {"ms_per_batch": round(g_ms, 4), "bytes_per_rank": 12 * n, "collective": "all_gather (RCCL)"}
+        except Exception as e:  # a failed measurement must not lose the throughput line
+            gather = {"error": str(e)[:200]}
     if dist is not None:
         t = torch.tensor([my_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -216,6 +238,14 @@ def main():
         parity = bool(np.array_equal(got_v[ok], ref["verdict"][ok]) and np.array_equal(got_h[ok], ref["flow_hash"][ok])
                       and np.array_equal(got_a[ok], ref["acl_hit"][ok]) and ((got_v[far] & 0xFF) == 18).all()
                       and np.array_equal(got_p, want_part))
+
+    # ---- live rule commit: host build + upload + publish of the same rule set, between
+    # batches (the double-buffer swap of dp_acl_rule_commit, dataplane/src/common/dp_cmd.c:1987-2053) ----
+    commit_ms = []
+    for _ in range(3):
+        tc0 = time.perf_counter()
+        acl = eng.commit(rules, default_action=1)
+        commit_ms.append((time.perf_counter() - tc0) * 1e3)
 
     # ---- host-inclusive rate (pinned host buffers, H2D + classify + D2H pipeline) ----
     host_mpps = None
@@ -293,9 +323,15 @@ def main():
             "cpu_baseline": cpu,
             "host_inclusive_mpps": round(host_mpps, 2) if host_mpps else None,
             "parity_sample_ok": parity,
-            "acl": {k: acl[k] for k in ("n_rules", "n_nodes", "max_depth", "blob_bytes", "lds_resident")},
+            "acl": {**{k: acl[k] for k in ("n_rules", "n_nodes", "max_depth", "blob_bytes", "lds_resident")},
+                    "build_ms": round(acl["build_ms"], 3), "commit_ms": round(float(np.median(commit_ms)), 3)},
             "launch": li,
         }
+        if gather is not None:
+            if "ms_per_batch" in gather:
+                gather["value_with_gather"] = round(n * world / ((my_ms / args.steps + gather["ms_per_batch"]) / 1e3)
+                                                    / 1e6, 2)
+            line["gather"] = gather
         print(json.dumps(line), flush=True)
     eng.close()
     if dist is not None:

@@ -955,7 +955,8 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     k.now = cfg ? cfg->now_seconds : 0u;
     k.nslots = t.nslots;
     k.cslots = c->d_cslots;
-    const uint32_t fg = flow_grid(c, (in->n + 63u) / 64u, PPE_FLOW_BLOCK_WAVES);
+    // grid-stride over the miss-tile list (usually short): a few workgroups per CU, not one per tile
+    const uint32_t fg = std::min(flow_grid(c, (in->n + 63u) / 64u, PPE_FLOW_BLOCK_WAVES), c->n_cu * 2u);
     // 2-5. claim, resolve, [revoke: only when the pool may overflow], finalize
     const bool may_overflow = t.live_ub + in->n > t.capacity;
     for (int kind : {PPE_FLOW_K_CLAIM, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_REVOKE, PPE_FLOW_K_FINALIZE}) {

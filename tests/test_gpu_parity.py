@@ -322,6 +322,27 @@ def test_commit_double_buffer_and_determinism(eng):
     assert np.array_equal(ra["acl_hit"], r1["acl_hit"])
 
 
+def test_live_commit_between_queued_batches(eng):
+    """Rule sets committed between batches already queued on the stream (the dp_acl_rule_commit double buffer,
+    dataplane/src/common/dp_cmd.c:1987-2053): every batch sees exactly the rule set published before it was queued."""
+    sets = [(synth.make_rules(256, seed=90 + i), i % 2) for i in range(4)]
+    pk = synth.make_packets(200_000, sets[0][0], seed=95, stride=64)
+    th = torch.from_numpy(pk["hdr"]).to(DEV)
+    tl = torch.from_numpy(pk["len"].view(np.int32)).to(DEV)
+    outs = []
+    for rules, dflt in sets:
+        eng.commit(rules, default_action=dflt)
+        o = {k: torch.empty(len(pk["len"]), dtype=torch.int32, device=DEV) for k in ("verdict", "acl_hit")}
+        eng.classify_torch(th, tl, o, cfg=eng.cfg(now_seconds=NOW))  # queued, not synchronised
+        outs.append(o)
+    torch.cuda.synchronize()
+    for (rules, dflt), o in zip(sets, outs):
+        orc = pyoracle.Oracle(rules, default_action=dflt)
+        ref = orc.classify_batch(pk["hdr"], pk["len"], cfg=orc.cfg(0, 1, NOW), nthreads=16)
+        assert np.array_equal(o["verdict"].cpu().numpy().view(np.uint32), ref["verdict"])
+        assert np.array_equal(o["acl_hit"].cpu().numpy(), ref["acl_hit"])
+
+
 def test_full_size_properties_c1(eng):
     """1M packets (the C1 bench batch): counters sum to n, every packet is in exactly one compaction class,
     the two halves classified separately equal the whole, and the flow hash is direction-symmetric."""
