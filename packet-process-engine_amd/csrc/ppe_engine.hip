@@ -63,12 +63,15 @@ struct FlowTable {
     uint64_t live_ub = 0;   // upper bound of live flows: a snapshot's count + n per batch since
     uint64_t tomb_ub = 0;   // upper bound of tombstones: a snapshot's count + n per batch that could revoke
     uint32_t rehashes = 0;
-    // asynchronous snapshot of ctl (pinned copy + event), taken when the bounds get close to a limit, so the host
+    // zero-copy snapshot of ctl in pinned host memory, written by every flow-mode classify launch (block 0) as it
+    // starts: {batches completed, live, tombstones}.  The host tightens its bounds from it without synchronising.
     // refreshes them without synchronising
-    unsigned long long *ctl_h = nullptr;
-    hipEvent_t snap_ev = nullptr;
-    bool snap_inflight = false;
-    uint64_t snap_n = 0, snap_n_rev = 0;  // packets (of batches that may revoke) submitted after the snapshot
+    unsigned long long *snap_h = nullptr, *snap_d = nullptr;  // host / device views
+    uint64_t snap_used = 0;            // highest snapshot sequence applied
+    // ring over the last kSnapRing batches: packets submitted before batch b (of batches that may revoke: _rev)
+    static constexpr uint32_t kSnapRing = 4096;
+    std::vector<uint64_t> cum_n, cum_rev;
+    uint64_t tot_n = 0, tot_rev = 0;
 };
 
 }  // namespace
@@ -806,6 +809,8 @@ static ppe_flowdev flow_dev(const FlowTable &t, int which) {
     d.parity = (uint32_t)(t.batches & 1u);
     d.fold_pkts = t.fold_pkts;
     d.fold_bytes = t.fold_bytes;
+    d.snap = t.snap_d;
+    d.seq = t.batches;
     d.last = a.last;
     d.creator = a.creator;
     d.ctl = t.ctl;
@@ -830,7 +835,7 @@ static int flow_sync_counts(ppe_ctx *c, unsigned long long *ctl_out) {
     HIPCHK(c, hipMemcpy(ctl_out, t.ctl, PPE_FCTL_WORDS * 8u, hipMemcpyDeviceToHost));
     t.live_ub = ctl_out[PPE_FCTL_LIVE];
     t.tomb_ub = ctl_out[PPE_FCTL_TOMBS];
-    t.snap_inflight = false;  // (the device is idle: any snapshot has landed and is superseded)
+    t.snap_used = t.batches;  // (the device is idle: this is the state after every submitted batch)
     return PPE_OK;
 }
 
@@ -867,8 +872,7 @@ int ppe_flow_destroy(ppe_ctx_t *c) {
     (void)hipDeviceSynchronize();
     FlowTable *t = c->flow;
     for (FlowArrays &a : t->arr) flow_free_arrays(a);
-    if (t->ctl_h) (void)hipHostFree(t->ctl_h);
-    if (t->snap_ev) (void)hipEventDestroy(t->snap_ev);
+    if (t->snap_h) (void)hipHostFree(t->snap_h);
     (void)hipFree(t->ctl);
     (void)hipFree(t->rec);
     (void)hipFree(t->rslot);
@@ -910,9 +914,12 @@ int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
         hipMalloc(&t->tile_new, (size_t)tiles * 8u) != hipSuccess)
         rc = fail(c, PPE_ENOMEM, "flow table: out of device memory");
     if (rc == PPE_OK && hipMemset(t->ctl, 0, PPE_FCTL_WORDS * 8u) != hipSuccess) rc = fail(c, PPE_EIO, "memset");
-    if (rc == PPE_OK && (hipHostMalloc(&t->ctl_h, PPE_FCTL_WORDS * 8u, hipHostMallocDefault) != hipSuccess ||
-                         hipEventCreateWithFlags(&t->snap_ev, hipEventDisableTiming) != hipSuccess))
+    if (rc == PPE_OK && (hipHostMalloc(&t->snap_h, 64, hipHostMallocMapped) != hipSuccess ||
+                         hipHostGetDevicePointer((void **)&t->snap_d, t->snap_h, 0) != hipSuccess))
         rc = fail(c, PPE_ENOMEM, "flow table: pinned snapshot buffer");
+    if (rc == PPE_OK) std::memset(t->snap_h, 0, 64);
+    t->cum_n.assign(FlowTable::kSnapRing, 0);
+    t->cum_rev.assign(FlowTable::kSnapRing, 0);
     if (rc == PPE_OK) rc = flow_clear_arrays(c, t->arr[0], ns, nullptr);
     if (rc == PPE_OK && hipDeviceSynchronize() != hipSuccess) rc = fail(c, PPE_EIO, "flow table init failed");
     if (rc != PPE_OK) ppe_flow_destroy(c);
@@ -929,10 +936,14 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     FlowTable &t = *c->flow;
     if (in->n > t.max_batch) return fail(c, PPE_EINVAL, "batch larger than the flow table's max_batch");
     HIPCHK(c, use_device(c));
-    if (t.snap_inflight && hipEventQuery(t.snap_ev) == hipSuccess) {  // a finished snapshot tightens the bounds
-        t.snap_inflight = false;
-        t.live_ub = std::min<uint64_t>(t.ctl_h[PPE_FCTL_LIVE] + t.snap_n, t.capacity);
-        t.tomb_ub = t.ctl_h[PPE_FCTL_TOMBS] + t.snap_n_rev;
+    {  // the latest snapshot (seqlock: the sequence word is written last and re-read here)
+        const volatile unsigned long long *sh = t.snap_h;
+        const uint64_t s0 = sh[0], live = sh[1], tombs = sh[2], s1 = sh[0];
+        if (s0 == s1 && s0 > t.snap_used && s0 <= t.batches && t.batches - s0 < FlowTable::kSnapRing) {
+            t.snap_used = s0;
+            t.live_ub = std::min<uint64_t>(live + (t.tot_n - t.cum_n[s0 % FlowTable::kSnapRing]), t.capacity);
+            t.tomb_ub = tombs + (t.tot_rev - t.cum_rev[s0 % FlowTable::kSnapRing]);
+        }
     }
     rc = flow_maybe_rehash(c);
     if (rc != PPE_OK) return rc;
@@ -964,18 +975,13 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         const int e = ppe_launch_flow(kind, &k, kind == PPE_FLOW_K_REVOKE ? 1u : fg, (void *)s);
         if (e != 0) return fail(c, PPE_EIO, "flow kernel %d launch failed: %s", kind, hipGetErrorString((hipError_t)e));
     }
+    t.cum_n[t.batches % FlowTable::kSnapRing] = t.tot_n;
+    t.cum_rev[t.batches % FlowTable::kSnapRing] = t.tot_rev;
+    t.tot_n += in->n;
+    if (may_overflow) t.tot_rev += in->n;
     ++t.batches;
     t.live_ub = std::min<uint64_t>(t.live_ub + in->n, t.capacity);
     if (may_overflow) t.tomb_ub += in->n;  // revoked claims leave tombstones
-    if (t.snap_inflight) {
-        t.snap_n += in->n;
-        if (may_overflow) t.snap_n_rev += in->n;
-    } else if (may_overflow || t.tomb_ub > t.nslots / 8u) {  // bounds near a limit: refresh them asynchronously
-        HIPCHK(c, hipMemcpyAsync(t.ctl_h, t.ctl, PPE_FCTL_WORDS * 8u, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipEventRecord(t.snap_ev, s));
-        t.snap_inflight = true;
-        t.snap_n = t.snap_n_rev = 0;
-    }
     return PPE_OK;
 }
 

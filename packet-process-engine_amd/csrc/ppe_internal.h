@@ -51,6 +51,8 @@ struct ppe_flowdev {
     uint32_t *miss_tiles;         /* tiles with pending packets (unordered), count in ctl[PPE_FCTL_MISS0 + parity]      */
     uint32_t parity;              /* batch sequence number & 1                                                         */
     unsigned long long fold_pkts, fold_bytes;  /* packed-counter fold thresholds (PPE_PK_FOLD_*; lowered by tests)   */
+    unsigned long long *snap;     /* pinned host words {seq, live, tombstones}: written by the classify launch        */
+    unsigned long long seq;       /* batches completed before this one                                                 */
     uint32_t gmask;               /* slot groups - 1                                                                   */
     uint32_t capacity;            /* flow pool size                                                                     */
 };

@@ -687,7 +687,14 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
 
     const uint64_t act_table = make_act_table(a.unsup_fw);
     // this batch's creator count, summed by the resolve kernel (which runs after this one)
-    if (FLOW && blockIdx.x == 0 && tid == 0) a.flow.ctl[PPE_FCTL_BATCH_NEW] = 0;
+    if (FLOW && blockIdx.x == 0 && tid == 0) {
+        a.flow.ctl[PPE_FCTL_BATCH_NEW] = 0;
+        // the table state after the previous batches, for the host's bounds (zero-copy, no stream stall)
+        a.flow.snap[1] = __hip_atomic_load(&a.flow.ctl[PPE_FCTL_LIVE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.flow.snap[2] = __hip_atomic_load(&a.flow.ctl[PPE_FCTL_TOMBS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();
+        __hip_atomic_store(&a.flow.snap[0], a.flow.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 
     unsigned long long rx_bytes = 0;  // STAT_RECV_PB_ADD (oct-rxtx.c:213) of this lane's packets
 
