@@ -287,6 +287,22 @@ int  ppe_flow_clear_stat(ppe_ctx_t *ctx);                           /* dp_clear_
 /* Copy up to `max` live flows to host (table order); *n = live flows.  Synchronises. */
 int  ppe_flow_dump(ppe_ctx_t *ctx, ppe_flow_entry_t *entries, uint32_t max, uint32_t *n);
 
+/* ---- Flow-hash steering across GPUs (the stateful path shards by flow, like Octeon's PIP tag
+ * steering of a flow to one core, dataplane/src/platform/oct-init.c:139-151) ----
+ * ppe_steer_partition: from a stateless ppe_classify of the batch (verdict + flow_hash), each packet's owner GPU is
+ * flow_hash % world if it reaches the flow table (PPE_F_L4), else `rank` (its stateless verdict is final anyway).
+ * perm[n] = packet indices grouped by owner, ascending within each owner; counts[world] = packets per owner.
+ * ppe_gather_rows: dst[i] = src[perm[i]]; ppe_scatter_rows: dst[perm[i]] = src[i] (rows of row_bytes, a multiple of
+ * 4, <= 256).  All device pointers, stream-ordered.  world <= 16.  The exchange itself is an all-to-all of the
+ * gathered windows (RCCL over xGMI), then ppe_classify_flow on the received packets and the reverse all-to-all of
+ * their verdicts: packet-process-engine_amd/ppe/dist.py steered_classify_flow. */
+int  ppe_steer_partition(ppe_ctx_t *ctx, const uint32_t *verdict, const uint32_t *flow_hash, uint32_t n,
+                         uint32_t world, uint32_t rank, uint32_t *perm, uint32_t *counts, void *stream);
+int  ppe_gather_rows(ppe_ctx_t *ctx, const void *src, uint32_t row_bytes, const uint32_t *perm, uint32_t n,
+                     void *dst, void *stream);
+int  ppe_scatter_rows(ppe_ctx_t *ctx, const void *src, uint32_t row_bytes, const uint32_t *perm, uint32_t n,
+                      void *dst, void *stream);
+
 /* Operator text of the reference's `show` commands, from counters / flow info read with ppe_counters_read /
  * ppe_flow_info: dp_show_pkt_stat (dataplane/src/common/dp_cmd.c:844-1818; same sections, names and order; the
  * reference's SELF_TEST build (flow.c:21) never counts output_*, and the I/O, ARP/ICMP/OSPF, defrag, TX and attack

@@ -104,6 +104,8 @@ struct ppe_ctx {
     uint32_t batches_per_launch = PPE_MAX_BATCH;  // PPE_BATCHES_PER_LAUNCH at context creation
     ppe_tuning_t tune;
     FlowTable *flow = nullptr;  // ppe_flow_create
+    uint32_t *d_steer = nullptr;  // ppe_steer_partition: per-tile owner counts / offsets
+    size_t steer_cap = 0;
     unsigned long long *trace = nullptr;  // ppe_debug_trace
     char err[256] = {0};
 };
@@ -409,6 +411,7 @@ int ppe_ctx_destroy(ppe_ctx_t *c) {
     for (hipEvent_t e : c->pipe_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->flow) ppe_flow_destroy(c);
+    if (c->d_steer) (void)hipFree(c->d_steer);
     for (auto &h : c->hs) {
         if (h.s) (void)hipStreamDestroy(h.s);
         (void)hipFree(h.hdr);
@@ -1078,6 +1081,74 @@ int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_
     }
     *n = k;
     return PPE_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Flow-hash steering across GPUs
+
+int ppe_steer_partition(ppe_ctx_t *c, const uint32_t *verdict, const uint32_t *flow_hash, uint32_t n, uint32_t world,
+                        uint32_t rank, uint32_t *perm, uint32_t *counts, void *stream) {
+    if (!c) return PPE_EINVAL;
+    if (world == 0 || world > PPE_STEER_MAX_WORLD || rank >= world)
+        return fail(c, PPE_EINVAL, "world must be 1..%d and rank < world", PPE_STEER_MAX_WORLD);
+    if (!counts || (n && (!verdict || !flow_hash || !perm))) return fail(c, PPE_EINVAL, "null argument");
+    HIPCHK(c, use_device(c));
+    const hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        HIPCHK(c, hipMemsetAsync(counts, 0, (size_t)world * 4u, s));
+        return PPE_OK;
+    }
+    const uint32_t tiles = (n + 63u) / 64u;
+    const size_t need = (size_t)tiles * world * 4u;
+    if (need > c->steer_cap) {
+        HIPCHK(c, hipStreamSynchronize(s));  // the old buffer may be in use by queued work
+        if (c->d_steer) HIPCHK(c, hipFree(c->d_steer));
+        c->d_steer = nullptr;
+        c->steer_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_steer, need));
+        c->steer_cap = need;
+    }
+    ppe_steer_kargs k;
+    std::memset(&k, 0, sizeof k);
+    k.verdict = verdict;
+    k.flow_hash = flow_hash;
+    k.n = n;
+    k.world = world;
+    k.rank = rank;
+    k.tcount = c->d_steer;
+    k.perm = perm;
+    k.counts = counts;
+    const uint32_t grid = std::max(1u, std::min((tiles + 3u) / 4u, c->n_cu * 8u));
+    for (int phase = 0; phase < 3; ++phase) {
+        const int e = ppe_launch_steer(phase, &k, grid, (void *)s);
+        if (e != 0) return fail(c, PPE_EIO, "steer kernel %d: %s", phase, hipGetErrorString((hipError_t)e));
+    }
+    return PPE_OK;
+}
+
+static int rows(ppe_ctx_t *c, const void *src, uint32_t row_bytes, const uint32_t *perm, uint32_t n, void *dst,
+                int scatter, void *stream) {
+    if (!c) return PPE_EINVAL;
+    if (row_bytes == 0 || row_bytes % 4u || row_bytes > 256u) return fail(c, PPE_EINVAL, "row_bytes: 4..256, x4");
+    if (n == 0) return PPE_OK;
+    if (!src || !dst || !perm) return fail(c, PPE_EINVAL, "null argument");
+    HIPCHK(c, use_device(c));
+    ppe_rows_kargs k = {(const uint8_t *)src, (uint8_t *)dst, perm, n, row_bytes, (uint32_t)scatter, 0u};
+    const uint64_t words = (uint64_t)n * (row_bytes / 4u);
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1u, std::min<uint64_t>((words + 255u) / 256u, c->n_cu * 16u));
+    const int e = ppe_launch_rows(&k, grid, stream);
+    if (e != 0) return fail(c, PPE_EIO, "rows kernel: %s", hipGetErrorString((hipError_t)e));
+    return PPE_OK;
+}
+
+int ppe_gather_rows(ppe_ctx_t *c, const void *src, uint32_t row_bytes, const uint32_t *perm, uint32_t n, void *dst,
+                    void *stream) {
+    return rows(c, src, row_bytes, perm, n, dst, 0, stream);
+}
+
+int ppe_scatter_rows(ppe_ctx_t *c, const void *src, uint32_t row_bytes, const uint32_t *perm, uint32_t n, void *dst,
+                     void *stream) {
+    return rows(c, src, row_bytes, perm, n, dst, 1, stream);
 }
 
 }  // extern "C"

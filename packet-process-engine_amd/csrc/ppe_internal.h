@@ -102,6 +102,25 @@ struct ppe_kargs {
     struct ppe_flowdev flow;    /* flow-table launches (ppe_classify_flow, one batch) */
 };
 
+/* flow-hash steering across GPUs (ppe_steer_partition / ppe_gather_rows / ppe_scatter_rows) */
+#define PPE_STEER_MAX_WORLD 16
+struct ppe_steer_kargs {
+    const uint32_t *verdict;      /* stateless verdict words (PPE_F_L4 in the flags) */
+    const uint32_t *flow_hash;
+    uint32_t n, world, rank, pad;
+    uint32_t *tcount;             /* [tiles][world]: per-tile owner counts, then exclusive offsets into perm */
+    uint32_t *perm;               /* [n]: packet indices grouped by owner, ascending within an owner */
+    uint32_t *counts;             /* [world] */
+};
+struct ppe_rows_kargs {
+    const uint8_t *src;
+    uint8_t *dst;
+    const uint32_t *perm;
+    uint32_t n, row_bytes;        /* row_bytes: a multiple of 4, <= 256 */
+    uint32_t scatter;             /* 0: dst[i] = src[perm[i]]; 1: dst[perm[i]] = src[i] */
+    uint32_t pad;
+};
+
 struct ppe_tuple_kargs {
     const uint32_t *tuple;    /* n × {sip, dip, sport | dport << 16, proto} */
     const uint32_t *macs;     /* optional n × {dmac lo, dmac hi, smac lo, smac hi} */
@@ -134,6 +153,9 @@ enum { PPE_FLOW_K_CLAIM = 0, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_REVOKE, PPE_FLOW_K_F
        PPE_FLOW_K_REHASH };
 int ppe_launch_flow(int kind, const struct ppe_flow_kargs *a, uint32_t grid, void *stream);
 #define PPE_FLOW_BLOCK 256      /* flow kernels' workgroup size */
+/* steering: 0 count, 1 scan (one workgroup), 2 scatter the permutation; rows: gather / scatter of fixed rows */
+int ppe_launch_steer(int phase, const struct ppe_steer_kargs *a, uint32_t grid, void *stream);
+int ppe_launch_rows(const struct ppe_rows_kargs *a, uint32_t grid, void *stream);
 #define PPE_FLOW_BLOCK_WAVES 4u /* waves (tiles in flight) per flow-kernel workgroup */
 int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block);
 uint32_t ppe_classify_fixed_lds(int block);

@@ -1122,6 +1122,95 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_rehash_kernel(ppe_flow_kargs a
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Flow-hash steering across GPUs (with the flow table, packets go to the GPU owning their flow,
+// as Octeon's PIP tag steering sends a flow to one core, dataplane/src/platform/oct-init.c:139-151).
+// owner(p) = flow_hash % world for packets that reach the flow table, the local rank for the rest; perm lists the
+// packets grouped by owner, ascending within an owner (a stable partition), so each owner sees every source's
+// packets in their original order.
+
+__device__ __forceinline__ uint32_t steer_owner(const ppe_steer_kargs &a, uint32_t p) {
+    const uint32_t v = a.verdict[p];
+    return ((v >> 16) & PPE_F_L4) ? a.flow_hash[p] % a.world : a.rank;
+}
+
+// one wave per 64-packet tile: owner counts of the tile (and, SCATTER, each packet's slot in perm)
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void ppe_steer_tile_kernel(ppe_steer_kargs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gw = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), W = gridDim.x * 4u;
+    const uint32_t ntiles = (a.n + 63u) >> 6;
+    for (uint32_t t = gw; t < ntiles; t += W) {
+        const uint32_t p = (t << 6) + lane;
+        const bool valid = p < a.n;
+        const uint32_t own = valid ? steer_owner(a, p) : 0xffffffffu;
+        uint32_t cnt = 0, rank_in = 0;
+        for (uint32_t o = 0; o < a.world; ++o) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64(own == o);
+            if (lane == o) cnt = (uint32_t)__popcll(m);
+            if (own == o)
+                rank_in = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        }
+        if (!SCATTER) {
+            if (lane < a.world) a.tcount[(size_t)t * a.world + lane] = cnt;
+        } else if (valid) {
+            a.perm[a.tcount[(size_t)t * a.world + own] + rank_in] = p;
+        }
+    }
+}
+
+// one workgroup: tcount[t][o] ← the offset in perm of tile t's first packet owned by o (owner-major, tile order)
+#define STEER_SCAN_T 512u
+__global__ __launch_bounds__(STEER_SCAN_T) void ppe_steer_scan_kernel(ppe_steer_kargs a) {
+    __shared__ uint32_t part[PPE_STEER_MAX_WORLD][STEER_SCAN_T];
+    __shared__ uint32_t base[PPE_STEER_MAX_WORLD];
+    const uint32_t tid = threadIdx.x, W = a.world, ntiles = (a.n + 63u) >> 6;
+    const uint32_t chunk = (ntiles + STEER_SCAN_T - 1u) / STEER_SCAN_T, lo = min(tid * chunk, ntiles),
+                   hi = min(lo + chunk, ntiles);
+    for (uint32_t o = 0; o < W; ++o) {
+        uint32_t sum = 0;
+        for (uint32_t t = lo; t < hi; ++t) sum += a.tcount[(size_t)t * W + o];
+        part[o][tid] = sum;
+    }
+    __syncthreads();
+    for (uint32_t off = 1; off < STEER_SCAN_T; off <<= 1) {  // inclusive scans, one per owner
+        uint32_t v[PPE_STEER_MAX_WORLD];
+        for (uint32_t o = 0; o < W; ++o) v[o] = tid >= off ? part[o][tid - off] : 0u;
+        __syncthreads();
+        for (uint32_t o = 0; o < W; ++o) part[o][tid] += v[o];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        uint32_t b = 0;
+        for (uint32_t o = 0; o < W; ++o) {
+            base[o] = b;
+            a.counts[o] = part[o][STEER_SCAN_T - 1u];
+            b += part[o][STEER_SCAN_T - 1u];
+        }
+    }
+    __syncthreads();
+    for (uint32_t o = 0; o < W; ++o) {
+        uint32_t run = base[o] + (tid ? part[o][tid - 1] : 0u);
+        for (uint32_t t = lo; t < hi; ++t) {
+            const uint32_t c = a.tcount[(size_t)t * W + o];
+            a.tcount[(size_t)t * W + o] = run;
+            run += c;
+        }
+    }
+}
+
+// fixed-size rows through a permutation, 4 B per lane-step
+__global__ __launch_bounds__(256) void ppe_rows_kernel(ppe_rows_kargs a) {
+    const uint32_t words = a.row_bytes >> 2;
+    const uint64_t total = (uint64_t)a.n * words;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 256u) {
+        const uint32_t r = (uint32_t)(i / words), w = (uint32_t)(i % words);
+        const uint32_t q = a.perm[r];
+        const uint64_t from = a.scatter ? r : q, to = a.scatter ? q : r;
+        ((uint32_t *)a.dst)[to * words + w] = ((const uint32_t *)a.src)[from * words + w];
+    }
+}
+
 // ACL-only lookup over pre-decoded tuples (the DP_Acl_Lookup(mbuf) entry, dataplane/src/flow/flow.c:232):
 // tuple = {sip, dip, sport | dport << 16, proto}, macs = {dmac lo, dmac hi, smac lo, smac hi} (optional).
 template <int MODE>
@@ -1235,6 +1324,19 @@ extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, in
 
 // LDS of a workgroup besides the staged image: the per-wave walk keys and the counter bins
 extern "C" uint32_t ppe_classify_fixed_lds(int block) { return (uint32_t)(block / 64) * KEY_WAVE_BYTES + PPE_LDS_FIXED; }
+
+extern "C" int ppe_launch_steer(int phase, const ppe_steer_kargs *a, uint32_t grid, void *stream) {
+    const hipStream_t s = (hipStream_t)stream;
+    if (phase == 0) hipLaunchKernelGGL(ppe_steer_tile_kernel<false>, dim3(grid), dim3(256), 0, s, *a);
+    else if (phase == 1) hipLaunchKernelGGL(ppe_steer_scan_kernel, dim3(1), dim3(STEER_SCAN_T), 0, s, *a);
+    else hipLaunchKernelGGL(ppe_steer_tile_kernel<true>, dim3(grid), dim3(256), 0, s, *a);
+    return (int)hipGetLastError();
+}
+
+extern "C" int ppe_launch_rows(const ppe_rows_kargs *a, uint32_t grid, void *stream) {
+    hipLaunchKernelGGL(ppe_rows_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a);
+    return (int)hipGetLastError();
+}
 
 extern "C" int ppe_launch_acl_tuples(const ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream) {
     const size_t keys = (size_t)ppe_classify_fixed_lds(PPE_BLOCK);

@@ -119,6 +119,7 @@ EXPORTS = [
     "ppe_launch_info", "ppe_debug_trace", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
     "ppe_get_tuning", "ppe_flow_create", "ppe_flow_destroy", "ppe_classify_flow", "ppe_flow_age", "ppe_flow_info",
     "ppe_flow_clear_stat", "ppe_flow_dump", "ppe_format_pkt_stat", "ppe_format_flow_stat",
+    "ppe_steer_partition", "ppe_gather_rows", "ppe_scatter_rows",
     # ppe_acl.h
     "ppe_rule_list_init", "ppe_rule_list_free", "Rule_add", "Rule_del_by_id", "Rule_del_all",
     "Rule_duplicate_check", "Rule_Load_Line", "ppe_rule_load_file", "DP_Acl_Rule_Init", "DP_Acl_Load_Rule",
@@ -195,6 +196,9 @@ def _open(p: Path, mode) -> C.CDLL:
         "ppe_flow_clear_stat": ([vp], C.c_int),
         "ppe_flow_dump": ([vp, vp, u32, C.POINTER(u32)], C.c_int),
         "ppe_format_pkt_stat": ([C.POINTER(Counters), C.c_char_p, C.c_size_t], C.c_int),
+        "ppe_steer_partition": ([vp, vp, vp, u32, u32, u32, vp, vp, vp], C.c_int),
+        "ppe_gather_rows": ([vp, vp, u32, vp, u32, vp, vp], C.c_int),
+        "ppe_scatter_rows": ([vp, vp, u32, vp, u32, vp, vp], C.c_int),
         "ppe_format_flow_stat": ([C.POINTER(FlowInfo), C.c_char_p, C.c_size_t], C.c_int),
         "ppe_rule_list_init": ([], C.c_int),
         "ppe_rule_list_free": ([], None),
