@@ -362,7 +362,11 @@ def run_flow(args, cfgd, dev, world, rank, dist):
     nbufs = args.nbufs or 8
     eng = Engine(int(os.environ.get("LOCAL_RANK", "0")))
     acl = eng.commit(rules, default_action=abi.ACL_RULE_ACTION_FW)
-    tseed = synth.SEED + 977 * (rank + 1)  # this rank's flow population (flow-hash sharding: disjoint per GPU)
+    # N = 1: one flow population.  N > 1: the ranks share one population and every batch is steered by flow hash
+    # to the owning GPU (ppe.dist.steered_classify_flow: all-to-all over RCCL), so flows span ranks as on a NIC that
+    # does not steer by flow
+    steer = world > 1
+    tseed = synth.SEED + 977 * (1 if steer else rank + 1)
 
     # parity sample first: a fresh table, four 64k batches, against the oracle's sequential flow table
     parity = None
@@ -387,7 +391,7 @@ def run_flow(args, cfgd, dev, world, rank, dist):
         parity = bool(ok and len(eng.flow_dump()) == ft.stats()["live"])
         ft.close()
 
-    eng.flow_create(2 * flows, n)
+    eng.flow_create(2 * flows, 2 * n if steer else n)  # a steered batch may exceed n (uneven owners)
     bufs = []
     for b in range(nbufs):
         pk = synth.make_flow_packets(n, rules, flows, seed=tseed + 7919 * (b + 1), template_seed=tseed, stride=stride)
@@ -408,7 +412,16 @@ def run_flow(args, cfgd, dev, world, rank, dist):
     cfgs = [eng.cfg(now_seconds=NOW + i) for i in range(args.warmup + 2 * args.steps + 1)]
     fn = eng.lib.ppe_classify_flow
 
+    sops = None
+    if steer:
+        from ppe.dist import DeviceSteerOps, steered_classify_flow
+        sops = DeviceSteerOps(eng)
+
     def step(i):
+        if steer:
+            hdr, lens, _, _, _ = bufs[i % nbufs]
+            steered_classify_flow(sops, dist, hdr, lens, cfgs[i], world, rank)
+            return
         bb, rr = calls[i % nbufs]
         rc = fn(eng.ctx, C.byref(bb), C.byref(rr), C.byref(cfgs[i]), sptr)
         if rc:
@@ -437,7 +450,11 @@ def run_flow(args, cfgd, dev, world, rank, dist):
     eng.timing(True)
     eng.timing_read(reset=True)
     for i in range(args.steps):
-        step(args.warmup + args.steps + i)
+        if steer:  # the kernel timing runs this rank's own batches through its table, without the exchange
+            bb, rr = calls[i % nbufs]
+            fn(eng.ctx, C.byref(bb), C.byref(rr), C.byref(cfgs[args.warmup + args.steps + i]), sptr)
+        else:
+            step(args.warmup + args.steps + i)
     kern_ms, launches = eng.timing_read(reset=True)
     eng.timing(False)
     info = eng.flow_info()
@@ -476,7 +493,7 @@ def run_flow(args, cfgd, dev, world, rank, dist):
             "config": {"workload": f"{args.config}: {n} x 64B IPv4/UDP packets per GPU per batch over {flows} "
                                    f"bidirectional flows, {cfgd['rules']} five-tuple ACL rules, default FW",
                        "packets_per_gpu": n, "flows": flows, "rules": cfgd["rules"], "resident_batches": nbufs,
-                       "parallelism": f"flow-sharded x{world}"},
+                       "parallelism": f"flow-sharded x{world}" + (" (all-to-all steering by flow hash)" if steer else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
                          "kernel": "ppe_classify_kernel<FLOW> (FlowFind + accounting; misses resolved by the flow "
