@@ -224,15 +224,17 @@ int  ppe_acl_image(ppe_ctx_t *ctx, uint32_t *words, uint32_t *n_words);
 typedef struct {
     uint32_t block;          /* workgroup size 256, 512 or 1024; 0 = chosen per classifier image   */
     uint32_t blocks_per_cu;  /* workgroups per CU (<= 32); 0 = resident count from the occupancy API */
-    uint32_t pipeline;       /* tile fetch: 0 auto (= 4), 1 first tile loaded at the loop top,
-                                4 first tile requested before the image staging; others PPE_EINVAL  */
+    uint32_t pipeline;       /* tile fetch: 0 auto (4 when the image fits in LDS, else 3), 1 first
+                                tile loaded at the loop top, 4 first tile requested before the image
+                                staging, 3 four tiles per wave loaded, decoded and walked together
+                                (one 1024-thread workgroup per CU); others PPE_EINVAL              */
     uint32_t lds_image;      /* 1 = stage the image (or its top) in LDS, 0 = read it from global   */
 } ppe_tuning_t;
 int  ppe_set_tuning(ppe_ctx_t *ctx, const ppe_tuning_t *t);
 int  ppe_get_tuning(ppe_ctx_t *ctx, ppe_tuning_t *t);
 
 /* Launch geometry in use (for profiling notes).  variant = image mode (0 global, 1 LDS, 2 split) | fetch << 4
- * (fetch 0 first tile at the loop top, 1 first tile requested before the image staging). */
+ * (fetch 0 first tile at the loop top, 1 first tile requested before the image staging, 3 four tiles per wave). */
 int  ppe_launch_info(ppe_ctx_t *ctx, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes, uint32_t *variant);
 
 /* Diagnostics: device buffer for per-wave phase timestamps written by a library built with -DPPE_TRACE (make

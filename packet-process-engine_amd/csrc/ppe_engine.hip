@@ -32,7 +32,7 @@ constexpr int kPipeStreams = 2;
 // before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering (next tile's window, or
 // only its first 16 B, requested before the current tile is processed) and an LDS-DMA next-tile pipeline were
 // measured slower and are not built.
-constexpr int kPfNone = 0, kPfHoist = 1;
+constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 
 struct HostStage {
@@ -142,7 +142,7 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl == 1 || pl == 4 ? (uint32_t)pl : 0u;
+    t.pipeline = pl == 1 || pl == 3 || pl == 4 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     return t;
 }
@@ -169,6 +169,10 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
     StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0};
     if (!c->tune.lds_image) {
         if (!c->tune.block) p.block = 256;
+        if (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && !c->tune.block)) {  // PF_MULTI over the global image
+            p.pipe = kPfMulti;
+            p.block = 1024u;
+        }
         return p;
     }
     // the whole image in LDS: the smallest workgroup (most copies per CU) whose share holds it
@@ -180,7 +184,16 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
             }
         }
     }
-    const uint32_t budget = image_budget(p.block);
+    uint32_t budget = image_budget(p.block);
+    // PF_MULTI (tuning pipeline 3, and the default) for images that do not fit whole: 1024-thread workgroups, one
+    // per CU, with the CU's whole LDS for the image prefix (C2 / C3 / C4 step 27.2 / 52.1 / 27.3 -> 23.6 / 42.8 /
+    // 22.7 us)
+    if ((c->tune.pipeline == 3 || c->tune.pipeline == 0) && bytes > budget && !c->tune.block) {
+        p.pipe = kPfMulti;
+        p.block = 1024u;
+        const uint32_t fixed = ppe_classify_fixed_lds(1024) + 1024u;
+        budget = 160u * 1024u - fixed;
+    }
     const uint32_t off_resid = img[PPE_IMG_W_OFFRESID], off_rules = img[PPE_IMG_W_OFFRULES];
     const uint32_t n_nodes = img[PPE_IMG_W_NNODES], off_nodes = img[PPE_IMG_W_OFFNODES];
     if (bytes <= budget) {
@@ -728,9 +741,10 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 4)
-        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top) or 4 (first tile's "
-                                   "loads before the image staging)");
+    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 3 && t->pipeline != 4)
+        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top), 3 (images that do "
+                                   "not fit in LDS: 4 tiles per wave walked together) or 4 (first tile's loads before "
+                                   "the image staging)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     c->tune = *t;
     c->tune.pipeline = t->pipeline;

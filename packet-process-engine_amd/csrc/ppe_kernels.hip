@@ -451,11 +451,26 @@ __device__ __forceinline__ void rule_read(bool in_lds, const uint32_t *gimg, uin
 // First-match ACL lookup: walk to the leaf, then check its candidates in priority order.
 // hit = the matching rule's index or -1; action = its action word, or the default action on a miss.
 template <int MODE, int IMGB, class Mac>
+__device__ __forceinline__ void acl_leaf(const uint32_t *__restrict__ gimg, const AclGeo &g, const uint4 nd,
+                                         uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                                         const Mac &mac, const uint64_t *tsp, uint32_t p, uint64_t now,
+                                         int32_t &hit, uint32_t &action);
+
+template <int MODE, int IMGB, class Mac>
 __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t lanebase,
                                            uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
                                            const Mac &mac, const uint64_t *tsp, uint32_t p, uint64_t now,
                                            int32_t &hit, uint32_t &action) {
     const uint4 nd = acl_walk<MODE, IMGB>(gimg, g, lanebase);
+    acl_leaf<MODE, IMGB>(gimg, g, nd, sip, dip, sport, dport, proto, mac, tsp, p, now, hit, action);
+}
+
+// The leaf's candidates in priority order (nd = the leaf node reached by the walk).
+template <int MODE, int IMGB, class Mac>
+__device__ __forceinline__ void acl_leaf(const uint32_t *__restrict__ gimg, const AclGeo &g, const uint4 nd,
+                                         uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                                         const Mac &mac, const uint64_t *tsp, uint32_t p, uint64_t now,
+                                         int32_t &hit, uint32_t &action) {
     const uint32_t rules_b = 4u * g.off_rules, resid_b = 4u * g.off_resid;
     const bool rules_lds = MODE == IMG_LDS || (MODE == IMG_SPLIT && g.lds_words >= g.off_resid);
     const bool resid_lds = MODE == IMG_LDS;
@@ -506,6 +521,64 @@ __device__ __forceinline__ void acl_lookup(const uint32_t *__restrict__ gimg, co
         action = m ? rb.z >> 16 : action;
         done = done || m;
         if (__builtin_amdgcn_ballot_w64(!done && j + 1u < cnt) == 0) break;
+    }
+}
+
+// Multi-tile walk (PF_MULTI, split / global images): the lanes of MT tiles walk in lockstep, so each level issues MT
+// independent node reads and one wave keeps MT walks in flight.  Keys come from registers (a 5-way select per level
+// instead of the LDS key slots); a lane stops reading at its leaf.
+__device__ __forceinline__ uint32_t key_sel(uint32_t d, const uint32_t (&k)[5]) {
+    return d == 0u ? k[0] : d == 1u ? k[1] : d == 2u ? k[2] : d == 3u ? k[3] : d == 4u ? k[4] : 0u;
+}
+
+template <int MODE, int IMGB, int MT>
+__device__ __forceinline__ void acl_walk_mt(const uint32_t *__restrict__ gimg, const AclGeo &g,
+                                            const uint32_t (&key)[MT][5], const bool (&need)[MT], uint4 (&nd)[MT]) {
+    uint32_t noff[MT], dim[MT];
+    bool done[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        noff[t] = 4u * PPE_IMG_HDR_WORDS;
+        dim[t] = g.root_ks >> 8;
+        if (g.jump) {
+            const uint32_t kk = key_sel(g.jump & 0xffu, key[t]);
+            const uint32_t jo = 4u * PPE_IMG_HDR_WORDS + 4u * (kk >> ((g.jump >> 8) & 0xffu));
+            const uint32_t e = (MODE == IMG_LDS || (MODE == IMG_SPLIT && g.lds_words >= g.off_nodes))
+                                   ? lds_u32(IMGB + jo) : gld<uint32_t>(gimg, jo);
+            noff[t] = e & 0xffffffu;
+            dim[t] = e >> 24;
+        }
+        done[t] = !need[t];
+        nd[t] = make_uint4(PPE_LEAF_THR, 0u, 0u, 0u);
+    }
+    const uint32_t n_lds = MODE == IMG_GLOBAL ? 0u : (MODE == IMG_LDS ? g.max_depth + 1u : g.lds_iters);
+#pragma unroll 1
+    for (uint32_t it = 0; it <= g.max_depth; ++it) {
+        uint4 x[MT];
+        if (it < n_lds) {
+#pragma unroll
+            for (int t = 0; t < MT; ++t) x[t] = lds_u128(IMGB + noff[t]);
+        } else {
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+                if (!done[t]) x[t] = gld<uint4>(gimg, noff[t]);
+        }
+        bool pending = false;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            if (!done[t]) {
+                nd[t] = x[t];
+                if (x[t].x == PPE_LEAF_THR) {
+                    done[t] = true;
+                } else {
+                    const bool gt = key_sel(dim[t], key[t]) > x[t].x;
+                    noff[t] = gt ? x[t].z : x[t].y;
+                    dim[t] = gt ? (x[t].w >> 24) : ((x[t].w >> 8) & 0xffu);
+                    pending = true;
+                }
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
     }
 }
 
@@ -640,12 +713,22 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
 // PF: when a tile's window is fetched
 #define PF_NONE 0   // at the top of its own iteration
 #define PF_HOIST 1  // as PF_NONE, but the first tile's loads are issued before the image staging
+#define PF_MULTI 3  // split / global images: each wave loads, decodes and walks PPE_MT tiles together (acl_walk_mt),
+                    // 4 waves/SIMD with 128 VGPRs, one 1024-thread workgroup per CU and its whole LDS for the image
+#ifndef PPE_MT
+#define PPE_MT 4
+#endif
+#ifndef PPE_MT_WAVES  // waves per SIMD the PF_MULTI kernel is compiled for (VGPR budget 512 / this)
+#define PPE_MT_WAVES 4
+#endif
 
 // FLOW: stateful flow-table mode (ppe_classify_flow, one batch): packets whose flow exists are accounted and
 // forwarded here; the rest are recorded for the claim / resolve / finalize kernels below, which complete their
 // tiles (verdict, compaction, counters).
 template <int MODE, int PF, int BLOCK, bool FLOW>
-__global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(ppe_kargs a) {
+__global__ __launch_bounds__(BLOCK, (PF == PF_MULTI && !FLOW) ? PPE_MT_WAVES : PPE_WAVES_PER_EU)
+void ppe_classify_kernel(ppe_kargs a) {
+    constexpr int MT = (PF == PF_MULTI && !FLOW) ? PPE_MT : 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     using L = Lds<BLOCK>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
@@ -673,7 +756,7 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
         qlen = gld<uint32_t>(B.len, 4u * pc);
     };
     // first window in flight during the image staging
-    bool have = PF == PF_HOIST && twave < ((B.n + 63u) >> 6);
+    bool have = PF == PF_HOIST && twave < ((B.n + 63u) >> 6);  // (PF_MULTI: first tiles loaded at the loop top)
     if (have) load_tile(twave);
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
@@ -698,50 +781,8 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
 
     unsigned long long rx_bytes = 0;  // STAT_RECV_PB_ADD (oct-rxtx.c:213) of this lane's packets
 
-    // one tile: decode, hash, ACL, stores, compaction, counters.  w = the window's first 52 bytes, wlen = wire length
-    auto process = [&](uint32_t tile, const uint32_t (&w)[13], uint32_t wlen) {
-        const uint32_t p = (tile << 6) + lane;
-        const bool valid = p < B.n;
-        if (!(PPE_ABLATE & 2) && valid) rx_bytes += wlen;
-        Dec k = decode(w, wlen, B.hdr, p, B.stride, a.syn_check);
-
-        uint32_t fh = 0;
-        int32_t hit = -1;
-        if (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4)) fh = flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport);
-        if (PPE_TRACE && titer < 4) {
-            asm volatile("" ::"v"(fh), "v"(k.st));  // decoded + hashed before the stamp
-            TRACE_AT(4 + 5 * titer);
-        }
-        bool pend = false;  // FLOW: flow not in the table; resolved by the kernels after this one
-        if (FLOW && (k.flags & PPE_F_L4)) {  // FlowGetFlowFromHash, flow.c:181-201
-            const uint32_t ports = k.sport | (k.dport << 16);
-            uint32_t fsip = 0, fports = 0;
-            const int32_t s = flow_find(a.flow, fh, k.sip, k.dip, ports, k.proto, fsip, fports);
-            if (s >= 0) {  // found: STAT_ACL_FW without an ACL lookup, then FlowHandlePacket's accounting
-                if (valid) k.flags |= flow_account(a.flow, (uint32_t)s, fsip, fports, k.sip, ports, wlen, a.now);
-                k.st = PPE_ST_ACL_FW;
-            } else {
-                pend = valid;
-            }
-        }
-        if ((PPE_ABLATE & 1) && k.st == ST_ACL) {
-            k.st = PPE_ST_ACL_FW;
-            k.flags |= PPE_F_ACL;
-        }
-        if (!(PPE_ABLATE & 1) && k.st == ST_ACL) {
-            uint32_t rule_act;
-            const MacFromWindow mac = {B.hdr, p, B.stride};
-            lds_st32(lanebase + 256u * PPE_DIM_SIP, k.sip);
-            lds_st32(lanebase + 256u * PPE_DIM_DIP, k.dip);
-            lds_st32(lanebase + 256u * PPE_DIM_SPORT, k.sport);
-            lds_st32(lanebase + 256u * PPE_DIM_DPORT, k.dport);
-            lds_st32(lanebase + 256u * PPE_DIM_PROTO, k.proto);
-            acl_lookup<MODE, L::IMGB>(a.img, geo, lanebase, k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts, p,
-                                      a.now, hit, rule_act);
-            const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
-            k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
-            k.flags |= PPE_F_ACL;
-        }
+    // after the ACL: verdict / hash / hit stores, FLOW pending records, compaction, counters
+    auto finish = [&](uint32_t tile, uint32_t p, bool valid, const Dec &k, uint32_t fh, int32_t hit, bool pend) {
         const uint32_t st = k.st;
         const uint32_t act = (uint32_t)(act_table >> (2u * st)) & 3u;
         if (PPE_TRACE && titer < 4) {
@@ -791,6 +832,112 @@ __global__ __launch_bounds__(BLOCK, PPE_WAVES_PER_EU) void ppe_classify_kernel(p
         ++titer;
     };
 
+    // one tile: decode, hash, ACL, stores, compaction, counters.  w = the window's first 52 bytes, wlen = wire length
+    auto process = [&](uint32_t tile, const uint32_t (&w)[13], uint32_t wlen) {
+        const uint32_t p = (tile << 6) + lane;
+        const bool valid = p < B.n;
+        if (!(PPE_ABLATE & 2) && valid) rx_bytes += wlen;
+        Dec k = decode(w, wlen, B.hdr, p, B.stride, a.syn_check);
+
+        uint32_t fh = 0;
+        int32_t hit = -1;
+        if (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4)) fh = flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport);
+        if (PPE_TRACE && titer < 4) {
+            asm volatile("" ::"v"(fh), "v"(k.st));  // decoded + hashed before the stamp
+            TRACE_AT(4 + 5 * titer);
+        }
+        bool pend = false;  // FLOW: flow not in the table; resolved by the kernels after this one
+        if (FLOW && (k.flags & PPE_F_L4)) {  // FlowGetFlowFromHash, flow.c:181-201
+            const uint32_t ports = k.sport | (k.dport << 16);
+            uint32_t fsip = 0, fports = 0;
+            const int32_t s = flow_find(a.flow, fh, k.sip, k.dip, ports, k.proto, fsip, fports);
+            if (s >= 0) {  // found: STAT_ACL_FW without an ACL lookup, then FlowHandlePacket's accounting
+                if (valid) k.flags |= flow_account(a.flow, (uint32_t)s, fsip, fports, k.sip, ports, wlen, a.now);
+                k.st = PPE_ST_ACL_FW;
+            } else {
+                pend = valid;
+            }
+        }
+        if ((PPE_ABLATE & 1) && k.st == ST_ACL) {
+            k.st = PPE_ST_ACL_FW;
+            k.flags |= PPE_F_ACL;
+        }
+        if (!(PPE_ABLATE & 1) && k.st == ST_ACL) {
+            uint32_t rule_act;
+            const MacFromWindow mac = {B.hdr, p, B.stride};
+            lds_st32(lanebase + 256u * PPE_DIM_SIP, k.sip);
+            lds_st32(lanebase + 256u * PPE_DIM_DIP, k.dip);
+            lds_st32(lanebase + 256u * PPE_DIM_SPORT, k.sport);
+            lds_st32(lanebase + 256u * PPE_DIM_DPORT, k.dport);
+            lds_st32(lanebase + 256u * PPE_DIM_PROTO, k.proto);
+            acl_lookup<MODE, L::IMGB>(a.img, geo, lanebase, k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts, p,
+                                      a.now, hit, rule_act);
+            const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
+            k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
+            k.flags |= PPE_F_ACL;
+        }
+        finish(tile, p, valid, k, fh, hit, pend);
+    };
+
+    if constexpr (MT > 1) {
+        // PF_MULTI: wave w takes tiles [MT w, MT w + MT), then + MT W, ...; all MT windows are requested together
+        for (uint32_t bi = 0; bi < a.nbatch; ++bi) {
+            if (bi) B = a.batch[bi];
+            const uint32_t ntiles = (B.n + 63u) >> 6;
+            for (uint32_t t0 = twave * MT; t0 < ntiles; t0 += stride_waves * MT) {
+                uint4 r0[MT], r1[MT], r2[MT];
+                uint32_t r3[MT], rl[MT];
+#pragma unroll
+                for (int t = 0; t < MT; ++t) {
+                    const uint32_t pc = min(((t0 + t) << 6) + lane, B.n - 1u);
+                    const uint32_t ro = pc * B.stride;
+                    r0[t] = gld<uint4>(B.hdr, ro);
+                    r1[t] = gld<uint4>(B.hdr, ro + 16u);
+                    r2[t] = gld<uint4>(B.hdr, ro + 32u);
+                    r3[t] = gld<uint32_t>(B.hdr, ro + 48u);
+                    rl[t] = gld<uint32_t>(B.len, 4u * pc);
+                }
+                Dec k[MT];
+                uint32_t fh[MT], key[MT][5];
+                bool need[MT];
+#pragma unroll
+                for (int t = 0; t < MT; ++t) {
+                    const uint32_t p = ((t0 + t) << 6) + lane;
+                    const bool valid = p < B.n;
+                    if (valid) rx_bytes += rl[t];
+                    const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
+                                            r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
+                    k[t] = decode(w, rl[t], B.hdr, p, B.stride, a.syn_check);
+                    fh[t] = (k[t].flags & PPE_F_L4) ? flow_hashfn_l4(k[t].proto == 6u, k[t].sip, k[t].dip, k[t].sport,
+                                                                     k[t].dport) : 0u;
+                    need[t] = k[t].st == ST_ACL;
+                    key[t][0] = k[t].sip;
+                    key[t][1] = k[t].dip;
+                    key[t][2] = k[t].sport;
+                    key[t][3] = k[t].dport;
+                    key[t][4] = k[t].proto;
+                }
+                uint4 nd[MT];
+                acl_walk_mt<MODE, L::IMGB, MT>(a.img, geo, key, need, nd);
+#pragma unroll
+                for (int t = 0; t < MT; ++t) {
+                    const uint32_t tile = t0 + t;
+                    if (tile >= ntiles) break;  // wave-uniform
+                    const uint32_t p = (tile << 6) + lane;
+                    int32_t hit = -1;
+                    if (need[t]) {
+                        uint32_t rule_act;
+                        const MacFromWindow mac = {B.hdr, p, B.stride};
+                        acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], k[t].sip, k[t].dip, k[t].sport, k[t].dport,
+                                                k[t].proto, mac, B.ts, p, a.now, hit, rule_act);
+                        k[t].st = rule_act == ACL_RULE_ACTION_DROP ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
+                        k[t].flags |= PPE_F_ACL;
+                    }
+                    finish(tile, p, p < B.n, k[t], fh[t], hit, false);
+                }
+            }
+        }
+    } else
     for (uint32_t bi = 0; bi < a.nbatch; ++bi) {
         if (bi) B = a.batch[bi];
         const uint32_t ntiles = (B.n + 63u) >> 6;
@@ -1284,6 +1431,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int block) {
 #define PPE_DISPATCH_P(FN, M, ...)                                   \
     do {                                                             \
         if (pipe == PF_NONE) PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__); \
+        if (pipe == PF_MULTI) PPE_DISPATCH_B(FN, M, PF_MULTI, __VA_ARGS__); \
         PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__);                \
     } while (0)
 #define PPE_DISPATCH(FN, ...)                                        \
