@@ -188,7 +188,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
     // PF_MULTI (tuning pipeline 3, and the default) for images that do not fit whole: 1024-thread workgroups, one
     // per CU, with the CU's whole LDS for the image prefix (C2 / C3 / C4 step 27.2 / 52.1 / 27.3 -> 23.6 / 42.8 /
     // 22.7 us)
-    if ((c->tune.pipeline == 3 || c->tune.pipeline == 0) && bytes > budget && !c->tune.block) {
+    if (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && bytes > budget && !c->tune.block)) {
         p.pipe = kPfMulti;
         p.block = 1024u;
         const uint32_t fixed = ppe_classify_fixed_lds(1024) + 1024u;
