@@ -54,8 +54,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
-                    help="2: the K batches go through one ppe_classify_batches call (launches of up to 8 batches "
-                         "alternating over two streams); 1: launches of 8 batches serialized on one stream, no "
+                    help="2: the K batches go through one ppe_classify_batches call (launches of 2 batches "
+                         "alternating over two streams); 1: launches of 2 batches serialized on one stream, no "
                          "overlap (profiling: kernel durations = step times)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (16 threads)")
@@ -141,7 +141,7 @@ def main():
 
     # the same batches as launches of GROUP batches each, serialized on `stream` (one ppe_classify_batches call per
     # group: its single launch goes on the caller's stream), so launch durations do not overlap
-    GROUP = 8
+    GROUP = 2  # = the engine's batches per launch (kBatchesPerLaunch): one launch per call
 
     def steps_grouped(k):
         for g0 in range(0, k, GROUP):
@@ -173,7 +173,7 @@ def main():
     ev1.record(stream)
     barrier()
     elapsed_ms = ev0.elapsed_time(ev1)
-    # timed region 2 (roofline): the same K batches as launches of 8 batches serialized on `stream` (no overlap
+    # timed region 2 (roofline): the same K batches as launches of 2 batches serialized on `stream` (no overlap
     # between launches), with the dispatch's own start / end timestamps (hipExtLaunchKernelGGL events) around each
     eng.timing(True)
     eng.timing_read(reset=True)

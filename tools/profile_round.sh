@@ -20,6 +20,6 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv 
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES --kernel-trace --output-format csv -d $O/sq -o c1 -- python3 $P > $O/sq.log 2>&1
 python3 tools/collect_traffic.py --fetch $O/fetch/c1_counter_collection.csv --write $O/write/c1_counter_collection.csv \
   --cal-fetch $O/cal_fetch/cal_counter_collection.csv --cal-write $O/cal_write/cal_counter_collection.csv \
-  --n $((8 * 1048576)) --out $O/${R}_traffic_C1.json > $O/traffic.log 2>&1
-python3 tools/pmc_summary.py $O/sq/c1_counter_collection.csv --tiles $((8 * 16384)) > $O/sq_summary.txt 2>&1
+  --n $((2 * 1048576)) --out $O/${R}_traffic_C1.json > $O/traffic.log 2>&1
+python3 tools/pmc_summary.py $O/sq/c1_counter_collection.csv --tiles $((2 * 16384)) > $O/sq_summary.txt 2>&1
 echo profile done
