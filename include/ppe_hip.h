@@ -176,7 +176,9 @@ int  ppe_classify(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out
 int  ppe_classify_batches(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, uint32_t nbatch,
                           const ppe_cfg_t *cfg, void *stream);
 
-/* Host-resident batch: pipelined H2D → classify → D2H over `chunk`-packet slices on internal streams.
+/* Host-resident batch.  When every buffer is pinned and device-mapped (hipHostMalloc, hipHostRegister, a pinned
+ * torch tensor), the kernel reads and writes them across PCIe directly (zero-copy; PPE_HOST_ZEROCOPY=0 disables);
+ * otherwise pipelined H2D → classify → D2H over `chunk`-packet slices on internal streams.
  * Output pointers are host pointers (NULL to skip).  Blocks until done. */
 int  ppe_classify_host(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
                        uint32_t chunk);

@@ -123,6 +123,33 @@ def test_golden_fixture_host_pipeline(eng, golden):
         check_compaction(res, len(g["len"]))
 
 
+@pytest.mark.parametrize("zerocopy", ["1", "0"])
+def test_host_pinned_buffers(eng, monkeypatch, zerocopy):
+    """ppe_classify_host on pinned host buffers: zero-copy (the kernel reads / writes host memory across PCIe) and,
+    with PPE_HOST_ZEROCOPY=0, the staged H2D / D2H pipeline — both bit-exact against the oracle."""
+    monkeypatch.setenv("PPE_HOST_ZEROCOPY", zerocopy)
+    rules = synth.make_rules(256, seed=61)
+    pk = synth.make_packets(100_003, rules, seed=62, kind="imix", stride=128, malformed_frac=0.02, with_ts=True)
+    eng.commit(rules, default_action=1)
+    n = len(pk["len"])
+    ph = torch.from_numpy(pk["hdr"]).pin_memory()
+    pl = torch.from_numpy(pk["len"].view(np.int32)).pin_memory()
+    pt = torch.from_numpy(pk["ts"].view(np.int64)).pin_memory()
+    out = {k: torch.full((n,), -7, dtype=torch.int32).pin_memory() for k in ("verdict", "flow_hash", "acl_hit", "part")}
+    b = abi.Batch(ph.data_ptr(), pl.data_ptr(), pt.data_ptr(), n, 128)
+    r = abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(),
+                   out["part"].data_ptr(), out["part"].data_ptr(), None, None)
+    cfg = eng.cfg(now_seconds=NOW)
+    assert eng.lib.ppe_classify_host(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), 1 << 14) == 0
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"], pk["len"], ts=pk["ts"], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    got = {k: v.numpy() for k, v in out.items()}
+    assert np.array_equal(got["verdict"].view(np.uint32), ref["verdict"])
+    assert np.array_equal(got["flow_hash"].view(np.uint32), ref["flow_hash"])
+    assert np.array_equal(got["acl_hit"], ref["acl_hit"])
+    check_partition({"verdict": got["verdict"].view(np.uint32), "part_idx": got["part"].view(np.uint32)}, n)
+
+
 def test_flow_hash_matches_reference_tluhash(eng, ref_hash):
     """Packets built from the reference-hashed tuples: the GPU flow hash equals the value the reference's own
     dataplane/src/flow/tluhash.h produced (fixture made by tests/golden/gen_golden.py from oracle/_ref)."""
