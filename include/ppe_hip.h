@@ -315,6 +315,96 @@ int  ppe_scatter_rows(ppe_ctx_t *ctx, const void *src, uint32_t row_bytes, const
 int  ppe_format_pkt_stat(const ppe_counters_t *c, char *buf, size_t cap);
 int  ppe_format_flow_stat(const ppe_flow_info_t *f, char *buf, size_t cap);
 
+/* ---- IPv4 reassembly (dataplane/src/decode/decode-defrag.c) ----
+ * ppe_classify PUNTs fragments (PPE_ST_FRAG).  ppe_defrag runs the reference's Defrag (decode-defrag.c:449-487) for
+ * a batch of them, with exactly the sequential semantics of one core handling the fragments in index order:
+ *   FragFind / fcb_create on (sip, dip, ip_id) (decode-defrag.c:115-146, 71-97; at most fcb_max FCBs, STAT_FRAG_FCB_FULL),
+ *   PACKET_HW2SW into a 2 KB buffer (mbuf.c:117-156: pkt_totallen > frag_buf_bytes drops, STAT_FRAG_HW2SW_ERR),
+ *   the DELETE / cache_max checks of Frag_defrag_begin (decode-defrag.c:412-446) and Frag_defrag_process
+ *   (decode-defrag.c:292-406) — ordered fragment chain, overlap ("teardrop") and last-fragment checks, including the
+ *   reference's chain scan that compares frag_len (not frag_offset) with the new offset (decode-defrag.c:344-349);
+ *   on completion Frag_defrag_reasm (decode-defrag.c:222-289): the head fragment's whole frame followed by every
+ *   later fragment's last frag_len bytes, ip_len = ihl*4 + total, ip_off = 0, header checksum recomputed (ICMP: the
+ *   head frame only, ip_off = 0).  A datagram whose buffer (total + L2 + ihl*4) exceeds reasm_buf_bytes fails as
+ *   STAT_FRAG_SETUP_ERR (MEM_8K_ALLOC, decode-defrag.c:173-183) and its fragments stay cached.
+ * Reassembled datagrams come out as a classify-ready batch: the reference continues with DecodeTCP / DecodeUDP /
+ * the flow table on them (decode-ipv4.c:241-290), which ppe_classify / ppe_classify_flow of that batch reproduce
+ * (their L2 / IPv4 checks pass by construction; the counters of that classify count the datagram once more).
+ * The datagram's verdict applies to all of its fragments (the reference forwards or frees the chain with it).
+ * Aging (Frag_defrag_timeout, decode-defrag.c:490-551, every second): ppe_defrag_age frees completed FCBs and those
+ * idle for more than timeout_seconds (FRAG_MAX_TIMEOUT 20 s), dropping the fragments they still hold. */
+enum ppe_defrag_status {
+    PPE_DF_CACHED = 0,        /* held in its FCB's chain                                  STAT_FRAG_CACHE_OK   */
+    PPE_DF_REASM = 1,         /* completed its datagram (dgram_of = its index)            STAT_FRAG_REASM_OK   */
+    PPE_DF_SETUP_ERR = 2,     /* completed, but the reassembly buffer is too small: held  STAT_FRAG_SETUP_ERR  */
+    PPE_DF_FCB_FULL = 3,      /* drop: fcb_max FCBs in use                                STAT_FRAG_FCB_FULL   */
+    PPE_DF_HW2SW_ERR = 4,     /* drop: frame longer than frag_buf_bytes                   STAT_FRAG_HW2SW_ERR  */
+    PPE_DF_DELETED = 5,       /* drop: its FCB already reassembled, awaiting aging (decode-defrag.c:422-427)    */
+    PPE_DF_CACHE_FULL = 6,    /* drop: cache_max fragments already held                   STAT_FRAG_CACHE_FULL */
+    PPE_DF_DEFRAG_ERR = 7,    /* drop: overlap / duplicate last fragment / short final    STAT_FRAG_DEFRAG_ERR */
+    PPE_DF_NOT_FRAG = 8,      /* input is not an IPv4 fragment Defrag would see (caller error; untouched)      */
+    PPE_DF__COUNT = 9
+};
+#define PPE_DF_TEARDROP 0x100u   /* | PPE_DF_DEFRAG_ERR: an overlap (DP_Teardrop_Attack_Monitor, decode-defrag.c:395-398) */
+
+typedef struct {
+    uint32_t fcb_max;          /* 0 → DEFRAG_FCB_MAX 1024 (decode-defrag.h:11)                                 */
+    uint32_t cache_max;        /* 0 → defrag_cache_max 8 (decode-defrag.c:24); <= 16                           */
+    uint32_t frag_buf_bytes;   /* 0 → 2024: the 2 KB small-buffer slice minus its 24-B control block
+                                  (mem_pool.c:249, mem_pool.h:62); <= 4096                                     */
+    uint32_t reasm_buf_bytes;  /* 0 → 8168: the 8 KB large-buffer slice minus its control block (mem_pool.c:269) */
+    uint32_t max_batch;        /* fragments per ppe_defrag call; 0 → 65536                                      */
+    uint32_t pad;
+} ppe_defrag_cfg_t;
+
+typedef struct {
+    const uint8_t  *pkt;       /* whole frames, frame i at pkt + off[i] (device)                                 */
+    const uint64_t *off;
+    const uint32_t *len;       /* n × pkt_totallen                                                              */
+    const uint64_t *id;        /* optional n × caller packet ids, echoed in dgram_frags (NULL → the batch index) */
+    uint32_t        n;
+    uint32_t        pad;
+    uint64_t        now_seconds;   /* FCB_UPDATE_TIMESTAMP of every FCB the batch touches                       */
+} ppe_frag_batch_t;
+
+typedef struct {
+    uint32_t *status;          /* n × (enum ppe_defrag_status | PPE_DF_TEARDROP)                                 */
+    uint32_t *dgram_of;        /* optional n: datagram index of a PPE_DF_REASM fragment, else 0xffffffff        */
+    uint8_t  *dgram_hdr;       /* n × hdr_stride: the first bytes of datagram j (a ppe_batch_t.hdr; zero-padded) */
+    uint32_t *dgram_len;       /* n: its pkt_totallen (a ppe_batch_t.len); 0 for j >= the datagram count        */
+    uint8_t  *dgram_pkt;       /* optional n × reasm_buf_bytes: the whole reassembled frames                    */
+    uint64_t *dgram_frags;     /* optional n × cache_max: ids of datagram j's fragments in chain order, ~0 pad   */
+    uint32_t *n_dgram;         /* optional device word: datagrams written                                      */
+    uint32_t  hdr_stride;      /* 64 or 128                                                                    */
+    uint32_t  pad;
+} ppe_defrag_out_t;
+
+typedef struct {
+    uint64_t running;          /* FCBs in use (fcb_running_num)                                                 */
+    uint64_t new_fcb, del_fcb; /* decode-defrag.c:15-16                                                         */
+    uint64_t st[PPE_DF__COUNT];/* fragments per enum ppe_defrag_status                                          */
+    uint64_t teardrop;         /* overlaps among PPE_DF_DEFRAG_ERR                                              */
+    uint64_t timeout_drop;     /* fragments dropped by ppe_defrag_age                                           */
+    uint64_t datagrams;        /* reassembled datagrams emitted                                                 */
+    uint32_t fcb_max, cache_max, frag_buf_bytes, reasm_buf_bytes, max_batch, slots;
+} ppe_defrag_info_t;
+
+typedef struct ppe_defrag_table ppe_defrag_t;
+/* FragModule_init (decode-defrag.c:582-625): a device FCB table on ctx's device.  cfg may be NULL (defaults). */
+int  ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t **out);
+int  ppe_defrag_destroy(ppe_defrag_t *d);                              /* FragModule_Release */
+/* Defrag for a device-resident batch of fragments, stream-ordered on `stream` (batches in call order).
+ * Every output is written for all n entries (dgram_* entries past the datagram count: length 0), so a
+ * ppe_classify of {dgram_hdr, dgram_len, n, hdr_stride} can follow on the same stream without a host sync. */
+int  ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out_t *out, void *stream);
+/* Frag_defrag_timeout: free FCBs that completed, or with now > last && now - last > timeout_seconds; the ids of
+ * the fragments they still held go to dropped[0..max) (host; may be NULL), *n_dropped = their count, *n_freed =
+ * FCBs freed (either may be NULL).  Synchronises. */
+int  ppe_defrag_age(ppe_defrag_t *d, uint64_t now_seconds, uint64_t timeout_seconds, uint64_t *dropped,
+                    uint32_t max, uint32_t *n_dropped, uint32_t *n_freed);
+int  ppe_defrag_info(ppe_defrag_t *d, ppe_defrag_info_t *info);      /* synchronises */
+const char *ppe_defrag_last_error(ppe_defrag_t *d);
+
 /* Human-readable last error of this context (static storage of the ctx). */
 const char *ppe_last_error(ppe_ctx_t *ctx);
 

@@ -86,6 +86,24 @@ uint64_t oracle_flow_age(oracle_flow_t *f, uint64_t now, uint64_t timeout);
 uint32_t oracle_flow_dump(const oracle_flow_t *f, ppe_flow_entry_t *out, uint32_t max);
 void oracle_flow_stats(const oracle_flow_t *f, uint64_t *live, uint64_t *new_flow, uint64_t *del_flow);
 
+/* ---- IPv4 reassembly (dataplane/src/decode/decode-defrag.c; ppe_oracle_defrag.c): one core's FCB table ---- */
+typedef struct oracle_defrag oracle_defrag_t;
+/* 0 → the reference defaults (1024 FCBs, 8 cached fragments, 2024-B / 8168-B buffers) */
+oracle_defrag_t *oracle_defrag_create(uint32_t fcb_max, uint32_t cache_max, uint32_t frag_buf, uint32_t reasm_buf);
+void oracle_defrag_destroy(oracle_defrag_t *d);
+/* Defrag for frames 0..n-1 in order (frame i: pkt + off[i], len[i] bytes); status[i] = enum ppe_defrag_status
+ * (| PPE_DF_TEARDROP); datagram j (completion order): dgram_pkt + j * reasm_buf (zero-filled), dgram_len[j],
+ * dgram_frags[j * cache_max ..] (ids in chain order, ~0 pad); dgram_of[i] = j for the completing fragment, else ~0.
+ * Output pointers other than status may be NULL.  Returns the datagram count. */
+uint32_t oracle_defrag_batch(oracle_defrag_t *d, const uint8_t *pkt, const uint64_t *off, const uint32_t *len,
+                             const uint64_t *ids, uint32_t n, uint64_t now, uint32_t *status, uint32_t *dgram_of,
+                             uint8_t *dgram_pkt, uint32_t *dgram_len, uint64_t *dgram_frags);
+/* Frag_defrag_timeout: returns the number of fragments dropped (first `max` ids copied), *n_freed = FCBs freed */
+uint32_t oracle_defrag_age(oracle_defrag_t *d, uint64_t now, uint64_t timeout, uint64_t *dropped, uint32_t max,
+                           uint32_t *n_freed);
+/* out[5 + PPE_DF__COUNT]: running, new_fcb, del_fcb, st[PPE_DF__COUNT], teardrop, timeout_drop, datagrams */
+void oracle_defrag_stats(const oracle_defrag_t *d, uint64_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,14 @@ def load():
         lib.oracle_flow_dump.argtypes = [vp, vp, u32]
         lib.oracle_flow_dump.restype = u32
         lib.oracle_flow_stats.argtypes = [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]
+        lib.oracle_defrag_create.argtypes = [u32, u32, u32, u32]
+        lib.oracle_defrag_create.restype = vp
+        lib.oracle_defrag_destroy.argtypes = [vp]
+        lib.oracle_defrag_batch.argtypes = [vp, vp, vp, vp, vp, u32, u64, vp, vp, vp, vp, vp]
+        lib.oracle_defrag_batch.restype = u32
+        lib.oracle_defrag_age.argtypes = [vp, u64, u64, vp, u32, C.POINTER(u32)]
+        lib.oracle_defrag_age.restype = u32
+        lib.oracle_defrag_stats.argtypes = [vp, vp]
         _lib = lib
     return _lib
 
@@ -166,6 +174,61 @@ class OracleFlow:
         a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
         self.lib.oracle_flow_stats(self.h, C.byref(a), C.byref(b), C.byref(c))
         return dict(live=a.value, new_flow=b.value, del_flow=c.value)
+
+
+DF_STATS = ["running", "new_fcb", "del_fcb", "st_cached", "st_reasm", "st_setup_err", "st_fcb_full", "st_hw2sw_err",
+            "st_deleted", "st_cache_full", "st_defrag_err", "st_not_frag", "teardrop", "timeout_drop", "datagrams"]
+
+
+class OracleDefrag:
+    """One core's IPv4 reassembly (dataplane/src/decode/decode-defrag.c) restated sequentially in C."""
+
+    def __init__(self, fcb_max=0, cache_max=0, frag_buf=0, reasm_buf=0):
+        self.lib = load()
+        self.h = self.lib.oracle_defrag_create(fcb_max, cache_max, frag_buf, reasm_buf)
+        if not self.h:
+            raise MemoryError("oracle_defrag_create")
+        self.cache_max = cache_max or 8
+        self.reasm_buf = reasm_buf or 8168
+        self.fcb_max = fcb_max or 1024
+
+    def close(self):
+        if self.h:
+            self.lib.oracle_defrag_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def batch(self, pkt, off, lens, now, ids=None, full=True):
+        pkt = np.ascontiguousarray(pkt, np.uint8)
+        off = np.ascontiguousarray(off, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        n = len(lens)
+        out = dict(status=np.zeros(n, np.uint32), dgram_of=np.zeros(n, np.uint32), dgram_len=np.zeros(n, np.uint32),
+                   dgram_frags=np.zeros((n, self.cache_max), np.uint64))
+        if full:
+            out["dgram_pkt"] = np.zeros((n, self.reasm_buf), np.uint8)
+        if ids is not None:
+            ids = np.ascontiguousarray(ids, np.uint64)
+        nd = self.lib.oracle_defrag_batch(self.h, pkt.ctypes.data, off.ctypes.data, lens.ctypes.data,
+                                          ids.ctypes.data if ids is not None else None, n, int(now),
+                                          out["status"].ctypes.data, out["dgram_of"].ctypes.data,
+                                          out["dgram_pkt"].ctypes.data if full else None, out["dgram_len"].ctypes.data,
+                                          out["dgram_frags"].ctypes.data)
+        out["n_dgram"] = int(nd)
+        return out
+
+    def age(self, now, timeout=20):
+        cap = self.fcb_max * self.cache_max
+        ids = np.zeros(cap, np.uint64)
+        nf = C.c_uint32(0)
+        nd = self.lib.oracle_defrag_age(self.h, int(now), int(timeout), ids.ctypes.data, cap, C.byref(nf))
+        return ids[:min(nd, cap)], nf.value
+
+    def stats(self) -> dict:
+        v = np.zeros(len(DF_STATS), np.uint64)
+        self.lib.oracle_defrag_stats(self.h, v.ctypes.data)
+        return {k: int(x) for k, x in zip(DF_STATS, v)}
 
 
 def ref_hash_lib():

@@ -1,0 +1,916 @@
+/*
+ * ppe_defrag.hip — IPv4 reassembly on the GPU (ppe_defrag_* in include/ppe_hip.h).
+ *
+ * The reference's Defrag (dataplane/src/decode/decode-defrag.c:449-487) is sequential per fragment: find or create
+ * the FCB of (sip, dip, ip_id), then run Frag_defrag_begin / Frag_defrag_process on it.  Different FCBs never
+ * interact except through the FCB cap (fcb_create, :71-97), so one batch runs as:
+ *
+ *   parse      one lane per fragment: re-derive the fields DecodeIPV4 stored in the mbuf (decode-ipv4.c:216-222) and
+ *              look the key up in the device FCB hash table (open addressing, linear probing);
+ *   claim      fragments whose FCB does not exist claim a slot (CAS, key = the claiming fragment's parsed key) and
+ *              record the lowest claiming index: that fragment is the one whose fcb_create runs;
+ *   admit      creators in index order (per-tile ballot counts, one-workgroup scan) get FCB records while
+ *              running + rank < fcb_max (fcb_create's fetch-and-add cap); the others fail, and with them every later
+ *              fragment of their key in this batch, because the running count cannot fall inside a batch;
+ *   group      stable LSD radix sort of the fragments by FCB record (8-bit digits, wave multisplit ranks), so each
+ *              FCB's fragments are contiguous and in arrival order;
+ *   process    one lane per FCB runs the reference state machine over its fragments in order (chain ≤ cache_max
+ *              entries, kept as a nibble list of store slots);
+ *   stash      one wave per held fragment copies its frame into the FCB's store slot (PACKET_HW2SW, mbuf.c:117-156);
+ *   place      completing fragments in index order get datagram indices (ballot counts + scan);
+ *   assemble   one workgroup per datagram concatenates the chain (Frag_defrag_reasm, decode-defrag.c:222-289),
+ *              patches ip_len / ip_off / the header checksum, and writes a classify-ready window + length.
+ *
+ * Aging (Frag_defrag_timeout, decode-defrag.c:490-551) is one workgroup: free completed / idle FCBs, then rebuild
+ * the hash table from the live records (which also clears the tombstones left by failed claims).
+ *
+ * Integer / byte work only: the rare path of the classifier (fragments are PUNTed), sized by the fragment count.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "ppe_hip.h"
+
+namespace {
+
+constexpr uint32_t kEmpty = 0u, kTomb = 1u, kLive = 2u, kPend = 0x80000000u;
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kBlock = 256;        // workgroup size of the per-fragment kernels
+constexpr uint32_t kScanT = 1024;       // one-workgroup scans
+constexpr uint32_t kSortBlock = 256;    // radix sort: elements (= threads) per workgroup
+
+// FCB record header word 0
+constexpr uint32_t kRecLive = 1u << 0;
+constexpr uint32_t kRecDelete = 1u << 1;    // DEFRAG_DELETE (decode-defrag.h:21)
+constexpr uint32_t kRecComplete = 1u << 2;  // DEFRAG_COMPLETE: the chain moved to the datagram
+constexpr uint32_t kFirstIn = 1u, kLastIn = 2u;  // DEFRAG_FIRST_IN / DEFRAG_LAST_IN (decode-defrag.h:18-19)
+// header words: 0 flags | last_in << 8 | cache_num << 16 | nlist << 24; 1 total_fraglen; 2 meat; 3 pad;
+//               4,5 chain order (4-bit store slots, position 0 in the low nibble); 6,7 pad
+constexpr uint32_t kRecWords = 8;
+
+// control words (u64)
+enum { C_RUNNING = 0, C_NEW, C_DEL, C_FREE_TOP, C_DGRAMS, C_TEARDROP, C_TIMEOUT_DROP, C_NDGRAM, C_ST0 = 8,
+       C_ADMIT_BASE = C_ST0 + PPE_DF__COUNT, C_FREE_BASE, C_CREATORS, C_AGE_DROPPED, C_AGE_FREED, C_SCRATCH,
+       C_WORDS = 24 };
+
+// parsed fragment record words (frec): sip, dip, id | proto << 16 | mf << 24, off | flen << 16, totlen,
+// l2 | ihl4 << 8, hash, valid
+constexpr uint32_t kFrecWords = 8;
+
+struct DfArgs {
+    // batch
+    const uint8_t *pkt;
+    const uint64_t *off;
+    const uint32_t *len;
+    const uint64_t *id;
+    uint32_t n;
+    uint32_t hdr_stride;
+    uint64_t now;
+    uint64_t timeout;
+    // outputs
+    uint32_t *status;
+    uint32_t *dgram_of;
+    uint8_t *dgram_hdr;
+    uint32_t *dgram_len;
+    uint8_t *dgram_pkt;
+    uint64_t *dgram_frags;
+    uint32_t *n_dgram;
+    // table
+    uint32_t *tstate, *tkey, *creator;
+    uint32_t smask;
+    // records
+    uint32_t *rhdr, *rdesc;
+    unsigned long long *rts, *rid;
+    uint8_t *store;
+    uint32_t *freestk;
+    unsigned long long *ctl;
+    uint32_t fcb_max, cache_max, frag_buf, reasm_buf, sstride;
+    // batch scratch
+    uint32_t *frec, *fslot, *inserted, *dgrec, *dgsrc, *tcnt;
+    uint32_t *skey[2], *sval[2], *hist;
+    uint32_t shift, sort_blocks, sent;   // radix pass: digit shift, workgroups, sentinel key (no record)
+    uint32_t flag_mode;                  // tile counts: 0 creators, 1 completing fragments
+    uint64_t *dropped;                   // age: ids of dropped fragments
+    uint32_t max_dropped;
+};
+
+__device__ __forceinline__ uint32_t ld_be16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
+__device__ __forceinline__ uint32_t ld_be32(const uint8_t *p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+__device__ __forceinline__ uint32_t key_hash(uint32_t sip, uint32_t dip, uint32_t id) {
+    // bucket choice only (the reference's jhash_3words bucket, decode-defrag.c:108-112, orders nothing observable)
+    uint32_t h = sip * 0x9e3779b1u ^ (dip + 0x7f4a7c15u) * 0x85ebca77u ^ (id + 0x165667b1u) * 0xc2b2ae3du;
+    h ^= h >> 15;
+    h *= 0x2c1b3c6du;
+    h ^= h >> 12;
+    return h;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const uint32_t lane = __lane_id();
+    return lane ? (~0ull >> (64u - lane)) : 0ull;
+}
+
+
+// ---- parse + find ------------------------------------------------------------------------------------------------
+// The fields DecodeIPV4 hands to Defrag (decode-ipv4.c:216-222): sip/dip (BE32 @12/16), defrag_id (BE16 @4),
+// frag_offset = (ip_off & 0x1fff) << 3, frag_len = L3 length − ihl*4 where the L3 length is what is left of
+// (uint16_t)pkt_totallen after the L2 header (Decode, decode.c:25; DecodeEthernet / DecodeVLAN len − 14 / − 4).
+// A frame that would not reach Defrag (any earlier drop, not a fragment, OSPF, frag_len 0) is PPE_DF_NOT_FRAG.
+__global__ void __launch_bounds__(kBlock) df_parse_kernel(DfArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const uint8_t *p = a.pkt + a.off[i];
+    const uint32_t tot = a.len[i];
+    const uint32_t L = tot & 0xffffu;
+    uint32_t valid = 0, l2 = 14, ihl4 = 0, sip = 0, dip = 0, idp = 0, offf = 0, dummy = 0;
+    if (L >= 14) {
+        bool mac0 = true, mac1 = true;
+        for (int b = 0; b < 6; ++b) {
+            mac0 = mac0 && p[b] == 0;
+            mac1 = mac1 && p[6 + b] == 0;
+        }
+        uint32_t et = ld_be16(p + 12);
+        bool ok = !mac0 && !mac1;
+        if (ok && (et == 0x8100u || et == 0x9100u)) {
+            ok = L >= 18 && ld_be16(p + 16) == 0x0800u;   // a second tag or another inner type never reaches IPv4
+            l2 = 18;
+        } else {
+            ok = ok && et == 0x0800u;
+        }
+        if (ok && L >= l2 + 20) {
+            const uint8_t *ip = p + l2;
+            const uint32_t l3 = L - l2;
+            ihl4 = (ip[0] & 0x0fu) * 4u;
+            const uint32_t iplen = ld_be16(ip + 2);
+            const uint32_t offw = ld_be16(ip + 6);
+            const uint32_t proto = ip[9];
+            const bool is_frag = (offw & 0x1fffu) != 0 || (offw & 0x2000u) != 0;
+            if ((ip[0] >> 4) == 4u && ihl4 >= 20 && iplen >= ihl4 && l3 >= iplen && is_frag && proto != 89u &&
+                l3 - ihl4 != 0) {
+                valid = 1;
+                sip = ld_be32(ip + 12);
+                dip = ld_be32(ip + 16);
+                idp = ld_be16(ip + 4) | (proto << 16) | (((offw >> 13) & 1u) << 24);
+                offf = ((offw & 0x1fffu) << 3) | (((l3 - ihl4) & 0xffffu) << 16);
+            }
+        }
+    }
+    (void)dummy;
+    uint32_t *fr = a.frec + (size_t)i * kFrecWords;
+    const uint32_t h = key_hash(sip, dip, idp & 0xffffu);
+    fr[0] = sip;
+    fr[1] = dip;
+    fr[2] = idp;
+    fr[3] = offf;
+    fr[4] = tot;
+    fr[5] = l2 | (ihl4 << 8);
+    fr[6] = h;
+    fr[7] = valid;
+    uint32_t slot = kNone;
+    if (valid) {
+        // FragFind (decode-defrag.c:124-146): ip4_frag_match compares id, sip, dip (not the protocol)
+        uint32_t s = h & a.smask;
+        for (uint32_t probe = 0; probe <= a.smask; ++probe, s = (s + 1) & a.smask) {
+            const uint32_t st = a.tstate[s];
+            if (st == kEmpty) break;
+            if (st == kLive) {
+                const uint32_t *k = a.tkey + (size_t)s * 4;
+                if (k[0] == sip && k[1] == dip && k[2] == (idp & 0xffffu)) {
+                    slot = s;
+                    break;
+                }
+            }
+        }
+    }
+    a.fslot[i] = valid ? slot : (kNone - 1);   // kNone: create; kNone − 1: not a fragment
+}
+
+// ---- claim: a slot per new key, lowest claiming index recorded ------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) df_claim_kernel(DfArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n || a.fslot[i] != kNone) return;
+    const uint32_t *fr = a.frec + (size_t)i * kFrecWords;
+    const uint32_t sip = fr[0], dip = fr[1], id = fr[2] & 0xffffu;
+    uint32_t s = fr[6] & a.smask;
+    // terminates: slots >= 2 (fcb_max + max_batch) > live + pending, and EMPTY / TOMB slots are claimable
+    for (;;) {
+        uint32_t st = __hip_atomic_load(a.tstate + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {
+            if (st == kEmpty || st == kTomb) {
+                const uint32_t old = atomicCAS(a.tstate + s, st, kPend | i);
+                if (old == st) {
+                    atomicMin(a.creator + s, i);
+                    a.fslot[i] = s;
+                    return;
+                }
+                st = old;   // re-examine this slot
+                continue;
+            }
+            if (st & kPend) {
+                const uint32_t *fc = a.frec + (size_t)(st & ~kPend) * kFrecWords;
+                if (fc[0] == sip && fc[1] == dip && (fc[2] & 0xffffu) == id) {
+                    atomicMin(a.creator + s, i);
+                    a.fslot[i] = s;
+                    return;
+                }
+            }
+            break;
+        }
+        s = (s + 1) & a.smask;
+    }
+}
+
+// ---- per-tile ballot counts of a flag, one-workgroup scan, ranked placement ------------------------------------------
+__device__ __forceinline__ bool df_flag(const DfArgs &a, uint32_t i) {
+    if (i >= a.n) return false;
+    if (a.flag_mode == 0) {
+        const uint32_t s = a.fslot[i];
+        if (s >= kNone - 1) return false;
+        return (a.tstate[s] & kPend) && a.creator[s] == i;
+    }
+    return a.dgrec[i] != kNone;
+}
+
+__global__ void __launch_bounds__(kBlock) df_tile_count_kernel(DfArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t b = __builtin_amdgcn_ballot_w64(df_flag(a, i));
+    if (__lane_id() == 0 && i < a.n) a.tcnt[i >> 6] = (uint32_t)__popcll(b);
+}
+
+// exclusive scan of cnt[0..m) in place by one workgroup of kScanT threads; total → *total
+__device__ void block_scan_inplace(uint32_t *cnt, uint32_t m, unsigned long long *total) {
+    __shared__ uint32_t wsum[kScanT / 64];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < m; base += kScanT) {
+        const uint32_t j = base + threadIdx.x;
+        const uint32_t v = j < m ? cnt[j] : 0u;
+        uint32_t x = v;   // inclusive wave scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if ((int)__lane_id() >= o) x += y;
+        }
+        const uint32_t w = threadIdx.x >> 6;
+        if (__lane_id() == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t before = carry;
+        for (uint32_t k = 0; k < w; ++k) before += wsum[k];
+        if (j < m) cnt[j] = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == kScanT - 1) carry = before + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// creators: base values for the admission kernel, then the running count / free-stack top after it
+__global__ void __launch_bounds__(kScanT) df_scan_kernel(DfArgs a) {
+    const uint32_t tiles = (a.n + 63) / 64;
+    block_scan_inplace(a.tcnt, tiles, a.flag_mode == 0 ? a.ctl + C_CREATORS : a.ctl + C_NDGRAM);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    if (a.flag_mode == 0) {
+        const unsigned long long run = a.ctl[C_RUNNING], creators = a.ctl[C_CREATORS];
+        const unsigned long long room = run < a.fcb_max ? a.fcb_max - run : 0ull;
+        const unsigned long long adm = creators < room ? creators : room;
+        a.ctl[C_ADMIT_BASE] = run;
+        a.ctl[C_FREE_BASE] = a.ctl[C_FREE_TOP];
+        a.ctl[C_RUNNING] = run + adm;
+        a.ctl[C_FREE_TOP] -= adm;
+        a.ctl[C_NEW] += adm;
+    } else {
+        a.ctl[C_DGRAMS] += a.ctl[C_NDGRAM];
+        if (a.n_dgram) *a.n_dgram = (uint32_t)a.ctl[C_NDGRAM];
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const bool f = df_flag(a, i);
+    const uint64_t b = __builtin_amdgcn_ballot_w64(f);
+    if (!f) return;
+    const uint32_t rank = a.tcnt[i >> 6] + (uint32_t)__popcll(b & lanemask_lt());
+    const uint32_t s = a.fslot[i];
+    a.creator[s] = kNone;
+    // fcb_create (decode-defrag.c:74-81): fetch-and-add, fail when the previous count reached DEFRAG_FCB_MAX
+    if (a.ctl[C_ADMIT_BASE] + rank < a.fcb_max) {
+        const uint32_t r = a.freestk[a.ctl[C_FREE_BASE] - 1 - rank];
+        const uint32_t *fr = a.frec + (size_t)i * kFrecWords;
+        uint32_t *k = a.tkey + (size_t)s * 4;
+        k[0] = fr[0];
+        k[1] = fr[1];
+        k[2] = fr[2] & 0xffffu;
+        k[3] = r;
+        uint32_t *h = a.rhdr + (size_t)r * kRecWords;
+        h[0] = kRecLive;   // memset(fcb, 0) + key (decode-defrag.c:91-95)
+        h[1] = h[2] = h[4] = h[5] = 0;
+        h[3] = fr[2] & 0xffffu;   // key copy for the table rebuild: id, sip, dip
+        h[6] = fr[0];
+        h[7] = fr[1];
+        a.rts[r] = a.now;
+        a.tstate[s] = kLive;
+    } else {
+        a.tkey[(size_t)s * 4 + 3] = kNone;
+        a.tstate[s] = kTomb;
+    }
+}
+
+// ---- stable LSD radix sort of (record, index) by record -------------------------------------------------------------
+__device__ __forceinline__ uint32_t df_sort_key(const DfArgs &a, uint32_t i) {
+    const uint32_t s = a.fslot[i];
+    if (s >= kNone - 1 || a.tstate[s] != kLive) return a.sent;   // not a fragment, or its FCB could not be created
+    return a.tkey[(size_t)s * 4 + 3];
+}
+
+__global__ void __launch_bounds__(kBlock) df_sort_init_kernel(DfArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    a.skey[0][i] = df_sort_key(a, i);
+    a.sval[0][i] = i;
+}
+
+// in: skey[0]/sval[0] → out: skey[1]/sval[1]; hist layout digit-major: hist[d * sort_blocks + block]
+template <bool SCATTER>
+__global__ void __launch_bounds__(kSortBlock) df_sort_pass_kernel(DfArgs a) {
+    __shared__ uint32_t cnt[kSortBlock / 64][256];
+    const uint32_t w = threadIdx.x >> 6;
+    for (uint32_t k = threadIdx.x; k < (kSortBlock / 64) * 256; k += kSortBlock) (&cnt[0][0])[k] = 0;
+    __syncthreads();
+    const uint32_t j = blockIdx.x * kSortBlock + threadIdx.x;
+    const bool v = j < a.n;
+    const uint32_t key = v ? a.skey[0][j] : 0u;
+    const uint32_t d = (key >> a.shift) & 0xffu;
+    // wave multisplit: lanes with the same digit
+    uint64_t peers = __builtin_amdgcn_ballot_w64(v);
+    for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(bit);
+        peers &= bit ? m : ~m;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+    if (v && rank == 0) cnt[w][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (!SCATTER) {
+        for (uint32_t dd = threadIdx.x; dd < 256; dd += kSortBlock) {
+            uint32_t t = 0;
+            for (uint32_t k = 0; k < kSortBlock / 64; ++k) t += cnt[k][dd];
+            a.hist[dd * a.sort_blocks + blockIdx.x] = t;
+        }
+        return;
+    }
+    if (!v) return;
+    uint32_t pos = a.hist[d * a.sort_blocks + blockIdx.x] + rank;
+    for (uint32_t k = 0; k < w; ++k) pos += cnt[k][d];
+    a.skey[1][pos] = key;
+    a.sval[1][pos] = a.sval[0][j];
+}
+
+__global__ void __launch_bounds__(kScanT) df_hist_scan_kernel(DfArgs a) {
+    block_scan_inplace(a.hist, 256u * a.sort_blocks, a.ctl + C_SCRATCH);
+}
+
+// ---- the reference state machine, one lane per FCB --------------------------------------------------------------------
+__device__ __forceinline__ uint32_t chain_at(uint64_t order, uint32_t pos) { return (uint32_t)(order >> (4 * pos)) & 15u; }
+
+__global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= a.n) return;
+    const uint32_t *key = a.skey[0];
+    const uint32_t r = key[j];
+    if (j > 0 && key[j - 1] == r) return;   // not the head of its FCB's segment
+    unsigned long long st[PPE_DF__COUNT] = {};
+    unsigned long long teardrop = 0;
+    if (r == a.sent) {
+        for (uint32_t q = j; q < a.n && key[q] == r; ++q) {
+            const uint32_t i = a.sval[0][q];
+            const bool frag = a.frec[(size_t)i * kFrecWords + 7] != 0;
+            const uint32_t s = frag ? PPE_DF_FCB_FULL : PPE_DF_NOT_FRAG;
+            a.status[i] = s;
+            a.inserted[i] = kNone;
+            a.dgrec[i] = kNone;
+            st[s]++;
+        }
+    } else {
+        uint32_t *h = a.rhdr + (size_t)r * kRecWords;
+        uint32_t flags = h[0] & 0xffu, last_in = (h[0] >> 8) & 0xffu, cache_num = (h[0] >> 16) & 0xffu,
+                 nlist = h[0] >> 24;
+        int total = (int)h[1], meat = (int)h[2];
+        uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
+        const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
+        uint32_t *descw = a.rdesc + (size_t)r * a.cache_max * 4;
+        for (uint32_t q = j; q < a.n && key[q] == r; ++q) {
+            const uint32_t i = a.sval[0][q];
+            const uint32_t *fr = a.frec + (size_t)i * kFrecWords;
+            uint32_t out = PPE_DF_CACHED, ins = kNone, done = kNone;
+            bool tear = false;
+            // FragFind / fcb_create refresh the FCB's timestamp (decode-defrag.c:139, 472); a.rts[r] = now below
+            if (fr[4] > a.frag_buf) {
+                out = PPE_DF_HW2SW_ERR;                    // PACKET_HW2SW (decode-defrag.c:415-420)
+            } else if (flags & kRecDelete) {
+                out = PPE_DF_DELETED;                      // decode-defrag.c:422-427 (no counter)
+            } else if (cache_num >= a.cache_max) {
+                out = PPE_DF_CACHE_FULL;                   // decode-defrag.c:429-437
+            } else {
+                // Frag_defrag_process (decode-defrag.c:292-406)
+                const int offset = (int)(fr[3] & 0xffffu);
+                const int flen = (int)(fr[3] >> 16);
+                const int end = offset + flen;
+                const bool mf = (fr[2] >> 24) & 1u;
+                bool err = false;
+                if (!mf) {
+                    if (end < total || (last_in & kLastIn)) err = true;
+                    else {
+                        last_in |= kLastIn;
+                        total = end;
+                    }
+                } else if (end > total) {
+                    if (last_in & kLastIn) err = true;
+                    else total = end;
+                }
+                uint32_t pos = nlist;       // insert before chain position pos
+                if (!err) {
+                    int prev = -1, next = -1;
+                    if (nlist == 0 || (int)(desc[chain_at(order, nlist - 1) * 4] & 0xffffu) < offset) {
+                        prev = nlist ? (int)chain_at(order, nlist - 1) : -1;
+                    } else {
+                        // the reference's scan compares the chained fragment's frag_len with the new offset
+                        // (decode-defrag.c:344-349)
+                        for (pos = 0; pos < nlist; ++pos) {
+                            const uint32_t k = chain_at(order, pos);
+                            if ((int)(desc[k * 4] >> 16) >= offset) {
+                                next = (int)k;
+                                break;
+                            }
+                            prev = (int)k;
+                        }
+                    }
+                    if (prev >= 0) {
+                        const uint32_t pd = desc[prev * 4];
+                        if ((int)(pd & 0xffffu) + (int)(pd >> 16) - offset > 0) err = tear = true;
+                    }
+                    if (!err && next >= 0 && (int)(desc[next * 4] & 0xffffu) - end < 0) err = tear = true;
+                }
+                if (err) {
+                    out = PPE_DF_DEFRAG_ERR;
+                    teardrop += tear ? 1u : 0u;
+                } else {
+                    const uint32_t k = cache_num;      // store slot: the fragment's arrival rank in this FCB
+                    descw[k * 4 + 0] = fr[3];
+                    descw[k * 4 + 1] = fr[4];
+                    descw[k * 4 + 2] = fr[5] | ((fr[2] >> 16) & 0xffu) << 16;
+                    descw[k * 4 + 3] = 0;
+                    a.rid[(size_t)r * a.cache_max + k] = a.id ? a.id[i] : (uint64_t)i;
+                    const uint64_t lo = order & ((1ull << (4 * pos)) - 1ull);
+                    const uint64_t hi = pos + 1 < 16 ? (order >> (4 * pos)) << (4 * (pos + 1)) : 0ull;
+                    order = lo | ((uint64_t)k << (4 * pos)) | hi;
+                    nlist++;
+                    cache_num++;
+                    meat += flen;
+                    if (offset == 0) last_in |= kFirstIn;
+                    ins = (r << 8) | k;
+                    if (last_in == (kFirstIn | kLastIn) && meat == total) {
+                        // Frag_defrag_reasm / Frag_defrag_setup: the buffer is total + L2 + ihl*4 bytes of an 8 KB
+                        // slice (ICMP: 1000 bytes, always available)
+                        const uint32_t hd = desc[chain_at(order, 0) * 4 + 2];
+                        const uint32_t need = (uint32_t)total + (hd & 0xffu) + ((hd >> 8) & 0xffu);
+                        if (((hd >> 16) & 0xffu) != 1u && need > a.reasm_buf) {
+                            out = PPE_DF_SETUP_ERR;
+                        } else {
+                            out = PPE_DF_REASM;
+                            flags |= kRecComplete | kRecDelete;
+                            done = r;
+                        }
+                    }
+                }
+            }
+            a.status[i] = out | (tear ? PPE_DF_TEARDROP : 0u);
+            a.inserted[i] = ins;
+            a.dgrec[i] = done;
+            st[out]++;
+        }
+        h[0] = flags | (last_in << 8) | (cache_num << 16) | (nlist << 24);
+        h[1] = (uint32_t)total;
+        h[2] = (uint32_t)meat;
+        h[4] = (uint32_t)order;
+        h[5] = (uint32_t)(order >> 32);
+        a.rts[r] = a.now;
+    }
+    for (int s = 0; s < PPE_DF__COUNT; ++s)
+        if (st[s]) atomicAdd(a.ctl + C_ST0 + s, st[s]);
+    if (teardrop) atomicAdd(a.ctl + C_TEARDROP, teardrop);
+}
+
+// ---- stash: copy held frames into their FCB's store slot (PACKET_HW2SW) ----------------------------------------------
+__global__ void __launch_bounds__(kBlock) df_stash_kernel(DfArgs a) {
+    const uint32_t i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const uint32_t ins = a.inserted[i];
+    if (ins == kNone) return;
+    const uint32_t r = ins >> 8, k = ins & 0xffu;
+    const uint8_t *src = a.pkt + a.off[i];
+    uint8_t *dst = a.store + ((size_t)r * a.cache_max + k) * a.sstride;
+    const uint32_t tot = a.len[i];
+    const uint32_t lane = __lane_id();
+    if (((uintptr_t)src & 3u) == 0) {
+        const uint32_t words = tot / 4;
+        for (uint32_t w = lane; w < words; w += 64) ((uint32_t *)dst)[w] = ((const uint32_t *)src)[w];
+        for (uint32_t b = words * 4 + lane; b < tot; b += 64) dst[b] = src[b];
+    } else {
+        for (uint32_t b = lane; b < tot; b += 64) dst[b] = src[b];
+    }
+}
+
+// ---- place: datagram index of each completing fragment, in index order ------------------------------------------------
+__global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const bool f = df_flag(a, i);
+    const uint64_t b = __builtin_amdgcn_ballot_w64(f);
+    if (i >= a.n) return;
+    uint32_t j = kNone;
+    if (f) {
+        j = a.tcnt[i >> 6] + (uint32_t)__popcll(b & lanemask_lt());
+        a.dgsrc[j] = i;
+    }
+    if (a.dgram_of) a.dgram_of[i] = j;
+}
+
+// ---- assemble: one workgroup per datagram slot ----------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
+    const uint32_t j = blockIdx.x;
+    const uint32_t nd = (uint32_t)a.ctl[C_NDGRAM];
+    uint8_t *win = a.dgram_hdr ? a.dgram_hdr + (size_t)j * a.hdr_stride : nullptr;
+    if (j >= nd) {
+        if (win)
+            for (uint32_t b = threadIdx.x; b < a.hdr_stride; b += kBlock) win[b] = 0;
+        if (threadIdx.x == 0 && a.dgram_len) a.dgram_len[j] = 0;
+        if (a.dgram_frags)
+            for (uint32_t k = threadIdx.x; k < a.cache_max; k += kBlock) a.dgram_frags[(size_t)j * a.cache_max + k] = ~0ull;
+        return;
+    }
+    const uint32_t i = a.dgsrc[j];
+    const uint32_t r = a.dgrec[i];
+    const uint32_t *h = a.rhdr + (size_t)r * kRecWords;
+    const uint32_t nlist = h[0] >> 24;
+    const uint32_t total = h[1];
+    const uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
+    const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
+    const uint32_t k0 = chain_at(order, 0);
+    const uint32_t hd = desc[k0 * 4 + 2];
+    const uint32_t l2 = hd & 0xffu, ihl4 = (hd >> 8) & 0xffu, proto = (hd >> 16) & 0xffu;
+    const uint32_t head_tot = desc[k0 * 4 + 1];
+    const bool icmp = proto == 1u;
+    const uint8_t *hsrc = a.store + ((size_t)r * a.cache_max + k0) * a.sstride;
+    // out_len = head frame + the later fragments' payloads (reasm_mb->pkt_totallen, decode-defrag.c:240-266)
+    uint32_t out_len = head_tot;
+    for (uint32_t p = 1; p < nlist; ++p) out_len += desc[chain_at(order, p) * 4] >> 16;
+    // header patch (non-ICMP: ip_len = ihl*4 + total, ip_off = 0, checksum; ICMP: ip_off = 0)
+    uint32_t w_iplen = ld_be16(hsrc + l2 + 2), w_csum = ld_be16(hsrc + l2 + 10);
+    if (!icmp) {
+        w_iplen = (ihl4 + total) & 0xffffu;
+        // IPV4CalculateChecksum (decode-ipv4.h:117-163) over the patched header: words 0-4, 6-9, then the options
+        uint32_t cs = ld_be16(hsrc + l2) + w_iplen + ld_be16(hsrc + l2 + 4) + 0u /* ip_off */ + ld_be16(hsrc + l2 + 8) +
+                      ld_be16(hsrc + l2 + 12) + ld_be16(hsrc + l2 + 14) + ld_be16(hsrc + l2 + 16) +
+                      ld_be16(hsrc + l2 + 18);
+        if (ihl4 <= 60)
+            for (uint32_t o = 20; o < ihl4; o += 2) cs += ld_be16(hsrc + l2 + o);
+        cs = (cs >> 16) + (cs & 0xffffu);
+        cs += cs >> 16;
+        w_csum = (~cs) & 0xffffu;
+    }
+    auto patched = [&](uint32_t b, uint32_t v) -> uint32_t {
+        const uint32_t o = b - l2;
+        if (b < l2 || o >= 12) return v;
+        if (o == 2) return w_iplen >> 8;
+        if (o == 3) return w_iplen & 0xffu;
+        if (o == 6 || o == 7) return 0u;
+        if (o == 10) return w_csum >> 8;
+        if (o == 11) return w_csum & 0xffu;
+        return v;
+    };
+    // the reassembled frame: segment 0 = the head frame, segment p = the last flen bytes of chain entry p
+    // (ICMP: the head frame only; the reference sizes the buffer but copies nothing else)
+    uint8_t *full = a.dgram_pkt ? a.dgram_pkt + (size_t)j * a.reasm_buf : nullptr;
+    const uint32_t stride = a.hdr_stride;
+    uint32_t dst0 = 0;
+    for (uint32_t p = 0; p < (icmp ? 1u : nlist); ++p) {
+        const uint32_t k = chain_at(order, p);
+        const uint32_t tot = desc[k * 4 + 1], flen = desc[k * 4] >> 16;
+        const uint8_t *src = a.store + ((size_t)r * a.cache_max + k) * a.sstride + (p == 0 ? 0u : tot - flen);
+        const uint32_t cnt = p == 0 ? tot : flen;
+        const uint32_t lim = full ? cnt : (dst0 < stride ? (cnt < stride - dst0 ? cnt : stride - dst0) : 0u);
+        for (uint32_t b = threadIdx.x; b < lim; b += kBlock) {
+            const uint32_t ob = dst0 + b;
+            const uint32_t v = patched(ob, src[b]);
+            if (full && ob < a.reasm_buf) full[ob] = (uint8_t)v;
+            if (win && ob < stride) win[ob] = (uint8_t)v;
+        }
+        dst0 += cnt;
+    }
+    if (icmp && full) {   // bytes the reference never wrote: zero
+        const uint32_t lim = out_len < a.reasm_buf ? out_len : a.reasm_buf;
+        for (uint32_t b = dst0 + threadIdx.x; b < lim; b += kBlock) full[b] = 0;
+    }
+    if (win)
+        for (uint32_t b = dst0 + threadIdx.x; b < stride; b += kBlock) win[b] = 0;
+    if (threadIdx.x == 0 && a.dgram_len) a.dgram_len[j] = out_len;
+    if (a.dgram_frags)
+        for (uint32_t p = threadIdx.x; p < a.cache_max; p += kBlock)
+            a.dgram_frags[(size_t)j * a.cache_max + p] =
+                p < nlist ? a.rid[(size_t)r * a.cache_max + chain_at(order, p)] : ~0ull;
+}
+
+// ---- aging + table rebuild (one workgroup) ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(kScanT) df_age_kernel(DfArgs a) {
+    __shared__ uint32_t nfreed, ndropped;
+    if (threadIdx.x == 0) nfreed = ndropped = 0;
+    __syncthreads();
+    const uint32_t top = (uint32_t)a.ctl[C_FREE_TOP];
+    for (uint32_t r = threadIdx.x; r < a.fcb_max; r += kScanT) {
+        uint32_t *h = a.rhdr + (size_t)r * kRecWords;
+        const uint32_t f = h[0];
+        if (!(f & kRecLive)) continue;
+        const unsigned long long t = a.rts[r];
+        // Frag_defrag_timeout (decode-defrag.c:515-520): idle past the timeout, or marked DEFRAG_DELETE
+        if (!((a.now > t && a.now - t > a.timeout) || (f & kRecDelete))) continue;
+        if (!(f & kRecComplete)) {
+            const uint32_t nlist = f >> 24;
+            const uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
+            for (uint32_t p = 0; p < nlist; ++p) {
+                const uint32_t slot = atomicAdd(&ndropped, 1u);
+                if (slot < a.max_dropped) a.dropped[slot] = a.rid[(size_t)r * a.cache_max + chain_at(order, p)];
+            }
+        }
+        h[0] = 0;
+        a.freestk[top + atomicAdd(&nfreed, 1u)] = r;
+    }
+    // rebuild the table from the live records (deleted keys and tombstones vanish)
+    for (uint32_t s = threadIdx.x; s <= a.smask; s += kScanT) {
+        a.tstate[s] = kEmpty;
+        a.creator[s] = kNone;
+    }
+    __threadfence();
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < a.fcb_max; r += kScanT) {
+        const uint32_t *h = a.rhdr + (size_t)r * kRecWords;
+        if (!(h[0] & kRecLive)) continue;
+        // the key of record r: the table keys are rebuilt from the record's copy
+        const uint32_t sip = h[6], dip = h[7], id = h[3];
+        uint32_t s = key_hash(sip, dip, id) & a.smask;
+        while (atomicCAS(a.tstate + s, kEmpty, kLive) != kEmpty) s = (s + 1) & a.smask;
+        uint32_t *k = a.tkey + (size_t)s * 4;
+        k[0] = sip;
+        k[1] = dip;
+        k[2] = id;
+        k[3] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.ctl[C_RUNNING] -= nfreed;
+        a.ctl[C_DEL] += nfreed;
+        a.ctl[C_FREE_TOP] = top + nfreed;
+        a.ctl[C_TIMEOUT_DROP] += ndropped;
+        a.ctl[C_AGE_DROPPED] = ndropped;
+        a.ctl[C_AGE_FREED] = nfreed;
+    }
+}
+
+__global__ void df_init_kernel(DfArgs a) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t <= a.smask) {
+        a.tstate[t] = kEmpty;
+        a.creator[t] = kNone;
+    }
+    if (t < a.fcb_max) {
+        a.freestk[t] = a.fcb_max - 1 - t;
+        a.rhdr[(size_t)t * kRecWords] = 0;
+    }
+    if (t < C_WORDS) a.ctl[t] = t == C_FREE_TOP ? a.fcb_max : 0ull;
+}
+
+}  // namespace
+
+struct ppe_defrag_table {
+    int device = 0;
+    ppe_defrag_cfg_t cfg{};
+    uint32_t nslots = 0, sstride = 0, passes = 0, sent = 0;
+    DfArgs base{};   // persistent device pointers + sizes
+    void *allocs[24] = {};
+    int nalloc = 0;
+    unsigned long long *h_ctl = nullptr;   // pinned
+    char err[256] = {0};
+};
+
+namespace {
+
+int dfail(ppe_defrag_t *d, int code, const char *fmt, ...) {
+    if (d) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(d->err, sizeof(d->err), fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+template <typename T>
+bool dalloc(ppe_defrag_t *d, T **p, size_t count) {
+    void *q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(count * sizeof(T), 64)) != hipSuccess) return false;
+    d->allocs[d->nalloc++] = q;
+    *p = (T *)q;
+    return true;
+}
+
+uint32_t blocks(uint64_t items, uint32_t per) { return (uint32_t)std::max<uint64_t>(1, (items + per - 1) / per); }
+
+int launched(ppe_defrag_t *d, const char *what) {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? PPE_OK : dfail(d, PPE_EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t **out) {
+    if (!ctx || !out) return PPE_EINVAL;
+    *out = nullptr;
+    ppe_defrag_cfg_t c = cfg ? *cfg : ppe_defrag_cfg_t{};
+    if (!c.fcb_max) c.fcb_max = 1024;
+    if (!c.cache_max) c.cache_max = 8;
+    if (!c.frag_buf_bytes) c.frag_buf_bytes = 2024;
+    if (!c.reasm_buf_bytes) c.reasm_buf_bytes = 8168;
+    if (!c.max_batch) c.max_batch = 65536;
+    if (c.cache_max > 16 || c.fcb_max > (1u << 20) || c.frag_buf_bytes > 4096 || c.reasm_buf_bytes > (1u << 20) ||
+        c.max_batch > (1u << 24))
+        return PPE_EINVAL;
+    const int dev = ppe_ctx_device(ctx);
+    if (dev < 0 || hipSetDevice(dev) != hipSuccess) return PPE_ENODEV;
+    ppe_defrag_t *d = new (std::nothrow) ppe_defrag_t();
+    if (!d) return PPE_ENOMEM;
+    d->device = dev;
+    d->cfg = c;
+    uint32_t ns = 1024;
+    while (ns < 2ull * ((uint64_t)c.fcb_max + c.max_batch)) ns <<= 1;
+    d->nslots = ns;
+    d->sstride = (c.frag_buf_bytes + 63u) & ~63u;
+    d->sent = c.fcb_max;   // sort key of fragments without a record
+    uint32_t bits = 1;
+    while ((1u << bits) <= d->sent) ++bits;
+    d->passes = (bits + 7) / 8;
+    DfArgs &a = d->base;
+    a.smask = ns - 1;
+    a.fcb_max = c.fcb_max;
+    a.cache_max = c.cache_max;
+    a.frag_buf = c.frag_buf_bytes;
+    a.reasm_buf = c.reasm_buf_bytes;
+    a.sstride = d->sstride;
+    a.sent = d->sent;
+    const uint32_t mb = c.max_batch;
+    const uint32_t sb = blocks(mb, kSortBlock);
+    bool ok = dalloc(d, &a.tstate, ns) && dalloc(d, &a.tkey, (size_t)ns * 4) && dalloc(d, &a.creator, ns) &&
+              dalloc(d, &a.rhdr, (size_t)c.fcb_max * kRecWords) &&
+              dalloc(d, &a.rdesc, (size_t)c.fcb_max * c.cache_max * 4) && dalloc(d, &a.rts, c.fcb_max) &&
+              dalloc(d, &a.rid, (size_t)c.fcb_max * c.cache_max) &&
+              dalloc(d, &a.store, (size_t)c.fcb_max * c.cache_max * d->sstride) && dalloc(d, &a.freestk, c.fcb_max) &&
+              dalloc(d, &a.ctl, C_WORDS) && dalloc(d, &a.frec, (size_t)mb * kFrecWords) && dalloc(d, &a.fslot, mb) &&
+              dalloc(d, &a.inserted, mb) && dalloc(d, &a.dgrec, mb) && dalloc(d, &a.dgsrc, mb) &&
+              dalloc(d, &a.tcnt, blocks(mb, 64)) && dalloc(d, &a.skey[0], mb) && dalloc(d, &a.sval[0], mb) &&
+              dalloc(d, &a.skey[1], mb) && dalloc(d, &a.sval[1], mb) && dalloc(d, &a.hist, (size_t)256 * sb) &&
+              dalloc(d, &a.dropped, (size_t)c.fcb_max * c.cache_max);
+    if (ok && hipHostMalloc((void **)&d->h_ctl, C_WORDS * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+        ok = false;
+    if (!ok) {
+        ppe_defrag_destroy(d);
+        return PPE_ENOMEM;
+    }
+    a.max_dropped = c.fcb_max * c.cache_max;
+    const uint32_t span = std::max(ns, std::max(c.fcb_max, (uint32_t)C_WORDS));
+    hipLaunchKernelGGL(df_init_kernel, dim3(blocks(span, 256)), dim3(256), 0, 0, a);
+    if (hipDeviceSynchronize() != hipSuccess) {
+        ppe_defrag_destroy(d);
+        return PPE_EIO;
+    }
+    *out = d;
+    return PPE_OK;
+}
+
+int ppe_defrag_destroy(ppe_defrag_t *d) {
+    if (!d) return PPE_EINVAL;
+    (void)hipSetDevice(d->device);
+    (void)hipDeviceSynchronize();
+    for (int k = 0; k < d->nalloc; ++k) (void)hipFree(d->allocs[k]);
+    if (d->h_ctl) (void)hipHostFree(d->h_ctl);
+    delete d;
+    return PPE_OK;
+}
+
+const char *ppe_defrag_last_error(ppe_defrag_t *d) { return d ? d->err : "null defrag table"; }
+
+int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out_t *out, void *stream) {
+    if (!d || !in || !out) return PPE_EINVAL;
+    if (in->n == 0) return PPE_OK;
+    if (in->n > d->cfg.max_batch) return dfail(d, PPE_EINVAL, "batch of %u fragments > max_batch %u", in->n,
+                                               d->cfg.max_batch);
+    if (!in->pkt || !in->off || !in->len || !out->status || !out->dgram_hdr || !out->dgram_len)
+        return dfail(d, PPE_EINVAL, "pkt/off/len and status/dgram_hdr/dgram_len are required");
+    if (out->hdr_stride != 64 && out->hdr_stride != 128) return dfail(d, PPE_EINVAL, "hdr_stride must be 64 or 128");
+    if (hipSetDevice(d->device) != hipSuccess) return PPE_ENODEV;
+    const hipStream_t s = (hipStream_t)stream;
+    DfArgs a = d->base;
+    a.pkt = in->pkt;
+    a.off = in->off;
+    a.len = in->len;
+    a.id = in->id;
+    a.n = in->n;
+    a.now = in->now_seconds;
+    a.status = out->status;
+    a.dgram_of = out->dgram_of;
+    a.dgram_hdr = out->dgram_hdr;
+    a.dgram_len = out->dgram_len;
+    a.dgram_pkt = out->dgram_pkt;
+    a.dgram_frags = out->dgram_frags;
+    a.n_dgram = out->n_dgram;
+    a.hdr_stride = out->hdr_stride;
+    const uint32_t g = blocks(a.n, kBlock);
+    a.sort_blocks = blocks(a.n, kSortBlock);
+    hipLaunchKernelGGL(df_parse_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(df_claim_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    a.flag_mode = 0;
+    hipLaunchKernelGGL(df_tile_count_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(df_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(df_admit_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(df_sort_init_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    for (uint32_t p = 0; p < d->passes; ++p) {
+        a.shift = 8 * p;
+        hipLaunchKernelGGL(df_sort_pass_kernel<false>, dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
+        hipLaunchKernelGGL(df_hist_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
+        hipLaunchKernelGGL(df_sort_pass_kernel<true>, dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
+        std::swap(a.skey[0], a.skey[1]);
+        std::swap(a.sval[0], a.sval[1]);
+    }
+    hipLaunchKernelGGL(df_process_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(df_stash_kernel, dim3(blocks(a.n, kBlock / 64)), dim3(kBlock), 0, s, a);
+    a.flag_mode = 1;
+    hipLaunchKernelGGL(df_tile_count_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(df_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
+    hipLaunchKernelGGL(df_place_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(df_assemble_kernel, dim3(a.n), dim3(kBlock), 0, s, a);
+    return launched(d, "ppe_defrag");
+}
+
+int ppe_defrag_age(ppe_defrag_t *d, uint64_t now_seconds, uint64_t timeout_seconds, uint64_t *dropped, uint32_t max,
+                   uint32_t *n_dropped, uint32_t *n_freed) {
+    if (!d) return PPE_EINVAL;
+    if (hipSetDevice(d->device) != hipSuccess) return PPE_ENODEV;
+    DfArgs a = d->base;
+    a.now = now_seconds;
+    a.timeout = timeout_seconds;
+    hipLaunchKernelGGL(df_age_kernel, dim3(1), dim3(kScanT), 0, 0, a);
+    if (hipDeviceSynchronize() != hipSuccess) return dfail(d, PPE_EIO, "ppe_defrag_age: kernel failed");
+    if (hipMemcpy(d->h_ctl, a.ctl, C_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return PPE_EIO;
+    const uint32_t nd = (uint32_t)d->h_ctl[C_AGE_DROPPED];
+    if (n_dropped) *n_dropped = nd;
+    if (n_freed) *n_freed = (uint32_t)d->h_ctl[C_AGE_FREED];
+    const uint32_t copy = std::min(std::min(nd, max), a.max_dropped);
+    if (dropped && copy &&
+        hipMemcpy(dropped, a.dropped, copy * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return PPE_EIO;
+    return PPE_OK;
+}
+
+int ppe_defrag_info(ppe_defrag_t *d, ppe_defrag_info_t *info) {
+    if (!d || !info) return PPE_EINVAL;
+    if (hipSetDevice(d->device) != hipSuccess) return PPE_ENODEV;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(d->h_ctl, d->base.ctl, C_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return dfail(d, PPE_EIO, "ppe_defrag_info: device error");
+    const unsigned long long *c = d->h_ctl;
+    memset(info, 0, sizeof(*info));
+    info->running = c[C_RUNNING];
+    info->new_fcb = c[C_NEW];
+    info->del_fcb = c[C_DEL];
+    for (int k = 0; k < PPE_DF__COUNT; ++k) info->st[k] = c[C_ST0 + k];
+    info->teardrop = c[C_TEARDROP];
+    info->timeout_drop = c[C_TIMEOUT_DROP];
+    info->datagrams = c[C_DGRAMS];
+    info->fcb_max = d->cfg.fcb_max;
+    info->cache_max = d->cfg.cache_max;
+    info->frag_buf_bytes = d->cfg.frag_buf_bytes;
+    info->reasm_buf_bytes = d->cfg.reasm_buf_bytes;
+    info->max_batch = d->cfg.max_batch;
+    info->slots = d->nslots;
+    return PPE_OK;
+}
+
+}  // extern "C"

@@ -4,4 +4,4 @@ Plumbing for tests and bench.py only: every classification runs in the HIP kerne
 """
 from . import abi, synth  # noqa: F401
 from .abi import RULE_DTYPE, ST, ST_NAME, COUNTERS, build_image  # noqa: F401
-from .engine import Engine, PPEError, decode_verdict  # noqa: F401
+from .engine import Defrag, Engine, PPEError, decode_verdict  # noqa: F401

@@ -109,6 +109,41 @@ class Tuples(C.Structure):
     _fields_ = [("tuple", C.c_void_p), ("macs", C.c_void_p), ("ts", C.c_void_p), ("n", C.c_uint32)]
 
 
+# ---- IPv4 reassembly (ppe_defrag_*) ----
+DF = dict(CACHED=0, REASM=1, SETUP_ERR=2, FCB_FULL=3, HW2SW_ERR=4, DELETED=5, CACHE_FULL=6, DEFRAG_ERR=7, NOT_FRAG=8)
+DF_NAME = {v: k for k, v in DF.items()}
+DF_TEARDROP = 0x100
+
+
+class DefragCfg(C.Structure):
+    _fields_ = [("fcb_max", C.c_uint32), ("cache_max", C.c_uint32), ("frag_buf_bytes", C.c_uint32),
+                ("reasm_buf_bytes", C.c_uint32), ("max_batch", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class FragBatch(C.Structure):
+    _fields_ = [("pkt", C.c_void_p), ("off", C.c_void_p), ("len", C.c_void_p), ("id", C.c_void_p),
+                ("n", C.c_uint32), ("pad", C.c_uint32), ("now_seconds", C.c_uint64)]
+
+
+class DefragOut(C.Structure):
+    _fields_ = [("status", C.c_void_p), ("dgram_of", C.c_void_p), ("dgram_hdr", C.c_void_p),
+                ("dgram_len", C.c_void_p), ("dgram_pkt", C.c_void_p), ("dgram_frags", C.c_void_p),
+                ("n_dgram", C.c_void_p), ("hdr_stride", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class DefragInfo(C.Structure):
+    _fields_ = [("running", C.c_uint64), ("new_fcb", C.c_uint64), ("del_fcb", C.c_uint64),
+                ("st", C.c_uint64 * 9), ("teardrop", C.c_uint64), ("timeout_drop", C.c_uint64),
+                ("datagrams", C.c_uint64), ("fcb_max", C.c_uint32), ("cache_max", C.c_uint32),
+                ("frag_buf_bytes", C.c_uint32), ("reasm_buf_bytes", C.c_uint32), ("max_batch", C.c_uint32),
+                ("slots", C.c_uint32)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "st"}
+        d.update({"st_" + DF_NAME[i].lower(): int(self.st[i]) for i in range(9)})
+        return d
+
+
 # every symbol include/*.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     # ppe_hip.h
@@ -120,6 +155,8 @@ EXPORTS = [
     "ppe_get_tuning", "ppe_flow_create", "ppe_flow_destroy", "ppe_classify_flow", "ppe_flow_age", "ppe_flow_info",
     "ppe_flow_clear_stat", "ppe_flow_dump", "ppe_format_pkt_stat", "ppe_format_flow_stat",
     "ppe_steer_partition", "ppe_gather_rows", "ppe_scatter_rows",
+    "ppe_defrag_create", "ppe_defrag_destroy", "ppe_defrag", "ppe_defrag_age", "ppe_defrag_info",
+    "ppe_defrag_last_error",
     # ppe_acl.h
     "ppe_rule_list_init", "ppe_rule_list_free", "Rule_add", "Rule_del_by_id", "Rule_del_all",
     "Rule_duplicate_check", "Rule_Load_Line", "ppe_rule_load_file", "DP_Acl_Rule_Init", "DP_Acl_Load_Rule",
@@ -200,6 +237,12 @@ def _open(p: Path, mode) -> C.CDLL:
         "ppe_gather_rows": ([vp, vp, u32, vp, u32, vp, vp], C.c_int),
         "ppe_scatter_rows": ([vp, vp, u32, vp, u32, vp, vp], C.c_int),
         "ppe_format_flow_stat": ([C.POINTER(FlowInfo), C.c_char_p, C.c_size_t], C.c_int),
+        "ppe_defrag_create": ([vp, C.POINTER(DefragCfg), C.POINTER(vp)], C.c_int),
+        "ppe_defrag_destroy": ([vp], C.c_int),
+        "ppe_defrag": ([vp, C.POINTER(FragBatch), C.POINTER(DefragOut), vp], C.c_int),
+        "ppe_defrag_age": ([vp, u64, u64, vp, u32, C.POINTER(u32), C.POINTER(u32)], C.c_int),
+        "ppe_defrag_info": ([vp, C.POINTER(DefragInfo)], C.c_int),
+        "ppe_defrag_last_error": ([vp], C.c_char_p),
         "ppe_rule_list_init": ([], C.c_int),
         "ppe_rule_list_free": ([], None),
         "Rule_add": ([vp, C.POINTER(u32)], C.c_int),

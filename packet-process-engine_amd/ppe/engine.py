@@ -218,3 +218,70 @@ class Engine:
 def decode_verdict(v: np.ndarray):
     v = np.asarray(v, dtype=np.uint32)
     return v & 0xFF, (v >> 8) & 0xFF, v >> 16
+
+
+class Defrag:
+    """One device FCB table (ppe_defrag_create) on an Engine's GPU: IPv4 reassembly of the fragments ppe_classify
+    PUNTs (dataplane/src/decode/decode-defrag.c).  Every call goes through libppe_hip.so."""
+
+    def __init__(self, engine: Engine, fcb_max=0, cache_max=0, frag_buf_bytes=0, reasm_buf_bytes=0, max_batch=0):
+        self.eng = engine
+        self.lib = engine.lib
+        self.h = C.c_void_p()
+        cfg = abi.DefragCfg(fcb_max, cache_max, frag_buf_bytes, reasm_buf_bytes, max_batch, 0)
+        rc = self.lib.ppe_defrag_create(engine.ctx, C.byref(cfg), C.byref(self.h))
+        if rc != 0:
+            raise PPEError(f"ppe_defrag_create failed: {rc}")
+        self.info_ = self.info()
+
+    def close(self):
+        if self.h:
+            self.lib.ppe_defrag_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def _check(self, rc, what):
+        if rc != 0:
+            err = self.lib.ppe_defrag_last_error(self.h)
+            raise PPEError(f"{what} failed: {rc}: {err.decode() if err else ''}")
+
+    def alloc_out(self, n: int, hdr_stride: int = 128, full: bool = True):
+        """Device output tensors for a batch of n fragments."""
+        import torch
+        dev = torch.device("cuda", self.eng.device)
+        cm = self.info_["cache_max"]
+        out = dict(status=torch.empty(n, dtype=torch.int32, device=dev),
+                   dgram_of=torch.empty(n, dtype=torch.int32, device=dev),
+                   dgram_hdr=torch.empty((n, hdr_stride), dtype=torch.uint8, device=dev),
+                   dgram_len=torch.empty(n, dtype=torch.int32, device=dev),
+                   dgram_frags=torch.empty((n, cm), dtype=torch.int64, device=dev),
+                   n_dgram=torch.zeros(1, dtype=torch.int32, device=dev))
+        if full:
+            out["dgram_pkt"] = torch.empty((n, self.info_["reasm_buf_bytes"]), dtype=torch.uint8, device=dev)
+        return out
+
+    def run_torch(self, pkt, off, lens, out: dict, now: int, ids=None, stream=None):
+        """ppe_defrag on tensors of the engine's GPU: pkt (u8 arena), off (i64), lens (i32), ids (i64, optional)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.eng.device)
+        n = lens.numel()
+        b = abi.FragBatch(pkt.data_ptr(), off.data_ptr(), lens.data_ptr(), ids.data_ptr() if ids is not None else None,
+                          n, 0, int(now))
+        g = lambda k: out[k].data_ptr() if out.get(k) is not None else None
+        o = abi.DefragOut(g("status"), g("dgram_of"), g("dgram_hdr"), g("dgram_len"), g("dgram_pkt"),
+                          g("dgram_frags"), g("n_dgram"), out["dgram_hdr"].shape[1], 0)
+        self._check(self.lib.ppe_defrag(self.h, C.byref(b), C.byref(o), s.cuda_stream), "ppe_defrag")
+
+    def age(self, now: int, timeout: int = 20):
+        """Frag_defrag_timeout: returns (dropped fragment ids, FCBs freed)."""
+        cap = self.info_["fcb_max"] * self.info_["cache_max"]
+        ids = np.zeros(cap, np.uint64)
+        nd, nf = C.c_uint32(0), C.c_uint32(0)
+        self._check(self.lib.ppe_defrag_age(self.h, int(now), int(timeout), ids.ctypes.data, cap, C.byref(nd),
+                                            C.byref(nf)), "ppe_defrag_age")
+        return ids[:min(nd.value, cap)], nf.value
+
+    def info(self) -> dict:
+        fi = abi.DefragInfo()
+        self._check(self.lib.ppe_defrag_info(self.h, C.byref(fi)), "ppe_defrag_info")
+        return fi.as_dict()
+

@@ -319,3 +319,97 @@ def _malform(hdr, lens, i, k, rng, stride):
         h[l3 + 9] = 6
         _set16(h, l3 + 2, 20 + int(rng.integers(0, 20)))
 
+
+
+# ---- IPv4 fragment streams (ppe_defrag) ------------------------------------------------------
+def _frag_frame(rng, proto, sip, dip, ip_id, off_bytes, mf, chunk, ihl, vlan_tag, pad):
+    hlen = ihl * 4
+    offw = (off_bytes >> 3) | (0x2000 if mf else 0)
+    ip = bytearray(hlen)
+    ip[0] = 0x40 | ihl
+    ip[2:4] = (hlen + len(chunk)).to_bytes(2, "big")
+    ip[4:6] = int(ip_id).to_bytes(2, "big")
+    ip[6:8] = offw.to_bytes(2, "big")
+    ip[8] = 64
+    ip[9] = proto
+    ip[12:16] = int(sip).to_bytes(4, "big")
+    ip[16:20] = int(dip).to_bytes(4, "big")
+    for k in range(20, hlen):
+        ip[k] = 1   # NOP options
+    l2 = bytes([2, 0x11, 0x22, 0x33, 0x44, 0x55, 2, 0x66, 0x77, 0x88, 0x99, 0xAA])
+    l2 += b"\x81\x00\x00\x05\x08\x00" if vlan_tag else b"\x08\x00"
+    return l2 + bytes(ip) + chunk + bytes(pad)
+
+
+def make_fragment_stream(n_dgrams: int, seed: int = SEED + 7, n_hosts: int = 64, oversize: float = 0.02,
+                         reorder: float = 0.15, dup: float = 0.04, lose: float = 0.04, overlap: float = 0.02,
+                         not_frag: float = 0.01, jumbo: float = 0.02, max_l4: int = 4000, align: int = 4):
+    """A deterministic stream of IPv4 fragments of n_dgrams datagrams (UDP / TCP-SYN / ICMP, 30 % VLAN, some IP
+    options and Ethernet padding), with the ways real fragment streams go wrong: reordered chains, duplicates, lost
+    fragments (never complete → aging), overlaps, frames too long for the 2 KB copy, datagrams too large for the
+    8 KB reassembly buffer, and a few non-fragments.
+    Fragments of one datagram stay near each other; datagrams interleave.  Returns (arena u8, off u64, len u32)."""
+    rng = np.random.default_rng(seed)
+    hosts = rng.integers(1, 2**32 - 1, size=n_hosts, dtype=np.uint64)
+    frames, keys = [], []
+    for d in range(n_dgrams):
+        r = rng.random()
+        proto = 17 if r < 0.6 else (6 if r < 0.95 else 1)
+        sip, dip = hosts[rng.integers(n_hosts)], hosts[rng.integers(n_hosts)]
+        ip_id = int(rng.integers(0, 65536))
+        ihl = 5 if rng.random() < 0.9 else int(rng.integers(6, 8))
+        vlan_tag = rng.random() < 0.3
+        is_jumbo = rng.random() < jumbo
+        l4n = int(rng.integers(16, max_l4)) if not is_jumbo else int(rng.integers(8150, 9000))
+        if proto == 17:
+            l4 = (int(rng.integers(1, 65536)).to_bytes(2, "big") + int(rng.integers(1, 65536)).to_bytes(2, "big") +
+                  l4n.to_bytes(2, "big") + b"\0\0" + rng.integers(0, 256, l4n - 8, dtype=np.uint8).tobytes())
+        elif proto == 6:
+            l4 = (int(rng.integers(1, 65536)).to_bytes(2, "big") + int(rng.integers(1, 65536)).to_bytes(2, "big") +
+                  b"\0\0\0\1\0\0\0\0\x50\x02\x04\x00\0\0\0\0" + rng.integers(0, 256, max(0, l4n - 20),
+                                                                            dtype=np.uint8).tobytes())
+        else:
+            l4 = rng.integers(0, 256, l4n, dtype=np.uint8).tobytes()
+        big = rng.random() < oversize
+        step = 8 * int(rng.integers(32, 186)) if not big else 8 * int(rng.integers(256, 400))
+        if is_jumbo:
+            step = 1480
+        chunks, o = [], 0
+        while o < len(l4):
+            c = l4[o:o + step]
+            chunks.append((o, c, o + step < len(l4)))
+            o += step
+        if len(chunks) == 1:   # make it a fragment: a lone chunk with MF set, or split once
+            if len(l4) > 8:
+                cut = 8 * max(1, (len(l4) // 2) // 8)
+                chunks = [(0, l4[:cut], True), (cut, l4[cut:], False)]
+            else:
+                chunks = [(0, l4, True)]
+        if rng.random() < overlap and len(chunks) > 1:
+            o2, c2, m2 = chunks[1]
+            chunks[1] = (max(0, o2 - 8), l4[max(0, o2 - 8):o2 - 8 + len(c2)], m2)
+        if rng.random() < lose and len(chunks) > 1:
+            del chunks[int(rng.integers(len(chunks)))]
+        if rng.random() < dup:
+            chunks.insert(int(rng.integers(len(chunks) + 1)), chunks[int(rng.integers(len(chunks)))])
+        if rng.random() < reorder:
+            rng.shuffle(chunks)
+        base = d + rng.random() * 3.0   # datagrams interleave; a chain keeps its (possibly perturbed) order
+        for k, (o, c, mf) in enumerate(chunks):
+            # Ethernet trailer padding counts in frag_len (L3 length = frame − L2): on a non-final fragment it
+            # overlaps the next one (decode-defrag.c:384-391), so only final fragments carry it here
+            pad = int(rng.integers(1, 12)) if (not mf and rng.random() < 0.05) else 0
+            frames.append(_frag_frame(rng, proto, sip, dip, ip_id, o, mf, c, ihl, vlan_tag, pad))
+            keys.append(base + 0.5 * k)
+        if rng.random() < not_frag:
+            frames.append(_frag_frame(rng, 17, sip, dip, ip_id, 0, False, l4[:64], 5, False, 0))
+            keys.append(base + rng.random() * 3.0)
+    order = np.argsort(np.asarray(keys), kind="stable")
+    lens = np.array([len(frames[i]) for i in order], np.uint32)
+    sizes = (lens.astype(np.uint64) + (align - 1)) // align * align
+    off = np.zeros(len(order), np.uint64)
+    off[1:] = np.cumsum(sizes)[:-1]
+    arena = np.zeros(int(sizes.sum()) + 64, np.uint8)
+    for j, i in enumerate(order):
+        arena[int(off[j]):int(off[j]) + int(lens[j])] = np.frombuffer(frames[i], np.uint8)
+    return arena, off, lens

@@ -42,3 +42,33 @@ def tcp_packet(sip=0xC0A80101, dip=0xC0A80102, sport=12345, dport=443, flags=0x0
     l4 = tcp(sport, dport, flags, payload=payload)
     l3 = ipv4(6, sip, dip, len(l4)) + l4
     return (eth(0x8100) + vlan(0x0800) if vlan_tag else eth(0x0800)) + l3
+
+
+def ip_frag(proto, sip, dip, ip_id, off_bytes, mf, chunk, ihl=5, vlan_tag=False, pad=0):
+    """One IPv4 fragment frame: fragment offset off_bytes (a multiple of 8), MF flag, payload chunk."""
+    hlen = ihl * 4
+    offw = (off_bytes >> 3) | (0x2000 if mf else 0)
+    h = struct.pack(">BBHHHBBHII", 0x40 | ihl, 0, hlen + len(chunk), ip_id, offw, 64, proto, 0, sip, dip)
+    h += b"\x01" * (hlen - 20)
+    l2 = eth(0x8100) + vlan(0x0800) if vlan_tag else eth(0x0800)
+    return l2 + h + chunk + b"\0" * pad
+
+
+def arena(frames, align=4):
+    """Pack frames into one byte arena: (arena u8, off u64, len u32)."""
+    import numpy as np
+    off, buf = [], bytearray()
+    for f in frames:
+        off.append(len(buf))
+        buf += f
+        buf += b"\0" * ((-len(buf)) % align)
+    buf += b"\0" * 64
+    return (np.frombuffer(bytes(buf), np.uint8).copy(), np.array(off, np.uint64),
+            np.array([len(f) for f in frames], np.uint32))
+
+
+def ip_checksum_ok(ip_header: bytes) -> bool:
+    s = sum(struct.unpack(">%dH" % (len(ip_header) // 2), ip_header))
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s == 0xFFFF

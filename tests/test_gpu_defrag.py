@@ -1,0 +1,182 @@
+"""GPU parity of IPv4 reassembly (ppe_defrag / ppe_defrag_age through the C ABI) against the oracle's sequential
+Defrag (tests/test_oracle_defrag.py pins the oracle to dataplane/src/decode/decode-defrag.c).
+
+Bar: bit-exact per-fragment status (with the teardrop bit), datagram index, datagram count, length, bytes, window and
+fragment-id list, the same fragments dropped by every aging step, and identical counters; then the reassembled
+datagrams classify exactly as the oracle classifies the oracle's datagrams."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import torch  # noqa: E402
+
+import pyoracle  # noqa: E402
+from pktbuild import arena, ip_frag, udp  # noqa: E402
+from ppe import Defrag, Engine, abi, synth  # noqa: E402
+from test_gpu_parity import gpu_classify  # noqa: E402
+
+DEV = torch.device("cuda:0")
+NOW = 1_000_000
+
+
+@pytest.fixture(scope="module")
+def eng():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+class DfPair:
+    """The HIP FCB table and the oracle's, fed the same fragment batches."""
+
+    def __init__(self, eng, stride=128, **cfg):
+        self.g = Defrag(eng, **cfg)
+        o_cfg = dict(fcb_max=cfg.get("fcb_max", 0), cache_max=cfg.get("cache_max", 0),
+                     frag_buf=cfg.get("frag_buf_bytes", 0), reasm_buf=cfg.get("reasm_buf_bytes", 0))
+        self.o = pyoracle.OracleDefrag(**o_cfg)
+        self.stride = stride
+        self.cm = self.g.info_["cache_max"]
+        self.rb = self.g.info_["reasm_buf_bytes"]
+
+    def close(self):
+        self.g.close()
+        self.o.close()
+
+    def batch(self, a, off, lens, now, ids=None):
+        n = len(lens)
+        ref = self.o.batch(a, off, lens, now, ids=ids)
+        out = self.g.alloc_out(n, self.stride)
+        for v in out.values():
+            v.fill_(-7) if v.dtype != torch.uint8 else v.fill_(0xA5)
+        ta = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+        to = torch.from_numpy(np.ascontiguousarray(off, np.uint64).view(np.int64)).to(DEV)
+        tl = torch.from_numpy(np.ascontiguousarray(lens, np.uint32).view(np.int32)).to(DEV)
+        ti = torch.from_numpy(np.ascontiguousarray(ids, np.uint64).view(np.int64)).to(DEV) if ids is not None else None
+        self.g.run_torch(ta, to, tl, out, now, ids=ti)
+        torch.cuda.synchronize()
+        got = {k: v.cpu().numpy() for k, v in out.items()}
+        nd = ref["n_dgram"]
+        st = got["status"].view(np.uint32)
+        if not np.array_equal(st, ref["status"]):
+            bad = np.nonzero(st != ref["status"])[0]
+            raise AssertionError(f"status: {len(bad)} mismatches, first {bad[:6].tolist()}: "
+                                 f"gpu={st[bad[:6]].tolist()} ref={ref['status'][bad[:6]].tolist()}")
+        assert int(got["n_dgram"][0]) == nd
+        assert np.array_equal(got["dgram_of"].view(np.uint32), ref["dgram_of"])
+        assert np.array_equal(got["dgram_len"].view(np.uint32), ref["dgram_len"])   # 0 past the count
+        assert np.array_equal(got["dgram_frags"].view(np.uint64)[:nd], ref["dgram_frags"][:nd])
+        assert (got["dgram_frags"].view(np.uint64)[nd:] == np.uint64(2**64 - 1)).all()
+        for j in range(nd):
+            m = int(ref["dgram_len"][j])
+            assert np.array_equal(got["dgram_pkt"][j, :m], ref["dgram_pkt"][j, :m]), f"datagram {j} bytes"
+            w = np.zeros(self.stride, np.uint8)
+            w[:min(m, self.stride)] = ref["dgram_pkt"][j, :min(m, self.stride)]
+            assert np.array_equal(got["dgram_hdr"][j], w), f"datagram {j} window"
+        assert (got["dgram_hdr"][nd:] == 0).all()
+        return got, ref
+
+    def age(self, now, timeout=20):
+        gi, gf = self.g.age(now, timeout)
+        oi, of = self.o.age(now, timeout)
+        assert gf == of
+        assert sorted(gi.tolist()) == sorted(oi.tolist())
+
+    def check_stats(self):
+        gi, os_ = self.g.info(), self.o.stats()
+        for k, v in os_.items():
+            assert gi[k] == v, (k, gi[k], v)
+
+
+def replay(eng, a, o, l, bsz, now0=NOW, every_age=1, timeout=20, **cfg):
+    p = DfPair(eng, **cfg)
+    try:
+        ids = (np.arange(len(l), dtype=np.uint64) * 3 + 11)
+        for k, b in enumerate(range(0, len(l), bsz)):
+            p.batch(a, o[b:b + bsz], l[b:b + bsz], now0 + k, ids=ids[b:b + bsz])
+            if (k + 1) % every_age == 0:
+                p.age(now0 + k, timeout)
+        p.age(now0 + 10**6, timeout)
+        p.check_stats()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("seed,bsz", [(1, 4096), (2, 512), (3, 7), (4, 65536)])
+def test_stream_vs_oracle(eng, seed, bsz):
+    a, o, l = synth.make_fragment_stream(1500 if bsz > 7 else 200, seed=seed)
+    replay(eng, a, o, l, bsz, every_age=3)
+
+
+def test_unaligned_frames_and_pressure(eng):
+    """Byte-aligned frames (the stash's byte path), a small FCB pool (FCB_FULL churn) and a short cache."""
+    a, o, l = synth.make_fragment_stream(1200, seed=9, align=1)
+    replay(eng, a, o, l, 1024, fcb_max=40, cache_max=3)
+
+
+def test_cache_max_16_and_big_buffers(eng):
+    a, o, l = synth.make_fragment_stream(800, seed=10, jumbo=0.1)
+    replay(eng, a, o, l, 2048, cache_max=16, reasm_buf_bytes=16384, timeout=5)
+
+
+def test_window_64(eng):
+    a, o, l = synth.make_fragment_stream(600, seed=11)
+    p = DfPair(eng, stride=64)
+    try:
+        p.batch(a, o, l, NOW)
+    finally:
+        p.close()
+
+
+def test_datagrams_classify_like_the_oracle(eng):
+    """Defrag → classify of the reassembled batch (DecodeTCP / DecodeUDP / flow hash / ACL on the datagram,
+    decode-ipv4.c:241-290) equals the oracle classifying the oracle's datagrams."""
+    from ppe import synth as s
+    rules = s.make_rules(256)
+    eng.commit(rules)
+    orc = pyoracle.Oracle(rules)
+    a, o, l = synth.make_fragment_stream(1500, seed=12)
+    p = DfPair(eng, stride=128)
+    try:
+        got, ref = p.batch(a, o, l, NOW)
+    finally:
+        p.close()
+    n = len(l)
+    res = gpu_classify(eng, got["dgram_hdr"], got["dgram_len"].view(np.uint32), cfg=eng.cfg(now_seconds=NOW))
+    nd = ref["n_dgram"]
+    assert nd > 100
+    win = np.zeros((n, 128), np.uint8)
+    win[:nd] = ref["dgram_pkt"][:nd, :128]
+    want = orc.classify_batch(win, ref["dgram_len"], cfg=orc.cfg(now_seconds=NOW))
+    for k in ("verdict", "flow_hash", "acl_hit"):
+        assert np.array_equal(res[k], want[k]), k
+    st = res["verdict"][:nd] & 0xFF
+    assert (st <= abi.ST["ACL_DROP"]).sum() > nd // 2          # most datagrams reach the ACL
+    assert (res["verdict"][nd:] & 0xFF == abi.ST["L2_HEADER_ERR"]).all()   # padding entries (length 0)
+
+
+def test_small_cases_and_errors(eng):
+    S, D = 0x0A000001, 0x0A000002
+    l4 = udp(1, 2, bytes(8))
+    p = DfPair(eng)
+    try:
+        frames = [ip_frag(17, S, D, 1, 0, True, l4[:8]), ip_frag(17, S, D, 1, 8, False, l4[8:]),
+                  ip_frag(17, S, D, 1, 0, True, l4[:8])]
+        a, o, l = arena(frames)
+        got, _ = p.batch(a, o, l, NOW)
+        assert list(got["status"]) == [0, 1, 5]
+        a, o, l = arena([frames[0]])
+        p.batch(a, o, l, NOW)                              # n = 1: DELETED
+        p.age(NOW + 1)
+        p.batch(a, o, l, NOW + 2)                          # a fresh FCB after aging
+        p.check_stats()
+        # empty batch: nothing launched, nothing changes
+        b = abi.FragBatch(None, None, None, None, 0, 0, NOW)
+        oo = abi.DefragOut()
+        assert p.g.lib.ppe_defrag(p.g.h, b, oo, None) == 0
+        # too many fragments
+        b = abi.FragBatch(1, 1, 1, None, p.g.info_["max_batch"] + 1, 0, NOW)
+        assert p.g.lib.ppe_defrag(p.g.h, b, oo, None) == -22
+    finally:
+        p.close()
