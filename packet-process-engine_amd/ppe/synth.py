@@ -24,6 +24,9 @@ CONFIGS = {
     "C4": dict(n=1 << 20, rules=4096, kind="udp64"),
     # stateful flow table: 1M-packet batches over 256k bidirectional UDP flows, default FW
     "F1": dict(n=1 << 20, rules=256, kind="udp64", flows=1 << 18),
+    # IPv4 reassembly: 65,536-fragment batches (ppe_defrag's default max_batch) of a
+    # make_fragment_stream mix, every batch over fresh datagrams; an FCB pool large enough that no batch hits FCB_FULL
+    "D1": dict(n=1 << 16, rules=256, kind="frag", fcb_max=1 << 20),
 }
 
 MAC_POOL = 16
