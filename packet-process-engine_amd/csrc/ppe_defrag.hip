@@ -374,8 +374,58 @@ __global__ void __launch_bounds__(kSortBlock) df_sort_pass_kernel(DfArgs a) {
     a.sval[1][pos] = a.sval[0][j];
 }
 
+// exclusive scan of the digit histogram (256 x sort_blocks words) by one workgroup: thread t owns the contiguous chunk
+// [t*c, (t+1)*c) (16-B loads and stores), so there is one block-wide scan instead of one per 1,024 words
 __global__ void __launch_bounds__(kScanT) df_hist_scan_kernel(DfArgs a) {
-    block_scan_inplace(a.hist, 256u * a.sort_blocks, a.ctl + C_SCRATCH);
+    __shared__ uint32_t wsum[kScanT / 64];
+    const uint32_t m = 256u * a.sort_blocks;
+    const uint32_t c = (((m + kScanT - 1) / kScanT) + 3u) & ~3u;   // words per thread, a multiple of 4
+    const uint32_t b0 = threadIdx.x * c;
+    constexpr uint32_t kHold = 16;   // chunks of up to 64 words (max_batch <= 65,536) stay in registers
+    uint4 held[kHold];
+    const bool hold = c <= 4 * kHold;
+    uint32_t sum = 0;
+    if (hold) {
+#pragma unroll
+        for (uint32_t q = 0; q < kHold; ++q) {
+            const uint32_t k = b0 + 4 * q;
+            held[q] = (4 * q < c && k < m) ? *(const uint4 *)(a.hist + k) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kHold; ++q) sum += held[q].x + held[q].y + held[q].z + held[q].w;
+    } else {
+        for (uint32_t k = b0; k < b0 + c && k < m; k += 4) {   // m = 256 * sort_blocks is a multiple of 4
+            const uint4 v = *(const uint4 *)(a.hist + k);
+            sum += v.x + v.y + v.z + v.w;
+        }
+    }
+    uint32_t x = sum;   // inclusive wave scan of the chunk sums
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if ((int)__lane_id() >= o) x += y;
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if (__lane_id() == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t run = x - sum;
+    for (uint32_t k = 0; k < w; ++k) run += wsum[k];
+    if (hold) {
+#pragma unroll
+        for (uint32_t q = 0; q < kHold; ++q) {
+            const uint32_t k = b0 + 4 * q;
+            const uint4 v = held[q];
+            if (4 * q < c && k < m)
+                *(uint4 *)(a.hist + k) = make_uint4(run, run + v.x, run + v.x + v.y, run + v.x + v.y + v.z);
+            run += v.x + v.y + v.z + v.w;
+        }
+        return;
+    }
+    for (uint32_t k = b0; k < b0 + c && k < m; k += 4) {
+        uint4 v = *(const uint4 *)(a.hist + k);
+        const uint4 e = make_uint4(run, run + v.x, run + v.x + v.y, run + v.x + v.y + v.z);
+        run += v.x + v.y + v.z + v.w;
+        *(uint4 *)(a.hist + k) = e;
+    }
 }
 
 // ---- the reference state machine, one lane per FCB --------------------------------------------------------------------
@@ -386,19 +436,18 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
     if (j >= a.n) return;
     const uint32_t *key = a.skey[0];
     const uint32_t r = key[j];
-    if (j > 0 && key[j - 1] == r) return;   // not the head of its FCB's segment
+    if (j > 0 && key[j - 1] == r && r != a.sent) return;   // not the head of its FCB's segment
     unsigned long long st[PPE_DF__COUNT] = {};
     unsigned long long teardrop = 0;
-    if (r == a.sent) {
-        for (uint32_t q = j; q < a.n && key[q] == r; ++q) {
-            const uint32_t i = a.sval[0][q];
-            const bool frag = a.frec[(size_t)i * kFrecWords + 7] != 0;
-            const uint32_t s = frag ? PPE_DF_FCB_FULL : PPE_DF_NOT_FRAG;
-            a.status[i] = s;
-            a.inserted[i] = kNone;
-            a.dgrec[i] = kNone;
-            st[s]++;
-        }
+    if (r == a.sent) {   // fragments without a record (no FCB, or not fragments): independent, one lane each
+        const uint32_t i = a.sval[0][j];
+        const bool frag = a.frec[(size_t)i * kFrecWords + 7] != 0;
+        const uint32_t s = frag ? PPE_DF_FCB_FULL : PPE_DF_NOT_FRAG;
+        a.status[i] = s;
+        a.inserted[i] = kNone;
+        a.dgrec[i] = kNone;
+        atomicAdd(a.ctl + C_ST0 + s, 1ull);
+        return;
     } else {
         uint32_t *h = a.rhdr + (size_t)r * kRecWords;
         uint32_t flags = h[0] & 0xffu, last_in = (h[0] >> 8) & 0xffu, cache_num = (h[0] >> 16) & 0xffu,
@@ -407,9 +456,19 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
         uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
         const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
         uint32_t *descw = a.rdesc + (size_t)r * a.cache_max * 4;
+        // the segment's fragments in order; the next one's index and record words are requested before the
+        // current one is processed (the chain is a serial dependence, the loads need not be)
+        uint32_t i_nx = a.sval[0][j];
+        uint4 f0_nx = *(const uint4 *)(a.frec + (size_t)i_nx * kFrecWords);
+        uint2 f1_nx = *(const uint2 *)(a.frec + (size_t)i_nx * kFrecWords + 4);
         for (uint32_t q = j; q < a.n && key[q] == r; ++q) {
-            const uint32_t i = a.sval[0][q];
-            const uint32_t *fr = a.frec + (size_t)i * kFrecWords;
+            const uint32_t i = i_nx;
+            const uint32_t fr[6] = {f0_nx.x, f0_nx.y, f0_nx.z, f0_nx.w, f1_nx.x, f1_nx.y};
+            if (q + 1 < a.n && key[q + 1] == r) {
+                i_nx = a.sval[0][q + 1];
+                f0_nx = *(const uint4 *)(a.frec + (size_t)i_nx * kFrecWords);
+                f1_nx = *(const uint2 *)(a.frec + (size_t)i_nx * kFrecWords + 4);
+            }
             uint32_t out = PPE_DF_CACHED, ins = kNone, done = kNone;
             bool tear = false;
             // FragFind / fcb_create refresh the FCB's timestamp (decode-defrag.c:139, 472); a.rts[r] = now below
@@ -543,17 +602,19 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
     if (a.dgram_of) a.dgram_of[i] = j;
 }
 
-// ---- assemble: one workgroup per datagram slot ----------------------------------------------------------------------
+// ---- assemble: one wave per datagram slot ----------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
-    const uint32_t j = blockIdx.x;
+    const uint32_t j = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);   // one wave per datagram slot
+    const uint32_t tid = __lane_id();
+    if (j >= a.n) return;
     const uint32_t nd = (uint32_t)a.ctl[C_NDGRAM];
     uint8_t *win = a.dgram_hdr ? a.dgram_hdr + (size_t)j * a.hdr_stride : nullptr;
     if (j >= nd) {
         if (win)
-            for (uint32_t b = threadIdx.x; b < a.hdr_stride; b += kBlock) win[b] = 0;
-        if (threadIdx.x == 0 && a.dgram_len) a.dgram_len[j] = 0;
+            for (uint32_t b = tid; b < a.hdr_stride; b += 64) win[b] = 0;
+        if (tid == 0 && a.dgram_len) a.dgram_len[j] = 0;
         if (a.dgram_frags)
-            for (uint32_t k = threadIdx.x; k < a.cache_max; k += kBlock) a.dgram_frags[(size_t)j * a.cache_max + k] = ~0ull;
+            for (uint32_t k = tid; k < a.cache_max; k += 64) a.dgram_frags[(size_t)j * a.cache_max + k] = ~0ull;
         return;
     }
     const uint32_t i = a.dgsrc[j];
@@ -601,29 +662,57 @@ __global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
     uint8_t *full = a.dgram_pkt ? a.dgram_pkt + (size_t)j * a.reasm_buf : nullptr;
     const uint32_t stride = a.hdr_stride;
     uint32_t dst0 = 0;
+    // whole output dwords are assembled from two aligned source dwords (a funnel shift) and stored as dwords; the
+    // partial dwords at a segment's ends are stored bytewise (the neighbouring segment owns their other bytes)
+    const bool wide = full && ((uintptr_t)full & 3u) == 0 && (a.reasm_buf & 3u) == 0;
     for (uint32_t p = 0; p < (icmp ? 1u : nlist); ++p) {
         const uint32_t k = chain_at(order, p);
         const uint32_t tot = desc[k * 4 + 1], flen = desc[k * 4] >> 16;
         const uint8_t *src = a.store + ((size_t)r * a.cache_max + k) * a.sstride + (p == 0 ? 0u : tot - flen);
         const uint32_t cnt = p == 0 ? tot : flen;
-        const uint32_t lim = full ? cnt : (dst0 < stride ? (cnt < stride - dst0 ? cnt : stride - dst0) : 0u);
-        for (uint32_t b = threadIdx.x; b < lim; b += kBlock) {
-            const uint32_t ob = dst0 + b;
-            const uint32_t v = patched(ob, src[b]);
-            if (full && ob < a.reasm_buf) full[ob] = (uint8_t)v;
-            if (win && ob < stride) win[ob] = (uint8_t)v;
+        if (win && dst0 < stride) {
+            const uint32_t wl = cnt < stride - dst0 ? cnt : stride - dst0;
+            for (uint32_t b = tid; b < wl; b += 64) win[dst0 + b] = (uint8_t)patched(dst0 + b, src[b]);
+        }
+        if (full) {
+            const uint32_t end = dst0 + cnt < a.reasm_buf ? dst0 + cnt : a.reasm_buf;   // output bytes [dst0, end)
+            if (wide && end > dst0) {
+                const uint32_t wa = (dst0 + 3u) >> 2, we = end >> 2;   // whole dwords [wa, we)
+                for (uint32_t w = wa + tid; w < we; w += 64) {
+                    const uint8_t *sp = src + (4u * w - dst0);
+                    const uint32_t *ap = (const uint32_t *)((uintptr_t)sp & ~(uintptr_t)3);
+                    const uint32_t sh = (uint32_t)((uintptr_t)sp & 3u) * 8u;
+                    uint32_t v = ap[0];
+                    if (sh) v = (v >> sh) | (ap[1] << (32u - sh));
+                    if (4u * w + 3u >= l2 && 4u * w < l2 + 12u) {
+                        uint32_t pv = 0;
+                        for (uint32_t q = 0; q < 4; ++q) pv |= patched(4u * w + q, (v >> (8u * q)) & 0xffu) << (8u * q);
+                        v = pv;
+                    }
+                    ((uint32_t *)full)[w] = v;
+                }
+                // head bytes [dst0, 4*wa) and tail bytes [4*we, end) (when the segment lies inside one dword, all)
+                const uint32_t hb = 4u * wa < end ? 4u * wa : end;
+                const uint32_t tb = 4u * we > hb ? 4u * we : hb;
+                const uint32_t t = tid;
+                if (t < hb - dst0) full[dst0 + t] = (uint8_t)patched(dst0 + t, src[t]);
+                if (t < end - tb) full[tb + t] = (uint8_t)patched(tb + t, src[tb - dst0 + t]);
+            } else {
+                for (uint32_t ob = dst0 + tid; ob < end; ob += 64)
+                    full[ob] = (uint8_t)patched(ob, src[ob - dst0]);
+            }
         }
         dst0 += cnt;
     }
     if (icmp && full) {   // bytes the reference never wrote: zero
         const uint32_t lim = out_len < a.reasm_buf ? out_len : a.reasm_buf;
-        for (uint32_t b = dst0 + threadIdx.x; b < lim; b += kBlock) full[b] = 0;
+        for (uint32_t b = dst0 + tid; b < lim; b += 64) full[b] = 0;
     }
     if (win)
-        for (uint32_t b = dst0 + threadIdx.x; b < stride; b += kBlock) win[b] = 0;
-    if (threadIdx.x == 0 && a.dgram_len) a.dgram_len[j] = out_len;
+        for (uint32_t b = dst0 + tid; b < stride; b += 64) win[b] = 0;
+    if (tid == 0 && a.dgram_len) a.dgram_len[j] = out_len;
     if (a.dgram_frags)
-        for (uint32_t p = threadIdx.x; p < a.cache_max; p += kBlock)
+        for (uint32_t p = tid; p < a.cache_max; p += 64)
             a.dgram_frags[(size_t)j * a.cache_max + p] =
                 p < nlist ? a.rid[(size_t)r * a.cache_max + chain_at(order, p)] : ~0ull;
 }
@@ -777,11 +866,12 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
     a.sent = d->sent;
     const uint32_t mb = c.max_batch;
     const uint32_t sb = blocks(mb, kSortBlock);
+    // the store carries 64 spare bytes: df_assemble_kernel reads whole aligned dwords past a frame's last byte
     bool ok = dalloc(d, &a.tstate, ns) && dalloc(d, &a.tkey, (size_t)ns * 4) && dalloc(d, &a.creator, ns) &&
               dalloc(d, &a.rhdr, (size_t)c.fcb_max * kRecWords) &&
               dalloc(d, &a.rdesc, (size_t)c.fcb_max * c.cache_max * 4) && dalloc(d, &a.rts, c.fcb_max) &&
               dalloc(d, &a.rid, (size_t)c.fcb_max * c.cache_max) &&
-              dalloc(d, &a.store, (size_t)c.fcb_max * c.cache_max * d->sstride) && dalloc(d, &a.freestk, c.fcb_max) &&
+              dalloc(d, &a.store, (size_t)c.fcb_max * c.cache_max * d->sstride + 64) && dalloc(d, &a.freestk, c.fcb_max) &&
               dalloc(d, &a.ctl, C_WORDS) && dalloc(d, &a.frec, (size_t)mb * kFrecWords) && dalloc(d, &a.fslot, mb) &&
               dalloc(d, &a.inserted, mb) && dalloc(d, &a.dgrec, mb) && dalloc(d, &a.dgsrc, mb) &&
               dalloc(d, &a.tcnt, blocks(mb, 64)) && dalloc(d, &a.skey[0], mb) && dalloc(d, &a.sval[0], mb) &&
@@ -864,7 +954,7 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
     hipLaunchKernelGGL(df_tile_count_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(df_place_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(df_assemble_kernel, dim3(a.n), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(df_assemble_kernel, dim3(blocks(a.n, kBlock / 64)), dim3(kBlock), 0, s, a);
     return launched(d, "ppe_defrag");
 }
 
