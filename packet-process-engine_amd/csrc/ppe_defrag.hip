@@ -42,7 +42,7 @@ constexpr uint32_t kEmpty = 0u, kTomb = 1u, kLive = 2u, kPend = 0x80000000u;
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kBlock = 256;        // workgroup size of the per-fragment kernels
 constexpr uint32_t kScanT = 1024;       // one-workgroup scans
-constexpr uint32_t kSortBlock = 256;    // radix sort: elements (= threads) per workgroup
+constexpr uint32_t kSortBlock = 1024;   // radix sort: elements (= threads) per workgroup (64k-word histogram)
 
 // FCB record header word 0
 constexpr uint32_t kRecLive = 1u << 0;
@@ -431,14 +431,14 @@ __global__ void __launch_bounds__(kScanT) df_hist_scan_kernel(DfArgs a) {
 // ---- the reference state machine, one lane per FCB --------------------------------------------------------------------
 __device__ __forceinline__ uint32_t chain_at(uint64_t order, uint32_t pos) { return (uint32_t)(order >> (4 * pos)) & 15u; }
 
-__global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
-    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= a.n) return;
+// cdesc: word 0 (offset | frag_len << 16) of the lane's FCB's chain descriptors, which the chain scan reads serially:
+// LDS round trips instead of global ones.  Private per lane ([slot][lane]: no bank conflicts), no barrier.
+__device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint32_t (*cdesc)[kBlock], uint32_t *st,
+                                               uint32_t &teardrop) {
+    const uint32_t tl = threadIdx.x;
     const uint32_t *key = a.skey[0];
     const uint32_t r = key[j];
     if (j > 0 && key[j - 1] == r && r != a.sent) return;   // not the head of its FCB's segment
-    unsigned long long st[PPE_DF__COUNT] = {};
-    unsigned long long teardrop = 0;
     if (r == a.sent) {   // fragments without a record (no FCB, or not fragments): independent, one lane each
         const uint32_t i = a.sval[0][j];
         const bool frag = a.frec[(size_t)i * kFrecWords + 7] != 0;
@@ -446,7 +446,7 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
         a.status[i] = s;
         a.inserted[i] = kNone;
         a.dgrec[i] = kNone;
-        atomicAdd(a.ctl + C_ST0 + s, 1ull);
+        st[s]++;
         return;
     } else {
         uint32_t *h = a.rhdr + (size_t)r * kRecWords;
@@ -456,6 +456,7 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
         uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
         const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
         uint32_t *descw = a.rdesc + (size_t)r * a.cache_max * 4;
+        for (uint32_t k = 0; k < cache_num && k < 16; ++k) cdesc[k][tl] = desc[k * 4];
         // the segment's fragments in order; the next one's index and record words are requested before the
         // current one is processed (the chain is a serial dependence, the loads need not be)
         uint32_t i_nx = a.sval[0][j];
@@ -498,14 +499,14 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
                 uint32_t pos = nlist;       // insert before chain position pos
                 if (!err) {
                     int prev = -1, next = -1;
-                    if (nlist == 0 || (int)(desc[chain_at(order, nlist - 1) * 4] & 0xffffu) < offset) {
+                    if (nlist == 0 || (int)(cdesc[chain_at(order, nlist - 1)][tl] & 0xffffu) < offset) {
                         prev = nlist ? (int)chain_at(order, nlist - 1) : -1;
                     } else {
                         // the reference's scan compares the chained fragment's frag_len with the new offset
                         // (decode-defrag.c:344-349)
                         for (pos = 0; pos < nlist; ++pos) {
                             const uint32_t k = chain_at(order, pos);
-                            if ((int)(desc[k * 4] >> 16) >= offset) {
+                            if ((int)(cdesc[k][tl] >> 16) >= offset) {
                                 next = (int)k;
                                 break;
                             }
@@ -513,10 +514,10 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
                         }
                     }
                     if (prev >= 0) {
-                        const uint32_t pd = desc[prev * 4];
+                        const uint32_t pd = cdesc[prev][tl];
                         if ((int)(pd & 0xffffu) + (int)(pd >> 16) - offset > 0) err = tear = true;
                     }
-                    if (!err && next >= 0 && (int)(desc[next * 4] & 0xffffu) - end < 0) err = tear = true;
+                    if (!err && next >= 0 && (int)(cdesc[next][tl] & 0xffffu) - end < 0) err = tear = true;
                 }
                 if (err) {
                     out = PPE_DF_DEFRAG_ERR;
@@ -524,6 +525,7 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
                 } else {
                     const uint32_t k = cache_num;      // store slot: the fragment's arrival rank in this FCB
                     descw[k * 4 + 0] = fr[3];
+                    cdesc[k][tl] = fr[3];
                     descw[k * 4 + 1] = fr[4];
                     descw[k * 4 + 2] = fr[5] | ((fr[2] >> 16) & 0xffu) << 16;
                     descw[k * 4 + 3] = 0;
@@ -563,9 +565,26 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
         h[5] = (uint32_t)(order >> 32);
         a.rts[r] = a.now;
     }
+}
+
+__global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
+    __shared__ uint32_t cdesc[16][kBlock];
+    __shared__ uint32_t wg[PPE_DF__COUNT + 1];   // per-status counts + teardrops of this workgroup
+    if (threadIdx.x <= PPE_DF__COUNT) wg[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t st[PPE_DF__COUNT] = {}, teardrop = 0;
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j < a.n) df_process_one(a, j, cdesc, st, teardrop);
+    // LDS atomics, then one global atomic per counter per workgroup: per-lane global atomics on the same few
+    // words serialise in one L2 channel (they were most of this kernel's time)
+#pragma unroll
     for (int s = 0; s < PPE_DF__COUNT; ++s)
-        if (st[s]) atomicAdd(a.ctl + C_ST0 + s, st[s]);
-    if (teardrop) atomicAdd(a.ctl + C_TEARDROP, teardrop);
+        if (st[s]) atomicAdd(&wg[s], st[s]);
+    if (teardrop) atomicAdd(&wg[PPE_DF__COUNT], teardrop);
+    __syncthreads();
+    if (threadIdx.x <= PPE_DF__COUNT && wg[threadIdx.x])
+        atomicAdd(a.ctl + (threadIdx.x < PPE_DF__COUNT ? C_ST0 + threadIdx.x : C_TEARDROP),
+                  (unsigned long long)wg[threadIdx.x]);
 }
 
 // ---- stash: copy held frames into their FCB's store slot (PACKET_HW2SW) ----------------------------------------------
