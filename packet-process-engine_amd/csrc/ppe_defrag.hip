@@ -599,8 +599,22 @@ __global__ void __launch_bounds__(kBlock) df_stash_kernel(DfArgs a) {
     const uint32_t tot = a.len[i];
     const uint32_t lane = __lane_id();
     if (((uintptr_t)src & 3u) == 0) {
+        // all of a pass's loads are issued before its stores (2 KB per pass: one pass for a frag_buf frame)
+        constexpr uint32_t U = 8;
         const uint32_t words = tot / 4;
-        for (uint32_t w = lane; w < words; w += 64) ((uint32_t *)dst)[w] = ((const uint32_t *)src)[w];
+        for (uint32_t base = 0; base < words; base += 64 * U) {
+            uint32_t v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t w = base + u * 64 + lane;
+                v[u] = w < words ? ((const uint32_t *)src)[w] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t w = base + u * 64 + lane;
+                if (w < words) ((uint32_t *)dst)[w] = v[u];
+            }
+        }
         for (uint32_t b = words * 4 + lane; b < tot; b += 64) dst[b] = src[b];
     } else {
         for (uint32_t b = lane; b < tot; b += 64) dst[b] = src[b];
@@ -697,18 +711,32 @@ __global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
             const uint32_t end = dst0 + cnt < a.reasm_buf ? dst0 + cnt : a.reasm_buf;   // output bytes [dst0, end)
             if (wide && end > dst0) {
                 const uint32_t wa = (dst0 + 3u) >> 2, we = end >> 2;   // whole dwords [wa, we)
-                for (uint32_t w = wa + tid; w < we; w += 64) {
-                    const uint8_t *sp = src + (4u * w - dst0);
-                    const uint32_t *ap = (const uint32_t *)((uintptr_t)sp & ~(uintptr_t)3);
-                    const uint32_t sh = (uint32_t)((uintptr_t)sp & 3u) * 8u;
-                    uint32_t v = ap[0];
-                    if (sh) v = (v >> sh) | (ap[1] << (32u - sh));
-                    if (4u * w + 3u >= l2 && 4u * w < l2 + 12u) {
-                        uint32_t pv = 0;
-                        for (uint32_t q = 0; q < 4; ++q) pv |= patched(4u * w + q, (v >> (8u * q)) & 0xffu) << (8u * q);
-                        v = pv;
+                // the segment's source shift is the same for every dword: aligned loads, funnel-shifted pairs
+                const uintptr_t s0 = (uintptr_t)(src + (4u * wa - dst0));
+                const uint32_t sh = (uint32_t)(s0 & 3u) * 8u;
+                const uint32_t *ap = (const uint32_t *)(s0 & ~(uintptr_t)3);   // source dword of output dword wa
+                constexpr uint32_t U = 4;   // 1 KB of output per pass, every load issued before the stores
+                for (uint32_t base = wa; base < we; base += 64 * U) {
+                    uint32_t lo[U], hi[U];
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        const uint32_t w = base + u * 64 + tid;
+                        lo[u] = w < we ? ap[w - wa] : 0u;
+                        hi[u] = (w < we && sh) ? ap[w - wa + 1] : 0u;
                     }
-                    ((uint32_t *)full)[w] = v;
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        const uint32_t w = base + u * 64 + tid;
+                        if (w >= we) continue;
+                        uint32_t v = sh ? (lo[u] >> sh) | (hi[u] << (32u - sh)) : lo[u];
+                        if (4u * w + 3u >= l2 && 4u * w < l2 + 12u) {
+                            uint32_t pv = 0;
+                            for (uint32_t q = 0; q < 4; ++q)
+                                pv |= patched(4u * w + q, (v >> (8u * q)) & 0xffu) << (8u * q);
+                            v = pv;
+                        }
+                        ((uint32_t *)full)[w] = v;
+                    }
                 }
                 // head bytes [dst0, 4*wa) and tail bytes [4*we, end) (when the segment lies inside one dword, all)
                 const uint32_t hb = 4u * wa < end ? 4u * wa : end;
