@@ -12,8 +12,9 @@
  *   admit      creators in index order (per-tile ballot counts, one-workgroup scan) get FCB records while
  *              running + rank < fcb_max (fcb_create's fetch-and-add cap); the others fail, and with them every later
  *              fragment of their key in this batch, because the running count cannot fall inside a batch;
- *   group      stable LSD radix sort of the fragments by FCB record (8-bit digits, wave multisplit ranks), so each
- *              FCB's fragments are contiguous and in arrival order;
+ *   group      stable LSD radix sort of the fragments by FCB, keyed by the FCB's first fragment index in the batch
+ *              (8-bit digits, wave multisplit ranks; 2 passes for 65,536 fragments), so each FCB's fragments are
+ *              contiguous and in arrival order;
  *   process    one lane per FCB runs the reference state machine over its fragments in order (chain ≤ cache_max
  *              entries, kept as a nibble list of store slots);
  *   stash      one wave per held fragment copies its frame into the FCB's store slot (PACKET_HW2SW, mbuf.c:117-156);
@@ -93,7 +94,7 @@ struct DfArgs {
     // batch scratch
     uint32_t *frec, *fslot, *inserted, *dgrec, *dgsrc, *tcnt;
     uint32_t *skey[2], *sval[2], *hist;
-    uint32_t shift, sort_blocks, sent;   // radix pass: digit shift, workgroups, sentinel key (no record)
+    uint32_t shift, sort_blocks;         // radix pass: digit shift, workgroups
     uint32_t flag_mode;                  // tile counts: 0 creators, 1 completing fragments
     uint64_t *dropped;                   // age: ids of dropped fragments
     uint32_t max_dropped;
@@ -196,7 +197,13 @@ __global__ void __launch_bounds__(kBlock) df_parse_kernel(DfArgs a) {
 // ---- claim: a slot per new key, lowest claiming index recorded ------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) df_claim_kernel(DfArgs a) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= a.n || a.fslot[i] != kNone) return;
+    if (i >= a.n) return;
+    const uint32_t fs = a.fslot[i];
+    if (fs < kNone - 1) {   // found in the table: the FCB's first fragment in this batch is its group key
+        atomicMin(a.creator + fs, i);
+        return;
+    }
+    if (fs != kNone) return;
     const uint32_t *fr = a.frec + (size_t)i * kFrecWords;
     const uint32_t sip = fr[0], dip = fr[1], id = fr[2] & 0xffffu;
     uint32_t s = fr[6] & a.smask;
@@ -300,7 +307,6 @@ __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
     if (!f) return;
     const uint32_t rank = a.tcnt[i >> 6] + (uint32_t)__popcll(b & lanemask_lt());
     const uint32_t s = a.fslot[i];
-    a.creator[s] = kNone;
     // fcb_create (decode-defrag.c:74-81): fetch-and-add, fail when the previous count reached DEFRAG_FCB_MAX
     if (a.ctl[C_ADMIT_BASE] + rank < a.fcb_max) {
         const uint32_t r = a.freestk[a.ctl[C_FREE_BASE] - 1 - rank];
@@ -327,8 +333,10 @@ __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
 // ---- stable LSD radix sort of (record, index) by record -------------------------------------------------------------
 __device__ __forceinline__ uint32_t df_sort_key(const DfArgs &a, uint32_t i) {
     const uint32_t s = a.fslot[i];
-    if (s >= kNone - 1 || a.tstate[s] != kLive) return a.sent;   // not a fragment, or its FCB could not be created
-    return a.tkey[(size_t)s * 4 + 3];
+    // fragments without a record (not a fragment, or its FCB could not be created) form singleton groups keyed by
+    // their own index, which no FCB group uses (a group's key is the index of one of its own fragments)
+    if (s >= kNone - 1 || a.tstate[s] != kLive) return i;
+    return a.creator[s];   // the FCB's first fragment in this batch: keys < n, so ceil(log2 n) / 8 radix passes
 }
 
 __global__ void __launch_bounds__(kBlock) df_sort_init_kernel(DfArgs a) {
@@ -437,10 +445,14 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
                                                uint32_t &teardrop) {
     const uint32_t tl = threadIdx.x;
     const uint32_t *key = a.skey[0];
-    const uint32_t r = key[j];
-    if (j > 0 && key[j - 1] == r && r != a.sent) return;   // not the head of its FCB's segment
-    if (r == a.sent) {   // fragments without a record (no FCB, or not fragments): independent, one lane each
-        const uint32_t i = a.sval[0][j];
+    const uint32_t g = key[j];
+    if (j > 0 && key[j - 1] == g) return;   // not the head of its FCB's segment
+    const uint32_t i0 = a.sval[0][j];
+    const uint32_t s0 = a.fslot[i0];
+    const bool rec = s0 < kNone - 1 && a.tstate[s0] == kLive;
+    if (s0 < kNone - 1) a.creator[s0] = kNone;   // the group key has been used: reset for the next batch
+    if (!rec) {   // a fragment without a record (no FCB, or not a fragment): a singleton group
+        const uint32_t i = i0;
         const bool frag = a.frec[(size_t)i * kFrecWords + 7] != 0;
         const uint32_t s = frag ? PPE_DF_FCB_FULL : PPE_DF_NOT_FRAG;
         a.status[i] = s;
@@ -449,6 +461,7 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
         st[s]++;
         return;
     } else {
+        const uint32_t r = a.tkey[(size_t)s0 * 4 + 3];
         uint32_t *h = a.rhdr + (size_t)r * kRecWords;
         uint32_t flags = h[0] & 0xffu, last_in = (h[0] >> 8) & 0xffu, cache_num = (h[0] >> 16) & 0xffu,
                  nlist = h[0] >> 24;
@@ -459,13 +472,13 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
         for (uint32_t k = 0; k < cache_num && k < 16; ++k) cdesc[k][tl] = desc[k * 4];
         // the segment's fragments in order; the next one's index and record words are requested before the
         // current one is processed (the chain is a serial dependence, the loads need not be)
-        uint32_t i_nx = a.sval[0][j];
+        uint32_t i_nx = i0;
         uint4 f0_nx = *(const uint4 *)(a.frec + (size_t)i_nx * kFrecWords);
         uint2 f1_nx = *(const uint2 *)(a.frec + (size_t)i_nx * kFrecWords + 4);
-        for (uint32_t q = j; q < a.n && key[q] == r; ++q) {
+        for (uint32_t q = j; q < a.n && key[q] == g; ++q) {
             const uint32_t i = i_nx;
             const uint32_t fr[6] = {f0_nx.x, f0_nx.y, f0_nx.z, f0_nx.w, f1_nx.x, f1_nx.y};
-            if (q + 1 < a.n && key[q + 1] == r) {
+            if (q + 1 < a.n && key[q + 1] == g) {
                 i_nx = a.sval[0][q + 1];
                 f0_nx = *(const uint4 *)(a.frec + (size_t)i_nx * kFrecWords);
                 f1_nx = *(const uint2 *)(a.frec + (size_t)i_nx * kFrecWords + 4);
@@ -837,7 +850,7 @@ __global__ void df_init_kernel(DfArgs a) {
 struct ppe_defrag_table {
     int device = 0;
     ppe_defrag_cfg_t cfg{};
-    uint32_t nslots = 0, sstride = 0, passes = 0, sent = 0;
+    uint32_t nslots = 0, sstride = 0;
     DfArgs base{};   // persistent device pointers + sizes
     void *allocs[24] = {};
     int nalloc = 0;
@@ -899,10 +912,6 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
     while (ns < 2ull * ((uint64_t)c.fcb_max + c.max_batch)) ns <<= 1;
     d->nslots = ns;
     d->sstride = (c.frag_buf_bytes + 63u) & ~63u;
-    d->sent = c.fcb_max;   // sort key of fragments without a record
-    uint32_t bits = 1;
-    while ((1u << bits) <= d->sent) ++bits;
-    d->passes = (bits + 7) / 8;
     DfArgs &a = d->base;
     a.smask = ns - 1;
     a.fcb_max = c.fcb_max;
@@ -910,7 +919,6 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
     a.frag_buf = c.frag_buf_bytes;
     a.reasm_buf = c.reasm_buf_bytes;
     a.sstride = d->sstride;
-    a.sent = d->sent;
     const uint32_t mb = c.max_batch;
     const uint32_t sb = blocks(mb, kSortBlock);
     // the store carries 64 spare bytes: df_assemble_kernel reads whole aligned dwords past a frame's last byte
@@ -987,7 +995,9 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
     hipLaunchKernelGGL(df_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(df_admit_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_sort_init_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    for (uint32_t p = 0; p < d->passes; ++p) {
+    uint32_t passes = 1;   // sort keys are batch indices < n
+    while (passes < 4 && (uint64_t)a.n > (1ull << (8 * passes))) ++passes;
+    for (uint32_t p = 0; p < passes; ++p) {
         a.shift = 8 * p;
         hipLaunchKernelGGL(df_sort_pass_kernel<false>, dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
         hipLaunchKernelGGL(df_hist_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
