@@ -339,15 +339,9 @@ __device__ __forceinline__ uint32_t df_sort_key(const DfArgs &a, uint32_t i) {
     return a.creator[s];   // the FCB's first fragment in this batch: keys < n, so ceil(log2 n) / 8 radix passes
 }
 
-__global__ void __launch_bounds__(kBlock) df_sort_init_kernel(DfArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    a.skey[0][i] = df_sort_key(a, i);
-    a.sval[0][i] = i;
-}
-
 // in: skey[0]/sval[0] → out: skey[1]/sval[1]; hist layout digit-major: hist[d * sort_blocks + block]
-template <bool SCATTER>
+// INIT (first histogram pass): the keys are computed here and written to skey[0] / sval[0] (no separate init launch)
+template <bool SCATTER, bool INIT>
 __global__ void __launch_bounds__(kSortBlock) df_sort_pass_kernel(DfArgs a) {
     __shared__ uint32_t cnt[kSortBlock / 64][256];
     const uint32_t w = threadIdx.x >> 6;
@@ -355,7 +349,14 @@ __global__ void __launch_bounds__(kSortBlock) df_sort_pass_kernel(DfArgs a) {
     __syncthreads();
     const uint32_t j = blockIdx.x * kSortBlock + threadIdx.x;
     const bool v = j < a.n;
-    const uint32_t key = v ? a.skey[0][j] : 0u;
+    uint32_t key = 0u;
+    if (INIT && v) {
+        key = df_sort_key(a, j);
+        a.skey[0][j] = key;
+        a.sval[0][j] = j;
+    } else if (v) {
+        key = a.skey[0][j];
+    }
     const uint32_t d = (key >> a.shift) & 0xffu;
     // wave multisplit: lanes with the same digit
     uint64_t peers = __builtin_amdgcn_ballot_w64(v);
@@ -649,15 +650,15 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
 }
 
 // ---- assemble: one wave per datagram slot ----------------------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
-    const uint32_t j = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);   // one wave per datagram slot
+__device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, uint32_t nd) {
     const uint32_t tid = __lane_id();
-    if (j >= a.n) return;
-    const uint32_t nd = (uint32_t)a.ctl[C_NDGRAM];
     uint8_t *win = a.dgram_hdr ? a.dgram_hdr + (size_t)j * a.hdr_stride : nullptr;
     if (j >= nd) {
-        if (win)
+        if (win && ((uintptr_t)win & 3u) == 0) {
+            if (tid < a.hdr_stride / 4) ((uint32_t *)win)[tid] = 0u;
+        } else if (win) {
             for (uint32_t b = tid; b < a.hdr_stride; b += 64) win[b] = 0;
+        }
         if (tid == 0 && a.dgram_len) a.dgram_len[j] = 0;
         if (a.dgram_frags)
             for (uint32_t k = tid; k < a.cache_max; k += 64) a.dgram_frags[(size_t)j * a.cache_max + k] = ~0ull;
@@ -671,14 +672,23 @@ __global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
     const uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
     const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
     const uint32_t k0 = chain_at(order, 0);
-    const uint32_t hd = desc[k0 * 4 + 2];
+    // lane p holds chain entry p's descriptor words 0 (offset | frag_len << 16), 1 (frame length), 2 (l2 | ihl*4 << 8
+    // | proto << 16): one round of loads for the whole chain, read below with lane broadcasts
+    uint32_t cd0 = 0, cd1 = 0, cd2 = 0;
+    if (tid < nlist) {
+        const uint32_t kk = chain_at(order, tid);
+        cd0 = desc[kk * 4];
+        cd1 = desc[kk * 4 + 1];
+        cd2 = desc[kk * 4 + 2];
+    }
+    const uint32_t hd = __shfl(cd2, 0, 64);
     const uint32_t l2 = hd & 0xffu, ihl4 = (hd >> 8) & 0xffu, proto = (hd >> 16) & 0xffu;
-    const uint32_t head_tot = desc[k0 * 4 + 1];
+    const uint32_t head_tot = __shfl(cd1, 0, 64);
     const bool icmp = proto == 1u;
     const uint8_t *hsrc = a.store + ((size_t)r * a.cache_max + k0) * a.sstride;
     // out_len = head frame + the later fragments' payloads (reasm_mb->pkt_totallen, decode-defrag.c:240-266)
     uint32_t out_len = head_tot;
-    for (uint32_t p = 1; p < nlist; ++p) out_len += desc[chain_at(order, p) * 4] >> 16;
+    for (uint32_t p = 1; p < nlist; ++p) out_len += __shfl(cd0, p, 64) >> 16;
     // header patch (non-ICMP: ip_len = ihl*4 + total, ip_off = 0, checksum; ICMP: ip_off = 0)
     uint32_t w_iplen = ld_be16(hsrc + l2 + 2), w_csum = ld_be16(hsrc + l2 + 10);
     if (!icmp) {
@@ -713,7 +723,7 @@ __global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
     const bool wide = full && ((uintptr_t)full & 3u) == 0 && (a.reasm_buf & 3u) == 0;
     for (uint32_t p = 0; p < (icmp ? 1u : nlist); ++p) {
         const uint32_t k = chain_at(order, p);
-        const uint32_t tot = desc[k * 4 + 1], flen = desc[k * 4] >> 16;
+        const uint32_t tot = __shfl(cd1, p, 64), flen = __shfl(cd0, p, 64) >> 16;
         const uint8_t *src = a.store + ((size_t)r * a.cache_max + k) * a.sstride + (p == 0 ? 0u : tot - flen);
         const uint32_t cnt = p == 0 ? tot : flen;
         if (win && dst0 < stride) {
@@ -775,6 +785,12 @@ __global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
         for (uint32_t p = tid; p < a.cache_max; p += 64)
             a.dgram_frags[(size_t)j * a.cache_max + p] =
                 p < nlist ? a.rid[(size_t)r * a.cache_max + chain_at(order, p)] : ~0ull;
+}
+
+// one wave per slot (a fixed grid striding over the slots measured slower: 50 vs 40 µs for D1)
+__global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
+    const uint32_t j = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (j < a.n) df_assemble_slot(a, j, (uint32_t)a.ctl[C_NDGRAM]);
 }
 
 // ---- aging + table rebuild (one workgroup) ----------------------------------------------------------------------------
@@ -994,14 +1010,16 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
     hipLaunchKernelGGL(df_tile_count_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(df_admit_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(df_sort_init_kernel, dim3(g), dim3(kBlock), 0, s, a);
     uint32_t passes = 1;   // sort keys are batch indices < n
     while (passes < 4 && (uint64_t)a.n > (1ull << (8 * passes))) ++passes;
     for (uint32_t p = 0; p < passes; ++p) {
         a.shift = 8 * p;
-        hipLaunchKernelGGL(df_sort_pass_kernel<false>, dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
+        if (p == 0)
+            hipLaunchKernelGGL((df_sort_pass_kernel<false, true>), dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((df_sort_pass_kernel<false, false>), dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
         hipLaunchKernelGGL(df_hist_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
-        hipLaunchKernelGGL(df_sort_pass_kernel<true>, dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
+        hipLaunchKernelGGL((df_sort_pass_kernel<true, false>), dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
         std::swap(a.skey[0], a.skey[1]);
         std::swap(a.sval[0], a.sval[1]);
     }
