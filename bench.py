@@ -630,14 +630,20 @@ def run_defrag(args, cfgd, dev, world, rank, dist):
     mfps = n * args.steps * world / (my_ms / 1e3) / 1e6
     call_ms = my_ms / args.steps
     # algorithmic bytes of one ppe_defrag call: every frame read once (parse reads its header
-    # bytes, the stash or the assembly its data), every held fragment's frame written to its FCB's store slot,
-    # every datagram's bytes read back from the store and written out (whole frame + classify window), and the
+    # bytes, the stash or the assembly its data), the frames left held written to their FCB's store slots,
+    # every datagram's bytes read (from the input or the store) and written out (whole frame + classify window), and the
     # per-fragment descriptors (offset 8, length 4, id 8 in; status 4, datagram index 4 out) and per-datagram
     # outputs (length 4, fragment ids 8 x cache_max)
     frame_bytes = float(lens.astype(np.int64).sum())
-    held_bytes = float(lens[np.isin(st, (0, 1, 2))].astype(np.int64).sum())
+    # held fragments stay in the store unless their datagram completed in this same batch (those are assembled
+    # straight from the input frames); every timed batch's datagrams are its own, so dgram_frags ids are batch indices
+    fr_ids = out["dgram_frags"][:n_dgram].cpu().numpy().view(np.uint64).ravel()
+    stored = np.isin(st, (0, 1, 2))
+    stored[fr_ids[fr_ids < n].astype(np.int64)] = False
+    held_bytes = float(lens[stored].astype(np.int64).sum())
     cm = d.info_["cache_max"]
     bytes_call = (frame_bytes + held_bytes + 2.0 * dlen + n_dgram * (hdr_stride + 4 + 8 * cm) + n * 28.0)
+    stored_frags = int(stored.sum())
     achieved = bytes_call / (call_ms / 1e3) / 1e9
 
     cpu = None
@@ -683,7 +689,7 @@ def run_defrag(args, cfgd, dev, world, rank, dist):
             "parity_sample_ok": parity,
             "parity_sample_stats": stats if rank == 0 else None,
             "defrag_info": info,
-            "held_fragments_per_batch": held,
+            "held_fragments_per_batch": held, "stored_fragments_per_batch": stored_frags,
             "new_fcb_in_timed_region": int(info["new_fcb"] - info0["new_fcb"]),
             "fcb_full_in_timed_region": int(info["st_fcb_full"] - info0["st_fcb_full"]),
         }

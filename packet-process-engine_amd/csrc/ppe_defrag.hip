@@ -442,8 +442,10 @@ __device__ __forceinline__ uint32_t chain_at(uint64_t order, uint32_t pos) { ret
 
 // cdesc: word 0 (offset | frag_len << 16) of the lane's FCB's chain descriptors, which the chain scan reads serially:
 // LDS round trips instead of global ones.  Private per lane ([slot][lane]: no bank conflicts), no barrier.
-__device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint32_t (*cdesc)[kBlock], uint32_t *st,
-                                               uint32_t &teardrop) {
+// cidx: batch index + 1 of the fragment each chain slot received in this batch (0: an earlier batch).  When the FCB
+// completes, these go to descriptor word 3 and the fragments are not stashed: the assembly reads them from the input.
+__device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint32_t (*cdesc)[kBlock],
+                                               uint32_t (*cidx)[kBlock], uint32_t *st, uint32_t &teardrop) {
     const uint32_t tl = threadIdx.x;
     const uint32_t *key = a.skey[0];
     const uint32_t g = key[j];
@@ -470,7 +472,10 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
         uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
         const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
         uint32_t *descw = a.rdesc + (size_t)r * a.cache_max * 4;
-        for (uint32_t k = 0; k < cache_num && k < 16; ++k) cdesc[k][tl] = desc[k * 4];
+        for (uint32_t k = 0; k < cache_num && k < 16; ++k) {
+            cdesc[k][tl] = desc[k * 4];
+            cidx[k][tl] = 0;
+        }
         // the segment's fragments in order; the next one's index and record words are requested before the
         // current one is processed (the chain is a serial dependence, the loads need not be)
         uint32_t i_nx = i0;
@@ -543,6 +548,7 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
                     descw[k * 4 + 1] = fr[4];
                     descw[k * 4 + 2] = fr[5] | ((fr[2] >> 16) & 0xffu) << 16;
                     descw[k * 4 + 3] = 0;
+                    cidx[k][tl] = i + 1;
                     a.rid[(size_t)r * a.cache_max + k] = a.id ? a.id[i] : (uint64_t)i;
                     const uint64_t lo = order & ((1ull << (4 * pos)) - 1ull);
                     const uint64_t hi = pos + 1 < 16 ? (order >> (4 * pos)) << (4 * (pos + 1)) : 0ull;
@@ -563,6 +569,13 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
                             out = PPE_DF_REASM;
                             flags |= kRecComplete | kRecDelete;
                             done = r;
+                            // this batch's fragments of the datagram are read from the input, not stashed
+                            for (uint32_t kk = 0; kk < cache_num; ++kk) {
+                                const uint32_t x = cidx[kk][tl];
+                                descw[kk * 4 + 3] = x;
+                                if (x && x - 1 != i) a.inserted[x - 1] = kNone;
+                            }
+                            ins = kNone;
                         }
                     }
                 }
@@ -583,12 +596,13 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
 
 __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
     __shared__ uint32_t cdesc[16][kBlock];
+    __shared__ uint32_t cidx[16][kBlock];
     __shared__ uint32_t wg[PPE_DF__COUNT + 1];   // per-status counts + teardrops of this workgroup
     if (threadIdx.x <= PPE_DF__COUNT) wg[threadIdx.x] = 0;
     __syncthreads();
     uint32_t st[PPE_DF__COUNT] = {}, teardrop = 0;
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    if (j < a.n) df_process_one(a, j, cdesc, st, teardrop);
+    if (j < a.n) df_process_one(a, j, cdesc, cidx, st, teardrop);
     // LDS atomics, then one global atomic per counter per workgroup: per-lane global atomics on the same few
     // words serialise in one L2 channel (they were most of this kernel's time)
 #pragma unroll
@@ -671,21 +685,30 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
     const uint32_t total = h[1];
     const uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
     const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
-    const uint32_t k0 = chain_at(order, 0);
     // lane p holds chain entry p's descriptor words 0 (offset | frag_len << 16), 1 (frame length), 2 (l2 | ihl*4 << 8
     // | proto << 16): one round of loads for the whole chain, read below with lane broadcasts
+    // and the base of its frame: the input frame when the fragment arrived in this batch (word 3 = index + 1), else
+    // its store slot
     uint32_t cd0 = 0, cd1 = 0, cd2 = 0;
+    uintptr_t cbase = 0;
     if (tid < nlist) {
         const uint32_t kk = chain_at(order, tid);
         cd0 = desc[kk * 4];
         cd1 = desc[kk * 4 + 1];
         cd2 = desc[kk * 4 + 2];
+        const uint32_t cd3 = desc[kk * 4 + 3];
+        cbase = cd3 ? (uintptr_t)(a.pkt + a.off[cd3 - 1])
+                    : (uintptr_t)(a.store + ((size_t)r * a.cache_max + kk) * a.sstride);
     }
+    auto seg_base = [&](uint32_t p) -> const uint8_t * {
+        const uint32_t lo = __shfl((uint32_t)cbase, p, 64), hi = __shfl((uint32_t)((uint64_t)cbase >> 32), p, 64);
+        return (const uint8_t *)(((uint64_t)hi << 32) | lo);
+    };
     const uint32_t hd = __shfl(cd2, 0, 64);
     const uint32_t l2 = hd & 0xffu, ihl4 = (hd >> 8) & 0xffu, proto = (hd >> 16) & 0xffu;
     const uint32_t head_tot = __shfl(cd1, 0, 64);
     const bool icmp = proto == 1u;
-    const uint8_t *hsrc = a.store + ((size_t)r * a.cache_max + k0) * a.sstride;
+    const uint8_t *hsrc = seg_base(0);
     // out_len = head frame + the later fragments' payloads (reasm_mb->pkt_totallen, decode-defrag.c:240-266)
     uint32_t out_len = head_tot;
     for (uint32_t p = 1; p < nlist; ++p) out_len += __shfl(cd0, p, 64) >> 16;
@@ -722,9 +745,8 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
     // partial dwords at a segment's ends are stored bytewise (the neighbouring segment owns their other bytes)
     const bool wide = full && ((uintptr_t)full & 3u) == 0 && (a.reasm_buf & 3u) == 0;
     for (uint32_t p = 0; p < (icmp ? 1u : nlist); ++p) {
-        const uint32_t k = chain_at(order, p);
         const uint32_t tot = __shfl(cd1, p, 64), flen = __shfl(cd0, p, 64) >> 16;
-        const uint8_t *src = a.store + ((size_t)r * a.cache_max + k) * a.sstride + (p == 0 ? 0u : tot - flen);
+        const uint8_t *src = seg_base(p) + (p == 0 ? 0u : tot - flen);
         const uint32_t cnt = p == 0 ? tot : flen;
         if (win && dst0 < stride) {
             const uint32_t wl = cnt < stride - dst0 ? cnt : stride - dst0;
