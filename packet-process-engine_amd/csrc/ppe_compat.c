@@ -123,10 +123,14 @@ void DP_Acl_Rule_Clean(TreeSet **tset, TreeNode **tnode) {
     }
 }
 
+static pthread_mutex_t g_classify_lock;
+
 void DP_Acl_Rule_Release(void) {
     pthread_mutex_lock(&g_lock);
+    pthread_mutex_lock(&g_classify_lock);  /* no burst is mid-classify on the context being destroyed */
     if (g_ctx) ppe_ctx_destroy(g_ctx);
     g_ctx = NULL;
+    pthread_mutex_unlock(&g_classify_lock);
     pthread_mutex_unlock(&g_lock);
 }
 
@@ -192,16 +196,45 @@ int DP_Acl_Lookup(mbuf_t *m) {
     return a;
 }
 
-/* ---- Decode burst ---- */
+/* ---- Decode burst ----
+ * One burst per thread (the reference decodes on the core that received the packet, main.c:301).  The GPU step of a
+ * flush is serialised per process (one engine context, thread-compatible); the output hooks run after it with no
+ * lock held. */
 #define PPE_COMPAT_STRIDE 128u
-static mbuf_t **g_burst = NULL;
-static uint32_t g_burst_n = 0, g_burst_cap = 4096;
-static pthread_mutex_t g_burst_lock = PTHREAD_MUTEX_INITIALIZER;
+typedef struct {
+    mbuf_t **m;
+    uint32_t n, alloc;
+} burst_t;
+
+static volatile uint32_t g_burst_cap = 4096;
+static pthread_mutex_t g_classify_lock = PTHREAD_MUTEX_INITIALIZER;
+static pthread_key_t g_burst_key;
+static pthread_once_t g_burst_once = PTHREAD_ONCE_INIT;
+static __thread burst_t *t_burst = NULL;
+
+static int flush_burst(burst_t *b);
+
+static void burst_exit(void *p) {  /* thread exit: deliver what the thread left queued, then free its burst */
+    burst_t *b = (burst_t *)p;
+    if (!b) return;
+    flush_burst(b);
+    free(b->m);
+    free(b);
+}
+
+static void burst_key_init(void) { pthread_key_create(&g_burst_key, burst_exit); }
+
+static burst_t *my_burst(void) {
+    if (!t_burst) {
+        pthread_once(&g_burst_once, burst_key_init);
+        t_burst = (burst_t *)calloc(1, sizeof(burst_t));
+        if (t_burst) pthread_setspecific(g_burst_key, t_burst);
+    }
+    return t_burst;
+}
 
 void Decode_Set_Burst(uint32_t n) {
-    pthread_mutex_lock(&g_burst_lock);
-    if (n) g_burst_cap = n;
-    pthread_mutex_unlock(&g_burst_lock);
+    if (n) __atomic_store_n(&g_burst_cap, n, __ATOMIC_RELAXED);
 }
 
 /* statuses on which the reference calls DP_Log_Func before dropping */
@@ -217,10 +250,8 @@ static int logged_drop(uint32_t st) {
     }
 }
 
-static int flush_locked(void) {
-    const uint32_t n = g_burst_n;
-    if (n == 0) return 0;
-    if (!g_ctx) return PPE_ENODEV;
+/* Classify `n` mbufs on the GPU (serialised) and fill their parse fields; returns PPE_OK or a PPE_E* code. */
+static int classify_mbufs(mbuf_t **mb, uint32_t n) {
     uint8_t *hdr = (uint8_t *)aligned_alloc(16, (size_t)n * PPE_COMPAT_STRIDE);
     uint32_t *len = (uint32_t *)malloc((size_t)n * 4), *verdict = (uint32_t *)malloc((size_t)n * 4);
     uint32_t *fh = (uint32_t *)malloc((size_t)n * 4), *tuple = (uint32_t *)malloc((size_t)n * 16);
@@ -230,7 +261,7 @@ static int flush_locked(void) {
     if (hdr && len && verdict && fh && tuple && ts && hit) {
         memset(hdr, 0, (size_t)n * PPE_COMPAT_STRIDE);
         for (uint32_t i = 0; i < n; i++) {
-            mbuf_t *m = g_burst[i];
+            mbuf_t *m = mb[i];
             const uint32_t c = m->pkt_totallen < PPE_COMPAT_STRIDE ? m->pkt_totallen : PPE_COMPAT_STRIDE;
             if (m->pkt_ptr && c) memcpy(hdr + (size_t)i * PPE_COMPAT_STRIDE, m->pkt_ptr, c);
             len[i] = m->pkt_totallen;
@@ -244,11 +275,13 @@ static int flush_locked(void) {
         r.acl_hit = hit;
         r.tuple = tuple;
         ppe_cfg_t cfg = {unsupport_proto_action ? 1u : 0u, syn_check ? 1u : 0u, 0};
-        rc = ppe_classify_host(g_ctx, &b, &r, &cfg, 0);
+        pthread_mutex_lock(&g_classify_lock);
+        rc = g_ctx ? ppe_classify_host(g_ctx, &b, &r, &cfg, 0) : PPE_ENODEV;
+        pthread_mutex_unlock(&g_classify_lock);
         if (rc == PPE_OK) {
             for (uint32_t i = 0; i < n; i++) {
-                mbuf_t *m = g_burst[i];
-                const uint32_t v = verdict[i], st = PPE_VERDICT_STATUS(v), fl = PPE_VERDICT_FLAGS(v);
+                mbuf_t *m = mb[i];
+                const uint32_t v = verdict[i], fl = PPE_VERDICT_FLAGS(v);
                 uint8_t *pkt = (uint8_t *)m->pkt_ptr;
                 m->ppe_verdict = v;
                 m->ppe_flow_hash = fh[i];
@@ -270,20 +303,7 @@ static int flush_locked(void) {
                     m->flags |= PKT_HAS_FLOW;
                 }
                 if (fl & PPE_F_FRAG) m->flags |= PKT_IP_FRAG;
-                switch (PPE_VERDICT_ACTION(v)) {
-                    case PPE_ACT_FW:
-                        if (out_fw) out_fw(m);
-                        break;
-                    case PPE_ACT_DROP:
-                        if (logged_drop(st)) DP_Log_Func(m);
-                        if (out_drop) out_drop(m);
-                        break;
-                    default:
-                        if (out_punt) out_punt(m);
-                        break;
-                }
             }
-            rc = (int)n;
         }
     }
     free(hdr);
@@ -293,31 +313,66 @@ static int flush_locked(void) {
     free(tuple);
     free(ts);
     free(hit);
-    g_burst_n = 0;
     return rc;
 }
 
+/* Take the burst's mbufs out (the burst is empty and reusable before any hook runs), classify, deliver. */
+static int flush_burst(burst_t *b) {
+    const uint32_t n = b->n;
+    if (n == 0) return 0;
+    mbuf_t **mb = (mbuf_t **)malloc(sizeof(mbuf_t *) * n);
+    if (!mb) {  /* cannot even hold them: drop in place, as the reference does on allocation failure */
+        b->n = 0;
+        return PPE_ENOMEM;
+    }
+    memcpy(mb, b->m, sizeof(mbuf_t *) * n);
+    b->n = 0;
+    const int rc = classify_mbufs(mb, n);
+    for (uint32_t i = 0; i < n; i++) {
+        mbuf_t *m = mb[i];
+        if (rc != PPE_OK) {  /* undelivered: every packet ends in output_drop_proc (decode.c:24-27) */
+            if (out_drop) out_drop(m);
+            continue;
+        }
+        const uint32_t v = m->ppe_verdict;
+        switch (PPE_VERDICT_ACTION(v)) {
+            case PPE_ACT_FW:
+                if (out_fw) out_fw(m);
+                break;
+            case PPE_ACT_DROP:
+                if (logged_drop(PPE_VERDICT_STATUS(v))) DP_Log_Func(m);
+                if (out_drop) out_drop(m);
+                break;
+            default:
+                if (out_punt) out_punt(m);
+                break;
+        }
+    }
+    free(mb);
+    return rc == PPE_OK ? (int)n : rc;
+}
+
 int Decode_Flush(void) {
-    pthread_mutex_lock(&g_burst_lock);
-    const int rc = flush_locked();
-    pthread_mutex_unlock(&g_burst_lock);
-    return rc;
+    burst_t *b = t_burst;
+    return b ? flush_burst(b) : 0;
 }
 
 void Decode(mbuf_t *m) {
     if (!m) return;
-    pthread_mutex_lock(&g_burst_lock);
-    if (!g_burst || g_burst_n >= g_burst_cap) {
-        if (g_burst_n) flush_locked();
-        mbuf_t **nb = (mbuf_t **)realloc(g_burst, sizeof(mbuf_t *) * g_burst_cap);
-        if (!nb) {
-            pthread_mutex_unlock(&g_burst_lock);
-            if (out_drop) out_drop(m);
-            return;
+    burst_t *b = my_burst();
+    const uint32_t cap = __atomic_load_n(&g_burst_cap, __ATOMIC_RELAXED);
+    if (b && b->n >= b->alloc) {  /* grow to the current cap (or one more slot when the cap was lowered) */
+        const uint32_t want = cap > b->n ? cap : b->n + 1;
+        mbuf_t **nb = (mbuf_t **)realloc(b->m, sizeof(mbuf_t *) * want);
+        if (nb) {
+            b->m = nb;
+            b->alloc = want;
         }
-        g_burst = nb;
     }
-    g_burst[g_burst_n++] = m;
-    if (g_burst_n >= g_burst_cap) flush_locked();
-    pthread_mutex_unlock(&g_burst_lock);
+    if (!b || b->n >= b->alloc) {  /* no memory for the burst slot */
+        if (out_drop) out_drop(m);
+        return;
+    }
+    b->m[b->n++] = m;
+    if (b->n >= cap) flush_burst(b);
 }

@@ -172,8 +172,10 @@ int Rule_Load_Line(FILE *fp, int line) {
         r.time_start = (uint64_t)t0;
         r.time_end = (uint64_t)t1;
         if (fscanf(fp, "%d", &action) != 1) return -1;
-        if (action != 0 && action != 1) return -1;  /* rule/rule.c:320-324 */
+        /* ReadActionInfo stores the int into the uint16_t field first (rule/rule.c:146-158) and the 0/1 check reads
+         * the narrowed field (rule/rule.c:320-324): "65537" is accepted as action 1 */
         r.action = (uint16_t)action;
+        if (r.action != 0 && r.action != 1) return -1;
         if (fscanf(fp, "%d", &logable) != 1) return -1;
         if (logable != 0 && logable != 1) return -1;  /* rule/rule.c:334-338 */
         r.logable = (uint32_t)logable;

@@ -62,3 +62,40 @@ def test_struct_layouts():
     assert C.sizeof(abi.Result) == 56
     assert C.sizeof(abi.Cfg) == 16
     assert C.sizeof(abi.Counters) == 256
+
+
+# LP64 offsets of the reference's mbuf_t (dataplane/src/include/mbuf.h:23-87, with cvmx_buf_ptr_t a 64-bit word and
+# TCPVars {TCPOpt[1]; TCPOpt *} = 24 B, decode-tcp.h:24-46), derived by hand from the declaration order; the
+# reference's own memset of the struct is 232 B (oct-rxtx.c:190-192)
+REF_MBUF_OFFSETS = dict(
+    magic_flag=0, pkt_space=4, flow_log=5, frag_len=6, packet_ptr=8, next=16, pkt_ptr=24, ethh=32, vlanh=40,
+    network_header=48, transport_header=56, input_port=64, eth_dst=68, eth_src=74, ipv4=80, sport=88, dport=90,
+    proto=92, vlan_idx=93, payload_len=94, vlan_id=96, defrag_id=98, timestamp=104, payload=112, tcpvars=120,
+    frag_offset=144, tcp_reasm_overlap=146, pkt_totallen=148, flags=152, fcb_hash=156, fcb=160, fragments=168,
+    flow=176, tcp_seg_raw=184, tcp_seg_raw_tail=192, tcp_seg_reassem=200, alState=208, FreeState=216, tag=224)
+
+
+def test_mbuf_layout_matches_reference(tmp_path):
+    """include/ppe_decode.h's mbuf_t keeps every reference field at its reference offset (compiled with gcc), and the
+    ctypes mirror (ppe.abi.Mbuf) agrees with the compiler."""
+    import subprocess
+    names = list(REF_MBUF_OFFSETS) + ["ppe_verdict", "ppe_flow_hash", "ppe_acl_hit", "user"]
+    src = tmp_path / "off.c"
+    src.write_text("#include <stdio.h>\n#include <stddef.h>\n#include \"ppe_decode.h\"\nint main(void){\n" +
+                   "".join(f'printf("{n} %zu\\n", offsetof(mbuf_t, {n}));\n' for n in names) +
+                   'printf("sizeof %zu\\n", sizeof(mbuf_t));\n'
+                   'mbuf_t m; m.tcpvars.ws = 0; (void)m;\nreturn 0;}\n')
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{ROOT / 'include'}", str(src), "-o", str(exe)],
+                   check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                       text=True).stdout.splitlines())
+    got = {k: int(v) for k, v in got.items()}
+    for k, off in REF_MBUF_OFFSETS.items():
+        assert got[k] == off, (k, got[k], off)
+    assert got["ppe_verdict"] >= 228
+    ct = {f[0]: getattr(abi.Mbuf, f[0]).offset for f in abi.Mbuf._fields_}
+    ct["ipv4"] = ct["sip"]
+    for k in names:
+        assert ct[k] == got[k], k
+    assert C.sizeof(abi.Mbuf) == got["sizeof"]

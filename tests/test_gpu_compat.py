@@ -15,15 +15,7 @@ from ppe import abi, synth  # noqa: E402
 from ppe.abi import ST  # noqa: E402
 
 
-class Mbuf(C.Structure):  # include/ppe_decode.h mbuf_t
-    _fields_ = [("pkt_ptr", C.c_void_p), ("pkt_totallen", C.c_uint32), ("input_port", C.c_uint32),
-                ("ethh", C.c_void_p), ("vlanh", C.c_void_p), ("network_header", C.c_void_p),
-                ("transport_header", C.c_void_p), ("eth_dst", C.c_uint8 * 6), ("eth_src", C.c_uint8 * 6),
-                ("sip", C.c_uint32), ("dip", C.c_uint32), ("sport", C.c_uint16), ("dport", C.c_uint16),
-                ("proto", C.c_uint8), ("vlan_idx", C.c_uint8), ("payload_len", C.c_uint16),
-                ("timestamp", C.c_uint64), ("payload", C.c_void_p), ("flags", C.c_uint32),
-                ("ppe_verdict", C.c_uint32), ("ppe_flow_hash", C.c_uint32), ("ppe_acl_hit", C.c_int32),
-                ("user", C.c_void_p)]
+Mbuf = abi.Mbuf
 
 
 HOOK = C.CFUNCTYPE(None, C.POINTER(Mbuf))

@@ -117,3 +117,31 @@ def test_rule_file_rejects(lib, tmp_path, line):
     f.write_text(line + "\n")
     assert lib.ppe_rule_load_file(str(f).encode()) == -1
     assert rl(lib).rule_entry_free == 10000
+
+
+@pytest.mark.parametrize("text,action", [("65537", 1), ("-65535", 1), ("65536", 0), ("1", 1)])
+def test_rule_file_action_narrowed_before_check(lib, tmp_path, text, action):
+    """ReadActionInfo stores the parsed int into the uint16_t `action` (rule/rule.c:146-158) and the 0/1 check reads
+    the narrowed field (rule/rule.c:320-324), so 65537 is accepted as action 1 and 65536 as action 0."""
+    f = tmp_path / "act"
+    f.write_text(f"@ 00:00:00:00:00:00 00:00:00:00:00:00 1.0.0.0/8 0.0.0.0/0 0 : 1 0 : 1 0 : 1 0 0 {text} 0\n")
+    assert lib.ppe_rule_load_file(str(f).encode()) == 1
+    t = np.frombuffer(bytes(rl(lib).rule_entry[0].tuple), RULE_DTYPE)[0]
+    assert t["action"] == action
+
+
+def test_rule_file_action_narrowed_still_rejects(lib, tmp_path):
+    f = tmp_path / "act"
+    f.write_text("@ 00:00:00:00:00:00 00:00:00:00:00:00 1.0.0.0/8 0.0.0.0/0 0 : 1 0 : 1 0 : 1 0 0 65538 0\n")
+    assert lib.ppe_rule_load_file(str(f).encode()) == -1
+
+
+def test_rule_file_port_and_proto_narrowed(lib, tmp_path):
+    """Ports and protocols go through unsigned int into uint16_t / uint8_t (rule/rule.c:80-108) before the
+    start <= end checks: 65616 is port 80 and 273 is protocol 17."""
+    f = tmp_path / "narrow"
+    f.write_text("@ 00:00:00:00:00:00 00:00:00:00:00:00 1.0.0.0/8 0.0.0.0/0 0 : 65616 80 : 65616 17 : 273 0 0 1 0\n")
+    assert lib.ppe_rule_load_file(str(f).encode()) == 1
+    t = np.frombuffer(bytes(rl(lib).rule_entry[0].tuple), RULE_DTYPE)[0]
+    assert (t["sport_start"], t["sport_end"], t["dport_start"], t["dport_end"]) == (0, 80, 80, 80)
+    assert (t["protocol_start"], t["protocol_end"]) == (17, 17)
