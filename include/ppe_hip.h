@@ -231,6 +231,8 @@ typedef struct {
                                 staging, 3 four tiles per wave loaded, decoded and walked together
                                 (one 1024-thread workgroup per CU); others PPE_EINVAL              */
     uint32_t lds_image;      /* 1 = stage the image (or its top) in LDS, 0 = read it from global   */
+    uint32_t batches_per_launch;  /* ppe_classify_batches: batches one launch takes (<= 4096); 0 = all
+                                     of a call's batches in ONE persistent launch (descriptor ring)  */
 } ppe_tuning_t;
 int  ppe_set_tuning(ppe_ctx_t *ctx, const ppe_tuning_t *t);
 int  ppe_get_tuning(ppe_ctx_t *ctx, ppe_tuning_t *t);

@@ -3,9 +3,11 @@
  * dataplane, layer by layer, with the reference's check order, uint16_t lengths and big-endian field reads
  * (the reference targets big-endian cnMIPS64 and reads header fields raw).
  */
+#define _GNU_SOURCE
 #include "ppe_oracle.h"
 
 #include <pthread.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -647,6 +649,26 @@ static void *run_shard(void *arg) {
     return NULL;
 }
 
+/* CPU pinning of the shard threads (the reference pins one mainloop pthread per core, main.c:422-425,
+ * dataplane/src/platform/oct-thread.c:18-55): thread t runs on g_pin[t % g_npin]; none when g_npin == 0 */
+static int g_pin[1024];
+static int g_npin = 0;
+
+int oracle_set_pin_cpus(const int *cpus, int n) {
+    if (n < 0 || n > 1024) return -1;
+    for (int i = 0; i < n; i++) g_pin[i] = cpus[i];
+    g_npin = n;
+    return 0;
+}
+
+static void pin_attr(pthread_attr_t *at, int t) {
+    if (g_npin <= 0) return;
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    CPU_SET(g_pin[t % g_npin], &cs);
+    pthread_attr_setaffinity_np(at, sizeof cs, &cs);
+}
+
 int oracle_classify_batch(const uint8_t *hdr, uint32_t stride, const uint32_t *len, const uint64_t *ts, uint32_t n,
                           const oracle_cfg_t *cfg, int nthreads, int use_tree, uint32_t *verdict,
                           uint32_t *flow_hash, int32_t *acl_hit, uint32_t *tuple, uint32_t *reach,
@@ -676,10 +698,17 @@ int oracle_classify_batch(const uint8_t *hdr, uint32_t stride, const uint32_t *l
         s->acl_hit = acl_hit;
         s->tuple = tuple;
         s->reach = reach;
-        if (nthreads == 1) run_shard(s);
-        else pthread_create(&th[t], NULL, run_shard, s);
+        if (nthreads == 1 && g_npin == 0) {
+            run_shard(s);
+        } else {
+            pthread_attr_t at;
+            pthread_attr_init(&at);
+            pin_attr(&at, t);
+            pthread_create(&th[t], &at, run_shard, s);
+            pthread_attr_destroy(&at);
+        }
     }
-    if (nthreads > 1)
+    if (nthreads > 1 || g_npin > 0)
         for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
     if (counters) {
         memset(counters, 0, 32 * sizeof(uint64_t));

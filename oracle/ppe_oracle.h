@@ -65,6 +65,8 @@ void oracle_classify(const uint8_t *pkt, uint32_t avail, uint32_t len, uint64_t 
 
 /* Batch over windows (n × stride bytes), optionally multi-threaded (run-to-completion shards like mainloop);
  * use_tree selects the image walk.  Any output pointer may be NULL.  Returns 0. */
+/* Pin the batch's shard threads: thread t on cpus[t % n] (n = 0: unpinned, the default). */
+int oracle_set_pin_cpus(const int *cpus, int n);
 int oracle_classify_batch(const uint8_t *hdr, uint32_t stride, const uint32_t *len, const uint64_t *ts, uint32_t n,
                           const oracle_cfg_t *cfg, int nthreads, int use_tree, uint32_t *verdict,
                           uint32_t *flow_hash, int32_t *acl_hit, uint32_t *tuple, uint32_t *reach,

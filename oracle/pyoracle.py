@@ -44,6 +44,8 @@ def load():
         lib.oracle_classify_batch.argtypes = [vp, u32, vp, vp, u32, C.POINTER(OCfg), C.c_int, C.c_int, vp, vp, vp,
                                               vp, vp, vp]
         lib.oracle_classify_batch.restype = C.c_int
+        lib.oracle_set_pin_cpus.argtypes = [C.POINTER(C.c_int), C.c_int]
+        lib.oracle_set_pin_cpus.restype = C.c_int
         lib.oracle_acl_linear.argtypes = [u32, u32, u32, u32, u32, vp, vp, u64, C.POINTER(u32)]
         lib.oracle_acl_linear.restype = C.c_int32
         lib.oracle_acl_tree.argtypes = [u32, u32, u32, u32, u32, vp, vp, u64, C.POINTER(u32)]
@@ -103,6 +105,12 @@ class Oracle:
         self.lib.oracle_classify(buf.ctypes.data, len(pkt), len(pkt) if length is None else int(length), int(ts),
                                  C.byref(cfg or self.cfg()), C.byref(r))
         return {k: getattr(r, k) for k, _ in OResult._fields_}
+
+    def pin(self, cpus):
+        """Pin classify_batch's shard threads, thread t on cpus[t % len(cpus)] (empty: unpinned)."""
+        arr = (C.c_int * max(len(cpus), 1))(*cpus)
+        if self.lib.oracle_set_pin_cpus(arr, len(cpus)) != 0:
+            raise ValueError("bad cpu list")
 
     def classify_batch(self, hdr, lens, ts=None, cfg=None, nthreads=1, use_tree=False):
         hdr = np.ascontiguousarray(hdr, np.uint8)

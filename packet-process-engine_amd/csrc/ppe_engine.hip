@@ -34,8 +34,9 @@ constexpr int kPipeStreams = 2;
 // measured slower and are not built.
 constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
-// ppe_classify_batches: batches per launch (C1 step, two streams: 1 / 2 / 8 per launch 18.4 / 17.2 / 18.0 us)
-constexpr uint32_t kBatchesPerLaunch = 2;
+// ppe_classify_batches: batches per launch.  0 = every batch of the call in one persistent launch (descriptor ring in
+// device memory): the launch ramp and tail are paid once per call instead of once per batch
+constexpr uint32_t kBatchesPerLaunch = 0;
 
 struct HostStage {
     hipStream_t s = nullptr;
@@ -103,7 +104,13 @@ struct ppe_ctx {
     hipStream_t pipe[kPipeStreams] = {};
     hipEvent_t pipe_ev[kPipeStreams + 1] = {};
     int pipe_mode = 1;  // PPE_PIPE_MODE at context creation (see ppe_classify_batches)
-    uint32_t batches_per_launch = kBatchesPerLaunch;  // PPE_BATCHES_PER_LAUNCH at context creation
+    // descriptor rings of launches over more than PPE_MAX_BATCH batches: two slots used alternately; a slot is
+    // rewritten only after the launch that read it has completed (ring_ev)
+    ppe_bdesc *d_ring[2] = {nullptr, nullptr};
+    ppe_bdesc *h_ring[2] = {nullptr, nullptr};  // pinned staging of the H2D descriptor copy
+    hipEvent_t ring_ev[2] = {nullptr, nullptr};
+    bool ring_pending[2] = {false, false};
+    int ring_next = 0;
     ppe_tuning_t tune;
     FlowTable *flow = nullptr;  // ppe_flow_create
     uint32_t *d_steer = nullptr;  // ppe_steer_partition: per-tile owner counts / offsets
@@ -146,6 +153,8 @@ ppe_tuning_t default_tuning() {
     const int pl = env_int("PPE_PIPELINE", 0);
     t.pipeline = pl == 1 || pl == 3 || pl == 4 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
+    t.batches_per_launch = (uint32_t)std::max(0, std::min(env_int("PPE_BATCHES_PER_LAUNCH", (int)kBatchesPerLaunch),
+                                                          PPE_MAX_RING));
     return t;
 }
 
@@ -274,8 +283,23 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     ppe_kargs a;
     std::memset(&a, 0, sizeof a);
     uint32_t tiles = 0;
+    const bool use_ring = nb > PPE_MAX_BATCH;
+    int rslot = 0;
+    if (use_ring) {
+        if (nb > PPE_MAX_RING) return fail(c, PPE_EINVAL, "more than %d batches in one launch", PPE_MAX_RING);
+        rslot = c->ring_next;
+        c->ring_next ^= 1;
+        // the launch that last read this slot (two ring launches ago) must be done before the slot is rewritten
+        if (c->ring_pending[rslot]) HIPCHK(c, hipEventSynchronize(c->ring_ev[rslot]));
+        c->ring_pending[rslot] = false;
+        if (!c->d_ring[rslot]) {
+            HIPCHK(c, hipMalloc(&c->d_ring[rslot], sizeof(ppe_bdesc) * PPE_MAX_RING));
+            HIPCHK(c, hipHostMalloc(&c->h_ring[rslot], sizeof(ppe_bdesc) * PPE_MAX_RING, hipHostMallocDefault));
+            if (!c->ring_ev[rslot]) HIPCHK(c, hipEventCreateWithFlags(&c->ring_ev[rslot], hipEventDisableTiming));
+        }
+    }
     for (uint32_t i = 0; i < nb; ++i) {
-        ppe_bdesc &d = a.batch[i];
+        ppe_bdesc &d = use_ring ? c->h_ring[rslot][i] : a.batch[i];
         d.hdr = in[i].hdr;
         d.len = in[i].len;
         d.ts = in[i].ts;
@@ -289,7 +313,13 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         d.tile_cnt = out[i].tile_cnt;
         d.tuple = out[i].tuple;
         d.idx_base = idx_base;
+        d.pad = 0;
         tiles = std::max(tiles, (in[i].n + 63u) / 64u);
+    }
+    if (use_ring) {
+        a.batch[0] = c->h_ring[rslot][0];
+        HIPCHK(c, hipMemcpyAsync(c->d_ring[rslot], c->h_ring[rslot], sizeof(ppe_bdesc) * nb, hipMemcpyHostToDevice, s));
+        a.ring = c->d_ring[rslot];
     }
     a.nbatch = nb;
     a.max_tiles = tiles;
@@ -341,6 +371,10 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         ppe_launch_classify(&a, grid, plan.mode, plan.pipe, (int)plan.block, fl != nullptr, (void *)s, (void *)e0,
                             (void *)e1);
     if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
+    if (use_ring) {
+        HIPCHK(c, hipEventRecord(c->ring_ev[rslot], s));
+        c->ring_pending[rslot] = true;
+    }
     c->img_used[r] = true;
     return PPE_OK;
 }
@@ -391,8 +425,6 @@ int ppe_ctx_create(int device, ppe_ctx_t **out) {
     c->max_grid = c->n_cu * kMaxBlocksPerCU;
     c->tune = default_tuning();
     c->pipe_mode = env_int("PPE_PIPE_MODE", 1);
-    c->batches_per_launch = (uint32_t)std::max(1, std::min(env_int("PPE_BATCHES_PER_LAUNCH", (int)kBatchesPerLaunch),
-                                                           PPE_MAX_BATCH));
     const size_t cs_bytes = (size_t)kSlotSets * c->max_grid * PPE_CSLOT_WORDS * sizeof(unsigned long long);
     int rc = PPE_OK;
     if (hipMalloc(&c->d_cslots, cs_bytes) != hipSuccess || hipMemset(c->d_cslots, 0, cs_bytes) != hipSuccess)
@@ -421,6 +453,11 @@ int ppe_ctx_destroy(ppe_ctx_t *c) {
     }
     if (c->d_cslots) (void)hipFree(c->d_cslots);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i) {
+        if (c->d_ring[i]) (void)hipFree(c->d_ring[i]);
+        if (c->h_ring[i]) (void)hipHostFree(c->h_ring[i]);
+        if (c->ring_ev[i]) (void)hipEventDestroy(c->ring_ev[i]);
+    }
     for (hipStream_t s : c->pipe)
         if (s) (void)hipStreamDestroy(s);
     for (hipEvent_t e : c->pipe_ev)
@@ -499,10 +536,11 @@ int ppe_classify_batches(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t
     for (int k = 0; k < kPipeStreams; ++k)
         if (q[k] != s) HIPCHK(c, hipStreamWaitEvent(q[k], c->pipe_ev[kPipeStreams], 0));
     // groups of up to PPE_MAX_BATCH non-empty batches per launch, launches alternating over the streams
-    ppe_batch_t gin[PPE_MAX_BATCH];
-    ppe_result_t gout[PPE_MAX_BATCH];
+    std::vector<ppe_batch_t> gin(std::min<uint32_t>(nbatch, PPE_MAX_RING));
+    std::vector<ppe_result_t> gout(gin.size());
     uint32_t ng = 0, nl = 0;
-    const uint32_t per = std::max(1u, std::min<uint32_t>(c->batches_per_launch, PPE_MAX_BATCH));
+    const uint32_t per = c->tune.batches_per_launch ? std::min<uint32_t>(c->tune.batches_per_launch, PPE_MAX_RING)
+                                                    : (uint32_t)PPE_MAX_RING;
     for (uint32_t i = 0; i <= nbatch; ++i) {
         if (i < nbatch && in[i].n == 0) continue;
         if (i < nbatch) {
@@ -511,7 +549,7 @@ int ppe_classify_batches(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t
             ++ng;
         }
         if (ng == per || (i == nbatch && ng)) {
-            const int rc = launch(c, gin, gout, ng, cfg, q[nl % kPipeStreams], 0);
+            const int rc = launch(c, gin.data(), gout.data(), ng, cfg, q[nl % kPipeStreams], 0);
             if (rc != PPE_OK) return rc;
             ng = 0;
             ++nl;
@@ -778,6 +816,7 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
                                    "not fit in LDS: 4 tiles per wave walked together) or 4 (first tile's loads before "
                                    "the image staging)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
+    if (t->batches_per_launch > PPE_MAX_RING) return fail(c, PPE_EINVAL, "batches_per_launch must be <= 4096");
     c->tune = *t;
     c->tune.pipeline = t->pipeline;
     c->tune.lds_image = t->lds_image ? 1u : 0u;

@@ -74,12 +74,17 @@ struct ppe_flow_kargs {
     struct ppe_flowdev dst;       /* rehash target */
 };
 
-/* batches per launch: the descriptors travel in the kernel arguments (8 × 96 B) */
+/* batches per launch whose descriptors travel in the kernel arguments (8 × 96 B); a launch over more batches reads
+ * them from a device descriptor ring (ppe_kargs.ring) */
 #define PPE_MAX_BATCH 8
+/* most batches one ring launch takes */
+#define PPE_MAX_RING 4096
 
 /* Kernel launch parameters, passed by value. */
 struct ppe_kargs {
     struct ppe_bdesc batch[PPE_MAX_BATCH];  /* [0, nbatch): processed in order by every wave, no barrier between */
+    const struct ppe_bdesc *ring;           /* non-NULL: the nbatch descriptors are ring[0, nbatch) in device memory
+                                               (one persistent launch over a whole queue of batches) */
     uint32_t nbatch;
     uint32_t max_tiles;       /* largest batch's tile count */
     const uint32_t *img;      /* device classifier image (ppe_image.h) */

@@ -79,10 +79,10 @@ class Counters(C.Structure):
 
 class Tuning(C.Structure):
     _fields_ = [("block", C.c_uint32), ("blocks_per_cu", C.c_uint32), ("pipeline", C.c_uint32),
-                ("lds_image", C.c_uint32)]
+                ("lds_image", C.c_uint32), ("batches_per_launch", C.c_uint32)]
 
-    def __init__(self, block=0, blocks_per_cu=0, pipeline=0, lds_image=1):
-        super().__init__(block, blocks_per_cu, pipeline, lds_image)
+    def __init__(self, block=0, blocks_per_cu=0, pipeline=0, lds_image=1, batches_per_launch=0):
+        super().__init__(block, blocks_per_cu, pipeline, lds_image, batches_per_launch)
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -142,6 +142,28 @@ class DefragInfo(C.Structure):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "st"}
         d.update({"st_" + DF_NAME[i].lower(): int(self.st[i]) for i in range(9)})
         return d
+
+
+class Mbuf(C.Structure):
+    """include/ppe_decode.h mbuf_t: the reference's mbuf_t field order (dataplane/src/include/mbuf.h:23-87) plus the
+    engine's appended results."""
+    _fields_ = [("magic_flag", C.c_uint32), ("pkt_space", C.c_uint8), ("flow_log", C.c_uint8),
+                ("frag_len", C.c_uint16), ("packet_ptr", C.c_uint64), ("next", C.c_void_p), ("pkt_ptr", C.c_void_p),
+                ("ethh", C.c_void_p), ("vlanh", C.c_void_p), ("network_header", C.c_void_p),
+                ("transport_header", C.c_void_p), ("input_port", C.c_uint32), ("eth_dst", C.c_uint8 * 6),
+                ("eth_src", C.c_uint8 * 6), ("sip", C.c_uint32), ("dip", C.c_uint32), ("sport", C.c_uint16),
+                ("dport", C.c_uint16), ("proto", C.c_uint8), ("vlan_idx", C.c_uint8), ("payload_len", C.c_uint16),
+                ("vlan_id", C.c_uint16), ("defrag_id", C.c_uint16), ("timestamp", C.c_uint64),
+                ("payload", C.c_void_p), ("tcpvars", C.c_uint8 * 24), ("frag_offset", C.c_uint16),
+                ("tcp_reasm_overlap", C.c_uint16), ("pkt_totallen", C.c_uint32), ("flags", C.c_uint32),
+                ("fcb_hash", C.c_uint32), ("fcb", C.c_void_p), ("fragments", C.c_void_p), ("flow", C.c_void_p),
+                ("tcp_seg_raw", C.c_void_p), ("tcp_seg_raw_tail", C.c_void_p), ("tcp_seg_reassem", C.c_void_p),
+                ("alState", C.c_void_p), ("FreeState", C.c_void_p), ("tag", C.c_uint32),
+                ("ppe_verdict", C.c_uint32), ("ppe_flow_hash", C.c_uint32), ("ppe_acl_hit", C.c_int32),
+                ("user", C.c_void_p)]
+
+
+MBUF_MAGIC_NUM = 0xAB00AB00
 
 
 # every symbol include/*.h declares (checked by tests/test_abi.py)

@@ -12,6 +12,7 @@ def main():
     ap.add_argument("csv", nargs="+")
     ap.add_argument("--kernel", default="ppe_classify_kernel")
     ap.add_argument("--tiles", type=int, default=16384)
+    ap.add_argument("--min-us", type=float, default=0.0, help="only dispatches at least this long")
     a = ap.parse_args()
     per = defaultdict(lambda: defaultdict(float))  # (file, dispatch) -> counter -> value
     dur = {}
@@ -23,6 +24,8 @@ def main():
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
             dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     cnt = defaultdict(list)
+    per = {k: v for k, v in per.items() if dur[k] >= a.min_us}
+    dur = {k: dur[k] for k in per}
     for key, d in per.items():
         for k, v in d.items():
             cnt[k].append(v)

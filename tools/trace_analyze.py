@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--nbufs", type=int, default=4)
     ap.add_argument("--tune", default="")
     ap.add_argument("--bins", type=float, default=1.0, help="timeline bin width, us")
+    ap.add_argument("--batches", type=int, default=1,
+                    help="batches in the traced launch (one ppe_classify_batches ring launch); build the library "
+                         "with -DPPE_TRACE_SKIP=k to sample tile iterations k..k+3 (mid-launch steady state)")
+    ap.add_argument("--skip", type=int, default=0, help="the library's PPE_TRACE_SKIP")
     a = ap.parse_args()
     c = synth.CONFIGS[a.config]
     n = c["n"]
@@ -59,8 +63,14 @@ def main():
         assert lib.ppe_classify(eng.ctx, C.byref(bb), C.byref(rr), C.byref(cfg), sp) == 0
     torch.cuda.synchronize()
     assert lib.ppe_debug_trace(eng.ctx, C.c_void_p(trace.data_ptr())) == 0
-    bb, rr = bufs[8 % a.nbufs][:2]
-    assert lib.ppe_classify(eng.ctx, C.byref(bb), C.byref(rr), C.byref(cfg), sp) == 0
+    if a.batches > 1:
+        ins = (abi.Batch * a.batches)(*(bufs[i % a.nbufs][0] for i in range(a.batches)))
+        outs = (abi.Result * a.batches)(*(bufs[i % a.nbufs][1] for i in range(a.batches)))
+        eng.tuning(batches_per_launch=0)
+        assert lib.ppe_classify_batches(eng.ctx, ins, outs, a.batches, C.byref(cfg), sp) == 0
+    else:
+        bb, rr = bufs[8 % a.nbufs][:2]
+        assert lib.ppe_classify(eng.ctx, C.byref(bb), C.byref(rr), C.byref(cfg), sp) == 0
     torch.cuda.synchronize()
     lib.ppe_debug_trace(eng.ctx, None)
     t = trace.cpu().numpy().reshape(waves, 32).astype(np.int64)
@@ -75,10 +85,11 @@ def main():
     print(f"epilogue (loop exit .. counters flushed): median {np.median(ep):.2f} p90 {np.percentile(ep, 90):.2f} us; "
           f"last flush at {us(t[:, 23]).max():.2f} us; last loop exit at {end:.2f} us")
     names = ["wait window", "decode+hash", "ACL", "outputs+counters", "to next top"]
-    for i in range(int(iters.max())):
+    skip = int(a.skip)
+    for i in range(int(iters.max()) - skip):
         if i >= 4:
             break
-        m = iters > i
+        m = iters > i + skip
         b = 2 + 5 * i
         seg = [us(t[m, b + k + 1]) - us(t[m, b + k]) for k in range(4)]
         start = us(t[m, b])
@@ -88,8 +99,8 @@ def main():
     # timeline: how many waves are in each phase per time bin
     nb = int(np.ceil(end / a.bins)) + 1
     hist = np.zeros((nb, 5))
-    for i in range(min(4, int(iters.max()))):
-        m = iters > i
+    for i in range(min(4, int(iters.max()) - skip)):
+        m = iters > i + skip
         b = 2 + 5 * i
         for k in range(4):
             lo, hi = us(t[m, b + k]), us(t[m, b + k + 1])
