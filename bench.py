@@ -1,23 +1,40 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident decode + 5-tuple ACL classify on MI355X (BASELINE.json metric).
 
-A step = one classify launch over one resident batch (default config C1: 1M × 64 B IPv4/UDP packets, 256
-five-tuple ACL rules).  Steps rotate over --nbufs distinct batches (inputs + outputs ≈ 84 MB each) so the working
-set exceeds the 256 MiB Infinity Cache and every step streams its packets from HBM.  The K timed steps go through
-ppe_classify_batches, which pipelines consecutive batches over two streams (a batch's launch ramp-up overlaps the
-previous one's tail), as a dataplane feeding batch after batch would.  With --gpus N (launched by
-torch.distributed.run) each rank classifies its own 1M-packet shard (weak scaling, no data-path collective);
-`value` = all packets processed ÷ the slowest rank's time.
+A step = one pass of the hot path over one resident batch.  `value` is config C1 (1M x 64-B IPv4/UDP packets per
+GPU, 256 five-tuple ACL rules, BASELINE configs[1]); the same JSON line carries C2 (IMIX 64/570/1500 B, Eth+VLAN,
+TCP/UDP, 4k rules: the metric's 1500-B leg), C3 (64k rules, HBM/L2-resident classifier) and C4 (64 B, 4k rules:
+BASELINE configs[4], the 1/2/4/8-GPU scaling config) under "configs", each timed and roofline-checked the same way.
 
-Prints ONE JSON line (rank 0).  Also: `roofline` from HIP-event kernel durations on the launch stream, and
-`cpu_baseline` = the oracle's C restatement (tree-walk ACL, run-to-completion pthread shards like mainloop) timed on
-this host's cores (rank 0, N=1 only).
+The K timed batches of a config go through ONE ppe_classify_batches call, which the engine runs as one persistent
+launch over the whole queue (device descriptor ring): as a dataplane draining a queue of resident batches would.
+The batches rotate over >= 8 distinct resident buffers (> 600 MB, more than twice the 256 MiB Infinity Cache), so
+every read is served by HBM.
+
+Multi-GPU: one process per GPU.  `--gpus N` without WORLD_SIZE in the environment starts
+`torch.distributed.run` with N ranks as a child process (before this process touches the GPU) and exits with its
+code; with WORLD_SIZE set (the driver's own torchrun launch) the rank count must equal --gpus.  Every rank
+classifies its own resident batches (batch-sharded, no data-path collective): weak scaling by default (1M packets
+per GPU per step), `--scaling strong` splits a fixed 8M-packet step across the ranks.  `value` = all ranks'
+packets / the slowest rank's time (barrier + synchronize around the timed region, MAX over ranks).  The RCCL
+verdict gather a consumer would add is timed apart (`gather`).
+
+`roofline`: the config's launch timed with its dispatch start/end timestamps (hipExtLaunchKernelGGL events on the
+launch stream); achieved = SURVEY.md 8(d)'s 80 algorithmic bytes per 64-B packet (68 read + 12 written; the kernel
+also writes a 4-B compacted-list entry, reported as `written_bytes_per_pkt`) x packets in the launch / its
+duration.  `traffic` = HBM bytes of the launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE profile of the
+same launch shape (per packet, scaled), when one exists.  `cpu_baseline` = the oracle's C restatement (tree-walk
+ACL) timed on this host's cores as pinned run-to-completion pthreads (rank 0, N = 1).
+
+`--dry-run`: the rank plumbing only (gloo, no GPU): spawn, rendezvous, MAX reduction, one JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -26,50 +43,92 @@ ROOT = Path(__file__).resolve().parent
 sys.path[:0] = [str(ROOT / "packet-process-engine_amd"), str(ROOT / "oracle")]
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402  (load torch's HIP runtime before libppe_hip.so so both share it)
+import torch  # noqa: E402  (load torch's HIP runtime before libppe_hip.so so both share it; no GPU call yet)
 
 from ppe import Engine, synth  # noqa: E402
 
 METRIC = "Mpps device-resident decode+ACL classify, 64B & 1500B pkts, 1/2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 NOW = 1_700_000_000
+STRONG_TOTAL = 8 << 20  # --scaling strong: packets per step over all ranks
+EXTRA_CONFIGS = ("C2", "C3", "C4")
 
 
-def algorithmic_bytes(stride: int) -> tuple[float, float]:
-    """(read, write) bytes per packet the kernel must move: the 64-B header window + 4-B length
-    read; verdict + flow hash + ACL hit (12 B) + the packet's entry in its tile's FW/PUNT/DROP partition list (4 B)
-    written.  Payload bytes past the window are never touched (IMIX included)."""
-    return float(min(stride, 64)) + 4.0, 12.0 + 4.0
+def algorithmic_bytes(stride_or_len: float) -> tuple[float, float]:
+    """(read, write) bytes per packet of SURVEY.md 8(d): the header window (min(len, 64) B) + the 4-B length read,
+    the 12-B verdict (status/action/flags, flow hash, ACL hit) written.  Payload bytes are never touched."""
+    return float(min(stride_or_len, 64)) + 4.0, 12.0
+
+
+def host_cores() -> list[int]:
+    """The CPUs this process may run on, capped like `nproc` by OMP_NUM_THREADS (16 on the GPU box)."""
+    cpus = sorted(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        cpus = cpus[:int(cap)]
+    return cpus
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn(args_list: list[str], n: int) -> int:
+    """Run this script under torch.distributed.run with n ranks (a child process: this one never touched the GPU)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve())] + args_list
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--config", default="C1", choices=sorted(synth.CONFIGS))
+    ap.add_argument("--configs", default=",".join(EXTRA_CONFIGS),
+                    help="extra stateless configs measured after --config and nested in the line ('' = none)")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"))
+    ap.add_argument("--n", type=int, default=0, help="packets per GPU per step (default: the config's; strong: "
+                                                      "8M / ranks)")
+    ap.add_argument("--stride", type=int, default=64)
+    ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: >= 8 and > 600 MB)")
+    ap.add_argument("--batches-per-launch", type=int, default=0,
+                    help="0: the K batches in one persistent launch (default); B: launches of B batches "
+                         "alternating over two streams")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (all cores)")
+    ap.add_argument("--dry-run", action="store_true", help="rank plumbing only (gloo, no GPU)")
+    return ap.parse_args(argv)
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=48)
-    ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--config", default="C1", choices=sorted(synth.CONFIGS))
-    ap.add_argument("--n", type=int, default=0, help="packets per GPU (default: the config's)")
-    ap.add_argument("--stride", type=int, default=64)
-    ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: >= 8 and > 600 MB total)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-host-inclusive", action="store_true")
-    ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
-                    help="2: the K batches go through one ppe_classify_batches call (launches of 2 batches "
-                         "alternating over two streams); 1: launches of 2 batches serialized on one stream, no "
-                         "overlap (profiling: kernel durations = step times)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (16 threads)")
-    args = ap.parse_args()
-
+    args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.dry_run:
+        return dry_run(args, world, rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"RCCL reports {dist.get_world_size()} ranks, expected {args.gpus}")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -78,264 +137,315 @@ def main():
         return run_flow(args, cfgd, dev, world, rank, dist)
     if cfgd["kind"] == "frag":
         return run_defrag(args, cfgd, dev, world, rank, dist)
-    n = args.n or cfgd["n"]
+    return run_stateless(args, dev, world, rank, dist)
+
+
+def dry_run(args, world, rank):
+    """Spawn + rendezvous + MAX-over-ranks plumbing on gloo (CPU only), one JSON line from rank 0."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([1.0 + rank], dtype=torch.float64)
+    if world > 1:
+        dist.barrier()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ranks = dist.get_world_size() if world > 1 else 1
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpps", "n_gpus": world, "ranks_reported": ranks,
+                          "max_over_ranks": float(t.item()), "scaling": args.scaling, "dry_run": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+class Resident:
+    """`nbufs` distinct device batches of one config (2 generated batches, cloned / tiled on the device: every
+    buffer is its own HBM allocation) with their output buffers and pre-built C argument blocks."""
+
+    def __init__(self, name, n, stride, nbufs, rules, rank, dev):
+        from ppe import abi
+        cfgd = synth.CONFIGS[name]
+        self.n, self.stride, self.nbufs = n, stride, nbufs
+        gen_n = min(n, 1 << 20)
+        self.host = []
+        for g in range(2):
+            self.host.append(synth.make_packets(gen_n, rules, seed=synth.SEED + 1 + 7919 * (rank * 64 + g),
+                                                kind=cfgd["kind"], stride=stride))
+        self.bufs = []
+        reps = (n + gen_n - 1) // gen_n
+        for b in range(nbufs):
+            pk = self.host[b % 2]
+            hdr = torch.from_numpy(pk["hdr"]).to(dev)
+            lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
+            if reps > 1:
+                hdr = hdr.repeat(reps, 1)[:n].contiguous()
+                lens = lens.repeat(reps)[:n].contiguous()
+            out = {k: torch.empty(n, dtype=torch.int32, device=dev)
+                   for k in ("verdict", "flow_hash", "acl_hit", "part_idx")}
+            bb = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, stride)
+            # the compacted FW / PUNT / DROP lists in the partition layout (one list, include/ppe_hip.h)
+            rr = abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(),
+                            out["part_idx"].data_ptr(), out["part_idx"].data_ptr(), None, None)
+            self.bufs.append((hdr, lens, out, bb, rr))
+        lens0 = self.host[0]["len"].astype(np.int64)
+        self.read_bytes_per_pkt = float(np.minimum(lens0 & 0xFFFF, 64).mean() + 4.0) if stride == 64 else None
+
+    def arrays(self, k):
+        from ppe import abi
+        ins = (abi.Batch * k)(*(self.bufs[i % self.nbufs][3] for i in range(k)))
+        outs = (abi.Result * k)(*(self.bufs[i % self.nbufs][4] for i in range(k)))
+        return ins, outs
+
+
+def parity_sample(eng, res, rules, name):
+    """Batch 0's outputs against the oracle on a sample: bit-exact verdict / flow hash / ACL hit (packets whose
+    headers reach past the window must be WINDOW_PUNT) and the partition list of those tiles."""
+    import pyoracle
+    pk = res.host[0]
+    m = min(res.n, 4096 if synth.CONFIGS[name]["rules"] > 10000 else 1 << 16)
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"][:m], pk["len"][:m], cfg=o.cfg(now_seconds=NOW), nthreads=8)
+    out = res.bufs[0][2]
+    got_v = out["verdict"][:m].cpu().numpy().view(np.uint32)
+    got_h = out["flow_hash"][:m].cpu().numpy().view(np.uint32)
+    got_a = out["acl_hit"][:m].cpu().numpy()
+    far = ref["reach"] > res.stride
+    ok = ~far
+    act = (got_v >> 8) & 0xFF
+    order = np.argsort((np.arange(m) // 64) * 4 + np.array([0, 2, 1], np.int64)[act], kind="stable")
+    want_part = (order.astype(np.uint32) | (act[order] << 30)).astype(np.uint32)
+    got_p = out["part_idx"][:m].cpu().numpy().view(np.uint32)
+    return bool(np.array_equal(got_v[ok], ref["verdict"][ok]) and np.array_equal(got_h[ok], ref["flow_hash"][ok])
+                and np.array_equal(got_a[ok], ref["acl_hit"][ok]) and ((got_v[far] & 0xFF) == 18).all()
+                and np.array_equal(got_p, want_part)), m
+
+
+def traffic_per_packet(name):
+    """HBM bytes per packet of this config's launch from the committed rocprofv3 profile (tools/collect_traffic.py
+    output: FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE, calibrated), or None."""
+    files = sorted((ROOT / "profiles").glob(f"r2*_traffic_{name}.json"))
+    if not files:
+        return None
+    tj = json.load(open(files[-1]))
+    if tj.get("n_packets"):
+        return tj["traffic_bytes"] / tj["n_packets"]
+    return None
+
+
+def measure_config(name, args, dev, world, rank, dist, primary):
+    """One stateless config: resident batches, K batches in one call, roofline launch, parity sample."""
+    from ppe import abi
+    import ctypes as C
+    cfgd = synth.CONFIGS[name]
+    if args.n:
+        n = args.n
+    elif args.scaling == "strong":
+        n = STRONG_TOTAL // world
+    else:
+        n = cfgd["n"]
     stride = args.stride
     rules = synth.make_rules(cfgd["rules"])
     per_buf = n * (stride + 4 + 16)
-    # distinct resident batches: at least PPE_MAX_BATCH (a ppe_classify_batches launch groups up to 8 batches, and no
-    # batch may repeat inside one launch) and > 2x the 256 MiB MALL, so every timed read is served by HBM
     nbufs = args.nbufs or max(8, int(np.ceil(600e6 / per_buf)))
-
-    eng = Engine(local)
+    eng = Engine(dev.index)
+    eng.tuning(batches_per_launch=args.batches_per_launch)
     acl = eng.commit(rules, default_action=1)
     cfg = eng.cfg(now_seconds=NOW)
-
-    bufs = []
-    lens0 = None
-    for b in range(nbufs):
-        pk = synth.make_packets(n, rules, seed=synth.SEED + 1 + 7919 * (rank * 64 + b), kind=cfgd["kind"],
-                                stride=stride)
-        if lens0 is None:
-            lens0 = pk["len"]
-        hdr = torch.from_numpy(pk["hdr"]).to(dev)
-        lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
-        out = {"verdict": torch.empty(n, dtype=torch.int32, device=dev),
-               "flow_hash": torch.empty(n, dtype=torch.int32, device=dev),
-               "acl_hit": torch.empty(n, dtype=torch.int32, device=dev),
-               # the ballot-compacted FW / DROP lists in the partition layout (one list, ppe_hip.h)
-               "part_idx": torch.empty(n, dtype=torch.int32, device=dev)}
-        bufs.append((hdr, lens, out, pk if b == 0 else None))
+    res = Resident(name, n, stride, nbufs, rules, rank, dev)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
-
-    # pre-built C argument blocks: a step is one ppe_classify call (no per-step Python object building)
-    import ctypes as C
-    from ppe import abi
-    calls = []
-    for hdr, lens, out, _ in bufs:
-        b = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, stride)
-        r = abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(),
-                       out["part_idx"].data_ptr(), out["part_idx"].data_ptr(), None, None)
-        calls.append((C.byref(b), C.byref(r), b, r))
-    cfg_ref = C.byref(cfg)
     sptr = C.c_void_p(stream.cuda_stream)
-    classify = eng.lib.ppe_classify
-    ctx = eng.ctx
+    cfg_ref = C.byref(cfg)
 
-    def step(i):
-        bb, rr, _, _ = calls[i % nbufs]
-        rc = classify(ctx, bb, rr, cfg_ref, sptr)
-        if rc:
-            raise RuntimeError(f"ppe_classify failed: {rc}")
-
-    # the throughput path: ppe_classify_batches, K batches (rotating over the resident ones) pipelined over the
-    # engine's two streams, stream-ordered on `stream` (one C call for the whole timed region)
-    def batch_arrays(k):
-        ins = (abi.Batch * k)(*(calls[i % nbufs][2] for i in range(k)))
-        outs = (abi.Result * k)(*(calls[i % nbufs][3] for i in range(k)))
-        return ins, outs
-
-    def steps_pipelined(arrs):
+    def run(arrs):
         ins, outs = arrs
-        rc = eng.lib.ppe_classify_batches(ctx, ins, outs, len(ins), cfg_ref, sptr)
+        rc = eng.lib.ppe_classify_batches(eng.ctx, ins, outs, len(ins), cfg_ref, sptr)
         if rc:
-            raise RuntimeError(f"ppe_classify_batches failed: {rc}")
-
-    # the same batches as launches of GROUP batches each, serialized on `stream` (one ppe_classify_batches call per
-    # group: its single launch goes on the caller's stream), so launch durations do not overlap
-    GROUP = 2  # = the engine's batches per launch (kBatchesPerLaunch): one launch per call
-
-    def steps_grouped(k):
-        for g0 in range(0, k, GROUP):
-            m = min(GROUP, k - g0)
-            ins = (abi.Batch * m)(*(calls[(g0 + i) % nbufs][2] for i in range(m)))
-            outs = (abi.Result * m)(*(calls[(g0 + i) % nbufs][3] for i in range(m)))
-            rc = eng.lib.ppe_classify_batches(ctx, ins, outs, m, cfg_ref, sptr)
-            if rc:
-                raise RuntimeError(f"ppe_classify_batches failed: {rc}")
+            raise RuntimeError(f"ppe_classify_batches failed: {rc} {eng.lib.ppe_last_error(eng.ctx)}")
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
-    warm, timed = batch_arrays(max(args.warmup, 1)), batch_arrays(args.steps)
-    if args.warmup and args.streams == 2:
-        steps_pipelined(warm)
-    elif args.warmup:
-        steps_grouped(args.warmup)
-    # timed region 1 (value): K batches, barrier + synchronize on both sides, no per-launch events
+    warm, timed = res.arrays(max(args.warmup, 1)), res.arrays(args.steps)
+    run(warm)
+    # timed region (value): K batches, barrier + synchronize on both sides
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     ev0.record(stream)
-    if args.streams == 2:
-        steps_pipelined(timed)
-    else:
-        steps_grouped(args.steps)
+    run(timed)
     ev1.record(stream)
     barrier()
-    elapsed_ms = ev0.elapsed_time(ev1)
-    # timed region 2 (roofline): the same K batches as launches of 2 batches serialized on `stream` (no overlap
-    # between launches), with the dispatch's own start / end timestamps (hipExtLaunchKernelGGL events) around each
+    my_ms = max(ev0.elapsed_time(ev1), 1e-9)
+    # roofline region: the same call with the kernel's own dispatch timestamps (hipExtLaunchKernelGGL events)
     eng.timing(True)
     eng.timing_read(reset=True)
     barrier()
-    steps_grouped(args.steps)
+    run(timed)
     barrier()
     kern_ms, launches = eng.timing_read(reset=True)
     eng.timing(False)
-    my_ms = max(elapsed_ms, 1e-9)
-    # N > 1: the consumer-side verdict gather, timed apart from `value` (the classify path itself
-    # exchanges nothing): all_gather over RCCL of one batch's verdict + flow hash + ACL hit (12 B per packet per rank)
+    if dist is not None:
+        t = torch.tensor([my_ms, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        my_ms, kern_ms = float(t[0].item()), float(t[1].item())
+    total_pkts = n * args.steps * world
+    mpps = total_pkts / (my_ms / 1e3) / 1e6
+    rd, wr = algorithmic_bytes(64)
+    if res.read_bytes_per_pkt is not None:  # IMIX: min(len, 64) + 4 read per packet
+        rd = res.read_bytes_per_pkt
+    alg = rd + wr
+    pk_launch = n * args.steps / max(launches, 1)
+    kern_avg_ms = kern_ms / max(launches, 1)
+    achieved = alg * pk_launch / (kern_avg_ms / 1e3) / 1e9
+    tpp = traffic_per_packet(name)
+    parity, psample = parity_sample(eng, res, rules, name) if rank == 0 else (None, 0)
+    out = {
+        "value": round(mpps, 2), "unit": "Mpps", "ms_per_step": round(my_ms / args.steps, 5),
+        "workload": f"{name}: {n} x {'64B IPv4/UDP' if cfgd['kind'] == 'udp64' else 'IMIX 64/570/1500B Eth+VLAN TCP/UDP'}"
+                    f" packets per GPU, {cfgd['rules']} five-tuple ACL rules",
+        "packets_per_gpu": n, "rules": cfgd["rules"], "resident_batches": nbufs,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": round(tpp * pk_launch) if tpp else None,
+                     "kernel": "ppe_classify_kernel", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
+                     "launches_timed": launches, "packets_per_launch": int(pk_launch),
+                     "bytes_per_pkt": round(alg, 3), "written_bytes_per_pkt": 16.0,
+                     "us_per_1M_packets": round(kern_avg_ms * 1e3 / (pk_launch / (1 << 20)), 3)},
+        "parity_sample_ok": parity, "parity_sample_packets": psample,
+        "acl": {**{k: acl[k] for k in ("n_rules", "n_nodes", "max_depth", "blob_bytes", "lds_resident")},
+                "build_ms": round(acl["build_ms"], 3)},
+        "launch": eng.launch_info(),
+    }
+    ctx = dict(eng=eng, res=res, rules=rules, cfg=cfg, n=n, my_ms=my_ms)
+    if not primary:
+        eng.close()
+        del res
+        torch.cuda.empty_cache()
+        return out, None
+    return out, ctx
+
+
+def run_stateless(args, dev, world, rank, dist):
+    line_cfg, ctx = measure_config(args.config, args, dev, world, rank, dist, primary=True)
+    eng, res, rules, cfg, n, my_ms = (ctx[k] for k in ("eng", "res", "rules", "cfg", "n", "my_ms"))
+
+    # N > 1: the consumer-side verdict gather (SURVEY.md 8(e)), timed apart from `value` (the classify path itself
+    # exchanges nothing): all_gather over RCCL of one batch's verdict + flow hash + ACL hit (12 B per packet)
     gather = None
     if dist is not None:
         try:
-            _, _, out0, _ = bufs[0]
+            out0 = res.bufs[0][2]
             src = torch.stack([out0["verdict"], out0["flow_hash"], out0["acl_hit"]])
             dst = torch.empty((world,) + tuple(src.shape), dtype=src.dtype, device=dev)
             ts = []
             for _ in range(6):
-                barrier()
+                dist.barrier()
+                torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 dist.all_gather_into_tensor(dst, src)
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t0)
-            g_ms = float(np.median(ts[1:])) * 1e3
-            gt = torch.tensor([g_ms], dtype=torch.float64, device=dev)
+            gt = torch.tensor([float(np.median(ts[1:])) * 1e3], dtype=torch.float64, device=dev)
             dist.all_reduce(gt, op=dist.ReduceOp.MAX)
             g_ms = float(gt.item())
-            gather = {"ms_per_batch": round(g_ms, 4), "bytes_per_rank": 12 * n, "collective": "all_gather (RCCL)"}
-        except Exception as e:  # a failed measurement must not lose the throughput line
+            gather = {"ms_per_batch": round(g_ms, 4), "bytes_per_rank": 12 * n, "collective": "all_gather (RCCL)",
+                      "value_with_gather": round(n * world / ((my_ms / args.steps + g_ms) / 1e3) / 1e6, 2)}
+        except Exception as e:  # a failed side measurement must not lose the throughput line
             gather = {"error": str(e)[:200]}
-    if dist is not None:
-        t = torch.tensor([my_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        my_ms = float(t.item())
 
-    total_pkts = n * args.steps * world
-    mpps = total_pkts / (my_ms / 1e3) / 1e6
-    rd, wr = algorithmic_bytes(stride)
-    kern_avg_ms = kern_ms / max(launches, 1)
-    achieved = (rd + wr) * n * args.steps / (kern_ms / 1e3) / 1e9
-
-    # ---- parity spot check of the timed buffers (batch 0) against the oracle, 1/16 sample ----
-    parity = None
-    if rank == 0:
-        import pyoracle
-        hdr, lens, out, pk = bufs[0]
-        o = pyoracle.Oracle(rules, default_action=1)
-        m = min(n, 1 << 16)
-        ref = o.classify_batch(pk["hdr"][:m], pk["len"][:m], cfg=o.cfg(now_seconds=NOW), nthreads=8)
-        got_v = out["verdict"][:m].cpu().numpy().view(np.uint32)
-        got_h = out["flow_hash"][:m].cpu().numpy().view(np.uint32)
-        got_a = out["acl_hit"][:m].cpu().numpy()
-        # packets whose headers reach past the window must be WINDOW_PUNT; every other one bit-exact
-        far = ref["reach"] > stride
-        ok = ~far
-        # the partition list of those tiles: FW, PUNT, DROP per tile, each ascending, entry = index | action << 30
-        act = (got_v >> 8) & 0xFF
-        order = np.argsort((np.arange(m) // 64) * 4 + np.array([0, 2, 1], np.int64)[act], kind="stable")
-        want_part = (order.astype(np.uint32) | (act[order] << 30)).astype(np.uint32)
-        got_p = out["part_idx"][:m].cpu().numpy().view(np.uint32)
-        parity = bool(np.array_equal(got_v[ok], ref["verdict"][ok]) and np.array_equal(got_h[ok], ref["flow_hash"][ok])
-                      and np.array_equal(got_a[ok], ref["acl_hit"][ok]) and ((got_v[far] & 0xFF) == 18).all()
-                      and np.array_equal(got_p, want_part))
-
-    # ---- live rule commit: host build + upload + publish of the same rule set, between
-    # batches (the double-buffer swap of dp_acl_rule_commit, dataplane/src/common/dp_cmd.c:1987-2053) ----
+    # live rule commit (SURVEY.md 8(f) row 2): host build + upload + publish of the same rule set between batches
     commit_ms = []
     for _ in range(3):
         tc0 = time.perf_counter()
-        acl = eng.commit(rules, default_action=1)
+        eng.commit(rules, default_action=1)
         commit_ms.append((time.perf_counter() - tc0) * 1e3)
 
-    # ---- host-inclusive rate (pinned host buffers, H2D + classify + D2H pipeline) ----
+    # host-inclusive rate (pinned host buffers: the kernel reads / writes them across PCIe), rank 0 at N = 1
     host_mpps = None
     if rank == 0 and world == 1 and not args.no_host_inclusive:
-        pk = bufs[0][3]
+        import ctypes as C
+        from ppe import abi
+        pk = res.host[0]
+        m = len(pk["len"])
         ph = torch.from_numpy(pk["hdr"]).pin_memory()
         pl = torch.from_numpy(pk["len"].view(np.int32)).pin_memory()
-        res = {k: torch.empty(n, dtype=torch.int32).pin_memory() for k in ("verdict", "flow_hash", "acl_hit")}
-        from ppe import abi
-        import ctypes as C
-        b = abi.Batch(ph.data_ptr(), pl.data_ptr(), None, n, stride)
-        r = abi.Result(res["verdict"].data_ptr(), res["flow_hash"].data_ptr(), res["acl_hit"].data_ptr(),
+        hres = {k: torch.empty(m, dtype=torch.int32).pin_memory() for k in ("verdict", "flow_hash", "acl_hit")}
+        b = abi.Batch(ph.data_ptr(), pl.data_ptr(), None, m, args.stride)
+        r = abi.Result(hres["verdict"].data_ptr(), hres["flow_hash"].data_ptr(), hres["acl_hit"].data_ptr(),
                        None, None, None, None)
-        reps = 5
         eng.lib.ppe_classify_host(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), 1 << 18)
+        reps = 5
         th = time.perf_counter()
         for _ in range(reps):
-            rc = eng.lib.ppe_classify_host(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), 1 << 18)
-            assert rc == 0
-        host_mpps = n * reps / (time.perf_counter() - th) / 1e6
+            if eng.lib.ppe_classify_host(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), 1 << 18) != 0:
+                raise RuntimeError("ppe_classify_host failed")
+        host_mpps = m * reps / (time.perf_counter() - th) / 1e6
 
-    # ---- CPU baseline: oracle restatement (tree-walk ACL) on this host, rank 0, N = 1 ----
+    # CPU baseline: the oracle's C restatement (tree-walk ACL over the same classifier image), rank 0, N = 1: all of
+    # this host's cores (nproc) as pinned run-to-completion shards, then one pinned thread
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import pyoracle
-        pk = bufs[0][3]
-        img = eng.image()
-        o = pyoracle.Oracle(rules, default_action=1, image=img)
-        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=thr, use_tree=True)
-        # bounded sample: whole passes over the batch until ~10 s of wall time (x thr cores), then a ~2 s 1-thread run
-        reps = 0
-        tc = time.perf_counter()
+        pk = res.host[0]
+        m = len(pk["len"])
+        o = pyoracle.Oracle(rules, default_action=1, image=eng.image())
+        cores = host_cores()
+        ocfg = o.cfg(now_seconds=NOW)
+        o.pin(cores)
+        o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=len(cores), use_tree=True)
+        reps, tc = 0, time.perf_counter()
         while time.perf_counter() - tc < args.cpu_seconds:
-            o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=thr, use_tree=True)
+            o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=len(cores), use_tree=True)
             reps += 1
         cpu_s = time.perf_counter() - tc
-        ones = 0
-        t1 = time.perf_counter()
-        while time.perf_counter() - t1 < args.cpu_seconds / 5:
-            o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW), nthreads=1, use_tree=True)
+        o.pin(cores[:1])
+        ones, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < args.cpu_seconds / 4:
+            o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=1, use_tree=True)
             ones += 1
         one_s = (time.perf_counter() - t1) / ones
-        cpu = {"value": n * reps / cpu_s / 1e6, "unit": "Mpps", "cores": thr, "kind": "port",
-               "sample": f"{reps} passes over the {n}-packet {args.config} batch ({n * reps} packets, {cpu_s:.1f} s), "
-                         f"{thr} pthreads run-to-completion shards; 1-thread rate {n / one_s / 1e6:.2f} Mpps "
-                         f"({ones} passes)",
-               "single_thread_mpps": n / one_s / 1e6}
+        o.pin([])
+        cpu = {"value": m * reps / cpu_s / 1e6, "unit": "Mpps", "cores": len(cores), "kind": "port",
+               "sample": f"{reps} passes over a {m}-packet {args.config} batch ({m * reps} packets, {cpu_s:.1f} s), "
+                         f"{len(cores)} pinned pthreads (nproc of this host) as run-to-completion shards "
+                         f"(mainloop, main.c:422-425); 1 pinned thread: {m / one_s / 1e6:.2f} Mpps ({ones} passes)",
+               "single_thread_mpps": m / one_s / 1e6}
 
-    # HBM bytes per launch from the committed rocprofv3 PMC profile of this config (tools/collect_traffic.py)
-    traffic = None
-    tfiles = sorted(Path(__file__).resolve().parent.glob(f"profiles/*traffic_{args.config}.json"))
-    if tfiles and n == cfgd["n"] and stride == 64:
-        tj = json.load(open(tfiles[-1]))
-        if tj.get("n_packets") == n * GROUP:  # per launch of GROUP batches
-            traffic = round(tj["traffic_bytes"])
+    eng.close()
+    del res
+    torch.cuda.empty_cache()
+    extra = {}
+    names = [c for c in args.configs.split(",") if c and c != args.config] if args.n == 0 else []
+    for name in names:
+        try:
+            extra[name], _ = measure_config(name, args, dev, world, rank, dist, primary=False)
+        except Exception as e:  # one config failing must not lose the headline line
+            extra[name] = {"error": str(e)[:300]}
 
     if rank == 0:
-        li = eng.launch_info()
+        rf = line_cfg["roofline"]
         line = {
-            "metric": METRIC, "value": round(mpps, 2), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(my_ms / args.steps, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"{args.config}: {n} x {'64B IPv4/UDP' if cfgd['kind'] == 'udp64' else 'IMIX'}"
-                                   f" packets per GPU, {cfgd['rules']} five-tuple ACL rules",
-                       "packets_per_gpu": n, "rules": cfgd["rules"], "window_bytes": stride, "resident_batches": nbufs,
-                       "streams": args.streams,
+            "metric": METRIC, "value": line_cfg["value"], "unit": "Mpps", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": line_cfg["ms_per_step"], "higher_is_better": True,
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": line_cfg["workload"], "packets_per_gpu": line_cfg["packets_per_gpu"],
+                       "global_batch": line_cfg["packets_per_gpu"] * world, "rules": line_cfg["rules"],
+                       "window_bytes": args.stride, "resident_batches": line_cfg["resident_batches"],
+                       "batches_per_launch": args.batches_per_launch or args.steps,
                        "parallelism": f"batch-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": rd + wr,
-                         "launches_timed": launches, "packets_per_launch": n * GROUP if args.steps % GROUP == 0 else None,
-                         # the value's own rate in the same bytes: consecutive batches overlap on two streams
-                         "pipelined_GBps": round(mpps * 1e6 / world * (rd + wr) / 1e9, 1)},
+            "roofline": rf,
             "cpu_baseline": cpu,
             "host_inclusive_mpps": round(host_mpps, 2) if host_mpps else None,
-            "parity_sample_ok": parity,
-            "acl": {**{k: acl[k] for k in ("n_rules", "n_nodes", "max_depth", "blob_bytes", "lds_resident")},
-                    "build_ms": round(acl["build_ms"], 3), "commit_ms": round(float(np.median(commit_ms)), 3)},
-            "launch": li,
+            "parity_sample_ok": line_cfg["parity_sample_ok"],
+            "ranks_reported": dist.get_world_size() if dist is not None else 1,
+            "acl": {**line_cfg["acl"], "commit_ms": round(float(np.median(commit_ms)), 3)},
+            "launch": line_cfg["launch"],
+            "configs": extra,
         }
         if gather is not None:
-            if "ms_per_batch" in gather:
-                gather["value_with_gather"] = round(n * world / ((my_ms / args.steps + gather["ms_per_batch"]) / 1e3)
-                                                    / 1e6, 2)
             line["gather"] = gather
         print(json.dumps(line), flush=True)
-    eng.close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -349,7 +459,7 @@ def flow_bytes(stride: int) -> float:
     16-B direction counters read and written (two 8-B atomics) and the 8-B last-seen store, and the 8-B tile mask
     per 64 packets."""
     rd, wr = algorithmic_bytes(stride)
-    return rd + wr + 16.0 + 32.0 + 8.0 + 8.0 / 64.0
+    return rd + wr + 4.0 + 16.0 + 32.0 + 8.0 + 8.0 / 64.0
 
 
 def run_flow(args, cfgd, dev, world, rank, dist):

@@ -110,8 +110,12 @@ struct ppe_ctx {
     ppe_bdesc *h_ring[2] = {nullptr, nullptr};  // pinned staging of the H2D descriptor copy
     hipEvent_t ring_ev[2] = {nullptr, nullptr};
     bool ring_pending[2] = {false, false};
+    uint32_t ring_n[2] = {0, 0};       // descriptors the slot holds (its content = h_ring[slot][0, ring_n))
+    hipStream_t ring_stream[2] = {nullptr, nullptr};  // stream of the slot's last launch
     int ring_next = 0;
+    std::vector<ppe_bdesc> ring_tmp;   // descriptors of the launch being built
     ppe_tuning_t tune;
+    std::vector<std::pair<uint64_t, uint32_t>> occ_cache;  // resident workgroups per CU by kernel variant
     FlowTable *flow = nullptr;  // ppe_flow_create
     uint32_t *d_steer = nullptr;  // ppe_steer_partition: per-tile owner counts / offsets
     size_t steer_cap = 0;
@@ -228,12 +232,18 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
 
 // Resident workgroups per CU: the occupancy API's answer (register and LDS limits) unless the tuning fixes it.
 // The persistent grid is CUs × this, so no workgroup waits for a second round.
-uint32_t blocks_per_cu(const ppe_ctx *c, const StagePlan &p) {
+uint32_t blocks_per_cu(ppe_ctx *c, const StagePlan &p) {
     const uint32_t cap = kMaxBlocksPerCU * 256u / p.block;
     if (c->tune.blocks_per_cu) return std::max(1u, std::min(c->tune.blocks_per_cu, cap));  // may exceed residency
+    // the occupancy query costs microseconds of host time per call: cached per kernel variant and LDS size
+    const uint64_t key = (uint64_t)p.lds_words | ((uint64_t)p.mode << 32) | ((uint64_t)p.pipe << 40) |
+                         ((uint64_t)p.block << 48);
+    for (const auto &e : c->occ_cache)
+        if (e.first == key) return e.second;
     const int occ = ppe_classify_occupancy(p.lds_words, p.mode, p.pipe, (int)p.block);
-    if (occ > 0) return std::min<uint32_t>((uint32_t)occ, cap);
-    return 1u;
+    const uint32_t r = occ > 0 ? std::min<uint32_t>((uint32_t)occ, cap) : 1u;
+    c->occ_cache.emplace_back(key, r);
+    return r;
 }
 
 int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const ppe_acl_stats_t *st) {
@@ -285,21 +295,13 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     uint32_t tiles = 0;
     const bool use_ring = nb > PPE_MAX_BATCH;
     int rslot = 0;
+    std::vector<ppe_bdesc> &rd = c->ring_tmp;
     if (use_ring) {
         if (nb > PPE_MAX_RING) return fail(c, PPE_EINVAL, "more than %d batches in one launch", PPE_MAX_RING);
-        rslot = c->ring_next;
-        c->ring_next ^= 1;
-        // the launch that last read this slot (two ring launches ago) must be done before the slot is rewritten
-        if (c->ring_pending[rslot]) HIPCHK(c, hipEventSynchronize(c->ring_ev[rslot]));
-        c->ring_pending[rslot] = false;
-        if (!c->d_ring[rslot]) {
-            HIPCHK(c, hipMalloc(&c->d_ring[rslot], sizeof(ppe_bdesc) * PPE_MAX_RING));
-            HIPCHK(c, hipHostMalloc(&c->h_ring[rslot], sizeof(ppe_bdesc) * PPE_MAX_RING, hipHostMallocDefault));
-            if (!c->ring_ev[rslot]) HIPCHK(c, hipEventCreateWithFlags(&c->ring_ev[rslot], hipEventDisableTiming));
-        }
+        rd.resize(nb);
     }
     for (uint32_t i = 0; i < nb; ++i) {
-        ppe_bdesc &d = use_ring ? c->h_ring[rslot][i] : a.batch[i];
+        ppe_bdesc &d = use_ring ? rd[i] : a.batch[i];
         d.hdr = in[i].hdr;
         d.len = in[i].len;
         d.ts = in[i].ts;
@@ -316,9 +318,36 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         d.pad = 0;
         tiles = std::max(tiles, (in[i].n + 63u) / 64u);
     }
+    bool ring_copy = false;
     if (use_ring) {
-        a.batch[0] = c->h_ring[rslot][0];
-        HIPCHK(c, hipMemcpyAsync(c->d_ring[rslot], c->h_ring[rslot], sizeof(ppe_bdesc) * nb, hipMemcpyHostToDevice, s));
+        // a slot already holding exactly these descriptors is reused as is (a dataplane cycling over a fixed set of
+        // batch buffers uploads its descriptor table once); otherwise the next slot is rewritten once the launch
+        // that last read it (two ring launches ago) has completed
+        const size_t bytes = sizeof(ppe_bdesc) * nb;
+        rslot = -1;
+        for (int k = 0; k < 2; ++k)
+            if (c->ring_n[k] == nb && c->h_ring[k] && std::memcmp(c->h_ring[k], rd.data(), bytes) == 0) rslot = k;
+        if (rslot < 0) {
+            rslot = c->ring_next;
+            c->ring_next ^= 1;
+            if (c->ring_pending[rslot]) HIPCHK(c, hipEventSynchronize(c->ring_ev[rslot]));
+            c->ring_pending[rslot] = false;
+            if (!c->d_ring[rslot]) {
+                HIPCHK(c, hipMalloc(&c->d_ring[rslot], sizeof(ppe_bdesc) * PPE_MAX_RING));
+                HIPCHK(c, hipHostMalloc(&c->h_ring[rslot], sizeof(ppe_bdesc) * PPE_MAX_RING, hipHostMallocDefault));
+                if (!c->ring_ev[rslot]) HIPCHK(c, hipEventCreateWithFlags(&c->ring_ev[rslot], hipEventDisableTiming));
+            }
+            std::memcpy(c->h_ring[rslot], rd.data(), bytes);
+            c->ring_n[rslot] = nb;
+            HIPCHK(c, hipMemcpyAsync(c->d_ring[rslot], c->h_ring[rslot], bytes, hipMemcpyHostToDevice, s));
+            ring_copy = true;
+        }
+        if (!ring_copy && c->ring_pending[rslot] && c->ring_stream[rslot] != s) {
+            // reused slot: its upload may have been queued on another stream; order this launch after it
+            if (hipEventQuery(c->ring_ev[rslot]) == hipSuccess) c->ring_pending[rslot] = false;
+            else HIPCHK(c, hipStreamWaitEvent(s, c->ring_ev[rslot], 0));
+        }
+        a.batch[0] = rd[0];
         a.ring = c->d_ring[rslot];
     }
     a.nbatch = nb;
@@ -371,9 +400,10 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         ppe_launch_classify(&a, grid, plan.mode, plan.pipe, (int)plan.block, fl != nullptr, (void *)s, (void *)e0,
                             (void *)e1);
     if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
-    if (use_ring) {
+    if (use_ring) {  // every launch that reads the slot: a later rewrite waits for the last of them
         HIPCHK(c, hipEventRecord(c->ring_ev[rslot], s));
         c->ring_pending[rslot] = true;
+        c->ring_stream[rslot] = s;
     }
     c->img_used[r] = true;
     return PPE_OK;
@@ -523,6 +553,23 @@ int ppe_classify_batches(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t
     HIPCHK(c, use_device(c));
     const hipStream_t s = (hipStream_t)stream;
     const int mode = c->pipe_mode;
+    const uint32_t per = c->tune.batches_per_launch ? std::min<uint32_t>(c->tune.batches_per_launch, PPE_MAX_RING)
+                                                    : (uint32_t)PPE_MAX_RING;
+    uint32_t nonempty = 0;
+    for (uint32_t i = 0; i < nbatch; ++i) nonempty += in[i].n != 0;
+    if (nonempty == 0) return PPE_OK;
+    if (nonempty <= per) {  // one launch: straight onto the caller's stream, no fork / join
+        std::vector<ppe_batch_t> gin;
+        std::vector<ppe_result_t> gout;
+        gin.reserve(nonempty);
+        gout.reserve(nonempty);
+        for (uint32_t i = 0; i < nbatch; ++i)
+            if (in[i].n) {
+                gin.push_back(in[i]);
+                gout.push_back(out[i]);
+            }
+        return launch(c, gin.data(), gout.data(), nonempty, cfg, s, 0);
+    }
     if (!c->pipe[0]) {
         for (int k = 0; k < kPipeStreams; ++k)
             HIPCHK(c, hipStreamCreateWithFlags(&c->pipe[k], mode == 2 ? hipStreamDefault : hipStreamNonBlocking));
@@ -539,8 +586,6 @@ int ppe_classify_batches(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t
     std::vector<ppe_batch_t> gin(std::min<uint32_t>(nbatch, PPE_MAX_RING));
     std::vector<ppe_result_t> gout(gin.size());
     uint32_t ng = 0, nl = 0;
-    const uint32_t per = c->tune.batches_per_launch ? std::min<uint32_t>(c->tune.batches_per_launch, PPE_MAX_RING)
-                                                    : (uint32_t)PPE_MAX_RING;
     for (uint32_t i = 0; i <= nbatch; ++i) {
         if (i < nbatch && in[i].n == 0) continue;
         if (i < nbatch) {

@@ -1,4 +1,6 @@
 set -o pipefail
-mkdir -p gpurun_out/r2a
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r2a/gputest.log 2>&1 && \
-for c in C1 C2 C3 C4; do timeout -k 10 240 python -u bench.py --config $c --no-cpu-baseline --no-host-inclusive > gpurun_out/r2a/bench_$c.json 2> gpurun_out/r2a/bench_$c.err || exit 1; done
+O=gpurun_out/${1:-r2j}
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputest.log 2>&1 && \
+timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err && \
+timeout -k 10 300 python -u bench.py --scaling strong --configs C4 --no-cpu-baseline --no-host-inclusive > $O/bench_strong.json 2> $O/bench_strong.err
