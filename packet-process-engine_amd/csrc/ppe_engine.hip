@@ -293,6 +293,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     ppe_kargs a;
     std::memset(&a, 0, sizeof a);
     uint32_t tiles = 0;
+    uint64_t tiles_total = 0;
     const bool use_ring = nb > PPE_MAX_BATCH;
     int rslot = 0;
     std::vector<ppe_bdesc> &rd = c->ring_tmp;
@@ -317,6 +318,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         d.idx_base = idx_base;
         d.pad = 0;
         tiles = std::max(tiles, (in[i].n + 63u) / 64u);
+        tiles_total += (uint64_t)((in[i].n + 63u) / 64u);
     }
     bool ring_copy = false;
     if (use_ring) {
@@ -332,11 +334,6 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
             c->ring_next ^= 1;
             if (c->ring_pending[rslot]) HIPCHK(c, hipEventSynchronize(c->ring_ev[rslot]));
             c->ring_pending[rslot] = false;
-            if (!c->d_ring[rslot]) {
-                HIPCHK(c, hipMalloc(&c->d_ring[rslot], sizeof(ppe_bdesc) * PPE_MAX_RING));
-                HIPCHK(c, hipHostMalloc(&c->h_ring[rslot], sizeof(ppe_bdesc) * PPE_MAX_RING, hipHostMallocDefault));
-                if (!c->ring_ev[rslot]) HIPCHK(c, hipEventCreateWithFlags(&c->ring_ev[rslot], hipEventDisableTiming));
-            }
             std::memcpy(c->h_ring[rslot], rd.data(), bytes);
             c->ring_n[rslot] = nb;
             HIPCHK(c, hipMemcpyAsync(c->d_ring[rslot], c->h_ring[rslot], bytes, hipMemcpyHostToDevice, s));
@@ -352,7 +349,9 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     }
     a.nbatch = nb;
     a.max_tiles = tiles;
-    const uint32_t want = (tiles + wpb - 1) / wpb;
+    // enough workgroups for every tile of every batch (the kernel splits its waves into batch groups), at most
+    // the resident grid
+    const uint32_t want = (uint32_t)std::min<uint64_t>((tiles_total + wpb - 1) / wpb, 1u << 30);
     const uint32_t maxg = c->n_cu * blocks_per_cu(c, plan);
     const uint32_t grid = std::max(1u, std::min(want, std::min(maxg, c->max_grid)));
     a.img = c->d_img[r];
@@ -461,6 +460,13 @@ int ppe_ctx_create(int device, ppe_ctx_t **out) {
         rc = PPE_ENOMEM;
     for (int i = 0; i < 2 && rc == PPE_OK; ++i)
         if (hipEventCreateWithFlags(&c->img_done[i], hipEventDisableTiming) != hipSuccess) rc = PPE_EIO;
+    // descriptor ring slots (launches over more than PPE_MAX_BATCH batches): allocated here, not on first use, so
+    // no batch call pays an allocation
+    for (int i = 0; i < 2 && rc == PPE_OK; ++i)
+        if (hipMalloc(&c->d_ring[i], sizeof(ppe_bdesc) * PPE_MAX_RING) != hipSuccess ||
+            hipHostMalloc(&c->h_ring[i], sizeof(ppe_bdesc) * PPE_MAX_RING, hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ring_ev[i], hipEventDisableTiming) != hipSuccess)
+            rc = PPE_ENOMEM;
     if (rc == PPE_OK) {
         // empty rule set, management default action DROP (mgrplane/src/srv/srvnet/srv_rule.c:84)
         rc = ppe_rules_commit(c, nullptr, nullptr, 0, ACL_RULE_ACTION_DROP, nullptr);

@@ -754,8 +754,18 @@ void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t stride_waves = gridDim.x * (BLOCK / 64);
-    const uint32_t twave = blockIdx.x * (BLOCK / 64) + wv;  // this wave's first tile of every batch
+    const uint32_t nwaves = gridDim.x * (BLOCK / 64);
+    const uint32_t twave = blockIdx.x * (BLOCK / 64) + wv;  // this wave's index in the grid (trace slot)
+    // Batch groups: the grid's waves split into G = min(waves, batches) equal groups; group g takes batches g,
+    // g + G, ..., and its Wb waves stride over each of them (wave wi of the group: tiles wi, wi + Wb, ...).  One batch
+    // (or few) → every wave on every batch as before; a long queue of batches → each wave walks many tiles of a batch
+    // before its per-batch setup (descriptor, pointer checks) comes round again (1M-packet batches over 8,192 waves:
+    // 64 tiles per batch setup instead of 2).  The remainder waves of the division idle.
+    const uint32_t ngroups = min(nwaves, a.nbatch);
+    const uint32_t stride_waves = nwaves / ngroups;              // Wb
+    const uint32_t grp = twave / stride_waves;
+    const uint32_t wtile = twave - grp * stride_waves;            // wi
+    const bool wave_live = grp < ngroups;
     uint32_t titer = 0;
     TRACE_AT(0);
     // the batch being processed (kernel-argument descriptor, or the device descriptor ring: scalar loads either way)
@@ -771,7 +781,7 @@ void ppe_classify_kernel(ppe_kargs a) {
         for (int k = 0; k < 6; ++k) d.w[k] = q[k];
         return __builtin_bit_cast(ppe_bdesc, d);
     };
-    ppe_bdesc B = bdesc(0);
+    ppe_bdesc B = bdesc(wave_live ? grp : 0u);
     // current tile's window: bytes 0..51 (w[0..12]) and the wire length.  Clamped (unconditional) loads: a lane past
     // the end of the batch re-reads the last packet.  Byte offsets are 32-bit (the engine keeps n * stride < 2^31).
     uint4 q0, q1, q2;
@@ -787,8 +797,8 @@ void ppe_classify_kernel(ppe_kargs a) {
     };
     auto load_tile = [&](uint32_t t) { load_at(B.hdr, B.len, B.n, B.stride, t); };
     // first window in flight during the image staging
-    bool have = PF == PF_HOIST && twave < ((B.n + 63u) >> 6);  // (PF_MULTI: first tiles loaded at the loop top)
-    if (have) load_tile(twave);
+    bool have = PF == PF_HOIST && wave_live && wtile < ((B.n + 63u) >> 6);  // (PF_MULTI: at the loop top)
+    if (have) load_tile(wtile);
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
     const uint32_t lanebase = wv * KEY_WAVE_BYTES + 4u * lane;  // this lane's key slot 0 (LDS byte address)
@@ -912,10 +922,10 @@ void ppe_classify_kernel(ppe_kargs a) {
 
     if constexpr (MT > 1) {
         // PF_MULTI: wave w takes tiles [MT w, MT w + MT), then + MT W, ...; all MT windows are requested together
-        for (uint32_t bi = 0; bi < a.nbatch; ++bi) {
-            if (bi) B = bdesc(bi);
+        for (uint32_t bi = grp; wave_live && bi < a.nbatch; bi += ngroups) {
+            if (bi != grp) B = bdesc(bi);
             const uint32_t ntiles = (B.n + 63u) >> 6;
-            for (uint32_t t0 = twave * MT; t0 < ntiles; t0 += stride_waves * MT) {
+            for (uint32_t t0 = wtile * MT; t0 < ntiles; t0 += stride_waves * MT) {
                 uint4 r0[MT], r1[MT], r2[MT];
                 uint32_t r3[MT], rl[MT];
 #pragma unroll
@@ -969,10 +979,10 @@ void ppe_classify_kernel(ppe_kargs a) {
             }
         }
     } else
-    for (uint32_t bi = 0; bi < a.nbatch; ++bi) {
-        if (bi) B = bdesc(bi);
+    for (uint32_t bi = grp; wave_live && bi < a.nbatch; bi += ngroups) {
+        if (bi != grp) B = bdesc(bi);
         const uint32_t ntiles = (B.n + 63u) >> 6;
-        for (uint32_t tile = twave; tile < ntiles; tile += stride_waves) {
+        for (uint32_t tile = wtile; tile < ntiles; tile += stride_waves) {
             if (PPE_TRACE && titer - PPE_TRACE_SKIP < 4u) TRACE_AT(2 + 5 * (titer - PPE_TRACE_SKIP));
             if (!have) load_tile(tile);
             have = false;
