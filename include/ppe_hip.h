@@ -311,11 +311,11 @@ int  ppe_scatter_rows(ppe_ctx_t *ctx, const void *src, uint32_t row_bytes, const
 
 /* Operator text of the reference's `show` commands, from counters / flow info read with ppe_counters_read /
  * ppe_flow_info: dp_show_pkt_stat (dataplane/src/common/dp_cmd.c:844-1818; same sections, names and order; the
- * reference's SELF_TEST build (flow.c:21) never counts output_*, and the I/O, ARP/ICMP/OSPF, defrag, TX and attack
- * counters have no source on this path: those lines print 0) and dp_show_flow_stat (dp_cmd.c:2346-2392).
+ * reference's SELF_TEST build (flow.c:21) never counts output_*, and the I/O, ARP/ICMP/OSPF, TX and other attack
+ * counters have no source on this path: those lines print 0) and dp_show_flow_stat (dp_cmd.c:2346-2392); the
+ * reassembly lines come from ppe_defrag_info (ppe_format_*_ex, declared with the reassembly API below).
  * snprintf semantics: returns the full length, writes at most cap bytes including the NUL. */
-int  ppe_format_pkt_stat(const ppe_counters_t *c, char *buf, size_t cap);
-int  ppe_format_flow_stat(const ppe_flow_info_t *f, char *buf, size_t cap);
+
 
 /* ---- IPv4 reassembly (dataplane/src/decode/decode-defrag.c) ----
  * ppe_classify PUNTs fragments (PPE_ST_FRAG).  ppe_defrag runs the reference's Defrag (decode-defrag.c:449-487) for
@@ -405,6 +405,17 @@ int  ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_ou
 int  ppe_defrag_age(ppe_defrag_t *d, uint64_t now_seconds, uint64_t timeout_seconds, uint64_t *dropped,
                     uint32_t max, uint32_t *n_dropped, uint32_t *n_freed);
 int  ppe_defrag_info(ppe_defrag_t *d, ppe_defrag_info_t *info);      /* synchronises */
+
+/* `show packet statistic` / `show flow statistic` text (dp_show_pkt_stat / dp_show_flow_stat,
+ * dataplane/src/common/dp_cmd.c:844-1818, 2346-2392) into buf (NUL-terminated, truncated to cap); returns the full
+ * length.  The _ex forms take the IPv4 reassembly table's counters (NULL: those lines print 0, as the plain forms
+ * do): the ip_frag_stat section, the new / del fcb lines and, while the teardrop monitor is enabled
+ * (teardrop_monitor != 0; off in the reference's default configuration), the attack section's teardrop line. */
+int  ppe_format_pkt_stat(const ppe_counters_t *c, char *buf, size_t cap);
+int  ppe_format_flow_stat(const ppe_flow_info_t *f, char *buf, size_t cap);
+int  ppe_format_pkt_stat_ex(const ppe_counters_t *c, const ppe_defrag_info_t *df, int teardrop_monitor, char *buf,
+                            size_t cap);
+int  ppe_format_flow_stat_ex(const ppe_flow_info_t *f, const ppe_defrag_info_t *df, char *buf, size_t cap);
 const char *ppe_defrag_last_error(ppe_defrag_t *d);
 
 /* Human-readable last error of this context (static storage of the ctx). */

@@ -89,7 +89,9 @@ struct ppe_ctx {
     std::vector<uint32_t> level_end[2];  // per image: number of tree nodes at depth <= d (BFS order)
     ppe_acl_stats_t stats[2];
     hipEvent_t img_done[2] = {nullptr, nullptr};
-    bool img_used[2] = {false, false};
+    std::vector<std::pair<hipStream_t, hipEvent_t>> img_readers[2];  // per slot: launch streams, event behind
+                                                                       // their last launch with it
+    hipStream_t aux = nullptr;                 // image uploads
     int running = 0;
     // counters
     unsigned long long *d_cslots = nullptr;
@@ -246,18 +248,41 @@ uint32_t blocks_per_cu(ppe_ctx *c, const StagePlan &p) {
     return r;
 }
 
+// a launch on stream s reads image slot r: an event (one per slot and stream) is recorded behind it, so a rewrite
+// of the slot waits for exactly the launches that read it (the event outlives the stream if the caller frees it)
+int note_image_reader(ppe_ctx *c, int r, hipStream_t s) {
+    hipEvent_t ev = nullptr;
+    for (auto &x : c->img_readers[r])
+        if (x.first == s) ev = x.second;
+    if (!ev) {
+        HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        c->img_readers[r].emplace_back(s, ev);
+    }
+    HIPCHK(c, hipEventRecord(ev, s));
+    return PPE_OK;
+}
+
 int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const ppe_acl_stats_t *st) {
-    // the back image may still be read by launches queued before the previous swap: wait for them (commits are
-    // control-plane events; launches themselves record nothing)
-    if (c->img_used[slot]) HIPCHK(c, hipDeviceSynchronize());
+    // The back image may still be read by launches queued before the previous swap.  Wait for exactly those (the
+    // events recorded behind them, note_image_reader): unrelated work on any stream is never waited on.
+    for (auto &x : c->img_readers[slot]) {
+        HIPCHK(c, hipEventSynchronize(x.second));
+        HIPCHK(c, hipEventDestroy(x.second));
+    }
+    c->img_readers[slot].clear();
+    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
     const size_t bytes = (size_t)n_words * 4u;
     if (bytes > c->img_cap[slot]) {
+        // (grown with headroom: a growing rule set reallocates rarely; the free of an unused slot is then safe)
+        const size_t cap = std::max(bytes + bytes / 2, (size_t)64 * 1024);
         if (c->d_img[slot]) HIPCHK(c, hipFree(c->d_img[slot]));
         c->d_img[slot] = nullptr;
-        HIPCHK(c, hipMalloc(&c->d_img[slot], bytes + 64));
-        c->img_cap[slot] = bytes;
+        HIPCHK(c, hipMalloc(&c->d_img[slot], cap + 64));
+        c->img_cap[slot] = cap;
     }
-    HIPCHK(c, hipMemcpy(c->d_img[slot], words, bytes, hipMemcpyHostToDevice));
+    // the copy runs on the engine's own non-blocking stream: no implicit synchronisation with other streams
+    HIPCHK(c, hipMemcpyAsync(c->d_img[slot], words, bytes, hipMemcpyHostToDevice, c->aux));
+    HIPCHK(c, hipStreamSynchronize(c->aux));
     c->h_img[slot].assign(words, words + n_words);
     // BFS node order: the nodes of depth <= d are exactly [0, level_end[d])
     {
@@ -277,7 +302,6 @@ int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const 
     }
     c->stats[slot] = *st;
     c->stats[slot].lds_resident = (uint32_t)stage_plan(c, c->h_img[slot]).mode;
-    c->img_used[slot] = false;
     return PPE_OK;
 }
 
@@ -404,8 +428,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         c->ring_pending[rslot] = true;
         c->ring_stream[rslot] = s;
     }
-    c->img_used[r] = true;
-    return PPE_OK;
+    return note_image_reader(c, r, s);
 }
 
 hipError_t use_device(ppe_ctx *c) {
@@ -496,6 +519,9 @@ int ppe_ctx_destroy(ppe_ctx_t *c) {
     }
     for (hipStream_t s : c->pipe)
         if (s) (void)hipStreamDestroy(s);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
+    for (auto &v : c->img_readers)
+        for (auto &x : v) (void)hipEventDestroy(x.second);
     for (hipEvent_t e : c->pipe_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->flow) ppe_flow_destroy(c);
@@ -733,8 +759,7 @@ int ppe_acl_lookup(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint32_t 
     const uint32_t grid = std::max(1u, std::min(want, c->n_cu * 8u));
     const int rc = ppe_launch_acl_tuples(&a, grid, lds ? 1 : 0, stream);
     if (rc != 0) return fail(c, PPE_EIO, "acl kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
-    c->img_used[r] = true;
-    return PPE_OK;
+    return note_image_reader(c, r, (hipStream_t)stream);
 }
 
 int ppe_acl_lookup_host(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint32_t *action,

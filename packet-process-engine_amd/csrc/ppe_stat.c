@@ -3,10 +3,16 @@
  * (dp_show_pkt_stat, dataplane/src/common/dp_cmd.c:844-1818; dp_show_flow_stat, :2346-2392), produced from this
  * engine's per-reason counters (ppe_counters_read) and flow-table totals (ppe_flow_info).
  *
- * Sections, line names and order follow the reference.  Lines whose counter has no source on the GPU path print 0:
- * the receive-error / from-linux / address counters of the Octeon I/O layer, ARP / ICMP / OSPF hand-offs to Linux,
- * the defragmenter's control-block counters, TX, the attack monitors (pass-through at default configuration), and
- * output_* (the reference's SELF_TEST build forwards without STAT_OUTPUT_*, flow.c:21,376-377).
+ * Sections, line names and order follow the reference.  The ip_frag_stat lines, the attack section's teardrop line and
+ * the flow text's fcb lines come from the IPv4 reassembly table (ppe_defrag_info) when one is given to the _ex forms:
+ * fragments per Defrag outcome are exactly the STAT_FRAG_* increments of decode-defrag.c (cache_ok :391, reasm_ok
+ * :279, setup_err :282, fcb_full :80, hw2sw_err :418, cache_full :437, defrag_err :401; fcb_no :87 is a memory-pool
+ * failure the device table cannot have, out_oversize is commented out at :285), new / del fcb are :481 / :526, and
+ * teardrop is counted only while the teardrop monitor is enabled (DP_Teardrop_Attack_Monitor, dataplane/src/attack/
+ * dp_attack.c:487-498; disabled in the default configuration).  Lines whose counter has no source on the GPU path
+ * print 0: the receive-error / from-linux / address counters of the Octeon I/O layer, ARP / ICMP / OSPF hand-offs to
+ * Linux, TX, the other attack monitors (pass-through at default configuration), and output_* (the reference's
+ * SELF_TEST build forwards without STAT_OUTPUT_*, flow.c:21,376-377).
  */
 #include <stdarg.h>
 #include <stdio.h>
@@ -15,6 +21,9 @@
 #include "ppe_hip.h"
 
 #define NONE (-1)
+/* reassembly-table sources (ppe_defrag_info_t), printed 0 without one */
+#define DF(st) (1000 + (st))   /* fragments with Defrag outcome st */
+#define DF_TEARDROP 2000       /* overlaps, while the teardrop monitor is enabled */
 
 typedef struct {
     const char *name;  /* printed as "<name>: %ld" */
@@ -46,10 +55,11 @@ static const stat_line_t k_ipv4[] = {{"headerlen_err", PPE_C_IPV4_HEADERLEN_ERR}
                                      {"rx_ok", PPE_C_IPV4_RX_OK},               {"icmp_se2linux_ok", NONE},
                                      {"icmp_se2linux_fail", NONE},              {"ospf_se2linux_ok", NONE},
                                      {"ospf_se2linux_fail", NONE}};
-static const stat_line_t k_frag[] = {{"fraglen_err", PPE_C_FRAG_FRAGLEN_ERR}, {"fcb_no", NONE}, {"hw2sw_err", NONE},
-                                     {"fcb_full", NONE}, {"cache_full", NONE}, {"defrag_err", NONE},
-                                     {"setup_err", NONE}, {"out_oversize", NONE}, {"cache_ok", NONE},
-                                     {"reasm_ok", NONE}};
+static const stat_line_t k_frag[] = {{"fraglen_err", PPE_C_FRAG_FRAGLEN_ERR}, {"fcb_no", NONE},
+                                     {"hw2sw_err", DF(PPE_DF_HW2SW_ERR)}, {"fcb_full", DF(PPE_DF_FCB_FULL)},
+                                     {"cache_full", DF(PPE_DF_CACHE_FULL)}, {"defrag_err", DF(PPE_DF_DEFRAG_ERR)},
+                                     {"setup_err", DF(PPE_DF_SETUP_ERR)}, {"out_oversize", NONE},
+                                     {"cache_ok", DF(PPE_DF_CACHED)}, {"reasm_ok", DF(PPE_DF_REASM)}};
 static const stat_line_t k_icmp[] = {{"rx_ok", NONE}, {"drop", NONE}};
 static const stat_line_t k_tcp[] = {{"headerlen_err", PPE_C_TCP_HEADERLEN_ERR}, {"pktlen_err", PPE_C_TCP_PKTLEN_ERR},
                                     {"rx_ok", PPE_C_TCP_RX_OK}};
@@ -63,7 +73,7 @@ static const stat_line_t k_out[] = {{"output_fw", NONE}, {"output_drop", NONE}, 
                                     {"output_unsupport", NONE}};
 static const stat_line_t k_tx[] = {{"port_err", NONE}, {"hw_send_err", NONE}, {"sw_desc_err", NONE},
                                    {"sw_send_err", NONE}, {"send_over", NONE}};
-static const stat_line_t k_att[] = {{"land_drop", NONE}, {"teardrop", NONE}, {"pingdeath", NONE},
+static const stat_line_t k_att[] = {{"land_drop", NONE}, {"teardrop", DF_TEARDROP}, {"pingdeath", NONE},
                                     {"ping flood drop", NONE}, {"udp flood drop", NONE}, {"syn flood drop", NONE},
                                     {"syncount", NONE}, {"portscan_drop", NONE}};
 
@@ -90,7 +100,19 @@ static void put(out_t *o, const char *fmt, ...) {
     if (k > 0) o->len += (size_t)k;
 }
 
+static long line_value(const ppe_counters_t *c, const ppe_defrag_info_t *df, int teardrop_monitor, int ci) {
+    if (ci == NONE) return 0L;
+    if (ci == DF_TEARDROP) return df && teardrop_monitor ? (long)df->teardrop : 0L;
+    if (ci >= 1000) return df ? (long)df->st[ci - 1000] : 0L;
+    return (long)c->c[ci];
+}
+
 int ppe_format_pkt_stat(const ppe_counters_t *c, char *buf, size_t cap) {
+    return ppe_format_pkt_stat_ex(c, NULL, 0, buf, cap);
+}
+
+int ppe_format_pkt_stat_ex(const ppe_counters_t *c, const ppe_defrag_info_t *df, int teardrop_monitor, char *buf,
+                           size_t cap) {
     if (!c) return PPE_EINVAL;
     out_t o = {buf, buf ? cap : 0, 0};
     if (buf && cap) buf[0] = 0;
@@ -103,7 +125,7 @@ int ppe_format_pkt_stat(const ppe_counters_t *c, char *buf, size_t cap) {
         put(&o, "----------------\n");
         for (int i = 0; i < sec->n; i++) {
             const int ci = sec->lines[i].counter;
-            put(&o, "%s: %ld\n", sec->lines[i].name, ci == NONE ? 0L : (long)c->c[ci]);
+            put(&o, "%s: %ld\n", sec->lines[i].name, line_value(c, df, teardrop_monitor, ci));
         }
         put(&o, "----------------\n");
         if (sec->blank_after) put(&o, "\n");
@@ -112,11 +134,16 @@ int ppe_format_pkt_stat(const ppe_counters_t *c, char *buf, size_t cap) {
 }
 
 int ppe_format_flow_stat(const ppe_flow_info_t *f, char *buf, size_t cap) {
+    return ppe_format_flow_stat_ex(f, NULL, buf, cap);
+}
+
+int ppe_format_flow_stat_ex(const ppe_flow_info_t *f, const ppe_defrag_info_t *df, char *buf, size_t cap) {
     if (!f) return PPE_EINVAL;
     out_t o = {buf, buf ? cap : 0, 0};
     if (buf && cap) buf[0] = 0;
     put(&o, "new flow is: %ld\ndel flow is: %ld\n", (long)f->new_flow, (long)f->del_flow);
-    put(&o, "new fcb is: %ld\ndel fcb is: %ld\n", 0L, 0L);  /* defrag control blocks: defrag is out of scope */
+    /* FCBs created / freed by the reassembly table (new_fcb / del_fcb, decode-defrag.c:15-16,481,526) */
+    put(&o, "new fcb is: %ld\ndel fcb is: %ld\n", df ? (long)df->new_fcb : 0L, df ? (long)df->del_fcb : 0L);
     put(&o, "new pcb is: %ld\ndel pcb is: %ld\n", 0L, 0L);
     return (int)o.len;
 }

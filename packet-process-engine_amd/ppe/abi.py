@@ -176,6 +176,7 @@ EXPORTS = [
     "ppe_launch_info", "ppe_debug_trace", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
     "ppe_get_tuning", "ppe_flow_create", "ppe_flow_destroy", "ppe_classify_flow", "ppe_flow_age", "ppe_flow_info",
     "ppe_flow_clear_stat", "ppe_flow_dump", "ppe_format_pkt_stat", "ppe_format_flow_stat",
+    "ppe_format_pkt_stat_ex", "ppe_format_flow_stat_ex",
     "ppe_steer_partition", "ppe_gather_rows", "ppe_scatter_rows",
     "ppe_defrag_create", "ppe_defrag_destroy", "ppe_defrag", "ppe_defrag_age", "ppe_defrag_info",
     "ppe_defrag_last_error",
@@ -259,6 +260,9 @@ def _open(p: Path, mode) -> C.CDLL:
         "ppe_gather_rows": ([vp, vp, u32, vp, u32, vp, vp], C.c_int),
         "ppe_scatter_rows": ([vp, vp, u32, vp, u32, vp, vp], C.c_int),
         "ppe_format_flow_stat": ([C.POINTER(FlowInfo), C.c_char_p, C.c_size_t], C.c_int),
+        "ppe_format_pkt_stat_ex": ([C.POINTER(Counters), C.POINTER(DefragInfo), C.c_int, C.c_char_p, C.c_size_t],
+                                   C.c_int),
+        "ppe_format_flow_stat_ex": ([C.POINTER(FlowInfo), C.POINTER(DefragInfo), C.c_char_p, C.c_size_t], C.c_int),
         "ppe_defrag_create": ([vp, C.POINTER(DefragCfg), C.POINTER(vp)], C.c_int),
         "ppe_defrag_destroy": ([vp], C.c_int),
         "ppe_defrag": ([vp, C.POINTER(FragBatch), C.POINTER(DefragOut), vp], C.c_int),

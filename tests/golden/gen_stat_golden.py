@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Generate tests/golden/pkt_stat_v1.txt + flow_stat_v1.txt: the text the reference's `show packet statistic` /
-`show flow statistic` would print for a fixed counter vector.
+"""Generate tests/golden/pkt_stat_v1.txt + flow_stat_v1.txt (engine counters only) and pkt_stat_v2.txt +
+flow_stat_v2.txt (plus the IPv4 reassembly table's counters, teardrop monitor enabled): the text the reference's
+`show packet statistic` / `show flow statistic` would print for a fixed counter vector.
 
 Run in the build container (needs /root/reference): it walks dp_show_pkt_stat / dp_show_flow_stat in
 dataplane/src/common/dp_cmd.c statement by statement — each `x += pktstat[i]-><field>` sum followed by its
@@ -36,6 +37,14 @@ FIELD = {
 }
 COUNTS = {name: 1000 + 17 * i for i, name in enumerate(COUNTERS)}  # distinct values per counter
 FLOW = {"new_flow": 123456, "del_flow": 7890}
+# v2: the reassembly table's per-outcome fragment counts (ppe_defrag_info_t.st[], enum ppe_defrag_status) and
+# teardrops, by the STAT_FRAG_* / STAT_ATTACK_TEARDROP site each outcome increments (decode-defrag.c)
+DF_FIELD = {"fragstat.cache_ok": "st0", "fragstat.reasm_ok": "st1", "fragstat.setup_err": "st2",
+            "fragstat.fcb_full": "st3", "fragstat.hw2sw_err": "st4", "fragstat.cache_full": "st6",
+            "fragstat.defrag_err": "st7", "attstat.teardrop": "teardrop"}
+DF_COUNTS = {"st0": 501, "st1": 502, "st2": 503, "st3": 504, "st4": 505, "st5": 506, "st6": 507, "st7": 508,
+             "st8": 509, "teardrop": 510}
+FCB = {"new_fcb": 4242, "del_fcb": 4141}
 
 
 def body(src: str, name: str) -> str:
@@ -48,13 +57,17 @@ PAT = re.compile(r'(?P<reset>\bx\s*=\s*0;)|x\s*\+=\s*pktstat\[i\]->(?P<field>[a-
                  r'|sprintf\(\(void \*\)ptr,\s*"(?P<fmt>(?:[^"\\]|\\.)*)"\s*(?P<arg>,\s*x)?\)')
 
 
-def eval_show(text: str) -> str:
+def eval_show(text: str, defrag: bool = False) -> str:
     out, x = [], 0
     for m in PAT.finditer(text):
         if m.group("reset"):
             x = 0
         elif m.group("field"):
-            x += COUNTS[FIELD[m.group("field")]] if m.group("field") in FIELD else 0
+            f = m.group("field")
+            if f in FIELD:
+                x += COUNTS[FIELD[f]]
+            elif defrag and f in DF_FIELD:
+                x += DF_COUNTS[DF_FIELD[f]]
         else:
             fmt = m.group("fmt").replace("\\n", "\n").replace("%ld", "%d")
             out.append(fmt % x if m.group("arg") else fmt)
@@ -72,7 +85,14 @@ def main():
     for kind, (n, d) in (("flow", (vals["new_flow"], vals["del_flow"])), ("fcb", (0, 0)), ("pcb", (0, 0))):
         lines.append(f"new {kind} is: {n}\ndel {kind} is: {d}\n")
     (OUT / "flow_stat_v1.txt").write_text("".join(lines))
-    print("wrote", OUT / "pkt_stat_v1.txt", OUT / "flow_stat_v1.txt")
+    (OUT / "pkt_stat_v2.txt").write_text(eval_show(body(src, "dp_show_pkt_stat"), defrag=True))
+    lines = []
+    for kind, (n, d) in (("flow", (vals["new_flow"], vals["del_flow"])), ("fcb", (FCB["new_fcb"], FCB["del_fcb"])),
+                         ("pcb", (0, 0))):
+        lines.append(f"new {kind} is: {n}\ndel {kind} is: {d}\n")
+    (OUT / "flow_stat_v2.txt").write_text("".join(lines))
+    print("wrote", OUT / "pkt_stat_v1.txt", OUT / "flow_stat_v1.txt", OUT / "pkt_stat_v2.txt",
+          OUT / "flow_stat_v2.txt")
 
 
 if __name__ == "__main__":

@@ -180,3 +180,38 @@ def test_small_cases_and_errors(eng):
         assert p.g.lib.ppe_defrag(p.g.h, b, oo, None) == -22
     finally:
         p.close()
+
+
+def test_show_text_after_reassembly(eng):
+    """`show packet statistic` / `show flow statistic` after defrag batches: the ip_frag_stat
+    lines, new / del fcb and (monitor on) teardrop formatted from the GPU table's ppe_defrag_info equal the text
+    formatted from the oracle's sequential Defrag counters for the same stream."""
+    import ctypes as C
+    a, o, l = synth.make_fragment_stream(3000, seed=21)
+    p = DfPair(eng, fcb_max=1 << 12)
+    try:
+        for k, b in enumerate(range(0, len(l), 4096)):
+            p.batch(a, o[b:b + 4096], l[b:b + 4096], NOW + k)
+        p.age(NOW + 10**6)
+        gi = abi.DefragInfo()
+        assert eng.lib.ppe_defrag_info(p.g.h, C.byref(gi)) == 0
+        os_ = p.o.stats()
+        oi = abi.DefragInfo()
+        for k, name in enumerate(abi.DF_NAME[i] for i in range(9)):
+            oi.st[k] = os_["st_" + name.lower()]
+        oi.teardrop, oi.new_fcb, oi.del_fcb = os_["teardrop"], os_["new_fcb"], os_["del_fcb"]
+        assert oi.st[abi.DF["REASM"]] > 0 and oi.new_fcb > 0
+        cnt = abi.Counters()
+        fi = abi.FlowInfo()
+        texts = []
+        for info in (gi, oi):
+            buf = C.create_string_buffer(8192)
+            eng.lib.ppe_format_pkt_stat_ex(C.byref(cnt), C.byref(info), 1, buf, 8192)
+            fbuf = C.create_string_buffer(512)
+            eng.lib.ppe_format_flow_stat_ex(C.byref(fi), C.byref(info), fbuf, 512)
+            texts.append((buf.value.decode(), fbuf.value.decode()))
+        assert texts[0] == texts[1]
+        assert f"reasm_ok: {oi.st[abi.DF['REASM']]}\n" in texts[0][0]
+        assert f"new fcb is: {oi.new_fcb}\n" in texts[0][1]
+    finally:
+        p.close()

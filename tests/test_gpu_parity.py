@@ -371,6 +371,33 @@ def test_live_commit_between_queued_batches(eng):
         assert np.array_equal(o["acl_hit"].cpu().numpy(), ref["acl_hit"])
 
 
+def test_commit_does_not_wait_for_unrelated_streams(eng):
+    """A rule commit waits only for the launches that read the image slot it rewrites (events behind them), never
+    for the whole device: a long kernel on another stream is still running when two commits (the second one
+    rewrites the slot the first batch read) have returned (upload_image called hipDeviceSynchronize)."""
+    rules = synth.make_rules(256, seed=98)
+    pk = synth.make_packets(100_000, rules, seed=99, stride=64)
+    th = torch.from_numpy(pk["hdr"]).to(DEV)
+    tl = torch.from_numpy(pk["len"].view(np.int32)).to(DEV)
+    work, other = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+    eng.commit(rules, default_action=1)
+    o = {k: torch.empty(len(pk["len"]), dtype=torch.int32, device=DEV) for k in ("verdict", "acl_hit")}
+    with torch.cuda.stream(work):
+        eng.classify_torch(th, tl, o, cfg=eng.cfg(now_seconds=NOW))
+    work.synchronize()
+    with torch.cuda.stream(other):
+        torch.cuda._sleep(4_000_000_000)  # seconds of spinning on `other`
+        done = torch.cuda.Event()
+        done.record(other)
+    eng.commit(synth.make_rules(256, seed=100), default_action=0)
+    eng.commit(rules, default_action=1)  # rewrites the slot the batch above read
+    assert not done.query(), "the commit waited for an unrelated stream"
+    torch.cuda.synchronize()
+    ref = pyoracle.Oracle(rules, default_action=1).classify_batch(pk["hdr"], pk["len"], cfg=pyoracle.Oracle(
+        rules, default_action=1).cfg(0, 1, NOW), nthreads=16)
+    assert np.array_equal(o["verdict"].cpu().numpy().view(np.uint32), ref["verdict"])
+
+
 def test_full_size_properties_c1(eng):
     """1M packets (the C1 bench batch): counters sum to n, every packet is in exactly one compaction class,
     the two halves classified separately equal the whole, and the flow hash is direction-symmetric."""
@@ -405,7 +432,7 @@ def test_full_size_properties_c1(eng):
         assert np.array_equal(whole[k][idx], ref[k]), k
 
 
-@pytest.mark.parametrize("per_launch", ["8", "2", "1"])
+@pytest.mark.parametrize("per_launch", ["0", "8", "2", "1"])
 def test_classify_batches_pipelined(monkeypatch, per_launch):
     """ppe_classify_batches: several batches (ragged sizes, an empty one, both window strides) grouped per launch
     (every wave walks its tiles of each batch in turn) and pipelined over two streams, stream-ordered on the caller's
@@ -460,3 +487,96 @@ def _classify_batches_case(eng):
     assert cnt["pkts"] == total
     # stream order: work queued on the caller's stream after the call sees every batch's outputs
     assert eng.lib.ppe_classify_batches(eng.ctx, ins, outs, 0, C.byref(cfg), C.c_void_p(s.cuda_stream)) == 0
+
+
+# ---------------------------------------------------------------- edges the reference's buffers have
+@pytest.mark.parametrize("stride", [64, 128])
+def test_nonzero_bytes_past_len(eng, stride):
+    """A NIC buffer behind a short frame is not zero: every window byte past the wire length is random and non-zero
+    (every malformed kind, IMIX).  The reference never reads past len before a length check fails (decode-*.c check
+    order), so the verdict, hash, hit and tuple must not depend on those bytes: bit-exact against the oracle, which
+    reads only min(len, stride) bytes."""
+    rules = synth.make_rules(512, seed=70, any_ip_frac=0.3)
+    pk = synth.make_packets(80_000, rules, seed=71 + stride, kind="imix", stride=stride, malformed_frac=0.6)
+    hdr = pk["hdr"].copy()
+    lens = pk["len"]
+    rng = np.random.default_rng(72)
+    junk = rng.integers(1, 256, size=hdr.shape, dtype=np.uint8)
+    past = np.arange(stride)[None, :] >= np.minimum(lens & 0xFFFF, stride)[:, None]
+    assert past.any(axis=1).mean() > 0.05  # plenty of short frames
+    hdr[past] = junk[past]
+    eng.commit(rules, default_action=1)
+    res = gpu_classify(eng, hdr, lens)
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(hdr, lens, cfg=o.cfg(0, 1, NOW), nthreads=16)
+    far = ref["reach"] > stride
+    ok = ~far
+    for k in ("verdict", "flow_hash", "acl_hit"):
+        assert np.array_equal(res[k][ok], ref[k][ok]), k
+    assert np.array_equal(res["tuple"][ok], ref["tuple"][ok])
+    assert ((res["verdict"][far] & 0xFF) == ST["WINDOW_PUNT"]).all()
+    # and the same packets with zeroed tails classify identically (the tail bytes change nothing)
+    z = pk["hdr"].copy()
+    z[past] = 0
+    res0 = gpu_classify(eng, z, lens)
+    for k in ("verdict", "flow_hash", "acl_hit", "tuple"):
+        assert np.array_equal(res0[k], res[k]), k
+
+
+def test_ring_launch_many_batches(eng):
+    """More batches than the kernel arguments hold (device descriptor ring, one persistent launch, batch groups of
+    waves): 40 ragged batches (empty, 1, 63, 64, 65, ... 150k packets, both strides) bit-exact against the oracle;
+    the same call again (descriptor slot reused as is), then a different subset (slot rewritten), and the counters
+    equal the packets submitted."""
+    rules = synth.make_rules(300, seed=95)
+    eng.commit(rules, default_action=1)
+    eng.tuning(batches_per_launch=0)
+    o = pyoracle.Oracle(rules, default_action=1)
+    rng = np.random.default_rng(96)
+    sizes = [0, 1, 63, 64, 65, 127, 129, 150_000] + [int(x) for x in rng.integers(1, 40_000, 32)]
+    keep = []
+    for j, n in enumerate(sizes):
+        stride = 64 if j % 3 else 128
+        m = max(n, 1)
+        pk = synth.make_packets(m, rules, seed=97 + j, kind="imix", stride=stride, malformed_frac=0.05)
+        th = torch.from_numpy(pk["hdr"].copy()).to(DEV)
+        tl = torch.from_numpy(pk["len"].view(np.int32).copy()).to(DEV)
+        out = {k: torch.full((m,), -7, dtype=torch.int32, device=DEV) for k in ("verdict", "flow_hash", "acl_hit", "part")}
+        b = abi.Batch(th.data_ptr(), tl.data_ptr(), None, n, stride)
+        r = abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(),
+                       out["part"].data_ptr(), out["part"].data_ptr(), None, None)
+        ref = o.classify_batch(pk["hdr"][:n], pk["len"][:n], cfg=o.cfg(0, 1, NOW), nthreads=8) if n else None
+        keep.append((b, r, th, tl, out, ref, n, stride))
+    s = torch.cuda.current_stream(DEV)
+    cfg = eng.cfg(now_seconds=NOW)
+
+    def call(sel):
+        for i in sel:
+            for v in keep[i][4].values():
+                v.fill_(-7)
+        ins = (abi.Batch * len(sel))(*(keep[i][0] for i in sel))
+        outs = (abi.Result * len(sel))(*(keep[i][1] for i in sel))
+        eng.clear_counters()
+        assert eng.lib.ppe_classify_batches(eng.ctx, ins, outs, len(sel), C.byref(cfg), C.c_void_p(s.cuda_stream)) == 0
+        torch.cuda.synchronize()
+        total = 0
+        for i in sel:
+            _, _, th, _, out, ref, n, stride = keep[i]
+            if not n:
+                assert (out["verdict"].cpu().numpy() == -7).all()
+                continue
+            got = {k: out[k].cpu().numpy() for k in out}
+            got = {k: (v if k == "acl_hit" else v.view(np.uint32)) for k, v in got.items()}
+            far = ref["reach"] > stride
+            for k in ("verdict", "flow_hash", "acl_hit"):
+                assert np.array_equal(got[k][~far], ref[k][~far]), (i, n, k)
+            assert ((got["verdict"][far] & 0xFF) == ST["WINDOW_PUNT"]).all()
+            check_partition({"verdict": got["verdict"], "part_idx": got["part"]}, n)
+            total += n
+        assert eng.counters()["pkts"] == total
+
+    everything = list(range(len(keep)))
+    call(everything)
+    call(everything)                      # identical descriptors: the slot is reused without an upload
+    call(everything[::-1][:25])           # another queue: a slot is rewritten
+    call(everything)

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20, help="packets per classify dispatch")
     ap.add_argument("--cal-n", type=int, default=1 << 20, help="packets per calibration-kernel dispatch")
     ap.add_argument("--cal-kernel", default="k_row<true>")
+    ap.add_argument("--read-per-pkt", type=float, default=68.0, help="algorithmic read bytes per packet (IMIX: "
+                    "min(len, 64) + 4 averaged)")
+    ap.add_argument("--config", default="C1")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     n = a.n
@@ -38,8 +41,8 @@ def main():
     cw = statistics.median(per_dispatch(a.cal_write, a.cal_kernel, "WRITE_SIZE"))
     cal_rd, cal_wr = a.cal_n * 68, a.cal_n * 16  # skeleton: 64-B window + 4-B length read, 4 x 4-B results written
     kr, kw = cal_rd / cf, cal_wr / cw  # bytes per counter unit for this access pattern
-    alg_rd, alg_wr = n * 68, n * 16  # partition-layout list: no tile counts
-    out = {"n_packets": n, "fetch_size_raw": f, "write_size_raw": w, "calib": {"fetch_raw": cf, "write_raw": cw,
+    alg_rd, alg_wr = n * a.read_per_pkt, n * 16  # written: 12-B verdict + 4-B partition-list entry
+    out = {"config": a.config, "n_packets": n, "read_per_pkt": a.read_per_pkt, "fetch_size_raw": f, "write_size_raw": w, "calib": {"fetch_raw": cf, "write_raw": cw,
            "bytes_per_fetch_unit": kr, "bytes_per_write_unit": kw, "kernel": a.cal_kernel},
            "read_bytes": f * kr, "write_bytes": w * kw, "traffic_bytes": f * kr + w * kw,
            "algorithmic_bytes": alg_rd + alg_wr,

@@ -36,8 +36,9 @@ def main():
     kv = {k: int(v) for k, v in (x.split("=") for x in a.tune.split(","))} if a.tune else {}
     eng.tuning(**{"batches_per_launch": 0, **kv})
     bufs = []
-    for b in range(a.nbufs):
-        pk = synth.make_packets(n, rules, seed=synth.SEED + 1 + 7919 * b, kind=c["kind"], stride=64)
+    gen = [synth.make_packets(n, rules, seed=synth.SEED + 1 + 7919 * g, kind=c["kind"], stride=64) for g in range(2)]
+    for b in range(a.nbufs):  # 2 generated batches, each buffer its own device allocation (as bench.py)
+        pk = gen[b % 2]
         hdr = torch.from_numpy(pk["hdr"]).to(dev)
         lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
         outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
@@ -51,7 +52,9 @@ def main():
     for _ in range(a.launches):
         assert eng.lib.ppe_classify_batches(eng.ctx, ins, outs, a.batches, C.byref(cfg), sp) == 0
     torch.cuda.synchronize()
-    print(f"{a.launches} ring launches x {a.batches} batches of {n} ({a.config}) {eng.launch_info()}")
+    rd = float(np.minimum(gen[0]["len"].astype(np.int64) & 0xFFFF, 64).mean() + 4.0)
+    print(f"{a.launches} ring launches x {a.batches} batches of {n} ({a.config}) {eng.launch_info()} "
+          f"algorithmic_read_per_pkt {rd:.3f}")
     eng.close()
 
 
