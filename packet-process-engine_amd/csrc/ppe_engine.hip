@@ -176,7 +176,7 @@ struct StagePlan {
 // the per-wave walk keys and counter bins, and the 1-KB rounding of the staged image
 uint32_t image_budget(uint32_t block) {
     const uint32_t per_wg = (160u * 1024u) / (2048u / block);
-    const uint32_t fixed = ppe_classify_fixed_lds((int)block) + 1024u;
+    const uint32_t fixed = ppe_classify_fixed_lds((int)block, kPfHoist) + 1024u;
     return per_wg > fixed ? per_wg - fixed : 0u;
 }
 
@@ -208,7 +208,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
     if (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && bytes > budget && !c->tune.block)) {
         p.pipe = kPfMulti;
         p.block = 1024u;
-        const uint32_t fixed = ppe_classify_fixed_lds(1024) + 1024u;
+        const uint32_t fixed = ppe_classify_fixed_lds(1024, kPfMulti) + 1024u;  // no key slots
         budget = 160u * 1024u - fixed;
     }
     const uint32_t off_resid = img[PPE_IMG_W_OFFRESID], off_rules = img[PPE_IMG_W_OFFRULES];
@@ -925,7 +925,7 @@ int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds
     if (grid) *grid = std::min(c->n_cu * blocks_per_cu(c, plan), c->max_grid);
     if (block) *block = plan.block;
     if (lds_bytes)
-        *lds_bytes = ppe_classify_fixed_lds((int)plan.block) + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u);
+        *lds_bytes = ppe_classify_fixed_lds((int)plan.block, plan.pipe) + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u);
     if (variant) *variant = (uint32_t)plan.mode | ((uint32_t)plan.pipe << 4);
     return PPE_OK;
 }

@@ -163,7 +163,7 @@ int ppe_launch_steer(int phase, const struct ppe_steer_kargs *a, uint32_t grid, 
 int ppe_launch_rows(const struct ppe_rows_kargs *a, uint32_t grid, void *stream);
 #define PPE_FLOW_BLOCK_WAVES 4u /* waves (tiles in flight) per flow-kernel workgroup */
 int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block);
-uint32_t ppe_classify_fixed_lds(int block);
+uint32_t ppe_classify_fixed_lds(int block, int pipe);  /* keys (not for the multi-tile pipe 3) + counter bins */
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
 #ifdef __cplusplus
 }

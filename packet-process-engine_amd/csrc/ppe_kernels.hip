@@ -68,8 +68,10 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // LDS geometry
 #define KEY_SLOTS 6u
 #define KEY_WAVE_BYTES (KEY_SLOTS * 256u)  // 1536
-template <int BLOCK> struct Lds {
-    static constexpr uint32_t KEYB = (BLOCK / 64) * KEY_WAVE_BYTES;
+// KEYS = false: the multi-tile kernel (PF_MULTI) walks with the keys in registers and has no key slots, so its
+// image starts right after the counter bins (24 KB more image per CU at 1024 threads)
+template <int BLOCK, bool KEYS = true> struct Lds {
+    static constexpr uint32_t KEYB = KEYS ? (BLOCK / 64) * KEY_WAVE_BYTES : 0u;
     static constexpr uint32_t BINS = KEYB;                   // 256 u32 bins, then 32 u32 counters
     static constexpr uint32_t IMGB = KEYB + PPE_LDS_FIXED;   // 16-B aligned (1152 = 72 × 16)
 };
@@ -748,7 +750,7 @@ __global__ __launch_bounds__(BLOCK, (PF == PF_MULTI && !FLOW) ? PPE_MT_WAVES : P
 void ppe_classify_kernel(ppe_kargs a) {
     constexpr int MT = (PF == PF_MULTI && !FLOW) ? PPE_MT : 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    using L = Lds<BLOCK>;
+    using L = Lds<BLOCK, MT == 1>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
     uint32_t *lcnt = bins + PPE_NBINS;       // [32] per-reason counters of this workgroup
     const uint32_t tid = threadIdx.x;
@@ -802,7 +804,7 @@ void ppe_classify_kernel(ppe_kargs a) {
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
     const uint32_t lanebase = wv * KEY_WAVE_BYTES + 4u * lane;  // this lane's key slot 0 (LDS byte address)
-    lds_st32(lanebase + 256u * PPE_NODE_LEAF, 0u);              // the leaves' zero key
+    if (MT == 1) lds_st32(lanebase + 256u * PPE_NODE_LEAF, 0u);  // the leaves' zero key
     if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img, smem + L::IMGB / 4u, a.lds_words, tid);
     __syncthreads();
     TRACE_AT(1);
@@ -1457,8 +1459,8 @@ static int occ_t(size_t shmem) {
                ? nb : -1;
 }
 
-static size_t classify_shmem(uint32_t lds_words, int mode, int block) {
-    const size_t base = (size_t)(block / 64) * KEY_WAVE_BYTES + PPE_LDS_FIXED;  // keys + counter bins
+static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block) {
+    const size_t base = ppe_classify_fixed_lds(block, pipe);  // keys (not PF_MULTI) + counter bins
     if (mode == IMG_GLOBAL) return base;
     return base + (((size_t)lds_words * 4u + 1023u) & ~(size_t)1023u);
 }
@@ -1484,7 +1486,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int block) {
 
 extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, int flow,
                                    void *stream, void *ev_start, void *ev_stop) {
-    const size_t shmem = classify_shmem(a->lds_words, mode, block);
+    const size_t shmem = classify_shmem(a->lds_words, mode, pipe, block);
     hipStream_t s = (hipStream_t)stream;
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     PPE_DISPATCH(launch_t, a, grid, shmem, s, e0, e1, flow);
@@ -1507,12 +1509,14 @@ extern "C" int ppe_launch_flow(int kind, const ppe_flow_kargs *a, uint32_t grid,
 
 // resident workgroups per CU for the kernel variant (the persistent grid is sized to exactly fill the chip)
 extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block) {
-    const size_t shmem = classify_shmem(lds_words, mode, block);
+    const size_t shmem = classify_shmem(lds_words, mode, pipe, block);
     PPE_DISPATCH(occ_t, shmem);
 }
 
 // LDS of a workgroup besides the staged image: the per-wave walk keys and the counter bins
-extern "C" uint32_t ppe_classify_fixed_lds(int block) { return (uint32_t)(block / 64) * KEY_WAVE_BYTES + PPE_LDS_FIXED; }
+extern "C" uint32_t ppe_classify_fixed_lds(int block, int pipe) {
+    return (pipe == PF_MULTI ? 0u : (uint32_t)(block / 64) * KEY_WAVE_BYTES) + PPE_LDS_FIXED;
+}
 
 extern "C" int ppe_launch_steer(int phase, const ppe_steer_kargs *a, uint32_t grid, void *stream) {
     const hipStream_t s = (hipStream_t)stream;
@@ -1528,7 +1532,7 @@ extern "C" int ppe_launch_rows(const ppe_rows_kargs *a, uint32_t grid, void *str
 }
 
 extern "C" int ppe_launch_acl_tuples(const ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream) {
-    const size_t keys = (size_t)ppe_classify_fixed_lds(PPE_BLOCK);
+    const size_t keys = (size_t)ppe_classify_fixed_lds(PPE_BLOCK, PF_NONE);
     if (lds_img) {
         const size_t shmem = keys + (((size_t)a->img_words * 4u + 1023u) & ~(size_t)1023u);
         hipLaunchKernelGGL(ppe_acl_tuple_kernel<IMG_LDS>, dim3(grid), dim3(PPE_BLOCK), shmem, (hipStream_t)stream, *a);
