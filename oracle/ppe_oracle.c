@@ -198,6 +198,47 @@ int32_t oracle_acl_tree(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dpo
     return -1;
 }
 
+/* Walk of the image's block section (format v5: 2-level blocks, what the GPU's multi-tile kernel walks), from the
+ * same jump bucket; the leaf reached must be the binary walk's (test_acl_build.py checks all three walks agree). */
+int32_t oracle_acl_blocks(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                          const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action) {
+    const uint32_t *im = g_img;
+    const uint32_t key[6] = {sip, dip, sport, dport, proto, 0u};
+    const uint32_t jw = im[PPE_IMG_W_JUMP];
+    uint32_t b = jw ? im[im[PPE_IMG_W_OFFBSEC] + (key[jw & 0xffu] >> ((jw >> 8) & 0xffu))] : 0u;
+    uint32_t x = 0;
+    for (int it = 0; it <= PPE_MAX_DEPTH + 1; it++) {
+        const uint32_t *w = im + im[PPE_IMG_W_OFFBLOCKS] + PPE_BLK_WORDS * b;
+        const int b0 = key[w[3] & 0xfu] > w[0];
+        const uint32_t k1 = (w[3] >> (b0 ? 8 : 4)) & 0xfu;
+        const int b1 = key[k1] > w[1 + b0];
+        x = w[4 + 2 * b0 + b1];
+        if (x & PPE_BLK_LEAF) break;
+        b = x;
+    }
+    x &= ~PPE_BLK_LEAF;
+    const uint32_t max_leaf = im[PPE_IMG_W_MAXLEAF];
+    const uint32_t *lf = im + im[PPE_IMG_W_OFFLEAF];
+    uint32_t first = 0, cnt = 1, one = x;
+    if (max_leaf <= 1) {
+        lf = &one;
+    } else {
+        first = x & 0x7fffffu;
+        cnt = (x >> 23) & 0xffu;
+        if (cnt == PPE_LEAF_CNT_ESC) cnt = lf[first++];
+    }
+    for (uint32_t j = 0; j < cnt; j++) {
+        const uint32_t slot = lf[first + j];
+        if (oracle_rule_match(im, slot, sip, dip, sport, dport, proto, dmac, smac, ts)) {
+            const uint32_t *r = im + im[PPE_IMG_W_OFFRULES] + 8u * slot;
+            if (action) *action = r[6] >> 16;
+            return (int32_t)(r[7] << 3) >> 3;
+        }
+    }
+    if (action) *action = im[PPE_IMG_W_DEFACT];
+    return -1;
+}
+
 /* ---- flow table: one core's flow_table[LOCAL_CPU_ID] (dataplane/src/flow/flow.c, flow.h) ----
  * FLOW_BUCKET_NUM chained buckets indexed by flow_hashfn & FLOW_BUCKET_MASK (flow.c:76-79, flow.h:87-88), items from
  * a fixed pool of `capacity` (the FPA flow-node pool, mem_pool.h:72), head insertion (FlowInsert, flow.c:69-72). */
@@ -258,7 +299,7 @@ static void flow_miss_drop(omb_t *m, uint32_t st, int c) {
 }
 
 /* ---- FlowHandlePacket, dataplane/src/flow/flow.c:271-310 with FlowGetFlowFromHash :181-245 ---- */
-static __thread int t_use_tree;  /* per shard: 1 = walk the image, 0 = linear first match */
+static __thread int t_use_tree;  /* per shard: 1 = walk the image's nodes, 2 = its blocks, 0 = linear first match */
 
 static void flow_handle_packet(omb_t *m) {
     oracle_result_t *r = m->r;
@@ -283,7 +324,9 @@ static void flow_handle_packet(omb_t *m) {
         /* PortScan_Detect disabled (portscan_able = 0) */
         uint32_t act;
         r->flags |= PPE_F_ACL;
-        r->acl_hit = t_use_tree ? oracle_acl_tree(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
+        r->acl_hit = t_use_tree == 2 ? oracle_acl_blocks(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac,
+                                                          m->smac, m->ts, &act)
+                   : t_use_tree ? oracle_acl_tree(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
                                                   m->ts, &act)
                                 : oracle_acl_linear(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
                                                     m->ts, &act);

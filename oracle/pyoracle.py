@@ -125,7 +125,7 @@ class Oracle:
             raise ValueError("use_tree needs set_image()")
         self.lib.oracle_classify_batch(hdr.ctypes.data, stride, lens.ctypes.data,
                                        ts.ctypes.data if ts is not None else None, n, C.byref(cfg or self.cfg()),
-                                       int(nthreads), 1 if use_tree else 0, out["verdict"].ctypes.data,
+                                       int(nthreads), int(use_tree), out["verdict"].ctypes.data,
                                        out["flow_hash"].ctypes.data, out["acl_hit"].ctypes.data,
                                        out["tuple"].ctypes.data, out["reach"].ctypes.data,
                                        out["counters"].ctypes.data)
@@ -162,7 +162,7 @@ class OracleFlow:
             ts = np.ascontiguousarray(ts, np.uint64)
         self.lib.oracle_flow_classify_batch(self.h, hdr.ctypes.data, stride, lens.ctypes.data,
                                             ts.ctypes.data if ts is not None else None, n,
-                                            C.byref(cfg or self.o.cfg()), 1 if use_tree else 0,
+                                            C.byref(cfg or self.o.cfg()), int(use_tree),
                                             out["verdict"].ctypes.data, out["flow_hash"].ctypes.data,
                                             out["acl_hit"].ctypes.data, out["tuple"].ctypes.data,
                                             out["counters"].ctypes.data)

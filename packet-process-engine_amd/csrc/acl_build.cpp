@@ -368,7 +368,53 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     bool any_resid = false;
     for (const Rule &r : R) any_resid |= r.resid != 0;
     const uint32_t off_resid = off_rules + 8u * (n_slots + 1u);
-    const uint32_t total = off_resid + (any_resid ? 8u * (n_slots + 1u) : 0u);
+    const uint32_t end_resid = off_resid + (any_resid ? 8u * (n_slots + 1u) : 0u);
+
+    // ---- 2-level blocks (block section, ppe_image.h): breadth-first over the forest's roots ----
+    auto is_leaf = [&](uint32_t x) { return nodes[x].dim == PPE_NODE_LEAF; };
+    auto c0 = [&](uint32_t x) { return is_leaf(x) ? x : nodes[x].left; };
+    auto c1 = [&](uint32_t x) { return is_leaf(x) ? x : nodes[x].left + 1u; };
+    auto thr = [&](uint32_t x) { return is_leaf(x) ? 0xffffffffu : nodes[x].thr; };  // leaf: pass-through
+    auto kslot = [&](uint32_t x) { return is_leaf(x) ? 0u : nodes[x].dim; };
+    auto leaf_exit = [&](uint32_t x) -> uint32_t {
+        const TNode &nd = nodes[x];
+        if (max_leaf > 1) return PPE_BLK_LEAF | nd.first | (std::min(nd.cnt, PPE_LEAF_CNT_ESC) << 23);
+        return PPE_BLK_LEAF | (nd.cnt ? leaf[nd.first] : n_slots);
+    };
+    if (max_leaf > 1 && lwords.size() >= (1u << 23)) return PPE_ENOMEM;  // leaf exits hold 23-bit list offsets
+    std::vector<uint32_t> bwords, bnode, bdepth;
+    auto add_block = [&](uint32_t x, uint32_t d) {
+        bnode.push_back(x);
+        bdepth.push_back(d);
+        bwords.resize(bwords.size() + PPE_BLK_WORDS, 0u);
+        return (uint32_t)bnode.size() - 1u;
+    };
+    for (uint32_t r = 0; r < best.n_roots; ++r) add_block(r, 1u);
+    uint32_t max_bdepth = 1;
+    for (size_t bi = 0; bi < bnode.size(); ++bi) {  // blocks appended while scanning: breadth-first order
+        const uint32_t x = bnode[bi], p1 = c0(x), p2 = c1(x);
+        uint32_t *o = &bwords[bi * PPE_BLK_WORDS];
+        o[0] = thr(x);
+        o[1] = thr(p1);
+        o[2] = thr(p2);
+        o[3] = kslot(x) | (kslot(p1) << 4) | (kslot(p2) << 8);
+        const uint32_t ex[4] = {c0(p1), c1(p1), c0(p2), c1(p2)};
+        for (int e = 0; e < 4; ++e) {  // (add_block may reallocate bwords: index, not the pointer above)
+            uint32_t v;
+            if (is_leaf(ex[e])) {
+                v = leaf_exit(ex[e]);
+            } else {
+                v = add_block(ex[e], bdepth[bi] + 1u);
+                max_bdepth = std::max(max_bdepth, bdepth[bi] + 1u);
+            }
+            bwords[bi * PPE_BLK_WORDS + 4 + e] = v;
+        }
+    }
+    const uint32_t n_blocks = (uint32_t)bnode.size();
+    if (n_blocks >= PPE_BLK_LEAF) return PPE_ENOMEM;
+    const uint32_t off_bsec = (end_resid + 7u) & ~7u;
+    const uint32_t off_blocks = (off_bsec + n_jump + 7u) & ~7u;
+    const uint32_t total = off_blocks + PPE_BLK_WORDS * n_blocks;
 
     uint32_t *img = (uint32_t *)std::calloc(total, sizeof(uint32_t));
     if (!img) return PPE_ENOMEM;
@@ -387,6 +433,10 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     img[PPE_IMG_W_TOTAL] = total;
     img[PPE_IMG_W_ROOTKS] = nodes[0].dim << 8;
     img[PPE_IMG_W_JUMP] = jbest.bits ? (jbest.dim | (jbest.shift << 8) | (jbest.bits << 16)) : 0u;
+    img[PPE_IMG_W_OFFBSEC] = off_bsec;
+    img[PPE_IMG_W_NBLOCKS] = n_blocks;
+    img[PPE_IMG_W_OFFBLOCKS] = off_blocks;
+    img[PPE_IMG_W_MAXBDEPTH] = max_bdepth;
     auto node_byte = [&](uint32_t k) { return 4u * off_nodes + 16u * k; };
     for (uint32_t k = 0; k < n_nodes; ++k) {
         const TNode &nd = nodes[k];
@@ -406,12 +456,15 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
             o[3] = (nodes[nd.left].dim << 8) | (nodes[nd.left + 1].dim << 24);
         }
     }
-    if (n_jump) {  // bucket → its subtree root: node byte offset | the root's key slot << 24
+    if (n_jump) {  // bucket → its subtree root: node byte offset | the root's key slot << 24; root block index
         uint32_t b = 0;
         for (uint32_t r = 0; r < best.n_roots; ++r)
-            for (uint32_t i = 0; i < best.runs[r]; ++i, ++b)
+            for (uint32_t i = 0; i < best.runs[r]; ++i, ++b) {
                 img[PPE_IMG_HDR_WORDS + b] = node_byte(r) | (nodes[r].dim << 24);
+                img[off_bsec + b] = r;  // root r's block is block r (the roots are the first blocks)
+            }
     }
+    std::memcpy(img + off_blocks, bwords.data(), bwords.size() * sizeof(uint32_t));
     if (!lwords.empty()) std::memcpy(img + off_leaf, lwords.data(), lwords.size() * sizeof(uint32_t));
     for (uint32_t s = 0; s <= n_slots; ++s) {
         uint32_t *o = img + off_rules + 8 * s;

@@ -169,7 +169,10 @@ struct StagePlan {
     int mode;            // 0 global, 1 whole image in LDS, 2 prefix in LDS
     int pipe;            // tile fetch (kPf*)
     uint32_t block;
-    uint32_t lds_words, lds_nodes;
+    uint32_t lds_words, lds_nodes;  // image words staged from word 0 (single-tile walks: binary nodes)
+    uint32_t stage_src, stage_words;  // what the kernel copies into LDS: image words [stage_src, + stage_words)
+    uint32_t lds_blocks;              // multi-tile walks: blocks [0, lds_blocks) in LDS
+    uint32_t bsec_lds, blk_lds;       // LDS byte offsets (from the image base in LDS) of the block section / block 0
 };
 
 // LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves): 160 KiB shared, minus
@@ -182,8 +185,31 @@ uint32_t image_budget(uint32_t block) {
 
 StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
     const int pf = c->tune.pipeline == 1 ? kPfNone : kPfHoist;
-    const uint32_t words = (uint32_t)img.size(), bytes = words * 4u;
-    StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0};
+    // the single-tile walk reads the binary nodes only: what it stages "whole" is the image before the block section
+    const uint32_t all_words = (uint32_t)img.size();
+    const uint32_t off_bsec = img[PPE_IMG_W_OFFBSEC], off_blocks = img[PPE_IMG_W_OFFBLOCKS];
+    const uint32_t n_blocks = img[PPE_IMG_W_NBLOCKS];
+    const uint32_t words = off_bsec, bytes = words * 4u;
+    StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0, 0, 0, 0, 0, 0};
+    // the multi-tile walk reads the 2-level blocks: whole image in LDS, else the block jump table and the first
+    // block levels (breadth-first), else global
+    auto mt_plan = [&](uint32_t budget) {
+        const uint32_t bjt = 4u * (off_blocks - off_bsec);
+        if (all_words * 4u <= budget) {
+            p.mode = 1;
+            p.lds_words = p.stage_words = all_words;
+            p.lds_blocks = n_blocks;
+            p.bsec_lds = 4u * off_bsec;
+            p.blk_lds = 4u * off_blocks;
+        } else if (budget >= bjt + 32u * 64u) {
+            p.mode = 2;
+            p.lds_blocks = std::min(n_blocks, (budget - bjt) / 32u);
+            p.stage_src = off_bsec;
+            p.stage_words = (off_blocks - off_bsec) + PPE_BLK_WORDS * p.lds_blocks;
+            p.bsec_lds = 0;
+            p.blk_lds = bjt;
+        }
+    };
     if (!c->tune.lds_image) {
         if (!c->tune.block) p.block = 256;
         if (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && !c->tune.block)) {  // PF_MULTI over the global image
@@ -210,6 +236,8 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
         p.block = 1024u;
         const uint32_t fixed = ppe_classify_fixed_lds(1024, kPfMulti) + 1024u;  // no key slots
         budget = 160u * 1024u - fixed;
+        mt_plan(budget);
+        return p;
     }
     const uint32_t off_resid = img[PPE_IMG_W_OFFRESID], off_rules = img[PPE_IMG_W_OFFRULES];
     const uint32_t n_nodes = img[PPE_IMG_W_NNODES], off_nodes = img[PPE_IMG_W_OFFNODES];
@@ -229,6 +257,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
         p.lds_nodes = std::min(n_nodes, (budget / 4u - off_nodes) / PPE_NODE_WORDS);
         p.lds_words = off_nodes + PPE_NODE_WORDS * p.lds_nodes;
     }
+    p.stage_words = p.lds_words;  // single-tile walks stage a prefix from word 0
     return p;
 }
 
@@ -238,11 +267,11 @@ uint32_t blocks_per_cu(ppe_ctx *c, const StagePlan &p) {
     const uint32_t cap = kMaxBlocksPerCU * 256u / p.block;
     if (c->tune.blocks_per_cu) return std::max(1u, std::min(c->tune.blocks_per_cu, cap));  // may exceed residency
     // the occupancy query costs microseconds of host time per call: cached per kernel variant and LDS size
-    const uint64_t key = (uint64_t)p.lds_words | ((uint64_t)p.mode << 32) | ((uint64_t)p.pipe << 40) |
+    const uint64_t key = (uint64_t)p.stage_words | ((uint64_t)p.mode << 32) | ((uint64_t)p.pipe << 40) |
                          ((uint64_t)p.block << 48);
     for (const auto &e : c->occ_cache)
         if (e.first == key) return e.second;
-    const int occ = ppe_classify_occupancy(p.lds_words, p.mode, p.pipe, (int)p.block);
+    const int occ = ppe_classify_occupancy(p.stage_words, p.mode, p.pipe, (int)p.block);
     const uint32_t r = occ > 0 ? std::min<uint32_t>((uint32_t)occ, cap) : 1u;
     c->occ_cache.emplace_back(key, r);
     return r;
@@ -385,6 +414,14 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     a.now = cfg ? cfg->now_seconds : 0u;
     a.default_action = c->h_img[r][PPE_IMG_W_DEFACT];
     a.lds_words = plan.lds_words;
+    a.stage_src = plan.stage_src;
+    a.stage_words = plan.stage_words;
+    a.lds_blocks = plan.lds_blocks;
+    a.bsec_lds = plan.bsec_lds;
+    a.blk_lds = plan.blk_lds;
+    a.off_bsec = c->h_img[r][PPE_IMG_W_OFFBSEC];
+    a.off_blocks = c->h_img[r][PPE_IMG_W_OFFBLOCKS];
+    a.max_bdepth = c->h_img[r][PPE_IMG_W_MAXBDEPTH];
     a.max_depth = c->h_img[r][PPE_IMG_W_MAXDEPTH];
     a.max_leaf = c->h_img[r][PPE_IMG_W_MAXLEAF];
     a.root_ks = c->h_img[r][PPE_IMG_W_ROOTKS];
@@ -741,7 +778,7 @@ int ppe_acl_lookup(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint32_t 
     if (!in->tuple) return fail(c, PPE_EINVAL, "tuple required");
     HIPCHK(c, hipSetDevice(c->device));
     const int r = c->running;
-    const uint32_t words = (uint32_t)c->h_img[r].size();
+    const uint32_t words = c->h_img[r][PPE_IMG_W_OFFBSEC];  // the binary walk's part of the image (no blocks)
     const bool lds = (size_t)words * 4u + 1024u <= PPE_LDS_IMG_MAX;
     ppe_tuple_kargs a;
     std::memset(&a, 0, sizeof a);
@@ -925,7 +962,8 @@ int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds
     if (grid) *grid = std::min(c->n_cu * blocks_per_cu(c, plan), c->max_grid);
     if (block) *block = plan.block;
     if (lds_bytes)
-        *lds_bytes = ppe_classify_fixed_lds((int)plan.block, plan.pipe) + (plan.mode ? ((plan.lds_words * 4u + 1023u) & ~1023u) : 0u);
+        *lds_bytes = ppe_classify_fixed_lds((int)plan.block, plan.pipe) +
+                     (plan.mode ? ((plan.stage_words * 4u + 1023u) & ~1023u) : 0u);
     if (variant) *variant = (uint32_t)plan.mode | ((uint32_t)plan.pipe << 4);
     return PPE_OK;
 }

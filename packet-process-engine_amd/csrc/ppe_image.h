@@ -1,5 +1,5 @@
 /*
- * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v4.
+ * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v5.
  *
  * The image is a HyperSplit-style binary decision tree over the five header dimensions, flattened in BFS order
  * (children of node k are numbered after k, so a walk strictly descends and always terminates), followed by the
@@ -14,7 +14,8 @@
  *  word 9   default_action    word 10 max_depth           word 11 total words     word 12 max leaf entries
  *  word 13  root key slot << 8 (the dimension the root splits on; PPE_NODE_LEAF when the root is a leaf)
  *  word 14  jump root: dim | shift << 8 | bits << 16, or 0 for a single tree rooted at node 0
- *  word 15  reserved
+ *  word 15  off_bsec: word offset of the block section (v5)   word 16  n_blocks   word 17  off_blocks (word offset,
+ *           32-B aligned)   word 18  max_bdepth: most blocks on a root-to-leaf path   words 19..31 reserved
  *
  *  jump table (format v4; present iff word 14 != 0): 2^bits words right after the header.  A walk starts at
  *      bucket b = key[dim] >> shift: word b = the byte offset of that bucket's subtree root | its key slot << 24.
@@ -47,13 +48,26 @@
  *      dmac bytes 0-3 (LE), dmac bytes 4-5, smac bytes 0-3, smac bytes 4-5,
  *      time_start lo, hi, time_end lo, hi
  *      resid bits: 1 = dmac must equal, 2 = smac must equal, 4 = time_start <= ts <= time_end
+ *
+ *  block section (v5, at off_bsec, after everything above): the same forest regrouped into 2-level BLOCKS, for the
+ *  multi-tile walk, which reads the tree from L2 for large rule sets: one 32-B read resolves two levels, so a walk
+ *  needs half the dependent memory round trips.
+ *      block jump table (present iff word 14 != 0): 2^bits words, bucket → its root block index
+ *      blocks (8 words, 32-B aligned, breadth-first by block depth: the LDS-staged prefix is whole block levels):
+ *        w0..w2  thresholds of the block's positions 0 (root), 1 (its left child), 2 (its right child)
+ *        w3      key slots: pos0 | pos1 << 4 | pos2 << 8
+ *        w4..w7  exits e = 2 b0 + b1 (b0: key(pos0) > w0, b1: key(pos 1 + b0) > w[1 + b0]):
+ *                PPE_BLK_LEAF | leaf payload (max_leaf <= 1: rule slot / sentinel; else first | count << 23), or the
+ *                index of the block rooted at that grandchild
+ *        A leaf at position 0..2 is a pass-through: threshold 0xffffffff (no key is greater) and both of its exits
+ *        carry the leaf, so every walk resolves exactly two levels per block.
  */
 #ifndef PPE_IMAGE_H
 #define PPE_IMAGE_H
 
 #define PPE_IMG_MAGIC   0x41455050u /* "PPEA" */
-#define PPE_IMG_VERSION 4u
-#define PPE_IMG_HDR_WORDS 16u
+#define PPE_IMG_VERSION 5u
+#define PPE_IMG_HDR_WORDS 32u
 
 #define PPE_IMG_W_NNODES   2
 #define PPE_IMG_W_NLEAF    3
@@ -68,6 +82,13 @@
 #define PPE_IMG_W_MAXLEAF  12
 #define PPE_IMG_W_ROOTKS   13
 #define PPE_IMG_W_JUMP     14
+#define PPE_IMG_W_OFFBSEC  15
+#define PPE_IMG_W_NBLOCKS  16
+#define PPE_IMG_W_OFFBLOCKS 17
+#define PPE_IMG_W_MAXBDEPTH 18
+
+#define PPE_BLK_WORDS 8u
+#define PPE_BLK_LEAF 0x80000000u  /* exit word: a leaf payload (else a block index) */
 
 #define PPE_NODE_WORDS 4u
 #define PPE_NODE_LEAF 5u          /* key slot of a leaf: the walk's zero key */

@@ -93,7 +93,12 @@ struct ppe_kargs {
     uint32_t syn_check;
     uint32_t default_action;
     uint64_t now;
-    uint32_t lds_words;       /* image words staged in LDS (IMG_LDS: all; IMG_SPLIT: header + top nodes [+ leaves]) */
+    uint32_t lds_words;       /* image words [0, lds_words) in LDS at its image base (single-tile walks; the leaf
+                                 lists / rule records of every walk are read from LDS when inside this prefix)   */
+    uint32_t stage_src, stage_words; /* the kernel stages image words [stage_src, + stage_words) at its LDS image base */
+    uint32_t lds_blocks;      /* multi-tile walks: 2-level blocks [0, lds_blocks) are in LDS                        */
+    uint32_t bsec_lds, blk_lds; /* LDS byte offsets (from the LDS image base) of the block section / of block 0     */
+    uint32_t off_bsec, off_blocks, max_bdepth; /* image header words 15, 17, 18                                  */
     uint32_t lds_iters;       /* IMG_SPLIT: walk levels (node reads) whose nodes are all in the staged BFS prefix      */
     uint32_t max_depth;       /* deepest leaf: the walk reads max_depth + 1 nodes                                     */
     uint32_t max_leaf;        /* longest leaf candidate list: uniform trip count of the leaf scan                     */

@@ -369,6 +369,10 @@ struct AclGeo {
     uint32_t default_action;
     uint32_t jump;        // jump root (image word PPE_IMG_W_JUMP): dim | shift << 8 | bits << 16, 0 = none
     uint32_t off_nodes;   // words (the jump table is [PPE_IMG_HDR_WORDS, off_nodes))
+    // multi-tile walks (2-level blocks, ppe_image.h block section)
+    uint32_t lds_blocks;  // blocks [0, lds_blocks) in LDS
+    uint32_t bsec_lds, blk_lds;  // LDS byte offsets from the staged image base: block jump table, block 0
+    uint32_t off_bsec, off_blocks, max_bdepth;
 };
 
 // One level of the walk, node and key both in flight: the node's child pointer carries the child's key slot, so
@@ -544,56 +548,66 @@ __device__ __forceinline__ void acl_leaf(const uint32_t *__restrict__ gimg, cons
     }
 }
 
-// Multi-tile walk (PF_MULTI, split / global images): the lanes of MT tiles walk in lockstep, so each level issues MT
-// independent node reads and one wave keeps MT walks in flight.  Keys come from registers (a 5-way select per level
-// instead of the LDS key slots); a lane stops reading at its leaf.
+// 5-way key select by key slot (multi-tile walks keep the keys in registers)
 __device__ __forceinline__ uint32_t key_sel(uint32_t d, const uint32_t (&k)[5]) {
     return d == 0u ? k[0] : d == 1u ? k[1] : d == 2u ? k[2] : d == 3u ? k[3] : d == 4u ? k[4] : 0u;
 }
 
+// Multi-tile walk over the image's 2-level blocks (PF_MULTI; ppe_image.h block section): the lanes of MT tiles walk
+// in lockstep, each step one 32-B block read per lane (LDS for the staged block levels, else L2 / HBM) resolving two
+// tree levels, so a deep walk through an L2-resident tree takes half the dependent round trips of a node walk.  Keys
+// come from registers; a lane stops reading at its leaf.  Returns, per tile, a node whose .z is the leaf payload in
+// the node format acl_leaf reads.
 template <int MODE, int IMGB, int MT>
-__device__ __forceinline__ void acl_walk_mt(const uint32_t *__restrict__ gimg, const AclGeo &g,
-                                            const uint32_t (&key)[MT][5], const bool (&need)[MT], uint4 (&nd)[MT]) {
-    uint32_t noff[MT], dim[MT];
+__device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ gimg, const AclGeo &g,
+                                                   const uint32_t (&key)[MT][5], const bool (&need)[MT],
+                                                   uint4 (&nd)[MT]) {
+    uint32_t blk[MT];
     bool done[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-        noff[t] = 4u * PPE_IMG_HDR_WORDS;
-        dim[t] = g.root_ks >> 8;
-        if (g.jump) {
+        blk[t] = 0u;  // single tree: root block 0
+        if (g.jump) {  // bucket → root block (the block jump table is staged with the blocks)
             const uint32_t kk = key_sel(g.jump & 0xffu, key[t]);
-            const uint32_t jo = 4u * PPE_IMG_HDR_WORDS + 4u * (kk >> ((g.jump >> 8) & 0xffu));
-            const uint32_t e = (MODE == IMG_LDS || (MODE == IMG_SPLIT && g.lds_words >= g.off_nodes))
-                                   ? lds_u32(IMGB + jo) : gld<uint32_t>(gimg, jo);
-            noff[t] = e & 0xffffffu;
-            dim[t] = e >> 24;
+            const uint32_t jo = 4u * (kk >> ((g.jump >> 8) & 0xffu));
+            blk[t] = MODE != IMG_GLOBAL ? lds_u32(IMGB + g.bsec_lds + jo) : gld<uint32_t>(gimg, 4u * g.off_bsec + jo);
         }
         done[t] = !need[t];
         nd[t] = make_uint4(PPE_LEAF_THR, 0u, 0u, 0u);
     }
-    const uint32_t n_lds = MODE == IMG_GLOBAL ? 0u : (MODE == IMG_LDS ? g.max_depth + 1u : g.lds_iters);
 #pragma unroll 1
-    for (uint32_t it = 0; it <= g.max_depth; ++it) {
-        uint4 x[MT];
-        if (it < n_lds) {
+    for (uint32_t it = 0; it < g.max_bdepth; ++it) {
+        uint4 lo[MT], hi[MT];
 #pragma unroll
-            for (int t = 0; t < MT; ++t) x[t] = lds_u128(IMGB + noff[t]);
-        } else {
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-                if (!done[t]) x[t] = gld<uint4>(gimg, noff[t]);
+        for (int t = 0; t < MT; ++t) {
+            if (!done[t]) {
+                if (MODE != IMG_GLOBAL && blk[t] < g.lds_blocks) {
+                    const uint32_t la = IMGB + g.blk_lds + 32u * blk[t];
+                    lo[t] = lds_u128(la);
+                    hi[t] = lds_u128(la + 16u);
+                } else {
+                    const uint32_t ga = 4u * g.off_blocks + 32u * blk[t];
+                    lo[t] = gld<uint4>(gimg, ga);
+                    hi[t] = gld<uint4>(gimg, ga + 16u);
+                }
+            }
         }
         bool pending = false;
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
             if (!done[t]) {
-                nd[t] = x[t];
-                if (x[t].x == PPE_LEAF_THR) {
+                // position 0 → b0; position 1 + b0 → b1; exit 2 b0 + b1 (a leaf position passes through: thr ~0)
+                const bool b0 = key_sel(lo[t].w & 15u, key[t]) > lo[t].x;
+                const uint32_t t1 = b0 ? lo[t].z : lo[t].y;
+                const uint32_t k1 = (lo[t].w >> (b0 ? 8u : 4u)) & 15u;
+                const bool b1 = key_sel(k1, key[t]) > t1;
+                const uint32_t x = b0 ? (b1 ? hi[t].w : hi[t].z) : (b1 ? hi[t].y : hi[t].x);
+                if (x & PPE_BLK_LEAF) {
                     done[t] = true;
+                    // leaf payload in node form: slot / sentinel, or first | count << 24 for leaf lists
+                    nd[t].z = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF) : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
                 } else {
-                    const bool gt = key_sel(dim[t], key[t]) > x[t].x;
-                    noff[t] = gt ? x[t].z : x[t].y;
-                    dim[t] = gt ? (x[t].w >> 24) : ((x[t].w >> 8) & 0xffu);
+                    blk[t] = x;
                     pending = true;
                 }
             }
@@ -733,7 +747,7 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
 // PF: when a tile's window is fetched
 #define PF_NONE 0   // at the top of its own iteration
 #define PF_HOIST 1  // as PF_NONE, but the first tile's loads are issued before the image staging
-#define PF_MULTI 3  // split / global images: each wave loads, decodes and walks PPE_MT tiles together (acl_walk_mt),
+#define PF_MULTI 3  // split / global images: each wave loads, decodes and walks PPE_MT tiles together (acl_walk_blocks_mt),
                     // 4 waves/SIMD with 128 VGPRs, one 1024-thread workgroup per CU and its whole LDS for the image
 #ifndef PPE_MT
 #define PPE_MT 4
@@ -805,11 +819,12 @@ void ppe_classify_kernel(ppe_kargs a) {
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
     const uint32_t lanebase = wv * KEY_WAVE_BYTES + 4u * lane;  // this lane's key slot 0 (LDS byte address)
     if (MT == 1) lds_st32(lanebase + 256u * PPE_NODE_LEAF, 0u);  // the leaves' zero key
-    if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img, smem + L::IMGB / 4u, a.lds_words, tid);
+    if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img + a.stage_src, smem + L::IMGB / 4u, a.stage_words, tid);
     __syncthreads();
     TRACE_AT(1);
     const AclGeo geo = {a.lds_iters, a.max_depth, a.max_leaf, a.root_ks, a.off_leaf, a.off_rules, a.off_resid,
-                        a.lds_words, a.default_action, a.jump, a.off_nodes};
+                        a.lds_words, a.default_action, a.jump, a.off_nodes, a.lds_blocks, a.bsec_lds, a.blk_lds,
+                        a.off_bsec, a.off_blocks, a.max_bdepth};
 
     const uint64_t act_table = make_act_table(a.unsup_fw);
     // this batch's creator count, summed by the resolve kernel (which runs after this one)
@@ -961,7 +976,7 @@ void ppe_classify_kernel(ppe_kargs a) {
                     key[t][4] = k[t].proto;
                 }
                 uint4 nd[MT];
-                acl_walk_mt<MODE, L::IMGB, MT>(a.img, geo, key, need, nd);
+                acl_walk_blocks_mt<MODE, L::IMGB, MT>(a.img, geo, key, need, nd);
 #pragma unroll
                 for (int t = 0; t < MT; ++t) {
                     const uint32_t tile = t0 + t;
@@ -1415,7 +1430,8 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
     const uint32_t depth = a.img[PPE_IMG_W_MAXDEPTH];
     const AclGeo geo = {0u, depth, a.img[PPE_IMG_W_MAXLEAF], a.img[PPE_IMG_W_ROOTKS], a.img[PPE_IMG_W_OFFLEAF],
                         a.img[PPE_IMG_W_OFFRULES], a.img[PPE_IMG_W_OFFRESID], MODE == IMG_LDS ? a.img_words : 0u,
-                        a.default_action, a.img[PPE_IMG_W_JUMP], a.img[PPE_IMG_W_OFFNODES]};
+                        a.default_action, a.img[PPE_IMG_W_JUMP], a.img[PPE_IMG_W_OFFNODES], 0u, 0u, 0u, 0u, 0u,
+                        0u};
     for (uint32_t i = blockIdx.x * PPE_BLOCK + tid; i < a.n; i += gridDim.x * PPE_BLOCK) {
         const uint4 t = ((const uint4 *)a.tuple)[i];
         uint4 m = make_uint4(0, 0, 0, 0);
@@ -1486,7 +1502,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block) 
 
 extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, int flow,
                                    void *stream, void *ev_start, void *ev_stop) {
-    const size_t shmem = classify_shmem(a->lds_words, mode, pipe, block);
+    const size_t shmem = classify_shmem(a->stage_words, mode, pipe, block);
     hipStream_t s = (hipStream_t)stream;
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     PPE_DISPATCH(launch_t, a, grid, shmem, s, e0, e1, flow);

@@ -16,8 +16,11 @@ def compare(rules, used, pk, default_action=1, binth=0, cfg=None):
     cfg = cfg or o.cfg(0, 1, NOW)
     lin = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4)
     tree = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4, use_tree=True)
+    # the image's 2-level block section (what the multi-tile kernel walks) must give the same answers
+    blocks = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4, use_tree=2)
     for k in ("verdict", "acl_hit", "flow_hash", "counters"):
         assert np.array_equal(lin[k], tree[k]), k
+        assert np.array_equal(lin[k], blocks[k]), k
     return img, st, lin
 
 
@@ -93,12 +96,13 @@ def test_large_ruleset_builds_bounded():
 
 
 def test_image_layout():
-    """Image format v4 (csrc/ppe_image.h): optional jump table after the header, 16-B nodes {threshold, left, right,
-    child key slots}, leaves as walk fixed points, the always-matching sentinel rule at slot n_rules."""
+    """Image format v5 (csrc/ppe_image.h): optional jump table after the 32-word header, 16-B nodes {threshold, left,
+    right, child key slots}, leaves as walk fixed points, the always-matching sentinel rule at slot n_rules, and the
+    2-level block section at the end."""
     for nrules in (64, 256):
         rules = synth.make_rules(nrules)
         img, st = abi.build_image(rules)
-        assert img[0] == 0x41455050 and img[1] == 4
+        assert img[0] == 0x41455050 and img[1] == 5
         assert img[2] == st["n_nodes"] and img[4] == nrules and img[11] == len(img)
         assert img[7] % 8 == 0  # rules 32-B aligned
         off = int(img[5])
@@ -106,10 +110,10 @@ def test_image_layout():
         nroots = 1
         if jw:  # jump root: 2^bits bucket entries -> subtree roots (the first nodes), with their key slots
             dim, shift, bits = jw & 0xFF, (jw >> 8) & 0xFF, (jw >> 16) & 0xFF
-            assert dim <= 4 and 1 <= bits <= 16 and off == 16 + (1 << bits)
+            assert dim <= 4 and 1 <= bits <= 16 and off == 32 + (1 << bits)
             width = 32 if dim <= 1 else (16 if dim <= 3 else 8)
             assert shift == width - bits
-            jt = img[16:off]
+            jt = img[32:off]
             roots = (jt & 0xFFFFFF).astype(np.int64)
             assert (np.diff(roots) >= 0).all() and roots[0] == 4 * off  # runs of buckets, in order
             nroots = len(np.unique(roots))
@@ -134,6 +138,17 @@ def test_image_layout():
         assert (ks_l <= 5).all() and (ks_r <= 5).all() and (img[13] >> 8) <= 5
         sent = img[img[7] + 8 * nrules: img[7] + 8 * (nrules + 1)]
         assert sent[1] == sent[3] == sent[5] == 0xFFFFFFFF and sent[7] == 0x1FFFFFFF
+        # block section: after the residual records, its jump table (root block = root node index), 32-B blocks;
+        # every non-leaf exit names a later block, every block but the roots is named exactly once
+        ob, nb, oblk = int(img[15]), int(img[16]), int(img[17])
+        assert ob >= int(img[8]) and ob % 8 == 0 and oblk % 8 == 0 and oblk + 8 * nb == len(img)
+        if jw:
+            assert np.array_equal(img[ob:ob + (1 << bits)].astype(np.int64), (roots - 4 * off) // 16)
+        blk = img[oblk:].reshape(nb, 8)
+        ex = blk[:, 4:].astype(np.int64)
+        inner_ex = ex[(ex & 0x80000000) == 0]
+        assert np.array_equal(np.sort(inner_ex), np.arange(nroots, nb))
+        assert ((ex & 0x7FFFFFFF)[(ex & 0x80000000) != 0] <= nrules).all()
 
 
 def test_long_leaf_list_escape():
