@@ -96,7 +96,8 @@ def parse(argv=None):
     ap.add_argument("--n", type=int, default=0, help="packets per GPU per step (default: the config's; strong: "
                                                       "8M / ranks)")
     ap.add_argument("--stride", type=int, default=64)
-    ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: >= 8 and > 600 MB)")
+    ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: >= 8, > 600 MB and >= "
+                                                          "the batches of one launch)")
     ap.add_argument("--batches-per-launch", type=int, default=0,
                     help="0: the K batches in one persistent launch (default); B: launches of B batches "
                          "alternating over two streams")
@@ -245,7 +246,9 @@ def measure_config(name, args, dev, world, rank, dist, primary):
     stride = args.stride
     rules = synth.make_rules(cfgd["rules"])
     per_buf = n * (stride + 4 + 16)
-    nbufs = args.nbufs or max(8, int(np.ceil(600e6 / per_buf)))
+    # distinct resident batches: more than twice the 256 MiB Infinity Cache, and at least as many as one launch takes
+    # (a launch's batch groups run concurrently, so a buffer repeated inside one launch would be re-read from cache)
+    nbufs = args.nbufs or max(8, int(np.ceil(600e6 / per_buf)), args.steps, max(args.warmup, 1))
     eng = Engine(dev.index)
     eng.tuning(batches_per_launch=args.batches_per_launch)
     acl = eng.commit(rules, default_action=1)

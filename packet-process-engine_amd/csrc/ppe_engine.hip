@@ -118,6 +118,10 @@ struct ppe_ctx {
     std::vector<ppe_bdesc> ring_tmp;   // descriptors of the launch being built
     ppe_tuning_t tune;
     std::vector<std::pair<uint64_t, uint32_t>> occ_cache;  // resident workgroups per CU by kernel variant
+    // batch groups of waves a launch may split into (PPE_GROUPS): more groups = more tiles per wave between batch
+    // setups, but more batches streamed at once (DRAM locality); C1, 20-32 batches per launch, per batch: 1 / 2 / 4
+    // / 8 / 32 groups 20.2 / 18.7 / 18.3 / 18.3 / 19.1 us (one run, tools/ab_bench.py)
+    uint32_t max_groups = 8;
     FlowTable *flow = nullptr;  // ppe_flow_create
     uint32_t *d_steer = nullptr;  // ppe_steer_partition: per-tile owner counts / offsets
     size_t steer_cap = 0;
@@ -422,6 +426,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     a.off_bsec = c->h_img[r][PPE_IMG_W_OFFBSEC];
     a.off_blocks = c->h_img[r][PPE_IMG_W_OFFBLOCKS];
     a.max_bdepth = c->h_img[r][PPE_IMG_W_MAXBDEPTH];
+    a.max_groups = c->max_groups;
     a.max_depth = c->h_img[r][PPE_IMG_W_MAXDEPTH];
     a.max_leaf = c->h_img[r][PPE_IMG_W_MAXLEAF];
     a.root_ks = c->h_img[r][PPE_IMG_W_ROOTKS];
@@ -513,6 +518,7 @@ int ppe_ctx_create(int device, ppe_ctx_t **out) {
         c->n_cu = (uint32_t)prop.multiProcessorCount;
     c->max_grid = c->n_cu * kMaxBlocksPerCU;
     c->tune = default_tuning();
+    c->max_groups = (uint32_t)std::max(1, env_int("PPE_GROUPS", 8));
     c->pipe_mode = env_int("PPE_PIPE_MODE", 1);
     const size_t cs_bytes = (size_t)kSlotSets * c->max_grid * PPE_CSLOT_WORDS * sizeof(unsigned long long);
     int rc = PPE_OK;

@@ -74,9 +74,9 @@ struct ppe_flow_kargs {
     struct ppe_flowdev dst;       /* rehash target */
 };
 
-/* batches per launch whose descriptors travel in the kernel arguments (8 × 96 B); a launch over more batches reads
+/* batches per launch whose descriptors travel in the kernel arguments (32 × 96 B); a launch over more batches reads
  * them from a device descriptor ring (ppe_kargs.ring) */
-#define PPE_MAX_BATCH 8
+#define PPE_MAX_BATCH 32
 /* most batches one ring launch takes */
 #define PPE_MAX_RING 4096
 
@@ -99,6 +99,7 @@ struct ppe_kargs {
     uint32_t lds_blocks;      /* multi-tile walks: 2-level blocks [0, lds_blocks) are in LDS                        */
     uint32_t bsec_lds, blk_lds; /* LDS byte offsets (from the LDS image base) of the block section / of block 0     */
     uint32_t off_bsec, off_blocks, max_bdepth; /* image header words 15, 17, 18                                  */
+    uint32_t max_groups;      /* most batch groups of waves (concurrently streamed batches)                          */
     uint32_t lds_iters;       /* IMG_SPLIT: walk levels (node reads) whose nodes are all in the staged BFS prefix      */
     uint32_t max_depth;       /* deepest leaf: the walk reads max_depth + 1 nodes                                     */
     uint32_t max_leaf;        /* longest leaf candidate list: uniform trip count of the leaf scan                     */

@@ -772,12 +772,13 @@ void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t nwaves = gridDim.x * (BLOCK / 64);
     const uint32_t twave = blockIdx.x * (BLOCK / 64) + wv;  // this wave's index in the grid (trace slot)
-    // Batch groups: the grid's waves split into G = min(waves, batches) equal groups; group g takes batches g,
-    // g + G, ..., and its Wb waves stride over each of them (wave wi of the group: tiles wi, wi + Wb, ...).  One batch
-    // (or few) → every wave on every batch as before; a long queue of batches → each wave walks many tiles of a batch
-    // before its per-batch setup (descriptor, pointer checks) comes round again (1M-packet batches over 8,192 waves:
-    // 64 tiles per batch setup instead of 2).  The remainder waves of the division idle.
-    const uint32_t ngroups = min(nwaves, a.nbatch);
+    // Batch groups: the grid's waves split into G = min(waves, batches, max_groups) equal groups; group g takes
+    // batches g, g + G, ..., and its Wb waves stride over each of them (wave wi of the group: tiles wi, wi + Wb, ...).
+    // One batch → every wave on it, as before; a queue of batches → each wave walks G times more tiles of a batch
+    // before its per-batch setup (descriptor, pointer checks, spilled scalars) comes round again (1M-packet batches
+    // over 8,192 waves: 16 tiles per setup at G = 8 instead of 2), while only G batches stream at once.  The
+    // remainder waves of the division idle.
+    const uint32_t ngroups = max(1u, min(min(nwaves, a.nbatch), a.max_groups));
     const uint32_t stride_waves = nwaves / ngroups;              // Wb
     const uint32_t grp = twave / stride_waves;
     const uint32_t wtile = twave - grp * stride_waves;            // wi

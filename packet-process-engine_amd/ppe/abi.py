@@ -208,10 +208,10 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
 
 def load_variant(path: str | os.PathLike) -> C.CDLL:
     """Load another build of the library side by side (RTLD_LOCAL), for in-process A/B timing."""
-    return _open(Path(path), C.RTLD_LOCAL)
+    return _open(Path(path), C.RTLD_LOCAL, strict=False)
 
 
-def _open(p: Path, mode) -> C.CDLL:
+def _open(p: Path, mode, strict: bool = True) -> C.CDLL:
     if not p.exists():
         raise OSError(f"{p} not found: build it with `make -C packet-process-engine_amd` (no CPU fallback exists)")
     lib = C.CDLL(str(p), mode=mode)
@@ -287,6 +287,8 @@ def _open(p: Path, mode) -> C.CDLL:
         "DP_Acl_Lookup_Burst": ([vp, u32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
+        if not strict and not hasattr(lib, name):  # an older build compared side by side: fewer entry points
+            continue
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res

@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--variant", action="append", required=True, help="name=libpath[:key=val,...]")
     ap.add_argument("--check", action="store_true", help="compare every variant's outputs with the first")
     args = ap.parse_args()
+    # every batch of one launch distinct: a launch's batch groups run concurrently (a repeated buffer would be
+    # re-read from the Infinity Cache)
+    args.nbufs = max(args.nbufs, args.steps)
     if args.binth:
         import os
         os.environ["PPE_BINTH"] = str(args.binth)
@@ -45,8 +48,10 @@ def main():
     rules = synth.make_rules(c["rules"])
     dev = torch.device("cuda:0")
     bufs = []
-    for b in range(args.nbufs):
-        pk = synth.make_packets(n, rules, seed=synth.SEED + 1 + 7919 * b, kind=c["kind"], stride=args.stride)
+    gen = [synth.make_packets(n, rules, seed=synth.SEED + 1 + 7919 * g, kind=c["kind"], stride=args.stride)
+           for g in range(2)]
+    for b in range(args.nbufs):  # 2 generated batches; every buffer its own device allocation
+        pk = gen[b % 2]
         hdr = torch.from_numpy(pk["hdr"]).to(dev)
         lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
         outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(5)] + \
@@ -66,6 +71,7 @@ def main():
             os.environ["PPE_PIPE_MODE"] = kvs.pop("pipemode")
         if "bpl" in kvs:  # ppe_classify_batches: batches per launch (PPE_BATCHES_PER_LAUNCH)
             os.environ["PPE_BATCHES_PER_LAUNCH"] = kvs.pop("bpl")
+        os.environ["PPE_GROUPS"] = kvs.pop("groups", "8")  # batch groups of waves (read at context creation)
         eng = Engine(0, lib=libs[path])
         # outs=sep (default): separate FW / DROP lists + tile counts; outs=part: one partition list, no tile counts
         mode = kvs.pop("outs", "sep")

@@ -23,7 +23,7 @@ def main():
     eng.commit(rules, default_action=1)
     pk = synth.make_packets(n, rules)
     bufs = []
-    for b in range(8):
+    for b in range(40):  # every batch of a launch distinct (batch groups run concurrently)
         hdr = torch.from_numpy(pk["hdr"]).to(dev)
         lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
         outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
@@ -33,10 +33,10 @@ def main():
     cfg = Engine.cfg(now_seconds=1_700_000_000)
     s = torch.cuda.current_stream(dev)
     sp = C.c_void_p(s.cuda_stream)
-    for K in (1, 2, 8, 32):
-        ins = (abi.Batch * K)(*(bufs[i % 8][0] for i in range(K)))
-        outs = (abi.Result * K)(*(bufs[i % 8][1] for i in range(K)))
-        for bpl in (0, 2):
+    for K in (1, 2, 8, 20, 32, 40):
+        ins = (abi.Batch * K)(*(bufs[i % 40][0] for i in range(K)))
+        outs = (abi.Result * K)(*(bufs[i % 40][1] for i in range(K)))
+        for bpl in (0,):
             eng.tuning(batches_per_launch=bpl)
             res = []
             for it in range(6):
@@ -58,8 +58,8 @@ def main():
                   f"host call {r[3]:7.1f} us  per batch ev {r[0] / K:7.2f} kern {r[1] / K:7.2f}")
     # the same calls without per-launch timing events
     for K in (32,):
-        ins = (abi.Batch * K)(*(bufs[i % 8][0] for i in range(K)))
-        outs = (abi.Result * K)(*(bufs[i % 8][1] for i in range(K)))
+        ins = (abi.Batch * K)(*(bufs[i % 40][0] for i in range(K)))
+        outs = (abi.Result * K)(*(bufs[i % 40][1] for i in range(K)))
         eng.tuning(batches_per_launch=0)
         for it in range(3):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

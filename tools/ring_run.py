@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--lib", default=None)
     ap.add_argument("--tune", default="")
     a = ap.parse_args()
+    a.nbufs = max(a.nbufs, a.batches)  # every batch of a launch distinct (its batch groups run concurrently)
     c = synth.CONFIGS[a.config]
     n = c["n"]
     rules = synth.make_rules(c["rules"])
