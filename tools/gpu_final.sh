@@ -1,0 +1,7 @@
+# round-end rehearsal on one box: the GPU test suite, smoke(), then the default bench line (what the driver runs)
+set -o pipefail
+O=gpurun_out/${1:-final}
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.txt 2>&1 && \
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1 && \
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err
