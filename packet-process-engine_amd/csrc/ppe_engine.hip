@@ -181,9 +181,9 @@ struct StagePlan {
 
 // LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves): 160 KiB shared, minus
 // the per-wave walk keys and counter bins, and the 1-KB rounding of the staged image
-uint32_t image_budget(uint32_t block) {
+uint32_t image_budget(uint32_t block, int mode) {
     const uint32_t per_wg = (160u * 1024u) / (2048u / block);
-    const uint32_t fixed = ppe_classify_fixed_lds((int)block, kPfHoist) + 1024u;
+    const uint32_t fixed = ppe_classify_fixed_lds((int)block, kPfHoist, mode) + 1024u;
     return per_wg > fixed ? per_wg - fixed : 0u;
 }
 
@@ -222,33 +222,46 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
         }
         return p;
     }
-    // the whole image in LDS: the smallest workgroup (most copies per CU) whose share holds it
+    // the whole image in LDS: the smallest workgroup (most copies per CU) whose share holds it.  A single-tile kernel
+    // that walks blocks (ppe_classify_st_blocks) needs the whole image, block section included; a node walk the
+    // part before it.
+    const bool stb = ppe_classify_st_blocks() != 0;
+    const uint32_t lds_bytes = stb ? all_words * 4u : bytes;
     if (!c->tune.block) {
         for (uint32_t b : {256u, 512u, 1024u}) {
-            if (bytes <= image_budget(b)) {
+            if (lds_bytes <= image_budget(b, 1)) {
                 p.block = b;
                 break;
             }
         }
     }
-    uint32_t budget = image_budget(p.block);
+    uint32_t budget = image_budget(p.block, 1);
     // PF_MULTI (tuning pipeline 3, and the default) for images that do not fit whole: 1024-thread workgroups, one
     // per CU, with the CU's whole LDS for the image prefix (C2 / C3 / C4 step 27.2 / 52.1 / 27.3 -> 23.6 / 42.8 /
     // 22.7 us)
-    if (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && bytes > budget && !c->tune.block)) {
+    if (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && lds_bytes > budget && !c->tune.block)) {
         p.pipe = kPfMulti;
         p.block = 1024u;
-        const uint32_t fixed = ppe_classify_fixed_lds(1024, kPfMulti) + 1024u;  // no key slots
+        const uint32_t fixed = ppe_classify_fixed_lds(1024, kPfMulti, 2) + 1024u;  // no key slots
         budget = 160u * 1024u - fixed;
         mt_plan(budget);
         return p;
     }
     const uint32_t off_resid = img[PPE_IMG_W_OFFRESID], off_rules = img[PPE_IMG_W_OFFRULES];
     const uint32_t n_nodes = img[PPE_IMG_W_NNODES], off_nodes = img[PPE_IMG_W_OFFNODES];
-    if (bytes <= budget) {
+    if (lds_bytes <= budget) {
         p.mode = 1;
-        p.lds_words = words;
-    } else if (off_resid * 4u <= budget) {  // nodes, leaf lists and rule records; residual records from global
+        p.lds_words = stb ? all_words : words;
+        if (stb) {
+            p.lds_blocks = n_blocks;
+            p.bsec_lds = 4u * off_bsec;
+            p.blk_lds = 4u * off_blocks;
+        }
+        p.stage_words = p.lds_words;
+        return p;
+    }
+    budget = image_budget(p.block, 2);  // node walks of a partly staged image keep their key slots
+    if (off_resid * 4u <= budget) {  // nodes, leaf lists and rule records; residual records from global
         p.mode = 2;
         p.lds_words = off_resid;
         p.lds_nodes = n_nodes;
@@ -968,7 +981,7 @@ int ppe_launch_info(ppe_ctx_t *c, uint32_t *grid, uint32_t *block, uint32_t *lds
     if (grid) *grid = std::min(c->n_cu * blocks_per_cu(c, plan), c->max_grid);
     if (block) *block = plan.block;
     if (lds_bytes)
-        *lds_bytes = ppe_classify_fixed_lds((int)plan.block, plan.pipe) +
+        *lds_bytes = ppe_classify_fixed_lds((int)plan.block, plan.pipe, plan.mode) +
                      (plan.mode ? ((plan.stage_words * 4u + 1023u) & ~1023u) : 0u);
     if (variant) *variant = (uint32_t)plan.mode | ((uint32_t)plan.pipe << 4);
     return PPE_OK;

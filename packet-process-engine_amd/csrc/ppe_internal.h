@@ -169,7 +169,8 @@ int ppe_launch_steer(int phase, const struct ppe_steer_kargs *a, uint32_t grid, 
 int ppe_launch_rows(const struct ppe_rows_kargs *a, uint32_t grid, void *stream);
 #define PPE_FLOW_BLOCK_WAVES 4u /* waves (tiles in flight) per flow-kernel workgroup */
 int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block);
-uint32_t ppe_classify_fixed_lds(int block, int pipe);  /* keys (not for the multi-tile pipe 3) + counter bins */
+uint32_t ppe_classify_fixed_lds(int block, int pipe, int mode);  /* key slots (node walks only) + counter bins */
+int ppe_classify_st_blocks(void);  /* 1: single-tile walks of a whole-LDS image use the block section */
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
 #ifdef __cplusplus
 }

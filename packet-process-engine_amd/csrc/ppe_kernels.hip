@@ -39,6 +39,10 @@
 //   [0] kernel entry  [1] image staged  [2 + 5i + k] tile iteration i < 4: k 0 loop top, 1 window in registers,
 //   2 decoded + hashed, 3 ACL done, 4 outputs + counters issued   [22] after the loop  [23] counters flushed
 //   [31] tiles processed
+#ifndef PPE_ST_BLOCKS  // 1: the single-tile kernel over a whole-LDS image walks the 2-level blocks, keys in registers
+                      // (C1 A/B: 19.1-19.7 vs 18.6-18.8 us per 1M for the node walk with LDS key slots: 0 kept)
+#define PPE_ST_BLOCKS 0
+#endif
 #ifndef PPE_TRACE
 #define PPE_TRACE 0
 #endif
@@ -764,7 +768,9 @@ __global__ __launch_bounds__(BLOCK, (PF == PF_MULTI && !FLOW) ? PPE_MT_WAVES : P
 void ppe_classify_kernel(ppe_kargs a) {
     constexpr int MT = (PF == PF_MULTI && !FLOW) ? PPE_MT : 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    using L = Lds<BLOCK, MT == 1>;
+    // single-tile walks over a whole-LDS image use its 2-level blocks with the keys in registers (no key slots)
+    constexpr bool STB = PPE_ST_BLOCKS && MT == 1 && MODE == IMG_LDS;
+    using L = Lds<BLOCK, MT == 1 && !STB>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
     uint32_t *lcnt = bins + PPE_NBINS;       // [32] per-reason counters of this workgroup
     const uint32_t tid = threadIdx.x;
@@ -819,7 +825,7 @@ void ppe_classify_kernel(ppe_kargs a) {
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
     const uint32_t lanebase = wv * KEY_WAVE_BYTES + 4u * lane;  // this lane's key slot 0 (LDS byte address)
-    if (MT == 1) lds_st32(lanebase + 256u * PPE_NODE_LEAF, 0u);  // the leaves' zero key
+    if (MT == 1 && !STB) lds_st32(lanebase + 256u * PPE_NODE_LEAF, 0u);  // the leaves' zero key
     if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img + a.stage_src, smem + L::IMGB / 4u, a.stage_words, tid);
     __syncthreads();
     TRACE_AT(1);
@@ -924,13 +930,22 @@ void ppe_classify_kernel(ppe_kargs a) {
         if (!(PPE_ABLATE & 1) && k.st == ST_ACL) {
             uint32_t rule_act;
             const MacFromWindow mac = {B.hdr, p, B.stride};
-            lds_st32(lanebase + 256u * PPE_DIM_SIP, k.sip);
-            lds_st32(lanebase + 256u * PPE_DIM_DIP, k.dip);
-            lds_st32(lanebase + 256u * PPE_DIM_SPORT, k.sport);
-            lds_st32(lanebase + 256u * PPE_DIM_DPORT, k.dport);
-            lds_st32(lanebase + 256u * PPE_DIM_PROTO, k.proto);
-            acl_lookup<MODE, L::IMGB>(a.img, geo, lanebase, k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts, p,
-                                      a.now, hit, rule_act);
+            if constexpr (STB) {
+                const uint32_t key[1][5] = {{k.sip, k.dip, k.sport, k.dport, k.proto}};
+                const bool need[1] = {true};
+                uint4 nd[1];
+                acl_walk_blocks_mt<MODE, L::IMGB, 1>(a.img, geo, key, need, nd);
+                acl_leaf<MODE, L::IMGB>(a.img, geo, nd[0], k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts, p,
+                                        a.now, hit, rule_act);
+            } else {
+                lds_st32(lanebase + 256u * PPE_DIM_SIP, k.sip);
+                lds_st32(lanebase + 256u * PPE_DIM_DIP, k.dip);
+                lds_st32(lanebase + 256u * PPE_DIM_SPORT, k.sport);
+                lds_st32(lanebase + 256u * PPE_DIM_DPORT, k.dport);
+                lds_st32(lanebase + 256u * PPE_DIM_PROTO, k.proto);
+                acl_lookup<MODE, L::IMGB>(a.img, geo, lanebase, k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts,
+                                          p, a.now, hit, rule_act);
+            }
             const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
             k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
             k.flags |= PPE_F_ACL;
@@ -1477,7 +1492,7 @@ static int occ_t(size_t shmem) {
 }
 
 static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block) {
-    const size_t base = ppe_classify_fixed_lds(block, pipe);  // keys (not PF_MULTI) + counter bins
+    const size_t base = ppe_classify_fixed_lds(block, pipe, mode);  // key slots (node walks) + counter bins
     if (mode == IMG_GLOBAL) return base;
     return base + (((size_t)lds_words * 4u + 1023u) & ~(size_t)1023u);
 }
@@ -1530,10 +1545,15 @@ extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, in
     PPE_DISPATCH(occ_t, shmem);
 }
 
-// LDS of a workgroup besides the staged image: the per-wave walk keys and the counter bins
-extern "C" uint32_t ppe_classify_fixed_lds(int block, int pipe) {
-    return (pipe == PF_MULTI ? 0u : (uint32_t)(block / 64) * KEY_WAVE_BYTES) + PPE_LDS_FIXED;
+// LDS of a workgroup besides the staged image: the per-wave key slots of node walks and the counter bins.  Block
+// walks (the multi-tile kernel; the single-tile kernel over a whole-LDS image) keep the keys in registers.
+extern "C" uint32_t ppe_classify_fixed_lds(int block, int pipe, int mode) {
+    const bool blocks = pipe == PF_MULTI || (PPE_ST_BLOCKS && mode == IMG_LDS);
+    return (blocks ? 0u : (uint32_t)(block / 64) * KEY_WAVE_BYTES) + PPE_LDS_FIXED;
 }
+
+// 1: the single-tile kernel walks the block section of a whole-LDS image (the engine stages the whole image)
+extern "C" int ppe_classify_st_blocks(void) { return PPE_ST_BLOCKS; }
 
 extern "C" int ppe_launch_steer(int phase, const ppe_steer_kargs *a, uint32_t grid, void *stream) {
     const hipStream_t s = (hipStream_t)stream;
@@ -1549,7 +1569,7 @@ extern "C" int ppe_launch_rows(const ppe_rows_kargs *a, uint32_t grid, void *str
 }
 
 extern "C" int ppe_launch_acl_tuples(const ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream) {
-    const size_t keys = (size_t)ppe_classify_fixed_lds(PPE_BLOCK, PF_NONE);
+    const size_t keys = (size_t)ppe_classify_fixed_lds(PPE_BLOCK, PF_NONE, IMG_GLOBAL);  // node walk: key slots
     if (lds_img) {
         const size_t shmem = keys + (((size_t)a->img_words * 4u + 1023u) & ~(size_t)1023u);
         hipLaunchKernelGGL(ppe_acl_tuple_kernel<IMG_LDS>, dim3(grid), dim3(PPE_BLOCK), shmem, (hipStream_t)stream, *a);
