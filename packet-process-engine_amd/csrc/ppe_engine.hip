@@ -364,6 +364,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     std::memset(&a, 0, sizeof a);
     uint32_t tiles = 0;
     uint64_t tiles_total = 0;
+    bool part = true;  // the throughput layout in every batch (ppe_kargs.part_layout)
     const bool use_ring = nb > PPE_MAX_BATCH;
     int rslot = 0;
     std::vector<ppe_bdesc> &rd = c->ring_tmp;
@@ -387,6 +388,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         d.tuple = out[i].tuple;
         d.idx_base = idx_base;
         d.pad = 0;
+        part = part && d.verdict && d.fhash && d.hit && d.fw_idx && d.fw_idx == d.drop_idx && !d.tile_cnt && !d.tuple;
         tiles = std::max(tiles, (in[i].n + 63u) / 64u);
         tiles_total += (uint64_t)((in[i].n + 63u) / 64u);
     }
@@ -418,6 +420,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         a.ring = c->d_ring[rslot];
     }
     a.nbatch = nb;
+    a.part_layout = (part && !fl && !env_int("PPE_NO_PART", 0)) ? 1u : 0u;
     a.max_tiles = tiles;
     // enough workgroups for every tile of every batch (the kernel splits its waves into batch groups), at most
     // the resident grid

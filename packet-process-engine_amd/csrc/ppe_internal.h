@@ -100,6 +100,8 @@ struct ppe_kargs {
     uint32_t bsec_lds, blk_lds; /* LDS byte offsets (from the LDS image base) of the block section / of block 0     */
     uint32_t off_bsec, off_blocks, max_bdepth; /* image header words 15, 17, 18                                  */
     uint32_t max_groups;      /* most batch groups of waves (concurrently streamed batches)                          */
+    uint32_t part_layout;     /* 1: every batch writes verdict + flow hash + ACL hit and one partition list (fw_idx ==
+                                 drop_idx), no tile counts, no tuple: the kernel variant with those checks compiled out */
     uint32_t lds_iters;       /* IMG_SPLIT: walk levels (node reads) whose nodes are all in the staged BFS prefix      */
     uint32_t max_depth;       /* deepest leaf: the walk reads max_depth + 1 nodes                                     */
     uint32_t max_leaf;        /* longest leaf candidate list: uniform trip count of the leaf scan                     */

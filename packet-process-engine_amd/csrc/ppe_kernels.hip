@@ -344,12 +344,15 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[13], uint32_t len32, c
     k.flags = ((l2_ok & is_vl & (vlen >= 4u)) ? PPE_F_VLAN : 0u) | (l4_ok ? PPE_F_L4 : 0u) |
               ((l4_ok & is_tcp) ? PPE_F_TCP : 0u) | ((l4_ok & is_tcp & syn) ? PPE_F_SYN : 0u) |
               ((ip_ok & frag) ? PPE_F_FRAG : 0u);
-    k.sip = ip_ok ? sip : 0u;
-    k.dip = ip_ok ? dip : 0u;
-    k.proto = ip_ok ? proto : 0u;
-    k.sport = l4_ok ? sport : 0u;
-    k.dport = l4_ok ? dport : 0u;
-    k.paylen = l4_ok ? (is_tcp ? l4len - thl : l4len - 8u) : 0u;
+    // zeroed by masks, not selects: the ROCm 7.2 compiler turned the select form into exec-masked blocks that left
+    // dport zeroed for NO_SYN packets in some builds (tools/variant_diff.py caught it; the product build was right)
+    const uint32_t ipm = ip_ok ? ~0u : 0u, l4m = l4_ok ? ~0u : 0u;
+    k.sip = sip & ipm;
+    k.dip = dip & ipm;
+    k.proto = proto & ipm;
+    k.sport = sport & l4m;
+    k.dport = dport & l4m;
+    k.paylen = (is_tcp ? l4len - thl : l4len - 8u) & l4m;
     return k;
 }
 
@@ -763,7 +766,10 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
 // FLOW: stateful flow-table mode (ppe_classify_flow, one batch): packets whose flow exists are accounted and
 // forwarded here; the rest are recorded for the claim / resolve / finalize kernels below, which complete their
 // tiles (verdict, compaction, counters).
-template <int MODE, int PF, int BLOCK, bool FLOW>
+// PART: every batch of the launch has the throughput layout (verdict, flow hash and ACL hit written, one partition
+// list, no tile counts, no tuple: ppe_kargs.part_layout), so the output checks are compile-time and the kernel holds
+// fewer scalars (C1 step -2..4 %, C4 -3.5 %: fewer SGPR spills to VGPR lanes)
+template <int MODE, int PF, int BLOCK, bool FLOW, bool PART = false>
 __global__ __launch_bounds__(BLOCK, (PF == PF_MULTI && !FLOW) ? PPE_MT_WAVES : PPE_WAVES_PER_EU)
 void ppe_classify_kernel(ppe_kargs a) {
     constexpr int MT = (PF == PF_MULTI && !FLOW) ? PPE_MT : 1;
@@ -857,10 +863,10 @@ void ppe_classify_kernel(ppe_kargs a) {
 
         const uint32_t po = 4u * p;  // byte offset of this packet's SoA output words
         if (valid) {
-            if (B.verdict) gst_nt<uint32_t>(B.verdict, po, st | (act << 8) | (k.flags << 16));
-            if (B.fhash) gst_nt<uint32_t>(B.fhash, po, fh);
-            if (B.hit) gst_nt<int32_t>(B.hit, po, hit);
-            if (B.tuple) {
+            if (PART || B.verdict) gst_nt<uint32_t>(B.verdict, po, st | (act << 8) | (k.flags << 16));
+            if (PART || B.fhash) gst_nt<uint32_t>(B.fhash, po, fh);
+            if (PART || B.hit) gst_nt<int32_t>(B.hit, po, hit);
+            if (!PART && B.tuple) {
                 uint4 t;
                 t.x = k.sip;
                 t.y = k.dip;
@@ -889,7 +895,9 @@ void ppe_classify_kernel(ppe_kargs a) {
             }
         }
         // ---- wave-ballot compaction of FW / DROP indices into this tile's 64-slot segment of each list ----
-        if (!(PPE_ABLATE & 4)) compact_tile(B.fw_idx, B.drop_idx, B.tile_cnt, B.n, B.idx_base, tile, lane, valid, act);
+        if (!(PPE_ABLATE & 4))
+            compact_tile(B.fw_idx, PART ? B.fw_idx : B.drop_idx, PART ? nullptr : B.tile_cnt, B.n, B.idx_base, tile, lane,
+                         valid, act);
 
         // ---- per-reason counters: one LDS add per packet into its (status, flags) bin ----
         if (!(PPE_ABLATE & 2) && valid) atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
@@ -1478,7 +1486,11 @@ static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t
         hipExtLaunchKernelGGL((ppe_classify_kernel<M, PF_HOIST, B, true>), dim3(grid), dim3(B), shmem, s, e0, e1, 0,
                               *a);
     } else {
-        hipExtLaunchKernelGGL((ppe_classify_kernel<M, P, B, false>), dim3(grid), dim3(B), shmem, s, e0, e1, 0, *a);
+        if (a->part_layout && P != PF_NONE)
+            hipExtLaunchKernelGGL((ppe_classify_kernel<M, (P == PF_NONE ? PF_HOIST : P), B, false, true>), dim3(grid),
+                                  dim3(B), shmem, s, e0, e1, 0, *a);
+        else
+            hipExtLaunchKernelGGL((ppe_classify_kernel<M, P, B, false>), dim3(grid), dim3(B), shmem, s, e0, e1, 0, *a);
     }
     return (int)hipGetLastError();
 }

@@ -580,3 +580,28 @@ def test_ring_launch_many_batches(eng):
     call(everything)                      # identical descriptors: the slot is reused without an upload
     call(everything[::-1][:25])           # another queue: a slot is rewritten
     call(everything)
+
+
+@pytest.mark.parametrize("nrules", [256, 4096, 65536])
+def test_partition_layout_kernel_variant(eng, monkeypatch, nrules):
+    """The throughput layout (verdict, flow hash, ACL hit, one partition list, no tile counts, no tuple) runs the
+    kernel variant with those output checks compiled out (ppe_kargs.part_layout).  It must equal the oracle and the
+    general kernel (PPE_NO_PART=1) bit for bit, on the LDS image (256 rules), the multi-tile kernel over a split image
+    (4096) and over an L2-resident one (64k), with malformed windows and TCP packets failing syn_check (whose hash a
+    miscompiled select once dropped the destination port from, in a variant build)."""
+    rules = synth.make_rules(nrules, seed=300 + nrules)
+    n = 65_536 if nrules < 65536 else 8_192
+    pk = synth.make_packets(n, rules, seed=301, kind="imix", stride=128, malformed_frac=0.1)
+    eng.commit(rules, default_action=1)
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    outs = ("verdict", "flow_hash", "acl_hit", "part_idx")
+    got = gpu_classify(eng, pk["hdr"], pk["len"], outs=outs)
+    assert_same(got, ref, keys=("verdict", "flow_hash", "acl_hit"))
+    check_partition(got, n)
+    monkeypatch.setenv("PPE_NO_PART", "1")
+    gen = gpu_classify(eng, pk["hdr"], pk["len"], outs=outs)
+    for k in ("verdict", "flow_hash", "acl_hit", "part_idx"):
+        assert np.array_equal(gen[k], got[k]), k
+    st = ref["verdict"] & 0xFF
+    assert (st == ST["FLOW_TCP_NO_SYN_FIRST"]).sum() > 10
