@@ -241,9 +241,13 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
     // 22.7 us)
     if (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && lds_bytes > budget && !c->tune.block)) {
         p.pipe = kPfMulti;
-        p.block = 1024u;
-        const uint32_t fixed = ppe_classify_fixed_lds(1024, kPfMulti, 2) + 1024u;  // no key slots
-        budget = 160u * 1024u - fixed;
+        // tuning knobs (A/B only): workgroup size and the LDS bytes each workgroup may take (default: all of it, one
+        // workgroup per CU); less LDS lets more workgroups share a CU
+        const int mb = env_int("PPE_MT_BLOCK", 1024);
+        p.block = (mb == 256 || mb == 512) ? (uint32_t)mb : 1024u;
+        const uint32_t fixed = ppe_classify_fixed_lds((int)p.block, kPfMulti, 2) + 1024u;  // no key slots
+        const uint32_t cap = (uint32_t)std::min(160 * 1024, std::max(8 * 1024, env_int("PPE_MT_LDS", 160 * 1024)));
+        budget = cap > fixed ? cap - fixed : 0u;
         mt_plan(budget);
         return p;
     }

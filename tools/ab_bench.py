@@ -7,6 +7,7 @@ rule 24).  Prints median / min kernel time and step time per variant.
       --variant b512=packet-process-engine_amd/libppe_hip.so:block=512
 """
 import argparse
+import os
 import ctypes as C
 import json
 import statistics
@@ -66,12 +67,15 @@ def main():
         if path not in libs:
             libs[path] = abi.load_variant(path)
         kvs = dict(x.split("=") for x in kv.split(",")) if kv else {}
+        # E_NAME=value: environment variable NAME set while this variant runs (knobs the engine reads per launch)
+        venv = {k[2:]: kvs.pop(k) for k in list(kvs) if k.startswith("E_")}
         import os
         if "pipemode" in kvs:  # ppe_classify_batches stream arrangement (PPE_PIPE_MODE, read at context creation)
             os.environ["PPE_PIPE_MODE"] = kvs.pop("pipemode")
         if "bpl" in kvs:  # ppe_classify_batches: batches per launch (PPE_BATCHES_PER_LAUNCH)
             os.environ["PPE_BATCHES_PER_LAUNCH"] = kvs.pop("bpl")
         os.environ["PPE_GROUPS"] = kvs.pop("groups", "8")  # batch groups of waves (read at context creation)
+        os.environ.update(venv)
         eng = Engine(0, lib=libs[path])
         # outs=sep (default): separate FW / DROP lists + tile counts; outs=part: one partition list, no tile counts
         mode = kvs.pop("outs", "sep")
@@ -98,12 +102,26 @@ def main():
             rr = abi.Result(*ptrs, None)
             calls.append((bb, rr))
         strs = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nstr - 1)]
-        variants.append(dict(name=name, eng=eng, calls=calls, kern=[], step=[], streams=strs, api=api))
+        variants.append(dict(name=name, eng=eng, calls=calls, kern=[], step=[], streams=strs, api=api, env=venv))
+        for k in venv:
+            os.environ.pop(k, None)
     cfg = Engine.cfg(now_seconds=NOW)
     stream = torch.cuda.current_stream(dev)
     sp = C.c_void_p(stream.cuda_stream)
 
     def run(v, steps, timed):
+        saved = {k: os.environ.get(k) for k in v["env"]}
+        os.environ.update(v["env"])
+        try:
+            run_(v, steps, timed)
+        finally:
+            for k, x in saved.items():
+                if x is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = x
+
+    def run_(v, steps, timed):
         fn, ctx = v["eng"].lib.ppe_classify, v["eng"].ctx
         if timed:  # kernel durations (dispatch timestamps), one stream
             v["eng"].timing(True)
