@@ -610,7 +610,8 @@ def run_flow(args, cfgd, dev, world, rank, dist):
                        "packets_per_gpu": n, "flows": flows, "rules": cfgd["rules"], "resident_batches": nbufs,
                        "parallelism": f"flow-sharded x{world}" + (" (all-to-all steering by flow hash)" if steer else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": round(traffic_per_packet(args.config) * n) if traffic_per_packet(args.config) else None,
                          "kernel": "ppe_classify_kernel<FLOW> (FlowFind + accounting; misses resolved by the flow "
                                    "kernels)",
                          "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": bpp,

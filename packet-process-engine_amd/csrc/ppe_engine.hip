@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1057,6 +1058,18 @@ static uint32_t flow_grid(const ppe_ctx *c, uint64_t items, uint32_t per_wg) {
 }
 
 // exact live / tombstone counts (synchronises)
+// Tighten the host's live / tombstone bounds from the latest snapshot the classify launches publish in pinned memory
+// (seqlock: the sequence word is written last and re-read here).
+static void flow_apply_snapshot(FlowTable &t) {
+    const volatile unsigned long long *sh = t.snap_h;
+    const uint64_t s0 = sh[0], live = sh[1], tombs = sh[2], s1 = sh[0];
+    if (s0 == s1 && s0 > t.snap_used && s0 <= t.batches && t.batches - s0 < FlowTable::kSnapRing) {
+        t.snap_used = s0;
+        t.live_ub = std::min<uint64_t>(live + (t.tot_n - t.cum_n[s0 % FlowTable::kSnapRing]), t.capacity);
+        t.tomb_ub = tombs + (t.tot_rev - t.cum_rev[s0 % FlowTable::kSnapRing]);
+    }
+}
+
 static int flow_sync_counts(ppe_ctx *c, unsigned long long *ctl_out) {
     FlowTable &t = *c->flow;
     HIPCHK(c, hipDeviceSynchronize());
@@ -1164,14 +1177,14 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     FlowTable &t = *c->flow;
     if (in->n > t.max_batch) return fail(c, PPE_EINVAL, "batch larger than the flow table's max_batch");
     HIPCHK(c, use_device(c));
-    {  // the latest snapshot (seqlock: the sequence word is written last and re-read here)
-        const volatile unsigned long long *sh = t.snap_h;
-        const uint64_t s0 = sh[0], live = sh[1], tombs = sh[2], s1 = sh[0];
-        if (s0 == s1 && s0 > t.snap_used && s0 <= t.batches && t.batches - s0 < FlowTable::kSnapRing) {
-            t.snap_used = s0;
-            t.live_ub = std::min<uint64_t>(live + (t.tot_n - t.cum_n[s0 % FlowTable::kSnapRing]), t.capacity);
-            t.tomb_ub = tombs + (t.tot_rev - t.cum_rev[s0 % FlowTable::kSnapRing]);
-        }
+    flow_apply_snapshot(t);
+    if (t.tomb_ub > t.nslots / 4u && t.snap_used + 1u < t.batches) {
+        // The tombstone bound counts every packet of every batch since the snapshot as a possible revocation, so with
+        // the host several batches ahead it passes the rehash threshold long before the table does.  Wait (bounded)
+        // for the latest submitted batch's classify launch to publish its snapshot — one batch stays in flight, the
+        // queue does not drain — and decide on that tighter bound before synchronising.
+        const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
+        while (t.snap_used + 1u < t.batches && std::chrono::steady_clock::now() < until) flow_apply_snapshot(t);
     }
     rc = flow_maybe_rehash(c);
     if (rc != PPE_OK) return rc;

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round evidence for the stateful rows (run on the GPU box from the repo root):
+#   bash tools/profile_stateful.sh <tag>     → gpurun_out/prof_<tag>/...
+# F1 (flow table): rocprofv3 --kernel-trace --stats of bench.py --config F1, FETCH_SIZE and WRITE_SIZE of the same
+# command in separate --pmc passes (tools/collect_traffic.py keeps the classify kernel's dispatches, calibrated on the
+# memory skeleton); D1 (reassembly): kernel stats.
+set -o pipefail
+T=${1:-r2}
+O=gpurun_out/prof_$T
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+if [ ! -f $O/cal_fetch/cal_counter_collection.csv ]; then
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/cal_fetch -o cal -- tools/calib/stream_calib 1048576 4 > $O/cal_fetch.log 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/cal_write -o cal -- tools/calib/stream_calib 1048576 4 > $O/cal_write.log 2>&1 || exit 1
+fi
+B="bench.py --config F1 --steps 16 --warmup 4 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_F1 -o k -- python3 $B > $O/kt_F1.log 2>&1 || exit 1
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch_F1 -o k -- python3 $B > $O/fetch_F1.log 2>&1 || exit 1
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write_F1 -o k -- python3 $B > $O/write_F1.log 2>&1 || exit 1
+python3 tools/collect_traffic.py --config F1 --fetch $O/fetch_F1/k_counter_collection.csv --write $O/write_F1/k_counter_collection.csv \
+  --cal-fetch $O/cal_fetch/cal_counter_collection.csv --cal-write $O/cal_write/cal_counter_collection.csv \
+  --n 1048576 --read-per-pkt 124.1 --out $O/${T}_traffic_F1.json > $O/traffic_F1.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_D1 -o k -- python3 bench.py --config D1 --no-cpu-baseline > $O/kt_D1.log 2>&1 || exit 1
+echo "stateful profiles done"
