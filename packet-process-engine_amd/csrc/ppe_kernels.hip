@@ -112,12 +112,44 @@ template <class T> __device__ __forceinline__ void gst(void *base, uint32_t off,
 #ifndef PPE_NT_STORE
 #define PPE_NT_STORE 1
 #endif
+// PPE_SC1_STORE (experiment): 4-B result stores as relaxed agent-scope atomic stores (global_store sc1: write-through,
+// the line leaves the XCD's L2 instead of displacing classifier-image lines)
+#ifndef PPE_SC1_STORE
+#define PPE_SC1_STORE 0
+#endif
 template <class T> __device__ __forceinline__ void gst_nt(void *base, uint32_t off, T v) {
     typedef typename GType<T>::type G;
-    if (PPE_NT_STORE)
+    if constexpr (PPE_SC1_STORE && sizeof(T) == 4) {
+        __hip_atomic_store((__attribute__((address_space(1))) uint32_t *)((char *)base + off),
+                           __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (PPE_NT_STORE)
         __builtin_nontemporal_store(__builtin_bit_cast(G, v), (__attribute__((address_space(1))) G *)((char *)base + off));
     else
         gst<T>(base, off, v);
+}
+// PPE_NT_WIN (experiment): the multi-tile kernel's window / length loads with the non-temporal (streaming) policy, so
+// the packet stream is evicted from L2 before the L2-resident half of the classifier image
+#ifndef PPE_NT_WIN
+#define PPE_NT_WIN 0
+#endif
+// PPE_PREFETCH (experiment): single-tile kernel over an LDS image requests tile t + 1's window before processing tile t
+#ifndef PPE_LAST_COND
+#define PPE_LAST_COND 0
+#endif
+#ifndef PPE_PREFETCH
+#define PPE_PREFETCH 0
+#endif
+// PPE_CMP_LDS (default on; C1 step -2 % in one A/B, profiles/r2b_experiments.md): the single-tile kernel's partition-list store is permuted through the wave's key slot 0
+// (free between walks) and leaves in lane order
+#ifndef PPE_CMP_LDS
+#define PPE_CMP_LDS 1
+#endif
+template <class T> __device__ __forceinline__ T gld_win(const void *base, uint32_t off) {
+    typedef typename GType<T>::type G;
+    if constexpr (PPE_NT_WIN != 0)
+        return __builtin_bit_cast(T, __builtin_nontemporal_load((const __attribute__((address_space(1))) G *)((const char *)base + off)));
+    else
+        return gld<T>(base, off);
 }
 
 __device__ __forceinline__ uint32_t be16_lo(uint32_t w) { return ((w & 0xffu) << 8) | ((w >> 8) & 0xffu); }
@@ -654,8 +686,11 @@ __device__ __forceinline__ uint64_t make_act_table(uint32_t unsup_fw) {
 
 // Wave-ballot compaction of a 64-packet tile's FW / DROP indices into the tile's 64-slot segment of each list (or
 // the partition layout when fw_idx == drop_idx), plus the tile count.  Every lane of the wave calls it.
+// scr: a wave-private 256-B LDS scratch (byte address) or ~0u.  With scratch, the partition layout's permuted store
+// goes through LDS (each lane writes its slot, then reads slot `lane`), so the global store is in lane order.
 __device__ __forceinline__ void compact_tile(uint32_t *fw_idx, uint32_t *drop_idx, uint32_t *tile_cnt, uint32_t n,
-                                             uint32_t idx_base, uint32_t tile, uint32_t lane, bool valid, uint32_t act) {
+                                             uint32_t idx_base, uint32_t tile, uint32_t lane, bool valid, uint32_t act,
+                                             uint32_t scr = ~0u) {
     const uint32_t p = (tile << 6) + lane;
     const bool is_fw = valid && act == PPE_ACT_FW;
     const bool is_drop = valid && act == PPE_ACT_DROP;
@@ -671,7 +706,13 @@ __device__ __forceinline__ void compact_tile(uint32_t *fw_idx, uint32_t *drop_id
         const uint32_t nv = min(n - (tile << 6), 64u);
         const uint32_t ndr = (uint32_t)__popcll(bdr), nfw = (uint32_t)__popcll(bfw);
         const uint32_t slot = is_fw ? pfw : (is_drop ? nv - ndr + pdr : nfw + lane - pfw - pdr);
-        if (valid) gst_nt<uint32_t>(fw_idx, (tile << 8) + 4u * slot, (p + idx_base) | (act << 30));
+        if (scr != ~0u) {  // (LDS ops of one wave complete in order: the read sees every lane's write)
+            if (valid) lds_st32(scr + 4u * slot, (p + idx_base) | (act << 30));
+            const uint32_t v = lds_u32(scr + 4u * lane);
+            if (lane < nv) gst_nt<uint32_t>(fw_idx, (tile << 8) + 4u * lane, v);
+        } else if (valid) {
+            gst_nt<uint32_t>(fw_idx, (tile << 8) + 4u * slot, (p + idx_base) | (act << 30));
+        }
     } else if (fw_idx && drop_idx) {  // both lists: one store instruction
         if (is_fw || is_drop) gst_nt<uint32_t>(is_fw ? fw_idx : drop_idx, so, p + idx_base);
     } else {
@@ -747,7 +788,10 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (!(PPE_ABLATE & 32)) f.last[s] = now;  // every packet of the batch stores the same batch time
+    // every packet of the batch carries the same batch time (PPE_LAST_COND, experiment: store only when it differs)
+    if (!(PPE_ABLATE & 32)) {
+        if (!PPE_LAST_COND || f.last[s] != now) f.last[s] = now;
+    }
     return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
 }
 
@@ -818,11 +862,19 @@ void ppe_classify_kernel(ppe_kargs a) {
     auto load_at = [&](const uint8_t *hdr, const uint32_t *lenp, uint32_t n, uint32_t stride, uint32_t t) {
         const uint32_t pc = min((t << 6) + lane, n - 1u);
         const uint32_t ro = pc * stride;
-        q0 = gld<uint4>(hdr, ro);
-        q1 = gld<uint4>(hdr, ro + 16u);
-        q2 = gld<uint4>(hdr, ro + 32u);
-        w12 = gld<uint32_t>(hdr, ro + 48u);
-        qlen = gld<uint32_t>(lenp, 4u * pc);
+        if constexpr (PPE_NT_WIN == 2) {  // experiment: single-tile kernel too
+            q0 = gld_win<uint4>(hdr, ro);
+            q1 = gld_win<uint4>(hdr, ro + 16u);
+            q2 = gld_win<uint4>(hdr, ro + 32u);
+            w12 = gld_win<uint32_t>(hdr, ro + 48u);
+            qlen = gld_win<uint32_t>(lenp, 4u * pc);
+        } else {
+            q0 = gld<uint4>(hdr, ro);
+            q1 = gld<uint4>(hdr, ro + 16u);
+            q2 = gld<uint4>(hdr, ro + 32u);
+            w12 = gld<uint32_t>(hdr, ro + 48u);
+            qlen = gld<uint32_t>(lenp, 4u * pc);
+        }
     };
     auto load_tile = [&](uint32_t t) { load_at(B.hdr, B.len, B.n, B.stride, t); };
     // first window in flight during the image staging
@@ -897,7 +949,7 @@ void ppe_classify_kernel(ppe_kargs a) {
         // ---- wave-ballot compaction of FW / DROP indices into this tile's 64-slot segment of each list ----
         if (!(PPE_ABLATE & 4))
             compact_tile(B.fw_idx, PART ? B.fw_idx : B.drop_idx, PART ? nullptr : B.tile_cnt, B.n, B.idx_base, tile, lane,
-                         valid, act);
+                         valid, act, (PPE_CMP_LDS && MT == 1 && !STB) ? lanebase - 4u * lane + 256u * PPE_DIM_SIP : ~0u);
 
         // ---- per-reason counters: one LDS add per packet into its (status, flags) bin ----
         if (!(PPE_ABLATE & 2) && valid) atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
@@ -973,11 +1025,11 @@ void ppe_classify_kernel(ppe_kargs a) {
                 for (int t = 0; t < MT; ++t) {
                     const uint32_t pc = min(((t0 + t) << 6) + lane, B.n - 1u);
                     const uint32_t ro = pc * B.stride;
-                    r0[t] = gld<uint4>(B.hdr, ro);
-                    r1[t] = gld<uint4>(B.hdr, ro + 16u);
-                    r2[t] = gld<uint4>(B.hdr, ro + 32u);
-                    r3[t] = gld<uint32_t>(B.hdr, ro + 48u);
-                    rl[t] = gld<uint32_t>(B.len, 4u * pc);
+                    r0[t] = gld_win<uint4>(B.hdr, ro);
+                    r1[t] = gld_win<uint4>(B.hdr, ro + 16u);
+                    r2[t] = gld_win<uint4>(B.hdr, ro + 32u);
+                    r3[t] = gld_win<uint32_t>(B.hdr, ro + 48u);
+                    rl[t] = gld_win<uint32_t>(B.len, 4u * pc);
                 }
                 Dec k[MT];
                 uint32_t fh[MT], key[MT][5];
@@ -1027,6 +1079,19 @@ void ppe_classify_kernel(ppe_kargs a) {
             if (PPE_TRACE && titer - PPE_TRACE_SKIP < 4u) TRACE_AT(2 + 5 * (titer - PPE_TRACE_SKIP));
             if (!have) load_tile(tile);
             have = false;
+            if constexpr (PPE_PREFETCH && MODE == IMG_LDS && !FLOW) {
+                // experiment: the next tile's window is requested before this tile is processed (one more window of
+                // registers; the LDS-image walk issues no global loads, so nothing waits on the prefetch)
+                const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
+                const uint32_t wl = qlen;
+                const uint32_t nt = tile + stride_waves;
+                if (nt < ntiles) {
+                    load_tile(nt);
+                    have = true;
+                }
+                process(tile, w, wl);
+                continue;
+            }
             if (PPE_TRACE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (PPE_TRACE && titer - PPE_TRACE_SKIP < 4u) TRACE_AT(3 + 5 * (titer - PPE_TRACE_SKIP));
             const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
