@@ -33,7 +33,7 @@ constexpr int kPipeStreams = 2;
 // before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering (next tile's window, or
 // only its first 16 B, requested before the current tile is processed) and an LDS-DMA next-tile pipeline were
 // measured slower and are not built.
-constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3;
+constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3, kPfSblk = 5;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 // ppe_classify_batches: batches per launch.  0 = every batch of the call in one persistent launch (descriptor ring in
 // device memory): the launch ramp and tail are paid once per call instead of once per batch
@@ -162,7 +162,7 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl == 1 || pl == 3 || pl == 4 ? (uint32_t)pl : 0u;
+    t.pipeline = pl == 1 || pl == 3 || pl == 4 || pl == 5 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     t.batches_per_launch = (uint32_t)std::max(0, std::min(env_int("PPE_BATCHES_PER_LAUNCH", (int)kBatchesPerLaunch),
                                                           PPE_MAX_RING));
@@ -188,7 +188,9 @@ uint32_t image_budget(uint32_t block, int mode) {
     return per_wg > fixed ? per_wg - fixed : 0u;
 }
 
-StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
+// single: the plan for the single-tile node-walk kernel only (the flow-table classify kernel is built for it: its
+// key slots and node prefix), never the multi-tile or block-walk plans
+StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool single = false) {
     const int pf = c->tune.pipeline == 1 ? kPfNone : kPfHoist;
     // the single-tile walk reads the binary nodes only: what it stages "whole" is the image before the block section
     const uint32_t all_words = (uint32_t)img.size();
@@ -217,7 +219,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
     };
     if (!c->tune.lds_image) {
         if (!c->tune.block) p.block = 256;
-        if (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && !c->tune.block)) {  // PF_MULTI over the global image
+        if (!single && (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && !c->tune.block))) {  // PF_MULTI, global image
             p.pipe = kPfMulti;
             p.block = 1024u;
         }
@@ -240,7 +242,16 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img) {
     // PF_MULTI (tuning pipeline 3, and the default) for images that do not fit whole: 1024-thread workgroups, one
     // per CU, with the CU's whole LDS for the image prefix (C2 / C3 / C4 step 27.2 / 52.1 / 27.3 -> 23.6 / 42.8 /
     // 22.7 us)
-    if (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && lds_bytes > budget && !c->tune.block)) {
+    // PF_SBLK (tuning pipeline 5): one tile per wave at 8 waves/SIMD, two 1024-thread workgroups per CU, each
+    // staging the block jump table and the block levels that fit half of the CU's LDS
+    if (!single && c->tune.pipeline == 5) {
+        p.pipe = kPfSblk;
+        p.block = 1024u;
+        const uint32_t fixed = ppe_classify_fixed_lds(1024, kPfSblk, 2) + 1024u;
+        mt_plan(80u * 1024u > fixed ? 80u * 1024u - fixed : 0u);
+        return p;
+    }
+    if (!single && (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && lds_bytes > budget && !c->tune.block))) {
         p.pipe = kPfMulti;
         // tuning knobs (A/B only): workgroup size and the LDS bytes each workgroup may take (default: all of it, one
         // workgroup per CU); less LDS lets more workgroups share a CU
@@ -363,7 +374,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
            uint32_t *grid_out = nullptr) {
     const int r = c->running;
     const uint32_t words = (uint32_t)c->h_img[r].size();
-    const StagePlan plan = stage_plan(c, c->h_img[r]);
+    const StagePlan plan = stage_plan(c, c->h_img[r], fl != nullptr);
     const uint32_t wpb = plan.block / 64u;
     ppe_kargs a;
     std::memset(&a, 0, sizeof a);
@@ -951,10 +962,11 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 3 && t->pipeline != 4)
+    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 3 && t->pipeline != 4 && t->pipeline != 5)
         return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top), 3 (images that do "
                                    "not fit in LDS: 4 tiles per wave walked together) or 4 (first tile's loads before "
-                                   "the image staging)");
+                                   "the image staging) or 5 (one tile per wave walking the image's blocks, for "
+                                   "split images)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     if (t->batches_per_launch > PPE_MAX_RING) return fail(c, PPE_EINVAL, "batches_per_launch must be <= 4096");
     c->tune = *t;

@@ -798,6 +798,9 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
 // PF: when a tile's window is fetched
 #define PF_NONE 0   // at the top of its own iteration
 #define PF_HOIST 1  // as PF_NONE, but the first tile's loads are issued before the image staging
+#define PF_SBLK 5   // split images whose block section fits a 1024-thread workgroup's half of the CU's LDS: one tile
+                    // per wave (8 waves/SIMD, two workgroups per CU), the 2-level block walk with the keys in registers
+                    // (staged block levels in LDS, the rest and the rule records from L2)
 #define PF_MULTI 3  // split / global images: each wave loads, decodes and walks PPE_MT tiles together (acl_walk_blocks_mt),
                     // 4 waves/SIMD with 128 VGPRs, one 1024-thread workgroup per CU and its whole LDS for the image
 #ifndef PPE_MT
@@ -819,7 +822,7 @@ void ppe_classify_kernel(ppe_kargs a) {
     constexpr int MT = (PF == PF_MULTI && !FLOW) ? PPE_MT : 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     // single-tile walks over a whole-LDS image use its 2-level blocks with the keys in registers (no key slots)
-    constexpr bool STB = PPE_ST_BLOCKS && MT == 1 && MODE == IMG_LDS;
+    constexpr bool STB = (PPE_ST_BLOCKS && MT == 1 && MODE == IMG_LDS) || PF == PF_SBLK;
     using L = Lds<BLOCK, MT == 1 && !STB>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
     uint32_t *lcnt = bins + PPE_NBINS;       // [32] per-reason counters of this workgroup
@@ -878,7 +881,7 @@ void ppe_classify_kernel(ppe_kargs a) {
     };
     auto load_tile = [&](uint32_t t) { load_at(B.hdr, B.len, B.n, B.stride, t); };
     // first window in flight during the image staging
-    bool have = PF == PF_HOIST && wave_live && wtile < ((B.n + 63u) >> 6);  // (PF_MULTI: at the loop top)
+    bool have = (PF == PF_HOIST || PF == PF_SBLK) && wave_live && wtile < ((B.n + 63u) >> 6);  // (PF_MULTI: at the loop top)
     if (have) load_tile(wtile);
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
@@ -1584,6 +1587,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block) 
     do {                                                             \
         if (pipe == PF_NONE) PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__); \
         if (pipe == PF_MULTI) PPE_DISPATCH_B(FN, M, PF_MULTI, __VA_ARGS__); \
+        if (pipe == PF_SBLK) return FN<M, PF_SBLK, 1024>(__VA_ARGS__);   \
         PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__);                \
     } while (0)
 #define PPE_DISPATCH(FN, ...)                                        \
@@ -1625,7 +1629,7 @@ extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, in
 // LDS of a workgroup besides the staged image: the per-wave key slots of node walks and the counter bins.  Block
 // walks (the multi-tile kernel; the single-tile kernel over a whole-LDS image) keep the keys in registers.
 extern "C" uint32_t ppe_classify_fixed_lds(int block, int pipe, int mode) {
-    const bool blocks = pipe == PF_MULTI || (PPE_ST_BLOCKS && mode == IMG_LDS);
+    const bool blocks = pipe == PF_MULTI || pipe == PF_SBLK || (PPE_ST_BLOCKS && mode == IMG_LDS);
     return (blocks ? 0u : (uint32_t)(block / 64) * KEY_WAVE_BYTES) + PPE_LDS_FIXED;
 }
 

@@ -105,6 +105,22 @@ def test_flow_batches_parity(eng, kind, stride):
         p.close()
 
 
+def test_flow_large_rule_set(eng):
+    """A 4,096-rule image does not fit a workgroup's LDS: the stateless classify runs a multi-tile plan, but the
+    flow-table classify kernel (node walk, per-lane key slots) must get its own single-tile plan (a prefix of the
+    node forest in LDS, the rest from L2).  Misses walk that image; the table is compared after every batch."""
+    rules = synth.make_rules(4096, seed=31)
+    p = Pair(eng, rules, capacity=100000, max_batch=1 << 16, default_action=0)
+    try:
+        for b in range(3):
+            pk = synth.make_flow_packets(30000, rules, n_flows=8000, seed=300 + b, template_seed=300, stride=64,
+                                         malformed_frac=0.01)
+            p.batch(pk["hdr"], pk["len"], NOW + b, part=(b == 1))
+            p.same_table()
+    finally:
+        p.close()
+
+
 def test_flow_pool_exhaustion(eng):
     """More new flows than the pool holds, within one batch and across batches: the creators past the free count
     (in packet order) fail with FLOW_NOMEM, exactly as one core running the batch in order."""

@@ -204,6 +204,14 @@ def test_c3_64k_rules_vs_oracle(eng):
     assert_same(res, ref)
     lin = o.classify_batch(pk["hdr"][:3000], pk["len"][:3000], cfg=o.cfg(0, 1, NOW), nthreads=16)
     assert np.array_equal(res["acl_hit"][:3000], lin["acl_hit"])
+    # the single-tile block walk (pipeline 5): fewer block levels in LDS, the rest from L2
+    old = eng.tuning()
+    try:
+        eng.tuning(pipeline=5)
+        assert eng.launch_info()["fetch"] == "sblk"
+        assert_same(gpu_classify(eng, pk["hdr"], pk["len"]), ref)
+    finally:
+        eng.tuning(**old)
 
 
 def test_residual_rules_with_timestamps(eng):
@@ -269,7 +277,7 @@ def test_argument_errors(eng):
     assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == 0
     t = abi.Tuning(block=300)
     assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
-    for pl in (2, 5):  # the register / LDS-DMA prefetch variants are not built
+    for pl in (2, 6):  # the register / LDS-DMA prefetch variants are not built
         t = abi.Tuning(pipeline=pl)
         assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
 
@@ -277,7 +285,7 @@ def test_argument_errors(eng):
 TUNINGS = [dict(lds_image=0), dict(block=512), dict(block=1024), dict(block=256), dict(pipeline=1),
            dict(pipeline=4), dict(pipeline=1, block=256), dict(pipeline=1, block=512), dict(pipeline=1, lds_image=0),
            dict(pipeline=4, lds_image=0), dict(pipeline=4, block=1024), dict(blocks_per_cu=16), dict(blocks_per_cu=1),
-           dict(pipeline=3), dict(pipeline=3, lds_image=0)]
+           dict(pipeline=3), dict(pipeline=3, lds_image=0), dict(pipeline=5), dict(pipeline=5, block=1024)]
 
 
 @pytest.mark.parametrize("tune", TUNINGS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))

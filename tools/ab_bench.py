@@ -36,10 +36,14 @@ def main():
     ap.add_argument("--binth", type=int, default=0)
     ap.add_argument("--variant", action="append", required=True, help="name=libpath[:key=val,...]")
     ap.add_argument("--check", action="store_true", help="compare every variant's outputs with the first")
+    ap.add_argument("--reuse", action="store_true",
+                    help="diagnostic: keep --nbufs buffers and reuse them within a launch (an on-die packet stream)")
     args = ap.parse_args()
     # every batch of one launch distinct: a launch's batch groups run concurrently (a repeated buffer would be
     # re-read from the Infinity Cache)
-    args.nbufs = max(args.nbufs, args.steps)
+    ap_reuse = args.reuse
+    if not ap_reuse:
+        args.nbufs = max(args.nbufs, args.steps)
     if args.binth:
         import os
         os.environ["PPE_BINTH"] = str(args.binth)
