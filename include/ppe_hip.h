@@ -229,7 +229,9 @@ typedef struct {
     uint32_t pipeline;       /* tile fetch: 0 auto (4 when the image fits in LDS, else 3), 1 first
                                 tile loaded at the loop top, 4 first tile requested before the image
                                 staging, 3 four tiles per wave loaded, decoded and walked together
-                                (one 1024-thread workgroup per CU); others PPE_EINVAL              */
+                                (one 1024-thread workgroup per CU), 5 one tile per wave walking the
+                                image's 2-level blocks (two 1024-thread workgroups per CU, each
+                                staging the block levels that fit half the LDS); others PPE_EINVAL */
     uint32_t lds_image;      /* 1 = stage the image (or its top) in LDS, 0 = read it from global   */
     uint32_t batches_per_launch;  /* ppe_classify_batches: batches one launch takes (<= 4096); 0 = all
                                      of a call's batches in ONE persistent launch (descriptor ring)  */
