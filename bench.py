@@ -105,6 +105,9 @@ def parse(argv=None):
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (all cores)")
     ap.add_argument("--dry-run", action="store_true", help="rank plumbing only (gloo, no GPU)")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, collectives over gloo "
+                         "(the rates are not a scaling result; stateless configs only)")
     return ap.parse_args(argv)
 
 
@@ -123,11 +126,16 @@ def main():
     if args.dry_run:
         return dry_run(args, world, rank)
     dist = None
+    if args.shared_gpu:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if args.shared_gpu:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"RCCL reports {dist.get_world_size()} ranks, expected {args.gpus}")
     dev = torch.device("cuda", local)
@@ -340,7 +348,8 @@ def run_stateless(args, dev, world, rank, dist):
         try:
             out0 = res.bufs[0][2]
             src = torch.stack([out0["verdict"], out0["flow_hash"], out0["acl_hit"]])
-            dst = torch.empty((world,) + tuple(src.shape), dtype=src.dtype, device=dev)
+            # the concatenated output form (rank r's 3 rows at [3r, 3r + 3)): RCCL and gloo both take it
+            dst = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=dev)
             ts = []
             for _ in range(6):
                 dist.barrier()
@@ -352,7 +361,8 @@ def run_stateless(args, dev, world, rank, dist):
             gt = torch.tensor([float(np.median(ts[1:])) * 1e3], dtype=torch.float64, device=dev)
             dist.all_reduce(gt, op=dist.ReduceOp.MAX)
             g_ms = float(gt.item())
-            gather = {"ms_per_batch": round(g_ms, 4), "bytes_per_rank": 12 * n, "collective": "all_gather (RCCL)",
+            gather = {"ms_per_batch": round(g_ms, 4), "bytes_per_rank": 12 * n,
+                      "collective": "all_gather (gloo, shared-GPU rehearsal)" if args.shared_gpu else "all_gather (RCCL)",
                       "value_with_gather": round(n * world / ((my_ms / args.steps + g_ms) / 1e3) / 1e6, 2)}
         except Exception as e:  # a failed side measurement must not lose the throughput line
             gather = {"error": str(e)[:200]}
@@ -448,6 +458,8 @@ def run_stateless(args, dev, world, rank, dist):
         }
         if gather is not None:
             line["gather"] = gather
+        if args.shared_gpu:
+            line["shared_gpu_rehearsal"] = True
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -44,3 +44,19 @@ def test_world_size_must_match_gpus():
     r = run(["--gpus", "2", "--dry-run"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
     assert "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.gpu
+def test_two_ranks_on_one_gpu():
+    """The N > 1 path end to end on real kernels (a one-GPU box: both ranks on cuda:0, gloo collectives): each rank
+    classifies its own resident batches, its parity sample is green, the MAX-over-ranks line counts both ranks'
+    packets, and the verdict gather runs.  RCCL itself is the driver's multi-GPU run."""
+    r = run(["--gpus", "2", "--shared-gpu", "--n", "262144", "--steps", "8", "--warmup", "2", "--configs", "",
+             "--no-cpu-baseline", "--no-host-inclusive"], timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["ranks_reported"] == 2 and d["shared_gpu_rehearsal"] is True
+    assert d["config"]["global_batch"] == 2 * 262144 and d["parity_sample_ok"] is True
+    assert d["value"] > 0 and "error" not in d["gather"], d.get("gather")
