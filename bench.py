@@ -77,6 +77,9 @@ def free_port() -> int:
 
 def spawn(args_list: list[str], n: int) -> int:
     """Run this script under torch.distributed.run with n ranks (a child process: this one never touched the GPU)."""
+    # torch.distributed.run's own parser would take `--n` as an ambiguous abbreviation of its options
+    args_list = ["--packets" if a == "--n" else ("--packets=" + a[4:] if a.startswith("--n=") else a)
+                 for a in args_list]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve())] + args_list
     env = dict(os.environ)
@@ -93,8 +96,8 @@ def parse(argv=None):
     ap.add_argument("--configs", default=",".join(EXTRA_CONFIGS),
                     help="extra stateless configs measured after --config and nested in the line ('' = none)")
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"))
-    ap.add_argument("--n", type=int, default=0, help="packets per GPU per step (default: the config's; strong: "
-                                                      "8M / ranks)")
+    ap.add_argument("--packets", "--n", dest="n", type=int, default=0,
+                    help="packets per GPU per step (default: the config's; strong: 8M / ranks)")
     ap.add_argument("--stride", type=int, default=64)
     ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: >= 8, > 600 MB and >= "
                                                           "the batches of one launch)")

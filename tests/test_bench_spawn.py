@@ -60,3 +60,11 @@ def test_two_ranks_on_one_gpu():
     assert d["n_gpus"] == 2 and d["ranks_reported"] == 2 and d["shared_gpu_rehearsal"] is True
     assert d["config"]["global_batch"] == 2 * 262144 and d["parity_sample_ok"] is True
     assert d["value"] > 0 and "error" not in d["gather"], d.get("gather")
+
+
+def test_spawn_forwards_packets_option():
+    """`--n` (packets per GPU) reaches the ranks: torch.distributed.run's parser would read it as an ambiguous
+    abbreviation of its own options, so the spawn forwards it as `--packets`."""
+    r = run(["--gpus", "2", "--dry-run", "--n", "4096"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json_lines(r.stdout)[0]["ranks_reported"] == 2
