@@ -440,6 +440,55 @@ def test_full_size_properties_c1(eng):
         assert np.array_equal(whole[k][idx], ref[k]), k
 
 
+@pytest.mark.parametrize("stride", [64, 128])
+def test_maximum_batch_size(eng, stride):
+    """The largest batch the ABI accepts (n * stride < 2^31: 2^25 - 1 packets of 64-B windows or 2^24 - 1 of 128-B
+    windows, a ragged last tile):
+    a 1M-packet batch repeated on the device classifies exactly like the 1M batch in every repetition, the
+    counters account for every packet, the partition list holds each tile's packets once; one packet more is
+    refused."""
+    rules = synth.make_rules(256, seed=81)
+    m = 1 << 20
+    pk = synth.make_packets(m, rules, seed=82, kind="imix", stride=stride, malformed_frac=0.02)
+    eng.commit(rules, default_action=1)
+    small = gpu_classify(eng, pk["hdr"], pk["len"])
+    nmax = (1 << 31) // stride
+    reps = nmax // m
+    n = nmax - 1
+    th = torch.from_numpy(pk["hdr"]).to(DEV).repeat(reps, 1)
+    tl = torch.from_numpy(pk["len"].view(np.int32)).to(DEV).repeat(reps)
+    big = {k: torch.full((nmax,), -7, dtype=torch.int32, device=DEV) for k in ("verdict", "flow_hash", "acl_hit",
+                                                                                   "part_idx")}
+    out = {k: v[:n] for k, v in big.items()}
+    eng.clear_counters()
+    eng.classify_torch(th[:n], tl[:n], out, cfg=eng.cfg(now_seconds=NOW))
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    assert cnt["pkts"] == n and cnt["out_fw"] + cnt["out_drop"] + cnt["out_punt"] == n
+    for k in ("verdict", "flow_hash", "acl_hit"):
+        got = out[k]
+        full = got[: (reps - 1) * m].view(reps - 1, m)
+        ref = torch.from_numpy(small[k].view(np.int32)).to(DEV)
+        assert bool((full == ref).all()), k
+        assert bool((got[(reps - 1) * m:] == ref[: n - (reps - 1) * m]).all()), k
+    part = out["part_idx"]
+    idx = (part & 0x3FFFFFFF).to(torch.int64)
+    tiles = torch.arange(n, device=DEV, dtype=torch.int64) // 64
+    assert bool((idx // 64 == tiles).all())  # every slot of tile t names a packet of tile t
+    seen = torch.zeros(n, dtype=torch.int32, device=DEV)
+    seen.index_add_(0, idx, torch.ones(n, dtype=torch.int32, device=DEV))
+    assert bool((seen == 1).all())  # ... and each packet exactly once
+    # one packet more: n * stride = 2^31 (every buffer holds that many entries, so a missing check could not write
+    # out of bounds)
+    r = abi.Result(big["verdict"].data_ptr(), big["flow_hash"].data_ptr(), big["acl_hit"].data_ptr(),
+                   big["part_idx"].data_ptr(), big["part_idx"].data_ptr(), None, None)
+    b = abi.Batch(th.data_ptr(), tl.data_ptr(), None, nmax, stride)
+    cfg = eng.cfg()
+    assert eng.lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == -22
+    torch.cuda.synchronize()
+    assert bool((big["verdict"][n:] == -7).all())
+
+
 @pytest.mark.parametrize("per_launch", ["0", "8", "2", "1"])
 def test_classify_batches_pipelined(monkeypatch, per_launch):
     """ppe_classify_batches: several batches (ragged sizes, an empty one, both window strides) grouped per launch
