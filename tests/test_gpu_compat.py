@@ -95,3 +95,127 @@ def test_rule_store_commit_decode_hooks():
     assert C.c_int.in_dll(lib, "gNumTreeNode").value > 0
     lib.ppe_rule_list_free()
     lib.DP_Acl_Rule_Release()
+    unhook(lib)
+
+
+def unhook(lib):
+    """The library keeps the hook pointers: clear them before this test's ctypes thunks are freed."""
+    lib.ppe_set_output_hooks(HOOK(), HOOK(), HOOK())
+    lib.reg_fw_alert(ALERT())
+
+
+def test_decode_from_several_threads():
+    """The reference calls Decode from N pinned pthreads (main.c:422-425).  Here 4 threads each queue their own
+    quarter of the mbufs into their own burst (per-thread, as per-core run-to-completion) with a small burst cap, so
+    full bursts are flushed from every thread while the others queue; every mbuf reaches exactly one hook with the
+    oracle's verdict."""
+    import threading
+    lib = abi.load()
+    lib.ppe_set_output_hooks.argtypes = [HOOK, HOOK, HOOK]
+    assert lib.DP_Acl_Rule_Init() == 0
+    lib.ppe_rule_list_free()
+    assert lib.ppe_rule_list_init() == 0
+    rules = synth.make_rules(300, seed=95)
+    for i in range(len(rules)):
+        rid = C.c_uint32()
+        assert lib.Rule_add(rules[i:i + 1].ctypes.data, C.byref(rid)) == 0
+    assert lib.DP_Acl_Rule_Commit() == 0
+    pk = synth.make_packets(8000, rules, seed=96, kind="imix", stride=128, malformed_frac=0.05)
+    n = len(pk["len"])
+    bufs = [C.create_string_buffer(bytes(pk["hdr"][i][: min(int(pk["len"][i]) & 0xFFFF, 128)]), 128)
+            for i in range(n)]
+    mbufs = (Mbuf * n)()
+    for i in range(n):
+        mbufs[i].pkt_ptr = C.cast(bufs[i], C.c_void_p)
+        mbufs[i].pkt_totallen = int(pk["len"][i])
+    base = C.addressof(mbufs)
+    got = {"fw": [], "drop": [], "punt": []}
+
+    def mk(key):
+        return HOOK(lambda m: got[key].append((C.addressof(m.contents) - base) // C.sizeof(Mbuf)))
+
+    logs = []
+
+    def alert(p):
+        logs.append(1)
+        return 0
+
+    hooks = (mk("fw"), mk("drop"), mk("punt"), ALERT(alert))
+    lib.ppe_set_output_hooks(*hooks[:3])
+    lib.reg_fw_alert.argtypes = [ALERT]
+    lib.reg_fw_alert(hooks[3])
+    lib.Decode_Set_Burst(256)
+    errors = []
+
+    def worker(t):
+        try:
+            for i in range(t, n, 4):
+                lib.Decode(C.byref(mbufs[i]))
+            if lib.Decode_Flush() < 0:
+                errors.append(t)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    assert not errors and not any(th.is_alive() for th in ths), errors
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, 0))
+    act = (ref["verdict"] >> 8) & 0xFF
+    assert sorted(got["fw"]) == np.nonzero(act == 0)[0].tolist()
+    assert sorted(got["drop"]) == np.nonzero(act == 1)[0].tolist()
+    assert sorted(got["punt"]) == np.nonzero(act == 2)[0].tolist()
+    v = np.array([mbufs[i].ppe_verdict for i in range(n)], np.uint32)
+    assert np.array_equal(v, ref["verdict"])
+    assert len(logs) == int(np.isin(ref["verdict"] & 0xFF, list(LOGGED)).sum())
+    lib.ppe_rule_list_free()
+    lib.DP_Acl_Rule_Release()
+    unhook(lib)
+
+
+def test_contexts_on_concurrent_threads():
+    """Two engine contexts (each its own classifier image and streams) driven from two host threads at once: the
+    library keeps no shared mutable state across contexts, so each thread's results equal the oracle's."""
+    import threading
+    from ppe import Engine
+    sets = [synth.make_rules(256, seed=97), synth.make_rules(4096, seed=98)]
+    pks = [synth.make_packets(200_000, sets[k], seed=99 + k, kind="imix", stride=64) for k in range(2)]
+    res, errors = [None, None], []
+
+    def worker(k):
+        try:
+            eng = Engine(0)
+            try:
+                eng.commit(sets[k], default_action=1)
+                dev = torch.device("cuda:0")
+                s = torch.cuda.Stream(dev)
+                with torch.cuda.stream(s):
+                    th = torch.from_numpy(pks[k]["hdr"]).to(dev)
+                    tl = torch.from_numpy(pks[k]["len"].view(np.int32)).to(dev)
+                    out = {x: torch.empty(len(tl), dtype=torch.int32, device=dev)
+                           for x in ("verdict", "flow_hash", "acl_hit")}
+                    for _ in range(20):  # keep both contexts busy at the same time
+                        eng.classify_torch(th, tl, out, cfg=eng.cfg(now_seconds=0), stream=s)
+                s.synchronize()
+                res[k] = {x: v.cpu().numpy() for x, v in out.items()}
+            finally:
+                eng.close()
+        except Exception as e:
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    assert not errors, errors
+    for k in range(2):
+        o = pyoracle.Oracle(sets[k], default_action=1)
+        ref = o.classify_batch(pks[k]["hdr"], pks[k]["len"], cfg=o.cfg(0, 1, 0), nthreads=8)
+        ok = ref["reach"] <= 64
+        assert np.array_equal(res[k]["verdict"].view(np.uint32)[ok], ref["verdict"][ok])
+        assert np.array_equal(res[k]["acl_hit"][ok], ref["acl_hit"][ok])
+        assert np.array_equal(res[k]["flow_hash"].view(np.uint32)[ok], ref["flow_hash"][ok])
