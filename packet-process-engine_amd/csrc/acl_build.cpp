@@ -142,6 +142,10 @@ std::vector<Work> cut_roots(const std::vector<Rule> &R, const Jump &j, std::vect
 // prefix of the node array for every L: the LDS-staged top of the image is whole levels)
 Forest build_forest(const std::vector<Rule> &R, std::vector<Work> roots, uint32_t binth) {
     Forest f;
+    // analysis knob (tools/walk_depth.py, not a product setting): a node at depth >= PPE_LEAF_CAP_DEPTH with at most
+    // PPE_LEAF_CAP_N candidates becomes a leaf list, bounding the depth of the walk's tail
+    static const uint32_t cap_depth = (uint32_t)std::max(0, std::atoi(std::getenv("PPE_LEAF_CAP_DEPTH") ? std::getenv("PPE_LEAF_CAP_DEPTH") : "0"));
+    static const uint32_t cap_leaf = (uint32_t)std::max(1, std::atoi(std::getenv("PPE_LEAF_CAP_N") ? std::getenv("PPE_LEAF_CAP_N") : "1"));
     std::vector<TNode> &nodes = f.nodes;
     const size_t node_budget = PPE_NODE_MAX - 2;
     std::deque<Work> q;
@@ -181,6 +185,7 @@ Forest build_forest(const std::vector<Rule> &R, std::vector<Work> roots, uint32_
 
         const bool first_certain = !S.empty() && R[S[0]].resid == 0 && covers(R[S[0]], w.lo, w.hi);
         if (S.empty() || first_certain || S.size() <= binth || w.depth + 1 >= PPE_MAX_DEPTH ||
+            (cap_depth && w.depth >= cap_depth && S.size() <= cap_leaf) ||
             nodes.size() + 2 > node_budget) {
             if (first_certain) S.resize(1);
             make_leaf(S);

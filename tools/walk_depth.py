@@ -38,6 +38,8 @@ def walk(img, keys):
     else:
         blk = np.zeros(n, np.int64)
     path = np.full((n, max_bd), -1, np.int64)
+    cnt = np.ones(n, np.int64)  # candidates of the leaf reached (leaf lists: count field of the exit)
+    lists = int(img[12]) > 1
     live = np.ones(n, bool)
     rows = np.arange(n)
     for it in range(max_bd):
@@ -54,9 +56,16 @@ def walk(img, keys):
         x = np.where(b0, np.where(b1, b[:, 7], b[:, 6]), np.where(b1, b[:, 5], b[:, 4])).astype(np.int64)
         leaf = (x & BLK_LEAF) != 0
         idx = rows[live]
+        if lists:
+            c = (x >> 23) & 0xFF
+            esc = c == 255
+            if esc.any():
+                off_leaf = int(img[6])
+                c[esc] = img[off_leaf + (x[esc] & 0x7FFFFF)]
+            cnt[idx[leaf]] = np.maximum(c[leaf], 1)
         live[idx[leaf]] = False
         blk[idx[~leaf]] = x[~leaf]
-    return path
+    return path, cnt
 
 
 def main():
@@ -76,7 +85,7 @@ def main():
     acl = ((ref["verdict"] >> 16) & 0x10) != 0  # PPE_F_ACL: packets that walk
     t = ref["tuple"]
     keys = np.stack([t[:, 0], t[:, 1], t[:, 2] & 0xFFFF, t[:, 2] >> 16, t[:, 3] & 0xFF], 1).astype(np.uint32)
-    path = walk(img, keys)
+    path, cnt = walk(img, keys)
     reads = (path >= 0).sum(1)
     l2 = ((path >= args.lds_blocks)).sum(1)
     reads[~acl] = 0
@@ -92,6 +101,12 @@ def main():
     l2steps = np.array([((path[i * g:(i + 1) * g] >= args.lds_blocks).any(0)).sum() for i in range(m // g)])
     print(f"lockstep groups of {g}: steps mean {steps.mean():.2f}, max {steps.max()}; steps with an L2 read mean "
           f"{l2steps.mean():.2f}")
+    # dependent round trips of the whole lookup: block reads + one rule read per candidate scanned (serial leaf-list
+    # loop; upper bound: every candidate of the leaf)
+    cost = reads + np.where(acl, cnt, 0)
+    cg = cost[:m].reshape(-1, g).max(1)
+    print(f"leaf candidates: mean {cnt[acl].mean():.2f}, max {cnt[acl].max()}; walk + rule round trips per group "
+          f"(deepest lane, candidates scanned serially): mean {cg.mean():.2f}, max {cg.max()}; image words {len(img)}")
 
 
 if __name__ == "__main__":
