@@ -11,4 +11,4 @@ run() {
     --variant cur=$L:api=batches,bpl=0 > $O/ab_$1.txt 2>&1 || exit 1
   grep "kernel med" $O/ab_$1.txt | sed "s/^/$1 /" >> $O/summary.txt
 }
-run off1 PPE_LEAF_CAP_DEPTH=0 && run drec1 X=1 && run off2 PPE_LEAF_CAP_DEPTH=0 && run drec2 X=1
+run off1 PPE_LEAF_CAP_DEPTH=0 && run drec1 X=1 && run d10 PPE_LEAF_CAP_DEPTH=10 && run off2 PPE_LEAF_CAP_DEPTH=0 && run drec2 X=1
