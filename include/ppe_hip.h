@@ -34,7 +34,9 @@
 extern "C" {
 #endif
 
-#define PPE_ABI_VERSION 1
+/* 2: ppe_tuning_t grew to 20 B (batches_per_launch) and mbuf_t (ppe_decode.h) took the reference's field layout;
+ * 3: ppe_tuple's word 3 carries the TCP window-scale option offset (bits 9-15) */
+#define PPE_ABI_VERSION 3
 
 /* error codes (negative return values) */
 #define PPE_OK       0

@@ -198,6 +198,8 @@ int32_t oracle_acl_tree(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dpo
     return -1;
 }
 
+static uint32_t oracle_rule_action(uint32_t id) { return id < g_nrules ? g_rules[id].action : 0u; }
+
 /* Walk of the image's block section (format v5: 2-level blocks, what the GPU's multi-tile kernel walks), from the
  * same jump bucket; the leaf reached must be the binary walk's (test_acl_build.py checks all three walks agree). */
 int32_t oracle_acl_blocks(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
@@ -217,6 +219,25 @@ int32_t oracle_acl_blocks(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t d
         b = x;
     }
     x &= ~PPE_BLK_LEAF;
+    if (im[PPE_IMG_W_OFFCREC]) {
+        /* compact leaf (image v6): the exit's flags + the slot's 16-B record (prefix marker bits, port spans); only
+         * TCP / UDP keys reach the ACL on the classify path, which is the only user of the block walk */
+        const uint32_t slot = x & PPE_CX_SLOT;
+        const uint32_t *r = im + im[PPE_IMG_W_OFFCREC] + PPE_CREC_WORDS * slot;
+        const uint32_t ms = (x & PPE_CX_S32) ? ~0u : ~(((r[0] & (0u - r[0])) << 1) - 1u);
+        const uint32_t md = (x & PPE_CX_D32) ? ~0u : ~(((r[1] & (0u - r[1])) << 1) - 1u);
+        const int m = ((sip ^ r[0]) & ms) == 0 && ((dip ^ r[1]) & md) == 0 &&
+                      (uint16_t)(sport - (r[2] & 0xffffu)) <= (r[3] & 0xffffu) &&
+                      (uint16_t)(dport - (r[2] >> 16)) <= (r[3] >> 16) &&
+                      (proto == 6 ? (x & PPE_CX_TCP) : proto == 17 ? (x & PPE_CX_UDP) : 0) != 0;
+        const uint32_t id = im[PPE_IMG_W_OFFIDTAB] ? im[im[PPE_IMG_W_OFFIDTAB] + slot] : slot;
+        const int drop = m ? (x & PPE_CX_DROP) != 0 : im[PPE_IMG_W_DEFACT] == ACL_RULE_ACTION_DROP;
+        (void)dmac; (void)smac; (void)ts;
+        /* the action word a drop-or-forward decision needs: the classify path compares it with DROP only */
+        if (action) *action = m && !(x & PPE_CX_NOHIT) ? (drop ? ACL_RULE_ACTION_DROP : oracle_rule_action(id))
+                                                        : im[PPE_IMG_W_DEFACT];
+        return m && !(x & PPE_CX_NOHIT) ? (int32_t)id : -1;
+    }
     const uint32_t max_leaf = im[PPE_IMG_W_MAXLEAF];
     const uint32_t *lf = im + im[PPE_IMG_W_OFFLEAF];
     uint32_t first = 0, cnt = 1, one = x;

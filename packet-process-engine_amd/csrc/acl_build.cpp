@@ -381,10 +381,26 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     auto c1 = [&](uint32_t x) { return is_leaf(x) ? x : nodes[x].left + 1u; };
     auto thr = [&](uint32_t x) { return is_leaf(x) ? 0xffffffffu : nodes[x].thr; };  // leaf: pass-through
     auto kslot = [&](uint32_t x) { return is_leaf(x) ? 0u : nodes[x].dim; };
+    // compact leaves (v6, ppe_image.h): one candidate per leaf and no residual fields; PPE_COMPACT=0 turns them off
+    // (A/B and tests of the v5 leaf path)
+    const char *ce = std::getenv("PPE_COMPACT");
+    const bool compact = max_leaf <= 1 && !any_resid && !(ce && *ce == '0');
+    auto cx_flags = [&](uint32_t slot) -> uint32_t {  // the compact exit's flag bits for the candidate in `slot`
+        if (slot == n_slots)  // the sentinel
+            return PPE_CX_NOHIT | PPE_CX_TCP | PPE_CX_UDP | (default_action == ACL_RULE_ACTION_DROP ? PPE_CX_DROP : 0u);
+        const Rule &r = R[slot];
+        uint32_t f = r.action == ACL_RULE_ACTION_DROP ? PPE_CX_DROP : 0u;
+        if (r.lo[PPE_DIM_PROTO] <= 6u && 6u <= r.hi[PPE_DIM_PROTO]) f |= PPE_CX_TCP;
+        if (r.lo[PPE_DIM_PROTO] <= 17u && 17u <= r.hi[PPE_DIM_PROTO]) f |= PPE_CX_UDP;
+        if (r.lo[PPE_DIM_SIP] == r.hi[PPE_DIM_SIP]) f |= PPE_CX_S32;
+        if (r.lo[PPE_DIM_DIP] == r.hi[PPE_DIM_DIP]) f |= PPE_CX_D32;
+        return f;
+    };
     auto leaf_exit = [&](uint32_t x) -> uint32_t {
         const TNode &nd = nodes[x];
         if (max_leaf > 1) return PPE_BLK_LEAF | nd.first | (std::min(nd.cnt, PPE_LEAF_CNT_ESC) << 23);
-        return PPE_BLK_LEAF | (nd.cnt ? leaf[nd.first] : n_slots);
+        const uint32_t slot = nd.cnt ? leaf[nd.first] : n_slots;
+        return PPE_BLK_LEAF | slot | (compact ? cx_flags(slot) : 0u);
     };
     if (max_leaf > 1 && lwords.size() >= (1u << 23)) return PPE_ENOMEM;  // leaf exits hold 23-bit list offsets
     std::vector<uint32_t> bwords, bnode, bdepth;
@@ -419,7 +435,15 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     if (n_blocks >= PPE_BLK_LEAF) return PPE_ENOMEM;
     const uint32_t off_bsec = (end_resid + 7u) & ~7u;
     const uint32_t off_blocks = (off_bsec + n_jump + 7u) & ~7u;
-    const uint32_t total = off_blocks + PPE_BLK_WORDS * n_blocks;
+    // compact records and the slot → index table follow the blocks, so the block section and the records they lead
+    // to are one contiguous range (the multi-tile kernel stages it whole when it fits the CU's LDS)
+    bool holes = false;
+    for (uint32_t sl = 0; sl < n_slots; ++sl) holes |= R[sl].id != sl;
+    const uint32_t off_crec = compact ? off_blocks + PPE_BLK_WORDS * n_blocks : 0u;
+    const uint32_t off_idtab = compact && holes ? off_crec + PPE_CREC_WORDS * (n_slots + 1u) : 0u;
+    const uint32_t total = !compact ? off_blocks + PPE_BLK_WORDS * n_blocks
+                           : off_idtab ? off_idtab + ((n_slots + 3u) & ~3u)
+                                       : off_crec + PPE_CREC_WORDS * (n_slots + 1u);
 
     uint32_t *img = (uint32_t *)std::calloc(total, sizeof(uint32_t));
     if (!img) return PPE_ENOMEM;
@@ -442,6 +466,29 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     img[PPE_IMG_W_NBLOCKS] = n_blocks;
     img[PPE_IMG_W_OFFBLOCKS] = off_blocks;
     img[PPE_IMG_W_MAXBDEPTH] = max_bdepth;
+    img[PPE_IMG_W_OFFCREC] = off_crec;
+    img[PPE_IMG_W_OFFIDTAB] = off_idtab;
+    if (compact) {
+        // prefix | marker bit (len 0..31), or the address of a /32
+        // (a prefix box spans 2^(32 - len) keys: its marker bit 1 << (31 - len) is half that count)
+        auto pfx = [](uint32_t lo, uint32_t hi) { return lo == hi ? lo : lo | (((hi - lo) >> 1) + 1u); };
+        for (uint32_t sl = 0; sl <= n_slots; ++sl) {
+            uint32_t *o = img + off_crec + PPE_CREC_WORDS * sl;
+            if (sl == n_slots) {  // sentinel: /0 addresses, every port
+                o[0] = o[1] = 0x80000000u;
+                o[2] = 0;
+                o[3] = 0xffffffffu;
+                continue;
+            }
+            const Rule &r = R[sl];
+            o[0] = pfx(r.lo[PPE_DIM_SIP], r.hi[PPE_DIM_SIP]);
+            o[1] = pfx(r.lo[PPE_DIM_DIP], r.hi[PPE_DIM_DIP]);
+            o[2] = r.lo[PPE_DIM_SPORT] | (r.lo[PPE_DIM_DPORT] << 16);
+            o[3] = (r.hi[PPE_DIM_SPORT] - r.lo[PPE_DIM_SPORT]) | ((r.hi[PPE_DIM_DPORT] - r.lo[PPE_DIM_DPORT]) << 16);
+        }
+        if (off_idtab)
+            for (uint32_t sl = 0; sl < n_slots; ++sl) img[off_idtab + sl] = R[sl].id;
+    }
     auto node_byte = [&](uint32_t k) { return 4u * off_nodes + 16u * k; };
     for (uint32_t k = 0; k < n_nodes; ++k) {
         const TNode &nd = nodes[k];

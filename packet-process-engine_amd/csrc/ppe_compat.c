@@ -36,6 +36,10 @@ struct ppe_tree_node {
 static ppe_ctx_t *g_ctx = NULL;
 static uint32_t g_generation = 0;
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+/* The engine context is thread-compatible, not thread-safe (include/ppe_hip.h): every call that uses g_ctx — a
+ * Decode flush's classify, a rule commit, an ACL lookup, the release — holds g_ctx_lock, always the innermost lock
+ * (g_lock and rulelist_mutex may be held around it, never taken inside it). */
+static pthread_mutex_t g_ctx_lock = PTHREAD_MUTEX_INITIALIZER;
 static fw_alert fw_log_fun = NULL;
 static ppe_output_fn out_fw = NULL, out_drop = NULL, out_punt = NULL;
 
@@ -77,7 +81,7 @@ static void publish_stats(const ppe_acl_stats_t *st) {
 }
 
 uint32_t DP_Acl_Load_Rule(rule_list_t *rl, TreeSet **tset, TreeNode **tnode) {
-    if (!rl || !g_ctx) return SEC_NO;
+    if (!rl) return SEC_NO;
     RCP_BLOCK_ACL_RULE_TUPLE *t = (RCP_BLOCK_ACL_RULE_TUPLE *)malloc(sizeof(*t) * RULE_ENTRY_MAX);
     uint8_t *used = (uint8_t *)malloc(RULE_ENTRY_MAX);
     if (!t || !used) {
@@ -90,7 +94,9 @@ uint32_t DP_Acl_Load_Rule(rule_list_t *rl, TreeSet **tset, TreeNode **tnode) {
         used[i] = (uint8_t)rl->rule_entry[i].entry_status;
     }
     ppe_acl_stats_t st;
-    const int rc = ppe_rules_commit(g_ctx, t, used, RULE_ENTRY_MAX, dp_acl_action_default, &st);
+    pthread_mutex_lock(&g_ctx_lock);
+    const int rc = g_ctx ? ppe_rules_commit(g_ctx, t, used, RULE_ENTRY_MAX, dp_acl_action_default, &st) : PPE_ENODEV;
+    pthread_mutex_unlock(&g_ctx_lock);
     free(t);
     free(used);
     if (rc != PPE_OK) return SEC_NO;
@@ -123,19 +129,17 @@ void DP_Acl_Rule_Clean(TreeSet **tset, TreeNode **tnode) {
     }
 }
 
-static pthread_mutex_t g_classify_lock;
-
 void DP_Acl_Rule_Release(void) {
     pthread_mutex_lock(&g_lock);
-    pthread_mutex_lock(&g_classify_lock);  /* no burst is mid-classify on the context being destroyed */
+    pthread_mutex_lock(&g_ctx_lock);  /* no flush, commit or lookup is using the context being destroyed */
     if (g_ctx) ppe_ctx_destroy(g_ctx);
     g_ctx = NULL;
-    pthread_mutex_unlock(&g_classify_lock);
+    pthread_mutex_unlock(&g_ctx_lock);
     pthread_mutex_unlock(&g_lock);
 }
 
 int DP_Acl_Rule_Commit(void) {
-    if (!g_ctx || !rule_list) return SEC_NO;
+    if (!rule_list) return SEC_NO;
     int rc = SEC_OK;
     pthread_mutex_lock(&rule_list->rulelist_mutex);
     if (rule_list->build_status != RULE_BUILD_COMMIT) {
@@ -162,7 +166,7 @@ static void mbuf_tuple(const mbuf_t *m, uint32_t *tw, uint32_t *mw) {
 }
 
 int DP_Acl_Lookup_Burst(mbuf_t **m, uint32_t n, int *actions) {
-    if (!g_ctx || !m) return PPE_EINVAL;
+    if (!m) return PPE_EINVAL;
     if (n == 0) return PPE_OK;
     uint32_t *tw = (uint32_t *)malloc((size_t)n * 16), *mw = (uint32_t *)malloc((size_t)n * 16);
     uint64_t *ts = (uint64_t *)malloc((size_t)n * 8);
@@ -175,7 +179,9 @@ int DP_Acl_Lookup_Burst(mbuf_t **m, uint32_t n, int *actions) {
             ts[i] = m[i]->timestamp;
         }
         ppe_tuples_t in = {tw, mw, ts, n};
-        rc = ppe_acl_lookup_host(g_ctx, &in, hit, act, 0);
+        pthread_mutex_lock(&g_ctx_lock);
+        rc = g_ctx ? ppe_acl_lookup_host(g_ctx, &in, hit, act, 0) : PPE_EINVAL;
+        pthread_mutex_unlock(&g_ctx_lock);
         if (rc == PPE_OK)
             for (uint32_t i = 0; i < n; i++) {
                 m[i]->ppe_acl_hit = hit[i];
@@ -207,10 +213,24 @@ typedef struct {
 } burst_t;
 
 static volatile uint32_t g_burst_cap = 4096;
-static pthread_mutex_t g_classify_lock = PTHREAD_MUTEX_INITIALIZER;
 static pthread_key_t g_burst_key;
 static pthread_once_t g_burst_once = PTHREAD_ONCE_INIT;
 static __thread burst_t *t_burst = NULL;
+
+/* Test hook (tests/test_compat_host.py only, not in the public headers): the next `k` allocations of the Decode
+ * path fail, so the allocation-failure branches can be exercised without exhausting memory. */
+static volatile uint32_t g_fail_alloc = 0;
+void ppe_compat_debug_fail_alloc(uint32_t k) { __atomic_store_n(&g_fail_alloc, k, __ATOMIC_RELAXED); }
+static int take_fail(void) {
+    uint32_t k = __atomic_load_n(&g_fail_alloc, __ATOMIC_RELAXED);
+    while (k)
+        if (__atomic_compare_exchange_n(&g_fail_alloc, &k, k - 1, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) return 1;
+    return 0;
+}
+static void *burst_alloc(size_t bytes, size_t align) {
+    if (take_fail()) return NULL;
+    return align ? aligned_alloc(align, (bytes + align - 1) / align * align) : malloc(bytes);
+}
 
 static int flush_burst(burst_t *b);
 
@@ -218,6 +238,8 @@ static void burst_exit(void *p) {  /* thread exit: deliver what the thread left 
     burst_t *b = (burst_t *)p;
     if (!b) return;
     flush_burst(b);
+    /* a Decode() from a later TLS destructor of this thread must start a new burst, not touch this one */
+    t_burst = NULL;
     free(b->m);
     free(b);
 }
@@ -252,11 +274,11 @@ static int logged_drop(uint32_t st) {
 
 /* Classify `n` mbufs on the GPU (serialised) and fill their parse fields; returns PPE_OK or a PPE_E* code. */
 static int classify_mbufs(mbuf_t **mb, uint32_t n) {
-    uint8_t *hdr = (uint8_t *)aligned_alloc(16, (size_t)n * PPE_COMPAT_STRIDE);
-    uint32_t *len = (uint32_t *)malloc((size_t)n * 4), *verdict = (uint32_t *)malloc((size_t)n * 4);
-    uint32_t *fh = (uint32_t *)malloc((size_t)n * 4), *tuple = (uint32_t *)malloc((size_t)n * 16);
-    uint64_t *ts = (uint64_t *)malloc((size_t)n * 8);
-    int32_t *hit = (int32_t *)malloc((size_t)n * 4);
+    uint8_t *hdr = (uint8_t *)burst_alloc((size_t)n * PPE_COMPAT_STRIDE, 16);
+    uint32_t *len = (uint32_t *)burst_alloc((size_t)n * 4, 0), *verdict = (uint32_t *)burst_alloc((size_t)n * 4, 0);
+    uint32_t *fh = (uint32_t *)burst_alloc((size_t)n * 4, 0), *tuple = (uint32_t *)burst_alloc((size_t)n * 16, 0);
+    uint64_t *ts = (uint64_t *)burst_alloc((size_t)n * 8, 0);
+    int32_t *hit = (int32_t *)burst_alloc((size_t)n * 4, 0);
     int rc = PPE_ENOMEM;
     if (hdr && len && verdict && fh && tuple && ts && hit) {
         memset(hdr, 0, (size_t)n * PPE_COMPAT_STRIDE);
@@ -275,9 +297,9 @@ static int classify_mbufs(mbuf_t **mb, uint32_t n) {
         r.acl_hit = hit;
         r.tuple = tuple;
         ppe_cfg_t cfg = {unsupport_proto_action ? 1u : 0u, syn_check ? 1u : 0u, 0};
-        pthread_mutex_lock(&g_classify_lock);
+        pthread_mutex_lock(&g_ctx_lock);
         rc = g_ctx ? ppe_classify_host(g_ctx, &b, &r, &cfg, 0) : PPE_ENODEV;
-        pthread_mutex_unlock(&g_classify_lock);
+        pthread_mutex_unlock(&g_ctx_lock);
         if (rc == PPE_OK) {
             for (uint32_t i = 0; i < n; i++) {
                 mbuf_t *m = mb[i];
@@ -316,17 +338,15 @@ static int classify_mbufs(mbuf_t **mb, uint32_t n) {
     return rc;
 }
 
-/* Take the burst's mbufs out (the burst is empty and reusable before any hook runs), classify, deliver. */
+/* Take the burst's mbufs out (the burst is empty and reusable before any hook runs), classify, deliver.  The queued
+ * array itself is taken, so a flush allocates nothing of its own: when the classify step cannot run (no context,
+ * no memory, a GPU error), every taken mbuf still reaches the drop hook (decode.c:24-27; ppe_decode.h). */
 static int flush_burst(burst_t *b) {
-    const uint32_t n = b->n;
+    const uint32_t n = b->n, alloc = b->alloc;
     if (n == 0) return 0;
-    mbuf_t **mb = (mbuf_t **)malloc(sizeof(mbuf_t *) * n);
-    if (!mb) {  /* cannot even hold them: drop in place, as the reference does on allocation failure */
-        b->n = 0;
-        return PPE_ENOMEM;
-    }
-    memcpy(mb, b->m, sizeof(mbuf_t *) * n);
-    b->n = 0;
+    mbuf_t **mb = b->m;
+    b->m = NULL;
+    b->n = b->alloc = 0;
     const int rc = classify_mbufs(mb, n);
     for (uint32_t i = 0; i < n; i++) {
         mbuf_t *m = mb[i];
@@ -348,7 +368,12 @@ static int flush_burst(burst_t *b) {
                 break;
         }
     }
-    free(mb);
+    if (b == t_burst && !b->m) {  /* no hook queued anything meanwhile: the array goes back to the burst */
+        b->m = mb;
+        b->alloc = alloc;
+    } else {
+        free(mb);
+    }
     return rc == PPE_OK ? (int)n : rc;
 }
 
@@ -363,7 +388,7 @@ void Decode(mbuf_t *m) {
     const uint32_t cap = __atomic_load_n(&g_burst_cap, __ATOMIC_RELAXED);
     if (b && b->n >= b->alloc) {  /* grow to the current cap (or one more slot when the cap was lowered) */
         const uint32_t want = cap > b->n ? cap : b->n + 1;
-        mbuf_t **nb = (mbuf_t **)realloc(b->m, sizeof(mbuf_t *) * want);
+        mbuf_t **nb = take_fail() ? NULL : (mbuf_t **)realloc(b->m, sizeof(mbuf_t *) * want);
         if (nb) {
             b->m = nb;
             b->alloc = want;

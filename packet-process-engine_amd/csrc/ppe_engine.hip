@@ -72,6 +72,9 @@ struct FlowTable {
     // refreshes them without synchronising
     unsigned long long *snap_h = nullptr, *snap_d = nullptr;  // host / device views
     uint64_t snap_used = 0;            // highest snapshot sequence applied
+    // recorded on the stream right before each batch's classify launch: once it completes, that launch is the next
+    // thing the stream runs, and its snapshot follows within microseconds (blocking-sync: the host sleeps on it)
+    hipEvent_t pre_launch = nullptr;
     // ring over the last kSnapRing batches: packets submitted before batch b (of batches that may revoke: _rev)
     static constexpr uint32_t kSnapRing = 4096;
     std::vector<uint64_t> cum_n, cum_rev;
@@ -108,13 +111,14 @@ struct ppe_ctx {
     hipEvent_t pipe_ev[kPipeStreams + 1] = {};
     int pipe_mode = 1;  // PPE_PIPE_MODE at context creation (see ppe_classify_batches)
     // descriptor rings of launches over more than PPE_MAX_BATCH batches: two slots used alternately; a slot is
-    // rewritten only after the launch that read it has completed (ring_ev)
+    // rewritten only after every launch that read it has completed (one event per slot and reading stream, like the
+    // image slots); a launch on another stream that reuses a slot's content waits only for its upload (ring_up)
     ppe_bdesc *d_ring[2] = {nullptr, nullptr};
     ppe_bdesc *h_ring[2] = {nullptr, nullptr};  // pinned staging of the H2D descriptor copy
-    hipEvent_t ring_ev[2] = {nullptr, nullptr};
-    bool ring_pending[2] = {false, false};
+    std::vector<std::pair<hipStream_t, hipEvent_t>> ring_readers[2];
+    hipEvent_t ring_up[2] = {nullptr, nullptr};  // behind the slot's last upload, on ring_up_stream
+    hipStream_t ring_up_stream[2] = {nullptr, nullptr};
     uint32_t ring_n[2] = {0, 0};       // descriptors the slot holds (its content = h_ring[slot][0, ring_n))
-    hipStream_t ring_stream[2] = {nullptr, nullptr};  // stream of the slot's last launch
     int ring_next = 0;
     std::vector<ppe_bdesc> ring_tmp;   // descriptors of the launch being built
     ppe_tuning_t tune;
@@ -178,6 +182,7 @@ struct StagePlan {
     uint32_t stage_src, stage_words;  // what the kernel copies into LDS: image words [stage_src, + stage_words)
     uint32_t lds_blocks;              // multi-tile walks: blocks [0, lds_blocks) in LDS
     uint32_t bsec_lds, blk_lds;       // LDS byte offsets (from the image base in LDS) of the block section / block 0
+    uint32_t crec_lds = ~0u, idtab_lds = ~0u;  // compact records / index table in LDS (byte offsets), ~0u = global
 };
 
 // LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves): 160 KiB shared, minus
@@ -200,9 +205,21 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
     StagePlan p = {0, pf, c->tune.block ? c->tune.block : 1024u, 0, 0, 0, 0, 0, 0, 0};
     // the multi-tile walk reads the 2-level blocks: whole image in LDS, else the block jump table and the first
     // block levels (breadth-first), else global
+    const uint32_t off_crec = img[PPE_IMG_W_OFFCREC], off_idtab = img[PPE_IMG_W_OFFIDTAB];
     auto mt_plan = [&](uint32_t budget) {
         const uint32_t bjt = 4u * (off_blocks - off_bsec);
-        if (all_words * 4u <= budget) {
+        if (off_crec && (all_words - off_bsec) * 4u <= budget) {
+            // compact image (v6): the block walk needs only the block section and the compact records after it, so
+            // the whole walk is LDS-resident when they fit (C2 / C4: 4,096 rules, ~140 KB)
+            p.mode = 1;
+            p.stage_src = off_bsec;
+            p.lds_words = p.stage_words = all_words - off_bsec;
+            p.lds_blocks = n_blocks;
+            p.bsec_lds = 0;
+            p.blk_lds = 4u * (off_blocks - off_bsec);
+            p.crec_lds = 4u * (off_crec - off_bsec);
+            if (off_idtab) p.idtab_lds = 4u * (off_idtab - off_bsec);
+        } else if (!off_crec && all_words * 4u <= budget) {
             p.mode = 1;
             p.lds_words = p.stage_words = all_words;
             p.lds_blocks = n_blocks;
@@ -272,6 +289,8 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
             p.lds_blocks = n_blocks;
             p.bsec_lds = 4u * off_bsec;
             p.blk_lds = 4u * off_blocks;
+            if (off_crec) p.crec_lds = 4u * off_crec;
+            if (off_idtab) p.idtab_lds = 4u * off_idtab;
         }
         p.stage_words = p.lds_words;
         return p;
@@ -420,18 +439,16 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         if (rslot < 0) {
             rslot = c->ring_next;
             c->ring_next ^= 1;
-            if (c->ring_pending[rslot]) HIPCHK(c, hipEventSynchronize(c->ring_ev[rslot]));
-            c->ring_pending[rslot] = false;
+            for (auto &x : c->ring_readers[rslot]) HIPCHK(c, hipEventSynchronize(x.second));  // its last readers
             std::memcpy(c->h_ring[rslot], rd.data(), bytes);
             c->ring_n[rslot] = nb;
             HIPCHK(c, hipMemcpyAsync(c->d_ring[rslot], c->h_ring[rslot], bytes, hipMemcpyHostToDevice, s));
+            HIPCHK(c, hipEventRecord(c->ring_up[rslot], s));
+            c->ring_up_stream[rslot] = s;
             ring_copy = true;
         }
-        if (!ring_copy && c->ring_pending[rslot] && c->ring_stream[rslot] != s) {
-            // reused slot: its upload may have been queued on another stream; order this launch after it
-            if (hipEventQuery(c->ring_ev[rslot]) == hipSuccess) c->ring_pending[rslot] = false;
-            else HIPCHK(c, hipStreamWaitEvent(s, c->ring_ev[rslot], 0));
-        }
+        if (!ring_copy && c->ring_up_stream[rslot] != s && hipEventQuery(c->ring_up[rslot]) != hipSuccess)
+            HIPCHK(c, hipStreamWaitEvent(s, c->ring_up[rslot], 0));  // reused on another stream: after the upload only
         a.batch[0] = rd[0];
         a.ring = c->d_ring[rslot];
     }
@@ -458,6 +475,10 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     a.off_bsec = c->h_img[r][PPE_IMG_W_OFFBSEC];
     a.off_blocks = c->h_img[r][PPE_IMG_W_OFFBLOCKS];
     a.max_bdepth = c->h_img[r][PPE_IMG_W_MAXBDEPTH];
+    a.off_crec = c->h_img[r][PPE_IMG_W_OFFCREC];
+    a.off_idtab = c->h_img[r][PPE_IMG_W_OFFIDTAB];
+    a.crec_lds = plan.crec_lds;
+    a.idtab_lds = plan.idtab_lds;
     a.max_groups = c->max_groups;
     a.max_depth = c->h_img[r][PPE_IMG_W_MAXDEPTH];
     a.max_leaf = c->h_img[r][PPE_IMG_W_MAXLEAF];
@@ -497,10 +518,15 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         ppe_launch_classify(&a, grid, plan.mode, plan.pipe, (int)plan.block, fl != nullptr, (void *)s, (void *)e0,
                             (void *)e1);
     if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
-    if (use_ring) {  // every launch that reads the slot: a later rewrite waits for the last of them
-        HIPCHK(c, hipEventRecord(c->ring_ev[rslot], s));
-        c->ring_pending[rslot] = true;
-        c->ring_stream[rslot] = s;
+    if (use_ring) {  // every launch that reads the slot: a later rewrite waits for the last of them on each stream
+        hipEvent_t ev = nullptr;
+        for (auto &x : c->ring_readers[rslot])
+            if (x.first == s) ev = x.second;
+        if (!ev) {
+            HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            c->ring_readers[rslot].emplace_back(s, ev);
+        }
+        HIPCHK(c, hipEventRecord(ev, s));
     }
     return note_image_reader(c, r, s);
 }
@@ -563,7 +589,7 @@ int ppe_ctx_create(int device, ppe_ctx_t **out) {
     for (int i = 0; i < 2 && rc == PPE_OK; ++i)
         if (hipMalloc(&c->d_ring[i], sizeof(ppe_bdesc) * PPE_MAX_RING) != hipSuccess ||
             hipHostMalloc(&c->h_ring[i], sizeof(ppe_bdesc) * PPE_MAX_RING, hipHostMallocDefault) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ring_ev[i], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&c->ring_up[i], hipEventDisableTiming) != hipSuccess)
             rc = PPE_ENOMEM;
     if (rc == PPE_OK) {
         // empty rule set, management default action DROP (mgrplane/src/srv/srvnet/srv_rule.c:84)
@@ -590,7 +616,8 @@ int ppe_ctx_destroy(ppe_ctx_t *c) {
     for (int i = 0; i < 2; ++i) {
         if (c->d_ring[i]) (void)hipFree(c->d_ring[i]);
         if (c->h_ring[i]) (void)hipHostFree(c->h_ring[i]);
-        if (c->ring_ev[i]) (void)hipEventDestroy(c->ring_ev[i]);
+        if (c->ring_up[i]) (void)hipEventDestroy(c->ring_up[i]);
+        for (auto &x : c->ring_readers[i]) (void)hipEventDestroy(x.second);
     }
     for (hipStream_t s : c->pipe)
         if (s) (void)hipStreamDestroy(s);
@@ -1126,6 +1153,7 @@ int ppe_flow_destroy(ppe_ctx_t *c) {
     FlowTable *t = c->flow;
     for (FlowArrays &a : t->arr) flow_free_arrays(a);
     if (t->snap_h) (void)hipHostFree(t->snap_h);
+    if (t->pre_launch) (void)hipEventDestroy(t->pre_launch);
     (void)hipFree(t->ctl);
     (void)hipFree(t->rec);
     (void)hipFree(t->rslot);
@@ -1171,6 +1199,9 @@ int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
                          hipHostGetDevicePointer((void **)&t->snap_d, t->snap_h, 0) != hipSuccess))
         rc = fail(c, PPE_ENOMEM, "flow table: pinned snapshot buffer");
     if (rc == PPE_OK) std::memset(t->snap_h, 0, 64);
+    if (rc == PPE_OK &&
+        hipEventCreateWithFlags(&t->pre_launch, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess)
+        rc = fail(c, PPE_EIO, "flow table: event");
     t->cum_n.assign(FlowTable::kSnapRing, 0);
     t->cum_rev.assign(FlowTable::kSnapRing, 0);
     if (rc == PPE_OK) rc = flow_clear_arrays(c, t->arr[0], ns, nullptr);
@@ -1194,14 +1225,21 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         // The tombstone bound counts every packet of every batch since the snapshot as a possible revocation, so with
         // the host several batches ahead it passes the rehash threshold long before the table does.  Wait (bounded)
         // for the latest submitted batch's classify launch to publish its snapshot — one batch stays in flight, the
-        // queue does not drain — and decide on that tighter bound before synchronising.
-        const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
-        while (t.snap_used + 1u < t.batches && std::chrono::steady_clock::now() < until) flow_apply_snapshot(t);
+        // queue does not drain — and decide on that tighter bound before synchronising.  The host sleeps on the
+        // event recorded just before that launch (no busy spin), then polls briefly, pausing, for the
+        // snapshot the launch's first workgroup writes as it starts.
+        HIPCHK(c, hipEventSynchronize(t.pre_launch));
+        const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
+        while (t.snap_used + 1u < t.batches && std::chrono::steady_clock::now() < until) {
+            __builtin_ia32_pause();
+            flow_apply_snapshot(t);
+        }
     }
     rc = flow_maybe_rehash(c);
     if (rc != PPE_OK) return rc;
     const hipStream_t s = (hipStream_t)stream;
     const ppe_flowdev d = flow_dev(t, t.cur);
+    HIPCHK(c, hipEventRecord(t.pre_launch, s));
     // 1. decode, hash, FlowFind; found flows are accounted and forwarded, the rest get syn_check + ACL
     rc = launch(c, in, out, 1, cfg, s, 0, 0, &d);
     if (rc != PPE_OK) return rc;

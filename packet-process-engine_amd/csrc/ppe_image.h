@@ -1,5 +1,5 @@
 /*
- * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v5.
+ * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v6.
  *
  * The image is a HyperSplit-style binary decision tree over the five header dimensions, flattened in BFS order
  * (children of node k are numbered after k, so a walk strictly descends and always terminates), followed by the
@@ -15,7 +15,10 @@
  *  word 13  root key slot << 8 (the dimension the root splits on; PPE_NODE_LEAF when the root is a leaf)
  *  word 14  jump root: dim | shift << 8 | bits << 16, or 0 for a single tree rooted at node 0
  *  word 15  off_bsec: word offset of the block section (v5)   word 16  n_blocks   word 17  off_blocks (word offset,
- *           32-B aligned)   word 18  max_bdepth: most blocks on a root-to-leaf path   words 19..31 reserved
+ *           32-B aligned)   word 18  max_bdepth: most blocks on a root-to-leaf path
+ *  word 19  off_crec: word offset of the compact records (v6), 0 = the image has none
+ *  word 20  off_idtab: word offset of the slot → rule index table, 0 = slot == rule index for every slot
+ *  words 21..31 reserved
  *
  *  jump table (format v4; present iff word 14 != 0): 2^bits words right after the header.  A walk starts at
  *      bucket b = key[dim] >> shift: word b = the byte offset of that bucket's subtree root | its key slot << 24.
@@ -66,7 +69,7 @@
 #define PPE_IMAGE_H
 
 #define PPE_IMG_MAGIC   0x41455050u /* "PPEA" */
-#define PPE_IMG_VERSION 5u
+#define PPE_IMG_VERSION 6u
 #define PPE_IMG_HDR_WORDS 32u
 
 #define PPE_IMG_W_NNODES   2
@@ -86,9 +89,19 @@
 #define PPE_IMG_W_NBLOCKS  16
 #define PPE_IMG_W_OFFBLOCKS 17
 #define PPE_IMG_W_MAXBDEPTH 18
+#define PPE_IMG_W_OFFCREC  19
+#define PPE_IMG_W_OFFIDTAB 20
 
 #define PPE_BLK_WORDS 8u
 #define PPE_BLK_LEAF 0x80000000u  /* exit word: a leaf payload (else a block index) */
+#define PPE_CX_SLOT   0x00ffffffu  /* compact leaf exit fields (v6) */
+#define PPE_CX_DROP   (1u << 24)
+#define PPE_CX_TCP    (1u << 25)
+#define PPE_CX_UDP    (1u << 26)
+#define PPE_CX_S32    (1u << 27)
+#define PPE_CX_D32    (1u << 28)
+#define PPE_CX_NOHIT  (1u << 29)
+#define PPE_CREC_WORDS 4u
 
 #define PPE_NODE_WORDS 4u
 #define PPE_NODE_LEAF 5u          /* key slot of a leaf: the walk's zero key */

@@ -82,9 +82,13 @@ struct ppe_flow_kargs {
 
 /* Kernel launch parameters, passed by value. */
 struct ppe_kargs {
-    struct ppe_bdesc batch[PPE_MAX_BATCH];  /* [0, nbatch): processed in order by every wave, no barrier between */
+    struct ppe_bdesc batch[PPE_MAX_BATCH];  /* [0, nbatch) when nbatch <= PPE_MAX_BATCH.  The grid's waves split into
+                                               G = min(waves, nbatch, max_groups) batch groups that run concurrently:
+                                               group g takes batches g, g + G, ... in turn (no barrier between them),
+                                               its waves striding over each batch's tiles */
     const struct ppe_bdesc *ring;           /* non-NULL: the nbatch descriptors are ring[0, nbatch) in device memory
-                                               (one persistent launch over a whole queue of batches) */
+                                               (one persistent launch over a whole queue of batches, nbatch beyond
+                                               PPE_MAX_BATCH); batch[0] then repeats ring[0] */
     uint32_t nbatch;
     uint32_t max_tiles;       /* largest batch's tile count */
     const uint32_t *img;      /* device classifier image (ppe_image.h) */
@@ -99,6 +103,8 @@ struct ppe_kargs {
     uint32_t lds_blocks;      /* multi-tile walks: 2-level blocks [0, lds_blocks) are in LDS                        */
     uint32_t bsec_lds, blk_lds; /* LDS byte offsets (from the LDS image base) of the block section / of block 0     */
     uint32_t off_bsec, off_blocks, max_bdepth; /* image header words 15, 17, 18                                  */
+    uint32_t off_crec, off_idtab; /* image header words 19, 20: compact leaf records / slot → index table (0 = none) */
+    uint32_t crec_lds, idtab_lds; /* their LDS byte offsets from the LDS image base, ~0u = read from global memory   */
     uint32_t max_groups;      /* most batch groups of waves (concurrently streamed batches)                          */
     uint32_t part_layout;     /* 1: every batch writes verdict + flow hash + ACL hit and one partition list (fw_idx ==
                                  drop_idx), no tile counts, no tuple: the kernel variant with those checks compiled out */

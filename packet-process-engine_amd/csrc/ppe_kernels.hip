@@ -412,6 +412,9 @@ struct AclGeo {
     uint32_t lds_blocks;  // blocks [0, lds_blocks) in LDS
     uint32_t bsec_lds, blk_lds;  // LDS byte offsets from the staged image base: block jump table, block 0
     uint32_t off_bsec, off_blocks, max_bdepth;
+    // compact leaves (image v6): record / index-table word offsets (0 = none), and their LDS byte offsets from the
+    // staged image base (~0u = read from global memory)
+    uint32_t off_crec, off_idtab, crec_lds, idtab_lds;
 };
 
 // One level of the walk, node and key both in flight: the node's child pointer carries the child's key slot, so
@@ -587,6 +590,31 @@ __device__ __forceinline__ void acl_leaf(const uint32_t *__restrict__ gimg, cons
     }
 }
 
+// Compact leaf (image v6, ppe_image.h): `x` = the leaf exit of the block walk (slot and the candidate's flags).  One
+// 16-B record read (LDS when staged) and ~20 VALU: the address prefixes by their marker bits, the ports by packed
+// 16-bit spans, the protocol by the exit's TCP / UDP bits (only TCP / UDP packets reach the ACL here).
+template <int IMGB>
+__device__ __forceinline__ void acl_leaf_compact(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t x,
+                                                 uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport,
+                                                 bool tcp, int32_t &hit, bool &drop) {
+    const uint32_t slot = x & PPE_CX_SLOT;
+    const uint32_t ro = 16u * slot;
+    const uint4 r = g.crec_lds != ~0u ? lds_u128(IMGB + g.crec_lds + ro) : gld<uint4>(gimg, 4u * g.off_crec + ro);
+    // (a /32 compares every bit; else the bits above the marker: ~((lowbit << 1) - 1), 0 for a /0)
+    const uint32_t ms = (x & PPE_CX_S32) ? ~0u : ~(((r.x & (0u - r.x)) << 1) - 1u);
+    const uint32_t md = (x & PPE_CX_D32) ? ~0u : ~(((r.y & (0u - r.y)) << 1) - 1u);
+    const u16x2 kp = __builtin_bit_cast(u16x2, sport | (dport << 16)), lo = __builtin_bit_cast(u16x2, r.z),
+                sp = __builtin_bit_cast(u16x2, r.w);
+    const bool pp = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(kp - lo, sp)) == r.w;
+    const bool m = (((sip ^ r.x) & ms) == 0u) & (((dip ^ r.y) & md) == 0u) & pp &
+                   ((x & (tcp ? PPE_CX_TCP : PPE_CX_UDP)) != 0u);
+    uint32_t id = slot;
+    if (g.off_idtab)  // unused rule entries before this one: the slot's rule index from the table
+        id = g.idtab_lds != ~0u ? lds_u32(IMGB + g.idtab_lds + 4u * slot) : gld<uint32_t>(gimg, 4u * g.off_idtab + 4u * slot);
+    hit = (m & !(x & PPE_CX_NOHIT)) ? (int32_t)id : -1;
+    drop = m ? (x & PPE_CX_DROP) != 0u : g.default_action == ACL_RULE_ACTION_DROP;
+}
+
 // 5-way key select by key slot (multi-tile walks keep the keys in registers)
 __device__ __forceinline__ uint32_t key_sel(uint32_t d, const uint32_t (&k)[5]) {
     return d == 0u ? k[0] : d == 1u ? k[1] : d == 2u ? k[2] : d == 3u ? k[3] : d == 4u ? k[4] : 0u;
@@ -644,6 +672,7 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
                 if (x & PPE_BLK_LEAF) {
                     done[t] = true;
                     // leaf payload in node form: slot / sentinel, or first | count << 24 for leaf lists
+                    // (compact images: slot | flags, acl_leaf_compact)
                     nd[t].z = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF) : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
                 } else {
                     blk[t] = x;
@@ -892,7 +921,7 @@ void ppe_classify_kernel(ppe_kargs a) {
     TRACE_AT(1);
     const AclGeo geo = {a.lds_iters, a.max_depth, a.max_leaf, a.root_ks, a.off_leaf, a.off_rules, a.off_resid,
                         a.lds_words, a.default_action, a.jump, a.off_nodes, a.lds_blocks, a.bsec_lds, a.blk_lds,
-                        a.off_bsec, a.off_blocks, a.max_bdepth};
+                        a.off_bsec, a.off_blocks, a.max_bdepth, a.off_crec, a.off_idtab, a.crec_lds, a.idtab_lds};
 
     const uint64_t act_table = make_act_table(a.unsup_fw);
     // this batch's creator count, summed by the resolve kernel (which runs after this one)
@@ -998,8 +1027,15 @@ void ppe_classify_kernel(ppe_kargs a) {
                 const bool need[1] = {true};
                 uint4 nd[1];
                 acl_walk_blocks_mt<MODE, L::IMGB, 1>(a.img, geo, key, need, nd);
-                acl_leaf<MODE, L::IMGB>(a.img, geo, nd[0], k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts, p,
-                                        a.now, hit, rule_act);
+                if (geo.off_crec) {
+                    bool drop;
+                    acl_leaf_compact<L::IMGB>(a.img, geo, nd[0].z, k.sip, k.dip, k.sport, k.dport, k.proto == 6u,
+                                              hit, drop);
+                    rule_act = drop ? ACL_RULE_ACTION_DROP : ACL_RULE_ACTION_FW;
+                } else {
+                    acl_leaf<MODE, L::IMGB>(a.img, geo, nd[0], k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts,
+                                            p, a.now, hit, rule_act);
+                }
             } else {
                 lds_st32(lanebase + 256u * PPE_DIM_SIP, k.sip);
                 lds_st32(lanebase + 256u * PPE_DIM_DIP, k.dip);
@@ -1063,11 +1099,18 @@ void ppe_classify_kernel(ppe_kargs a) {
                     const uint32_t p = (tile << 6) + lane;
                     int32_t hit = -1;
                     if (need[t]) {
-                        uint32_t rule_act;
-                        const MacFromWindow mac = {B.hdr, p, B.stride};
-                        acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], k[t].sip, k[t].dip, k[t].sport, k[t].dport,
-                                                k[t].proto, mac, B.ts, p, a.now, hit, rule_act);
-                        k[t].st = rule_act == ACL_RULE_ACTION_DROP ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
+                        bool drop;
+                        if (geo.off_crec) {
+                            acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, k[t].sip, k[t].dip, k[t].sport, k[t].dport,
+                                                      k[t].proto == 6u, hit, drop);
+                        } else {
+                            uint32_t rule_act;
+                            const MacFromWindow mac = {B.hdr, p, B.stride};
+                            acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], k[t].sip, k[t].dip, k[t].sport, k[t].dport,
+                                                    k[t].proto, mac, B.ts, p, a.now, hit, rule_act);
+                            drop = rule_act == ACL_RULE_ACTION_DROP;
+                        }
+                        k[t].st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
                         k[t].flags |= PPE_F_ACL;
                     }
                     finish(tile, p, p < B.n, k[t], fh[t], hit, false);
@@ -1523,7 +1566,7 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
     const AclGeo geo = {0u, depth, a.img[PPE_IMG_W_MAXLEAF], a.img[PPE_IMG_W_ROOTKS], a.img[PPE_IMG_W_OFFLEAF],
                         a.img[PPE_IMG_W_OFFRULES], a.img[PPE_IMG_W_OFFRESID], MODE == IMG_LDS ? a.img_words : 0u,
                         a.default_action, a.img[PPE_IMG_W_JUMP], a.img[PPE_IMG_W_OFFNODES], 0u, 0u, 0u, 0u, 0u,
-                        0u};
+                        0u, 0u, 0u, ~0u, ~0u};
     for (uint32_t i = blockIdx.x * PPE_BLOCK + tid; i < a.n; i += gridDim.x * PPE_BLOCK) {
         const uint4 t = ((const uint4 *)a.tuple)[i];
         uint4 m = make_uint4(0, 0, 0, 0);

@@ -194,6 +194,9 @@ EXPORTED_DATA = ["rule_list", "dp_acl_action_default", "gWstDepth", "gAvgDepth",
 _lib = None
 
 
+ABI_VERSION = 3  # include/ppe_hip.h PPE_ABI_VERSION
+
+
 def load(path: str | os.PathLike | None = None) -> C.CDLL:
     """Load libppe_hip.so (raises OSError if it was not built — no fallback)."""
     global _lib
@@ -201,6 +204,8 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         return _lib
     p = Path(path) if path else Path(os.environ.get("PPE_LIB", LIB_PATH))
     lib = _open(p, C.RTLD_GLOBAL)
+    if lib.ppe_abi_version() != ABI_VERSION:  # structs below would not match the library's
+        raise OSError(f"{p}: ABI version {lib.ppe_abi_version()}, this binding expects {ABI_VERSION} (rebuild)")
     if path is None:
         _lib = lib
     return lib

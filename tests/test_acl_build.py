@@ -96,13 +96,13 @@ def test_large_ruleset_builds_bounded():
 
 
 def test_image_layout():
-    """Image format v5 (csrc/ppe_image.h): optional jump table after the 32-word header, 16-B nodes {threshold, left,
-    right, child key slots}, leaves as walk fixed points, the always-matching sentinel rule at slot n_rules, and the
-    2-level block section at the end."""
+    """Image format v6 (csrc/ppe_image.h): optional jump table after the 32-word header, 16-B nodes {threshold, left,
+    right, child key slots}, leaves as walk fixed points, the always-matching sentinel rule at slot n_rules, the
+    2-level block section, and the compact records after it (one candidate per leaf, no residual rules)."""
     for nrules in (64, 256):
         rules = synth.make_rules(nrules)
         img, st = abi.build_image(rules)
-        assert img[0] == 0x41455050 and img[1] == 5
+        assert img[0] == 0x41455050 and img[1] == 6
         assert img[2] == st["n_nodes"] and img[4] == nrules and img[11] == len(img)
         assert img[7] % 8 == 0  # rules 32-B aligned
         off = int(img[5])
@@ -141,14 +141,21 @@ def test_image_layout():
         # block section: after the residual records, its jump table (root block = root node index), 32-B blocks;
         # every non-leaf exit names a later block, every block but the roots is named exactly once
         ob, nb, oblk = int(img[15]), int(img[16]), int(img[17])
-        assert ob >= int(img[8]) and ob % 8 == 0 and oblk % 8 == 0 and oblk + 8 * nb == len(img)
+        oc, oi = int(img[19]), int(img[20])
+        assert oc == oblk + 8 * nb and oi == 0 and oc + 4 * (nrules + 1) == len(img)  # compact, no holes
+        assert ob >= int(img[8]) and ob % 8 == 0 and oblk % 8 == 0
         if jw:
             assert np.array_equal(img[ob:ob + (1 << bits)].astype(np.int64), (roots - 4 * off) // 16)
-        blk = img[oblk:].reshape(nb, 8)
+        blk = img[oblk:oc].reshape(nb, 8)
         ex = blk[:, 4:].astype(np.int64)
         inner_ex = ex[(ex & 0x80000000) == 0]
         assert np.array_equal(np.sort(inner_ex), np.arange(nroots, nb))
-        assert ((ex & 0x7FFFFFFF)[(ex & 0x80000000) != 0] <= nrules).all()
+        leaf_ex = ex[(ex & 0x80000000) != 0]
+        slot = leaf_ex & 0xFFFFFF
+        assert (slot <= nrules).all()
+        assert (((leaf_ex >> 29) & 1) == (slot == nrules)).all()  # NOHIT exactly on the sentinel
+        crec = img[oc:].reshape(nrules + 1, 4)
+        assert np.array_equal(crec[nrules], [0x80000000, 0x80000000, 0, 0xFFFFFFFF])
 
 
 def test_long_leaf_list_escape():
@@ -194,3 +201,30 @@ def test_jump_root_equals_linear(monkeypatch, jump, nrules, resid, any_ip):
     jw = int(img[14])
     assert (jw >> 16) & 0xFF == int(jump) and (jump == "0") == (jw == 0)
     assert (lin["acl_hit"] >= 0).sum() > 500
+
+
+@pytest.mark.parametrize("compact", ["1", "0"])
+def test_compact_leaves_edge_cases(monkeypatch, compact):
+    """Compact leaf exits and 16-B records (image v6) against the linear definition: prefix lengths 0, 1, 31 and 32
+    (the /32 flag), protocol ranges containing 6 and / or 17 or neither (only TCP / UDP reach the ACL), actions other
+    than 0 / 1 (only DROP drops), unused entries (the slot → index table), default FW and DROP; and the same rules
+    built without compact leaves (PPE_COMPACT=0, the v5 leaf path)."""
+    monkeypatch.setenv("PPE_COMPACT", compact)
+    rng = np.random.default_rng(77)
+    n = 1500
+    r = synth.make_rules(n, seed=78)
+    r["sip_mask"] = rng.choice([0, 1, 2, 8, 24, 30, 31, 32], n)
+    r["dip_mask"] = rng.choice([0, 1, 16, 31, 32], n)
+    pr = rng.integers(0, 6, n)
+    r["protocol_start"] = np.choose(pr, [6, 17, 0, 5, 7, 18])
+    r["protocol_end"] = np.choose(pr, [6, 17, 255, 7, 16, 255])
+    r["action"] = rng.choice([0, 1, 2, 0xFFFF], n)
+    used = (rng.random(n) < 0.8).astype(np.uint8)
+    for da in (0, 1):
+        pk = synth.make_packets(8000, r, seed=79 + da, kind="imix", stride=128, malformed_frac=0.02, hit_frac=0.9)
+        img, st, lin = compare(r, used, pk, default_action=da)
+        assert (int(img[19]) != 0) == (compact == "1") and (int(img[20]) != 0) == (compact == "1")
+        assert (lin["acl_hit"] >= 0).sum() > 2000
+        # every protocol kind and prefix kind is hit
+        hit = lin["acl_hit"][lin["acl_hit"] >= 0]
+        assert len(np.unique(pr[hit])) >= 4 and (r["sip_mask"][hit] == 32).any() and (r["sip_mask"][hit] == 0).any()

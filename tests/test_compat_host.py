@@ -120,3 +120,61 @@ def test_bursts_are_per_thread(lib):
     base = C.addressof(mb)
     assert sorted((a - base) // C.sizeof(abi.Mbuf) for a in got["drop"]) == [3, 4, 5]
     assert lib.Decode_Flush() == -19 and len(got["drop"]) == 6
+
+
+def test_allocation_failures_still_reach_the_drop_hook(lib):
+    """an allocation failure anywhere on the Decode path must not lose an mbuf.  With the test hook
+    ppe_compat_debug_fail_alloc(k) the next k allocations fail: a flush whose classify buffers cannot be allocated
+    returns PPE_ENOMEM and hands every queued mbuf to the drop hook; a Decode() whose burst cannot grow drops that
+    one packet at once; afterwards the path works again."""
+    lib.ppe_compat_debug_fail_alloc.argtypes = [C.c_uint32]
+    got = {}
+    hooks = install(lib, got)  # noqa: F841
+    mb = (abi.Mbuf * 12)()
+    base = C.addressof(mb)
+    idx = lambda key: sorted((a - base) // C.sizeof(abi.Mbuf) for a in got.get(key, []))  # noqa: E731
+    lib.Decode_Set_Burst(100)
+    for i in range(5):
+        lib.Decode(C.byref(mb[i]))
+    lib.ppe_compat_debug_fail_alloc(1)  # the flush's first buffer
+    assert lib.Decode_Flush() == -12  # PPE_ENOMEM
+    assert idx("drop") == [0, 1, 2, 3, 4]
+    assert lib.Decode_Flush() == 0  # nothing left queued
+    # the burst array was handed back to the burst; a fresh thread's first Decode must allocate it
+    res = []
+
+    def fresh():
+        lib.ppe_compat_debug_fail_alloc(1)
+        lib.Decode(C.byref(mb[5]))  # the burst cannot grow: dropped at once
+        res.append(idx("drop"))
+        lib.Decode(C.byref(mb[6]))
+        res.append(lib.Decode_Flush())  # no context: PPE_ENODEV, mb[6] dropped
+    t = threading.Thread(target=fresh)
+    t.start()
+    t.join(10)
+    assert res[0] == [0, 1, 2, 3, 4, 5] and res[1] == -19
+    assert idx("drop") == list(range(7)) and "fw" not in got and "punt" not in got
+    lib.ppe_compat_debug_fail_alloc(0)
+
+
+def test_thread_exit_flushes_its_burst(lib):
+    """A thread that exits with mbufs queued delivers them (the burst's TLS destructor), exactly once."""
+    got = {}
+    hooks = install(lib, got)  # noqa: F841
+    mb = (abi.Mbuf * 3)()
+    lib.Decode_Set_Burst(100)
+
+    def worker():
+        for i in range(3):
+            lib.Decode(C.byref(mb[i]))
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join(10)
+    # (Python's join returns when the thread's interpreter state is gone; the TLS destructors run just after)
+    import time
+    for _ in range(200):
+        if len(got.get("drop", [])) >= 3:
+            break
+        time.sleep(0.01)
+    base = C.addressof(mb)
+    assert sorted((a - base) // C.sizeof(abi.Mbuf) for a in got["drop"]) == [0, 1, 2]

@@ -192,6 +192,61 @@ def test_config_batches_vs_oracle(eng, cfgname, n):
     check_compaction(res, n)
 
 
+BENCH_SAMPLE = {"C1": 1 << 16, "C2": 1 << 16, "C3": 1 << 14, "C4": 1 << 16}
+
+
+@pytest.mark.parametrize("cfgname", ["C1", "C2", "C3", "C4"])
+def test_config_exact_workload_vs_oracle(eng, cfgname):
+    """The exact bench workload of each BASELINE config (bench.py's Resident: the two generated 1M-packet batches of
+    rank 0 with the bench's seeds, the config's packet kind and rule count, 64-B windows, the partition-list layout),
+    through ppe_classify_batches as the bench calls it: 34 descriptors over the two batches (more than the 32 the
+    kernel arguments hold: the device descriptor ring, batch groups running different batches at once), every
+    descriptor with its own outputs.  The first BENCH_SAMPLE packets of each batch, and a strided sample of the rest,
+    must equal the oracle's LINEAR first-match definition (not a walk of the GPU's own image); every descriptor of a
+    batch must equal that batch's first descriptor bit for bit.  Reference semantics: flow.c:204-237 (syn_check,
+    then the ACL on a flow miss; every packet a miss on the stateless path)."""
+    c = synth.CONFIGS[cfgname]
+    n = c["n"]
+    rules = synth.make_rules(c["rules"])
+    eng.commit(rules, default_action=1)
+    eng.tuning(batches_per_launch=0)
+    host = [synth.make_packets(n, rules, seed=synth.SEED + 1 + 7919 * g, kind=c["kind"], stride=64) for g in range(2)]
+    dev_in = [(torch.from_numpy(pk["hdr"]).to(DEV), torch.from_numpy(pk["len"].view(np.int32)).to(DEV)) for pk in host]
+    ndesc = 34
+    outs, bats, ress = [], [], []
+    for d in range(ndesc):
+        th, tl = dev_in[d % 2]
+        o = {k: torch.full((n,), -7, dtype=torch.int32, device=DEV) for k in ("verdict", "flow_hash", "acl_hit", "part")}
+        outs.append(o)
+        bats.append(abi.Batch(th.data_ptr(), tl.data_ptr(), None, n, 64))
+        ress.append(abi.Result(o["verdict"].data_ptr(), o["flow_hash"].data_ptr(), o["acl_hit"].data_ptr(),
+                               o["part"].data_ptr(), o["part"].data_ptr(), None, None))
+    ins, rs = (abi.Batch * ndesc)(*bats), (abi.Result * ndesc)(*ress)
+    cfg = eng.cfg(now_seconds=NOW)
+    s = torch.cuda.current_stream(DEV)
+    eng.clear_counters()
+    assert eng.lib.ppe_classify_batches(eng.ctx, ins, rs, ndesc, C.byref(cfg), C.c_void_p(s.cuda_stream)) == 0
+    torch.cuda.synchronize()
+    assert eng.counters()["pkts"] == ndesc * n
+    o = pyoracle.Oracle(rules, default_action=1)
+    m = BENCH_SAMPLE[cfgname]
+    for g, pk in enumerate(host):
+        got = {k: outs[g][k].cpu().numpy() for k in outs[g]}
+        got = {k: (v if k == "acl_hit" else v.view(np.uint32)) for k, v in got.items()}
+        for d in range(g + 2, ndesc, 2):  # every descriptor over this batch wrote the same outputs
+            for k in outs[d]:
+                assert torch.equal(outs[d][k], outs[g][k]), (cfgname, d, k)
+        idx = np.concatenate([np.arange(m), np.arange(m, n, max(1, (n - m) // m))])
+        ref = o.classify_batch(pk["hdr"][idx], pk["len"][idx], cfg=o.cfg(0, 1, NOW), nthreads=16)
+        far = ref["reach"] > 64
+        for k in ("verdict", "flow_hash", "acl_hit"):
+            gk = got[k][idx]
+            assert np.array_equal(gk[~far], ref[k][~far]), (cfgname, g, k, np.nonzero(gk[~far] != ref[k][~far])[0][:5])
+        assert ((got["verdict"][idx][far] & 0xFF) == ST["WINDOW_PUNT"]).all()
+        assert (got["acl_hit"][idx] >= 0).sum() > len(idx) // 8  # the sample exercises rule hits, not just misses
+        check_partition({"verdict": got["verdict"][:m], "part_idx": got["part"][:m]}, m)
+
+
 def test_c3_64k_rules_vs_oracle(eng):
     rules = synth.make_rules(65536)
     pk = synth.make_packets(100_000, rules, seed=32, stride=64)
@@ -202,8 +257,9 @@ def test_c3_64k_rules_vs_oracle(eng):
     o = pyoracle.Oracle(rules, default_action=1, image=img)
     ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16, use_tree=True)
     assert_same(res, ref)
-    lin = o.classify_batch(pk["hdr"][:3000], pk["len"][:3000], cfg=o.cfg(0, 1, NOW), nthreads=16)
-    assert np.array_equal(res["acl_hit"][:3000], lin["acl_hit"])
+    # the compiler too, not only the walk: 16,384 packets against the linear first-match definition
+    lin = o.classify_batch(pk["hdr"][:16384], pk["len"][:16384], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    assert_same({k: v[:16384] for k, v in res.items()}, lin)
     # the single-tile block walk (pipeline 5): fewer block levels in LDS, the rest from L2
     old = eng.tuning()
     try:
