@@ -31,6 +31,7 @@ ACL) timed on this host's cores as pinned run-to-completion pthreads (rank 0, N 
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -95,6 +96,8 @@ def parse(argv=None):
     ap.add_argument("--config", default="C1", choices=sorted(synth.CONFIGS))
     ap.add_argument("--configs", default=",".join(EXTRA_CONFIGS),
                     help="extra stateless configs measured after --config and nested in the line ('' = none)")
+    ap.add_argument("--stateful", default="F1,D1",
+                    help="stateful configs (flow table, reassembly) nested in the default line ('' = none)")
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"))
     ap.add_argument("--packets", "--n", dest="n", type=int, default=0,
                     help="packets per GPU per step (default: the config's; strong: 8M / ranks)")
@@ -231,6 +234,103 @@ def parity_sample(eng, res, rules, name):
                 and np.array_equal(got_p, want_part)), m
 
 
+class _CalibBatch(ctypes.Structure):  # csrc/ppe_calib.hip ppe_calib_batch
+    _fields_ = [("hdr", ctypes.c_void_p), ("len", ctypes.c_void_p), ("o0", ctypes.c_void_p), ("o1", ctypes.c_void_p),
+                ("o2", ctypes.c_void_p), ("o3", ctypes.c_void_p), ("n", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+class _CalibArgs(ctypes.Structure):  # ppe_calib_args
+    _fields_ = [("b", _CalibBatch * 32), ("nb", ctypes.c_uint32), ("mode", ctypes.c_uint32), ("clk", ctypes.c_void_p)]
+
+
+def sample_clocks(busy):
+    """sclk / mclk (MHz) from rocm-smi, sampled while `busy()` keeps the GPU loaded (relaunched until rocm-smi has
+    answered, at most a few seconds).  None where the tool is absent or says nothing parseable."""
+    import re
+    try:
+        p = subprocess.Popen(["rocm-smi", "--showclocks", "--json"], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                             text=True)
+    except OSError:
+        return {}
+    t0 = time.perf_counter()
+    while p.poll() is None and time.perf_counter() - t0 < 8.0:
+        busy()
+    try:
+        out, _ = p.communicate(timeout=5)
+        card = next(iter(json.loads(out).values()))
+    except Exception:
+        return {}
+    got = {}
+    for k, v in card.items():
+        m = re.search(r"(\d+)\s*Mhz", str(v), re.I)
+        if m and k.lower().startswith(("sclk", "mclk", "fclk")):
+            got[k.split()[0].lower() + "_mhz"] = int(m.group(1))
+    return got
+
+
+def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
+    """Same-run memory ceilings beside the classify launch: the kernel's own traffic with no decode / ACL
+    work (skeleton: 52 + 4 B read and four 4-B results written per packet, one persistent launch over the same
+    resident batches), the reads alone (read-only), and a 16-B-per-lane copy of 1 GiB; each with the shader clock it
+    ran at (in-kernel s_memtime over s_memrealtime), plus rocm-smi's sclk / mclk sampled under load."""
+    import ctypes as C
+    lib = C.CDLL(str(ROOT / "packet-process-engine_amd" / "libppe_calib.so"))
+    lib.ppe_calib_stream_timed.argtypes = [C.POINTER(_CalibArgs), C.c_uint32, C.c_void_p, C.POINTER(C.c_double)]
+    lib.ppe_calib_copy_timed.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_void_p,
+                                         C.POINTER(C.c_double)]
+    stream = torch.cuda.current_stream(dev)
+    sptr = C.c_void_p(stream.cuda_stream)
+    clk = torch.zeros(4, dtype=torch.int64, device=dev)
+    nb = min(args.steps, 32, res.nbufs)
+    a = _CalibArgs()
+    for i in range(nb):
+        hdr, lens, out = res.bufs[i][:3]
+        a.b[i] = _CalibBatch(hdr.data_ptr(), lens.data_ptr(), out["verdict"].data_ptr(), out["flow_hash"].data_ptr(),
+                             out["acl_hit"].data_ptr(), out["part_idx"].data_ptr(), res.n, 0)
+    a.nb, a.clk = nb, clk.data_ptr()
+    pk = res.n * nb
+
+    def sclk():
+        c = clk.cpu().tolist()
+        return round((c[1] - c[0]) / max(c[3] - c[2], 1) * 100.0, 0)
+
+    def stream_run(mode):
+        a.mode = mode
+        ms, t = C.c_double(), []
+        for _ in range(3):  # one warm launch, then the faster of two
+            if lib.ppe_calib_stream_timed(C.byref(a), 0, sptr, C.byref(ms)) != 0:
+                raise RuntimeError("ppe_calib_stream failed")
+            t.append(ms.value)
+        return min(t[1:]), sclk()
+
+    skel_ms, skel_clk = stream_run(0)
+    ro_ms, ro_clk = stream_run(1)
+    nbytes = 1 << 30
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    ms = C.c_double()
+    cms = []
+    for _ in range(3):
+        if lib.ppe_calib_copy_timed(src.data_ptr(), dst.data_ptr(), nbytes, 0, clk.data_ptr(), sptr, C.byref(ms)):
+            raise RuntimeError("ppe_calib_copy failed")
+        cms.append(ms.value)
+    copy_ms, copy_clk = min(cms[1:]), sclk()
+    del src, dst
+    clocks = sample_clocks(lambda: lib.ppe_calib_stream_timed(C.byref(a), 0, sptr, C.byref(ms)))
+    torch.cuda.synchronize()
+    us_1m = lambda t: round(t * 1e3 / (pk / (1 << 20)), 3)  # noqa: E731
+    return {
+        "skeleton": {"us_per_1M_packets": us_1m(skel_ms), "frac": round(alg * pk / (skel_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "real_GBps": round(84.0 * pk / (skel_ms / 1e3) / 1e9, 1), "sclk_mhz": skel_clk,
+                     "bytes_per_pkt": "52 + 4 read, 16 written (the kernel's own traffic)"},
+        "read_only": {"us_per_1M_packets": us_1m(ro_ms), "real_GBps": round(56.0 * pk / (ro_ms / 1e3) / 1e9, 1),
+                      "frac_at_68B": round(68.0 * pk / (ro_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "sclk_mhz": ro_clk},
+        "copy": {"GBps": round(2.0 * nbytes / (copy_ms / 1e3) / 1e9, 1), "bytes": nbytes, "sclk_mhz": copy_clk},
+        "kernel_over_skeleton": round(skel_ms / (kern_avg_ms * nb * res.n / pk_launch), 4),
+        "launch_packets": pk, "rocm_smi_under_load": clocks,
+    }
+
+
 def traffic_per_packet(name):
     """HBM bytes per packet of this config's launch from the committed rocprofv3 profile (tools/collect_traffic.py
     output: FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE, calibrated), or None."""
@@ -241,6 +341,29 @@ def traffic_per_packet(name):
     if tj.get("n_packets"):
         return tj["traffic_bytes"] / tj["n_packets"]
     return None
+
+
+WARM_SECONDS = 0.25
+
+
+def warm_up(fn, seconds=WARM_SECONDS):
+    """The W untimed warmup steps, repeated until the GPU has been busy for `seconds`: after the seconds of host-side
+    input generation before every config the GPU idles at low clocks, and one short warmup launch (~0.1 ms) does
+    not ramp them up before the timed region starts (a 24.5-us hole in C1's timed call only)."""
+    t0 = time.perf_counter()
+    while True:
+        fn()
+        torch.cuda.synchronize()
+        if time.perf_counter() - t0 >= seconds:
+            return
+
+
+def gpu_busy(dev, seconds=WARM_SECONDS):
+    """Memory-bound filler work right before a stateful config's timed region (its warmup steps change the table, so
+    they are not repeated): the same clock ramp as warm_up()."""
+    x = torch.empty(64 << 20, dtype=torch.int32, device=dev)
+    warm_up(lambda: x.add_(1), seconds)
+    del x
 
 
 def measure_config(name, args, dev, world, rank, dist, primary):
@@ -282,7 +405,7 @@ def measure_config(name, args, dev, world, rank, dist, primary):
         torch.cuda.synchronize()
 
     warm, timed = res.arrays(max(args.warmup, 1)), res.arrays(args.steps)
-    run(warm)
+    warm_up(lambda: run(warm))
     # timed region (value): K batches, barrier + synchronize on both sides
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
@@ -331,6 +454,11 @@ def measure_config(name, args, dev, world, rank, dist, primary):
                 "build_ms": round(acl["build_ms"], 3)},
         "launch": eng.launch_info(),
     }
+    if primary and rank == 0:
+        try:
+            out["roofline"]["ceiling"] = ceiling(res, args, dev, kern_avg_ms, pk_launch, alg)
+        except Exception as e:  # the ceiling is context, never worth losing the line over
+            out["roofline"]["ceiling"] = {"error": str(e)[:200]}
     ctx = dict(eng=eng, res=res, rules=rules, cfg=cfg, n=n, my_ms=my_ms)
     if not primary:
         eng.close()
@@ -438,6 +566,15 @@ def run_stateless(args, dev, world, rank, dist):
             extra[name], _ = measure_config(name, args, dev, world, rank, dist, primary=False)
         except Exception as e:  # one config failing must not lose the headline line
             extra[name] = {"error": str(e)[:300]}
+    # the stateful paths: the flow table (FlowHandlePacket) and IPv4 reassembly
+    # (Defrag), each with its own roofline and parity sample
+    for name in [c for c in args.stateful.split(",") if c] if args.n == 0 else []:
+        fn = run_flow if "flows" in synth.CONFIGS[name] else run_defrag
+        try:
+            extra[name] = fn(args, synth.CONFIGS[name], dev, world, rank, dist, name=name, nested=True)
+        except Exception as e:
+            extra[name] = {"error": str(e)[:300]}
+        torch.cuda.empty_cache()
 
     if rank == 0:
         rf = line_cfg["roofline"]
@@ -480,12 +617,15 @@ def flow_bytes(stride: int) -> float:
     return rd + wr + 4.0 + 16.0 + 32.0 + 8.0 + 8.0 / 64.0
 
 
-def run_flow(args, cfgd, dev, world, rank, dist):
+def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     """--config F1: ppe_classify_flow batch after batch (one stream: each batch sees the table the previous ones
-    left) over a fixed population of bidirectional flows established during the warmup."""
+    left) over a fixed population of bidirectional flows established during the warmup.  nested: measured after the
+    stateless configs of the default line and returned as its configs.F1 entry (no CPU baseline; at N > 1 every
+    rank owns its flows, as the reference's cores do behind the NIC's flow steering: no exchange)."""
     import ctypes as C
     from ppe import abi
-    n = args.n or cfgd["n"]
+    name = name or args.config
+    n = (0 if nested else args.n) or cfgd["n"]
     stride = args.stride
     rules = synth.make_rules(cfgd["rules"])
     flows = cfgd["flows"]
@@ -495,7 +635,7 @@ def run_flow(args, cfgd, dev, world, rank, dist):
     # N = 1: one flow population.  N > 1: the ranks share one population and every batch is steered by flow hash
     # to the owning GPU (ppe.dist.steered_classify_flow: all-to-all over RCCL), so flows span ranks as on a NIC that
     # does not steer by flow
-    steer = world > 1
+    steer = world > 1 and not nested
     tseed = synth.SEED + 977 * (1 if steer else rank + 1)
 
     # parity sample first: a fresh table, four 64k batches, against the oracle's sequential flow table
@@ -564,6 +704,7 @@ def run_flow(args, cfgd, dev, world, rank, dist):
 
     for i in range(max(args.warmup, 1)):
         step(i)
+    gpu_busy(dev)
     eng.clear_counters()
     new0 = eng.flow_info()["new_flow"]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -598,7 +739,7 @@ def run_flow(args, cfgd, dev, world, rank, dist):
     achieved = bpp * n / (kern_avg_ms / 1e3) / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not nested:
         import pyoracle
         pk = bufs[0][4]
         o = pyoracle.Oracle(rules, default_action=abi.ACL_RULE_ACTION_FW, image=eng.image())
@@ -615,18 +756,20 @@ def run_flow(args, cfgd, dev, world, rank, dist):
                          f"{n}-packet batch after the flows were established ({n * reps} packets, {cpu_s:.1f} s); the "
                          f"reference keeps one table per core, so cores scale it by flow-hash sharding"}
 
+    line = None
     if rank == 0:
+        tpp = traffic_per_packet(name)
         line = {
             "metric": FLOW_METRIC, "value": round(mpps, 2), "unit": "Mpps", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(my_ms / args.steps, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"{args.config}: {n} x 64B IPv4/UDP packets per GPU per batch over {flows} "
+            "config": {"workload": f"{name}: {n} x 64B IPv4/UDP packets per GPU per batch over {flows} "
                                    f"bidirectional flows, {cfgd['rules']} five-tuple ACL rules, default FW",
                        "packets_per_gpu": n, "flows": flows, "rules": cfgd["rules"], "resident_batches": nbufs,
                        "parallelism": f"flow-sharded x{world}" + (" (all-to-all steering by flow hash)" if steer else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": round(traffic_per_packet(args.config) * n) if traffic_per_packet(args.config) else None,
+                         "traffic": round(tpp * n) if tpp else None,
                          "kernel": "ppe_classify_kernel<FLOW> (FlowFind + accounting; misses resolved by the flow "
                                    "kernels)",
                          "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": bpp,
@@ -638,8 +781,11 @@ def run_flow(args, cfgd, dev, world, rank, dist):
             "counters": {k: cnt[k] for k in ("pkts", "acl_fw", "acl_drop", "flow_proc_ok", "flow_proc_fail",
                                              "flow_node_nomem")},
         }
-        print(json.dumps(line), flush=True)
+        if not nested:
+            print(json.dumps(line), flush=True)
     eng.close()
+    if nested:
+        return nested_line(line)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -661,14 +807,28 @@ def defrag_batch_variants(arena, off, lens, count):
     return pos, variant
 
 
-def run_defrag(args, cfgd, dev, world, rank, dist):
+def nested_line(line):
+    """A stateful config's own line, reduced to what a nested configs entry carries."""
+    if line is None:
+        return None
+    out = {k: line[k] for k in ("metric", "value", "unit", "ms_per_step", "roofline", "parity_sample_ok") if k in line}
+    out["workload"] = line["config"]["workload"]
+    for k in ("flow_table", "new_flows_in_timed_region", "counters", "defrag_info", "held_fragments_per_batch",
+              "new_fcb_in_timed_region", "fcb_full_in_timed_region"):
+        if k in line:
+            out[k] = line[k]
+    return out
+
+
+def run_defrag(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     """--config D1: ppe_defrag batch after batch on one stream.  Every batch is the same
     65,536-fragment slice of a make_fragment_stream mix with a different source-address byte, so every batch
     creates fresh FCBs (none meets an earlier batch's datagrams); the warmup's FCBs are aged out before the timed
     region.  N > 1: each rank reassembles its own batches (fragments are steered to GPUs by (sip, dip, ip_id)
     upstream, as the reference's cores own their FCB tables), weak scaling with no data-path collective."""
     from ppe import Defrag
-    n = args.n or cfgd["n"]
+    name = name or args.config
+    n = (0 if nested else args.n) or cfgd["n"]
     hdr_stride = 128
     nvar = max(args.warmup, 1) + args.steps
     if nvar > 255:
@@ -738,6 +898,7 @@ def run_defrag(args, cfgd, dev, world, rank, dist):
         step(i, NOW)
     torch.cuda.synchronize()
     d.age(NOW + 10**6, 20)   # free the warmup's FCBs (Frag_defrag_timeout), untimed
+    gpu_busy(dev)
     info0 = d.info()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
@@ -776,7 +937,7 @@ def run_defrag(args, cfgd, dev, world, rank, dist):
     achieved = bytes_call / (call_ms / 1e3) / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not nested:
         import pyoracle
         o = pyoracle.OracleDefrag(fcb_max=cfgd["fcb_max"])
         host = [variant(v + 2) for v in range(min(nvar, 16))]
@@ -800,12 +961,13 @@ def run_defrag(args, cfgd, dev, world, rank, dist):
                          f"assembled) over the {n}-fragment batch ({n * reps} fragments, {cpu_s:.1f} s); the "
                          f"reference keeps one FCB table per core"}
 
+    line = None
     if rank == 0:
         line = {
             "metric": DEFRAG_METRIC, "value": round(mfps, 2), "unit": "Mfps", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(call_ms, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"{args.config}: {n} IPv4 fragments per GPU per batch (make_fragment_stream mix: "
+            "config": {"workload": f"{name}: {n} IPv4 fragments per GPU per batch (make_fragment_stream mix: "
                                    f"UDP/TCP/ICMP, reordered, duplicated, lost, overlapping, oversize), "
                                    f"fcb_max {cfgd['fcb_max']}, cache_max {cm}",
                        "fragments_per_gpu": n, "mean_frame_bytes": round(frame_bytes / n, 1),
@@ -822,9 +984,12 @@ def run_defrag(args, cfgd, dev, world, rank, dist):
             "new_fcb_in_timed_region": int(info["new_fcb"] - info0["new_fcb"]),
             "fcb_full_in_timed_region": int(info["st_fcb_full"] - info0["st_fcb_full"]),
         }
-        print(json.dumps(line), flush=True)
+        if not nested:
+            print(json.dumps(line), flush=True)
     d.close()
     eng.close()
+    if nested:
+        return nested_line(line)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -55,8 +55,10 @@ typedef struct TCPOpt_ {
 
 typedef struct TCPVars_ {
     TCPOpt tcp_opts[1];
-    TCPOpt *ws;
+    TCPOpt *ws;                /* the window-scale option DecodeTCPOptions recorded (decode-tcp.c:61-70), filled by
+                                  Decode from the kernel's option parse; NULL (as allocated) when there is none */
 } TCPVars;
+#define TCP_OPTS tcpvars.tcp_opts  /* m->TCP_OPTS[0], decode-tcp.c:66-68 */
 #endif
 
 typedef void (*FreeAlState)(void *s);

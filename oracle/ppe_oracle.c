@@ -467,8 +467,9 @@ static int decode_udp(omb_t *m, const uint8_t *pkt, uint16_t len) {
     return DEC_OK;
 }
 
-/* dataplane/src/decode/decode-tcp.c:18-131 — only the window-scale option is recorded; no verdict effect */
-static void decode_tcp_options(omb_t *m, const uint8_t *pkt, uint16_t len) {
+/* dataplane/src/decode/decode-tcp.c:18-131 — only the window-scale option is recorded (:61-70: the first valid one,
+ * a duplicate is ignored), as its byte offset from the TCP header `th`; no verdict effect */
+static void decode_tcp_options(omb_t *m, const uint8_t *th, const uint8_t *pkt, uint16_t len) {
     uint16_t plen = len;
     while (plen) {
         const uint32_t off = (uint32_t)(pkt - m->frame);
@@ -478,7 +479,7 @@ static void decode_tcp_options(omb_t *m, const uint8_t *pkt, uint16_t len) {
         if (plen < 2) break;
         const uint8_t ol = off + 1 < m->avail ? pkt[1] : 0;
         if (ol > plen || ol < 2) return;
-        if (t == 3 && ol == 3) m->r->tcp_ws = 1;
+        if (t == 3 && ol == 3 && !m->r->tcp_ws) m->r->tcp_ws = (uint32_t)(pkt - th);
         pkt += ol;
         plen = (uint16_t)(plen - ol);
     }
@@ -505,7 +506,7 @@ static int decode_tcp(omb_t *m, const uint8_t *pkt, uint16_t len) {
     }
     m->r->flags |= PPE_F_TCP;
     if (rd8(m, pkt + 13) & 0x02) m->r->flags |= PPE_F_SYN;  /* land / SYN-flood monitors pass at default config */
-    if (opt_len > 0) decode_tcp_options(m, pkt + 20, opt_len);
+    if (opt_len > 0) decode_tcp_options(m, pkt, pkt + 20, opt_len);
     m->r->sport = rd16(m, pkt);
     m->r->dport = rd16(m, pkt + 2);
     m->r->paylen = (uint16_t)(len - hlen);
@@ -704,7 +705,8 @@ static void *run_shard(void *arg) {
             s->tuple[4 * (size_t)i + 0] = r.sip;
             s->tuple[4 * (size_t)i + 1] = r.dip;
             s->tuple[4 * (size_t)i + 2] = r.sport | (r.dport << 16);
-            s->tuple[4 * (size_t)i + 3] = r.proto | (((r.flags & PPE_F_VLAN) ? 1u : 0u) << 8) | (r.paylen << 16);
+            s->tuple[4 * (size_t)i + 3] = r.proto | (((r.flags & PPE_F_VLAN) ? 1u : 0u) << 8) | (r.tcp_ws << 9) |
+                                          (r.paylen << 16);
         }
         for (int c = 0; c < 32; c++)
             if (r.counters & (1u << c)) s->counters[c]++;

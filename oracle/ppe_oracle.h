@@ -39,7 +39,8 @@ typedef struct {
     uint32_t sip, dip, sport, dport, proto, paylen;
     uint32_t counters;   /* bit i set = counter i (enum ppe_counter) incremented once */
     uint32_t reach;      /* 1 + highest frame byte offset the verdict depends on */
-    uint32_t tcp_ws;     /* 1 if DecodeTCPOptions recorded a window-scale option (informational) */
+    uint32_t tcp_ws;     /* byte offset (from the TCP header) of the window-scale option DecodeTCPOptions recorded
+                            (m->tcpvars.ws, decode-tcp.c:61-70), 0 = none; no verdict effect */
 } oracle_result_t;
 
 /* rule set used by oracle_classify (pointer kept; caller owns the memory) */

@@ -323,6 +323,21 @@ static int classify_mbufs(mbuf_t **mb, uint32_t n) {
                     m->dport = (uint16_t)(tuple[4 * i + 2] >> 16);
                     m->payload_len = (uint16_t)(tuple[4 * i + 3] >> 16);
                     m->flags |= PKT_HAS_FLOW;
+                    if (pkt) {  /* the header pointers DecodeIPV4 / DecodeTCP|UDP set (decode-ipv4.c:42, :131-157) */
+                        uint8_t *l3 = pkt + 14 + (m->vlan_idx ? 4 : 0);
+                        m->network_header = l3;
+                        m->transport_header = l3 + (l3[0] & 0x0fu) * 4u;
+                        /* DecodeTCPOptions' window-scale record (decode-tcp.c:61-70), found by the kernel: its offset
+                         * from the TCP header in bits 9-15 of the tuple */
+                        const uint32_t ws = (tuple[4 * i + 3] >> 9) & 0x7fu;
+                        if ((fl & PPE_F_TCP) && ws) {
+                            uint8_t *o = (uint8_t *)m->transport_header + ws;
+                            m->tcpvars.tcp_opts[0].type = o[0];
+                            m->tcpvars.tcp_opts[0].len = o[1];
+                            m->tcpvars.tcp_opts[0].data = o + 2;
+                            m->tcpvars.ws = &m->tcpvars.tcp_opts[0];
+                        }
+                    }
                 }
                 if (fl & PPE_F_FRAG) m->flags |= PKT_IP_FRAG;
             }

@@ -46,6 +46,9 @@
 #ifndef PPE_TRACE
 #define PPE_TRACE 0
 #endif
+#ifndef PPE_TUPLE_SELECT
+#define PPE_TUPLE_SELECT 0
+#endif
 // (trace the wave's tile iterations PPE_TRACE_SKIP .. + 3: a skip > 0 samples the steady state of a long launch)
 #ifndef PPE_TRACE_SKIP
 #define PPE_TRACE_SKIP 0u
@@ -222,10 +225,50 @@ __device__ __forceinline__ void ld_mac_sync(const uint8_t *q, uint32_t &a, uint3
     b = v.y;
     c = v.z;
 }
+__device__ __forceinline__ uint32_t ld_u32_sync(const uint32_t *q) {
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(q) : "memory");
+    return v;
+}
 __device__ __forceinline__ uint64_t ld_u64_sync(const uint64_t *q) {
     uint64_t v;
     asm volatile("global_load_dwordx2 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(q) : "memory");
     return v;
+}
+
+// DecodeTCPOptions (dataplane/src/decode/decode-tcp.c:18-131) over a TCP header's options in the window `row`:
+// opt = Dec.tcpopt.  Returns the byte offset of the first valid window-scale option (type 3, length 3) from the TCP
+// header, what the reference records as m->tcpvars.ws (:61-70, a duplicate is ignored), or 0.  Bytes past the
+// window or the wire length read as 0 (an EOL), like the oracle's.  Rare path (tuple output only): dword loads
+// with their own wait.
+__device__ __forceinline__ uint32_t tcp_ws_offset(const uint8_t *row, uint32_t opt) {
+    const uint32_t th = opt & 0xffu, avail = opt >> 16;
+    uint32_t plen = (opt >> 8) & 0xffu, pos = th + 20u, ws = 0, dwi = ~0u, dw = 0;
+    auto byte_at = [&](uint32_t b) -> uint32_t {
+        if (b >= avail) return 0u;
+        if ((b >> 2) != dwi) {
+            dwi = b >> 2;
+            dw = ld_u32_sync((const uint32_t *)row + dwi);
+        }
+        return (dw >> (8u * (b & 3u))) & 0xffu;
+    };
+#pragma unroll 1
+    while (plen) {
+        const uint32_t t = byte_at(pos);
+        if (t == 0u) break;  // EOL
+        if (t == 1u) {       // NOP
+            ++pos;
+            --plen;
+            continue;
+        }
+        if (plen < 2u) break;
+        const uint32_t ol = byte_at(pos + 1u);
+        if (ol > plen || ol < 2u) break;  // invalid length: return -1 (the option already recorded stays)
+        if (t == 3u && ol == 3u && ws == 0u) ws = pos - th;
+        pos += ol;
+        plen -= ol;
+    }
+    return ws;
 }
 
 // Where a residual MAC rule gets the packet's MACs: re-read from the header window (classify kernel: rare path, keeps
@@ -286,6 +329,7 @@ __device__ __forceinline__ uint32_t bin_counters(uint32_t key, uint64_t act_tabl
 struct Dec {
     uint32_t st, flags;
     uint32_t sip, dip, sport, dport, proto, paylen;
+    uint32_t tcpopt;  // TCP with options: window byte offset of the TCP header | option bytes << 8 | avail << 16
 };
 
 // Decode of one packet, straight-line: every check of the reference is evaluated, then the terminal status is
@@ -372,10 +416,23 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[13], uint32_t len32, c
     st = l2_bad ? (uint32_t)PPE_ST_L2_HEADER_ERR : st;
 
     const bool l4_ok = (st == ST_ACL) | (st == PPE_ST_FLOW_TCP_NO_SYN_FIRST);  // reached FlowHandlePacket
+    // DecodeTCPOptions (decode-tcp.c:175-177) runs for every TCP header that passed its length checks; only the
+    // tuple output reports what it records (the window-scale option), so the PART kernel never reads this
+    k.tcpopt = (l4_ok & is_tcp & (thl > 20u)) ? l4off | ((thl - 20u) << 8) | (min(len, stride) << 16) : 0u;
     k.st = st;
     k.flags = ((l2_ok & is_vl & (vlen >= 4u)) ? PPE_F_VLAN : 0u) | (l4_ok ? PPE_F_L4 : 0u) |
               ((l4_ok & is_tcp) ? PPE_F_TCP : 0u) | ((l4_ok & is_tcp & syn) ? PPE_F_SYN : 0u) |
               ((ip_ok & frag) ? PPE_F_FRAG : 0u);
+#if PPE_TUPLE_SELECT
+    // (diagnostic build, make variant VFLAGS=-DPPE_TUPLE_SELECT=1: the select form one round-2 variant build
+    // miscompiled, kept to re-test it; profiles/r2b_experiments.md)
+    k.sip = ip_ok ? sip : 0u;
+    k.dip = ip_ok ? dip : 0u;
+    k.proto = ip_ok ? proto : 0u;
+    k.sport = l4_ok ? sport : 0u;
+    k.dport = l4_ok ? dport : 0u;
+    k.paylen = l4_ok ? (is_tcp ? l4len - thl : l4len - 8u) : 0u;
+#else
     // zeroed by masks, not selects: the ROCm 7.2 compiler turned the select form into exec-masked blocks that left
     // dport zeroed for NO_SYN packets in some builds (tools/variant_diff.py caught it; the product build was right)
     const uint32_t ipm = ip_ok ? ~0u : 0u, l4m = l4_ok ? ~0u : 0u;
@@ -385,6 +442,7 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[13], uint32_t len32, c
     k.sport = sport & l4m;
     k.dport = dport & l4m;
     k.paylen = (is_tcp ? l4len - thl : l4len - 8u) & l4m;
+#endif
     return k;
 }
 
@@ -955,7 +1013,9 @@ void ppe_classify_kernel(ppe_kargs a) {
                 t.x = k.sip;
                 t.y = k.dip;
                 t.z = k.sport | (k.dport << 16);
-                t.w = k.proto | (((k.flags & PPE_F_VLAN) ? 1u : 0u) << 8) | (k.paylen << 16);
+                // bits 9-15: the window-scale option's offset in the TCP header (DecodeTCPOptions), 0 = none
+                const uint32_t ws = k.tcpopt ? tcp_ws_offset(B.hdr + (size_t)p * B.stride, k.tcpopt) : 0u;
+                t.w = k.proto | (((k.flags & PPE_F_VLAN) ? 1u : 0u) << 8) | (ws << 9) | (k.paylen << 16);
                 gst_nt<uint4>(B.tuple, 4u * po, t);
             }
         }

@@ -144,6 +144,14 @@ class DefragInfo(C.Structure):
         return d
 
 
+class TCPOpt(C.Structure):  # include/ppe_decode.h (decode-tcp.h:24-28)
+    _fields_ = [("type", C.c_uint8), ("len", C.c_uint8), ("data", C.c_void_p)]
+
+
+class TCPVars(C.Structure):  # decode-tcp.h:34-46: one option slot and the window-scale pointer
+    _fields_ = [("tcp_opts", TCPOpt * 1), ("ws", C.c_void_p)]
+
+
 class Mbuf(C.Structure):
     """include/ppe_decode.h mbuf_t: the reference's mbuf_t field order (dataplane/src/include/mbuf.h:23-87) plus the
     engine's appended results."""
@@ -154,7 +162,7 @@ class Mbuf(C.Structure):
                 ("eth_src", C.c_uint8 * 6), ("sip", C.c_uint32), ("dip", C.c_uint32), ("sport", C.c_uint16),
                 ("dport", C.c_uint16), ("proto", C.c_uint8), ("vlan_idx", C.c_uint8), ("payload_len", C.c_uint16),
                 ("vlan_id", C.c_uint16), ("defrag_id", C.c_uint16), ("timestamp", C.c_uint64),
-                ("payload", C.c_void_p), ("tcpvars", C.c_uint8 * 24), ("frag_offset", C.c_uint16),
+                ("payload", C.c_void_p), ("tcpvars", TCPVars), ("frag_offset", C.c_uint16),
                 ("tcp_reasm_overlap", C.c_uint16), ("pkt_totallen", C.c_uint32), ("flags", C.c_uint32),
                 ("fcb_hash", C.c_uint32), ("fcb", C.c_void_p), ("fragments", C.c_void_p), ("flow", C.c_void_p),
                 ("tcp_seg_raw", C.c_void_p), ("tcp_seg_raw_tail", C.c_void_p), ("tcp_seg_reassem", C.c_void_p),

@@ -148,10 +148,22 @@ def test_tcp_options_window_scale_no_verdict_effect(orc):
     opts = b"\x01\x03\x03\x07"  # NOP + WS(7)
     p = eth(0x0800) + ipv4(6, 1, 2, 24) + tcp(1, 2, off=6, opts=opts)
     r = run(orc, p)
-    assert r["status"] == ST["ACL_FW"] and r["tcp_ws"] == 1
+    # m->tcpvars.ws = the option at TCP header byte 21 (decode-tcp.c:61-70); the tuple carries it in bits 9-15
+    assert r["status"] == ST["ACL_FW"] and r["tcp_ws"] == 21
     bad = b"\x03\x09\x00\x00"  # option length past the option space: DecodeTCPOptions returns -1, ignored
     r = run(orc, eth(0x0800) + ipv4(6, 1, 2, 24) + tcp(1, 2, off=6, opts=bad))
-    assert r["status"] == ST["ACL_FW"]
+    assert r["status"] == ST["ACL_FW"] and r["tcp_ws"] == 0
+    cases = [
+        (b"\x02\x04\x05\xb4" + b"\x03\x03\x02" + b"\x01", 24),      # MSS, then WS at 24
+        (b"\x03\x03\x01" + b"\x03\x03\x09" + b"\x00\x00", 20),      # duplicate WS: the first is kept (:63-66)
+        (b"\x03\x04\x01\x01" + b"\x03\x03\x09\x00", 24),           # WS of length 4 is not recorded (:60-62)
+        (b"\x03\x03\x01" + b"\x08\x0a" + b"\x00" * 3, 20),            # recorded, then an invalid length (:43-47)
+        (b"\x00" + b"\x03\x03\x01" + b"\x00" * 4, 0),                  # EOL first: nothing after it is parsed
+        (b"\x01" * 7 + b"\x03", 0),                                     # a kind byte with no length byte left
+    ]
+    for opts, want in cases:
+        r = run(orc, eth(0x0800) + ipv4(6, 1, 2, 28) + tcp(1, 2, off=7, opts=opts))
+        assert r["status"] == ST["ACL_FW"] and r["tcp_ws"] == want, (opts, r["tcp_ws"])
 
 
 def test_syn_check(orc):  # flow.c:204-214
