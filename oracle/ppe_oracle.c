@@ -209,12 +209,18 @@ int32_t oracle_acl_blocks(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t d
     const uint32_t jw = im[PPE_IMG_W_JUMP];
     uint32_t b = jw ? im[im[PPE_IMG_W_OFFBSEC] + (key[jw & 0xffu] >> ((jw >> 8) & 0xffu))] : 0u;
     uint32_t x = 0;
+    const uint32_t K = im[PPE_IMG_W_BLKLV] == 3u ? 3u : 2u, npos = (1u << K) - 1u;
     for (int it = 0; it <= PPE_MAX_DEPTH + 1; it++) {
-        const uint32_t *w = im + im[PPE_IMG_W_OFFBLOCKS] + PPE_BLK_WORDS * b;
-        const int b0 = key[w[3] & 0xfu] > w[0];
-        const uint32_t k1 = (w[3] >> (b0 ? 8 : 4)) & 0xfu;
-        const int b1 = key[k1] > w[1 + b0];
-        x = w[4 + 2 * b0 + b1];
+        /* K levels per block: position p (children 2p + 1, 2p + 2), key slots at bits 4p of word 2^K - 1, exits
+         * after it indexed by the K comparison bits (ppe_image.h) */
+        const uint32_t *w = im + im[PPE_IMG_W_OFFBLOCKS] + (npos + 1u) * 2u * b;
+        uint32_t p = 0, e = 0;
+        for (uint32_t l = 0; l < K; l++) {
+            const uint32_t bit = key[(w[npos] >> (4u * p)) & 0xfu] > w[p];
+            e = 2u * e + bit;
+            p = 2u * p + 1u + bit;
+        }
+        x = w[npos + 1u + e];
         if (x & PPE_BLK_LEAF) break;
         b = x;
     }

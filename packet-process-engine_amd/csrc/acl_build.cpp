@@ -32,6 +32,10 @@
 
 namespace {
 
+// LDS bytes a 1024-thread multi-tile workgroup has for the block section and compact records (160 KiB less the
+// counter bins and the staging round-up): beyond it the image gets 3-level blocks
+constexpr uint32_t kBlock2LdsBudget = 158u * 1024u;
+
 struct Rule {
     uint32_t lo[PPE_NDIMS], hi[PPE_NDIMS];
     uint32_t id;
@@ -403,45 +407,70 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         return PPE_BLK_LEAF | slot | (compact ? cx_flags(slot) : 0u);
     };
     if (max_leaf > 1 && lwords.size() >= (1u << 23)) return PPE_ENOMEM;  // leaf exits hold 23-bit list offsets
-    std::vector<uint32_t> bwords, bnode, bdepth;
-    auto add_block = [&](uint32_t x, uint32_t d) {
-        bnode.push_back(x);
-        bdepth.push_back(d);
-        bwords.resize(bwords.size() + PPE_BLK_WORDS, 0u);
-        return (uint32_t)bnode.size() - 1u;
-    };
-    for (uint32_t r = 0; r < best.n_roots; ++r) add_block(r, 1u);
-    uint32_t max_bdepth = 1;
-    for (size_t bi = 0; bi < bnode.size(); ++bi) {  // blocks appended while scanning: breadth-first order
-        const uint32_t x = bnode[bi], p1 = c0(x), p2 = c1(x);
-        uint32_t *o = &bwords[bi * PPE_BLK_WORDS];
-        o[0] = thr(x);
-        o[1] = thr(p1);
-        o[2] = thr(p2);
-        o[3] = kslot(x) | (kslot(p1) << 4) | (kslot(p2) << 8);
-        const uint32_t ex[4] = {c0(p1), c1(p1), c0(p2), c1(p2)};
-        for (int e = 0; e < 4; ++e) {  // (add_block may reallocate bwords: index, not the pointer above)
-            uint32_t v;
-            if (is_leaf(ex[e])) {
-                v = leaf_exit(ex[e]);
-            } else {
-                v = add_block(ex[e], bdepth[bi] + 1u);
-                max_bdepth = std::max(max_bdepth, bdepth[bi] + 1u);
+    // K-level blocks (ppe_image.h block section): position p of a block holds node pos[p] (p's children are 2p + 1
+    // and 2p + 2); a leaf passes through (threshold ~0, both children itself); the 2^K exits lead to the next
+    // blocks or carry leaf payloads.  Breadth-first from every root.
+    std::vector<uint32_t> bwords;
+    uint32_t max_bdepth = 1, KL = 2;
+    auto build_blocks = [&](uint32_t K) {
+        const uint32_t npos = (1u << K) - 1u, bw = K == 2 ? PPE_BLK_WORDS : PPE_BLK3_WORDS;
+        std::vector<uint32_t> bnode, bdepth;
+        bwords.clear();
+        max_bdepth = 1;
+        auto add_block = [&](uint32_t x, uint32_t d) {
+            bnode.push_back(x);
+            bdepth.push_back(d);
+            bwords.resize(bwords.size() + bw, 0u);
+            return (uint32_t)bnode.size() - 1u;
+        };
+        for (uint32_t r = 0; r < best.n_roots; ++r) add_block(r, 1u);
+        uint32_t pos[15];
+        for (size_t bi = 0; bi < bnode.size(); ++bi) {  // blocks appended while scanning: breadth-first order
+            pos[0] = bnode[bi];
+            for (uint32_t q = 1; q < npos; ++q) pos[q] = (q & 1u) ? c0(pos[(q - 1u) / 2u]) : c1(pos[(q - 1u) / 2u]);
+            uint32_t slots = 0;
+            for (uint32_t q = 0; q < npos; ++q) {
+                bwords[bi * bw + q] = thr(pos[q]);
+                slots |= kslot(pos[q]) << (4u * q);
             }
-            bwords[bi * PPE_BLK_WORDS + 4 + e] = v;
+            bwords[bi * bw + npos] = slots;
+            for (uint32_t e = 0; e <= npos; ++e) {  // (add_block may reallocate bwords: index, not a pointer)
+                const uint32_t par = pos[npos / 2u + (e >> 1)];
+                const uint32_t ch = (e & 1u) ? c1(par) : c0(par);
+                uint32_t v;
+                if (is_leaf(ch)) {
+                    v = leaf_exit(ch);
+                } else {
+                    v = add_block(ch, bdepth[bi] + 1u);
+                    max_bdepth = std::max(max_bdepth, bdepth[bi] + 1u);
+                }
+                bwords[bi * bw + npos + 1u + e] = v;
+            }
         }
+        return (uint32_t)bnode.size();
+    };
+    // K = 3 when the 2-level walk (block jump table, blocks, compact records) would not be LDS-resident: the L2 part
+    // of the walk then takes one round trip per three levels instead of two (C3: lockstep group steps with an L2
+    // read 4.6 -> 2.4, tools/block_levels.py).  PPE_BLOCK_LEVELS=2|3 forces it (tests, A/B).
+    const char *bl = std::getenv("PPE_BLOCK_LEVELS");
+    const int force_k = bl && *bl ? std::atoi(bl) : 0;
+    uint32_t n_blocks = build_blocks(2);
+    if (force_k == 3 || (force_k != 2 && 4.0 * n_jump + 32.0 * n_blocks + (compact ? 16.0 * (n_slots + 1) : 0.0) >
+                                             (double)kBlock2LdsBudget)) {
+        KL = 3;
+        n_blocks = build_blocks(3);
     }
-    const uint32_t n_blocks = (uint32_t)bnode.size();
     if (n_blocks >= PPE_BLK_LEAF) return PPE_ENOMEM;
+    const uint32_t balign = KL == 2 ? 7u : 15u;  // 32- / 64-B aligned blocks
     const uint32_t off_bsec = (end_resid + 7u) & ~7u;
-    const uint32_t off_blocks = (off_bsec + n_jump + 7u) & ~7u;
+    const uint32_t off_blocks = (off_bsec + n_jump + balign) & ~balign;
     // compact records and the slot → index table follow the blocks, so the block section and the records they lead
     // to are one contiguous range (the multi-tile kernel stages it whole when it fits the CU's LDS)
     bool holes = false;
     for (uint32_t sl = 0; sl < n_slots; ++sl) holes |= R[sl].id != sl;
-    const uint32_t off_crec = compact ? off_blocks + PPE_BLK_WORDS * n_blocks : 0u;
+    const uint32_t off_crec = compact ? off_blocks + (uint32_t)bwords.size() : 0u;
     const uint32_t off_idtab = compact && holes ? off_crec + PPE_CREC_WORDS * (n_slots + 1u) : 0u;
-    const uint32_t total = !compact ? off_blocks + PPE_BLK_WORDS * n_blocks
+    const uint32_t total = !compact ? off_blocks + (uint32_t)bwords.size()
                            : off_idtab ? off_idtab + ((n_slots + 3u) & ~3u)
                                        : off_crec + PPE_CREC_WORDS * (n_slots + 1u);
 
@@ -468,6 +497,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     img[PPE_IMG_W_MAXBDEPTH] = max_bdepth;
     img[PPE_IMG_W_OFFCREC] = off_crec;
     img[PPE_IMG_W_OFFIDTAB] = off_idtab;
+    img[PPE_IMG_W_BLKLV] = KL;
     if (compact) {
         // prefix | marker bit (len 0..31), or the address of a /32
         // (a prefix box spans 2^(32 - len) keys: its marker bit 1 << (31 - len) is half that count)

@@ -33,7 +33,7 @@ constexpr int kPipeStreams = 2;
 // before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering (next tile's window, or
 // only its first 16 B, requested before the current tile is processed) and an LDS-DMA next-tile pipeline were
 // measured slower and are not built.
-constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3, kPfSblk = 5;
+constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3, kPfSblk = 5, kPfMulti3 = 6, kPfSblk3 = 7;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 // ppe_classify_batches: batches per launch.  0 = every batch of the call in one persistent launch (descriptor ring in
 // device memory): the launch ramp and tail are paid once per call instead of once per batch
@@ -206,6 +206,8 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
     // the multi-tile walk reads the 2-level blocks: whole image in LDS, else the block jump table and the first
     // block levels (breadth-first), else global
     const uint32_t off_crec = img[PPE_IMG_W_OFFCREC], off_idtab = img[PPE_IMG_W_OFFIDTAB];
+    const bool k3 = img[PPE_IMG_W_BLKLV] == 3u;  // 3-level (64-B) blocks: the PF_MULTI3 / PF_SBLK3 kernels
+    const uint32_t bbytes = k3 ? 64u : 32u;
     auto mt_plan = [&](uint32_t budget) {
         const uint32_t bjt = 4u * (off_blocks - off_bsec);
         if (off_crec && (all_words - off_bsec) * 4u <= budget) {
@@ -225,11 +227,11 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
             p.lds_blocks = n_blocks;
             p.bsec_lds = 4u * off_bsec;
             p.blk_lds = 4u * off_blocks;
-        } else if (budget >= bjt + 32u * 64u) {
+        } else if (budget >= bjt + bbytes * 64u) {
             p.mode = 2;
-            p.lds_blocks = std::min(n_blocks, (budget - bjt) / 32u);
+            p.lds_blocks = std::min(n_blocks, (budget - bjt) / bbytes);
             p.stage_src = off_bsec;
-            p.stage_words = (off_blocks - off_bsec) + PPE_BLK_WORDS * p.lds_blocks;
+            p.stage_words = (off_blocks - off_bsec) + (bbytes / 4u) * p.lds_blocks;
             p.bsec_lds = 0;
             p.blk_lds = bjt;
         }
@@ -237,7 +239,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
     if (!c->tune.lds_image) {
         if (!c->tune.block) p.block = 256;
         if (!single && (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && !c->tune.block))) {  // PF_MULTI, global image
-            p.pipe = kPfMulti;
+            p.pipe = k3 ? kPfMulti3 : kPfMulti;
             p.block = 1024u;
         }
         return p;
@@ -262,18 +264,18 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
     // PF_SBLK (tuning pipeline 5): one tile per wave at 8 waves/SIMD, two 1024-thread workgroups per CU, each
     // staging the block jump table and the block levels that fit half of the CU's LDS
     if (!single && c->tune.pipeline == 5) {
-        p.pipe = kPfSblk;
+        p.pipe = k3 ? kPfSblk3 : kPfSblk;
         p.block = 1024u;
         const uint32_t fixed = ppe_classify_fixed_lds(1024, kPfSblk, 2) + 1024u;
         mt_plan(80u * 1024u > fixed ? 80u * 1024u - fixed : 0u);
         return p;
     }
-    if (!single && (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && lds_bytes > budget && !c->tune.block))) {
-        p.pipe = kPfMulti;
+    if (!single && (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && (lds_bytes > budget || k3) && !c->tune.block))) {
+        p.pipe = k3 ? kPfMulti3 : kPfMulti;
         // tuning knobs (A/B only): workgroup size and the LDS bytes each workgroup may take (default: all of it, one
-        // workgroup per CU); less LDS lets more workgroups share a CU
+        // workgroup per CU); less LDS lets more workgroups share a CU (the 3-level kernel is built for 1024 only)
         const int mb = env_int("PPE_MT_BLOCK", 1024);
-        p.block = (mb == 256 || mb == 512) ? (uint32_t)mb : 1024u;
+        p.block = (!k3 && (mb == 256 || mb == 512)) ? (uint32_t)mb : 1024u;
         const uint32_t fixed = ppe_classify_fixed_lds((int)p.block, kPfMulti, 2) + 1024u;  // no key slots
         const uint32_t cap = (uint32_t)std::min(160 * 1024, std::max(8 * 1024, env_int("PPE_MT_LDS", 160 * 1024)));
         budget = cap > fixed ? cap - fixed : 0u;

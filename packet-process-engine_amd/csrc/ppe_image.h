@@ -18,7 +18,9 @@
  *           32-B aligned)   word 18  max_bdepth: most blocks on a root-to-leaf path
  *  word 19  off_crec: word offset of the compact records (v6), 0 = the image has none
  *  word 20  off_idtab: word offset of the slot → rule index table, 0 = slot == rule index for every slot
- *  words 21..31 reserved
+ *  word 21  block levels K: 2 (32-B blocks, the default) or 3 (64-B blocks: images whose block section and compact
+ *           records do not fit the CU's LDS, so more of the walk is L2 reads)
+ *  words 22..31 reserved
  *
  *  jump table (format v4; present iff word 14 != 0): 2^bits words right after the header.  A walk starts at
  *      bucket b = key[dim] >> shift: word b = the byte offset of that bucket's subtree root | its key slot << 24.
@@ -56,14 +58,31 @@
  *  multi-tile walk, which reads the tree from L2 for large rule sets: one 32-B read resolves two levels, so a walk
  *  needs half the dependent memory round trips.
  *      block jump table (present iff word 14 != 0): 2^bits words, bucket → its root block index
- *      blocks (8 words, 32-B aligned, breadth-first by block depth: the LDS-staged prefix is whole block levels):
- *        w0..w2  thresholds of the block's positions 0 (root), 1 (its left child), 2 (its right child)
- *        w3      key slots: pos0 | pos1 << 4 | pos2 << 8
- *        w4..w7  exits e = 2 b0 + b1 (b0: key(pos0) > w0, b1: key(pos 1 + b0) > w[1 + b0]):
- *                PPE_BLK_LEAF | leaf payload (max_leaf <= 1: rule slot / sentinel; else first | count << 23), or the
- *                index of the block rooted at that grandchild
- *        A leaf at position 0..2 is a pass-through: threshold 0xffffffff (no key is greater) and both of its exits
- *        carry the leaf, so every walk resolves exactly two levels per block.
+ *      blocks (K = 2: 8 words, 32-B aligned; K = 3: 16 words, 64-B aligned; breadth-first by block depth: the
+ *      LDS-staged prefix is whole block levels).  A block holds K tree levels: positions p = 0 .. 2^K - 2 in BFS
+ *      order (position p's children are 2p + 1 and 2p + 2), then 2^K exits:
+ *        w[p]    threshold of position p                         (K = 2: w0..w2; K = 3: w0..w6)
+ *        w[2^K - 1]  key slots: position p's at bits 4p..4p+3
+ *        w[2^K .. 2^(K+1) - 1]  exits e = the K comparison bits, first level most significant (K = 2: 2 b0 + b1,
+ *                K = 3: 4 b0 + 2 b1 + b2; b0: key(pos 0) > w0, b1: key(pos 1 + b0) > w[1 + b0], ...):
+ *                PPE_BLK_LEAF | leaf payload (max_leaf <= 1: rule slot / sentinel, or the compact exit below;
+ *                else first | count << 23), or the index of the block rooted at that position's child
+ *        A leaf at a position is a pass-through: threshold 0xffffffff (no key is greater) and both of its children
+ *        positions / exits carry the leaf, so every walk resolves exactly K levels per block.
+ *
+ *  compact leaves (v6; present iff word 19 != 0: one candidate per leaf (max_leaf <= 1) and no rule with a residual
+ *  MAC / time field).  The block walk is the classify kernel's, and only TCP / UDP packets reach the ACL there
+ *  (decode-ipv4.c:131-157), so a rule's protocol range matters only through "contains 6" and "contains 17".  A leaf
+ *  exit then carries everything about its candidate except the address prefixes and port ranges:
+ *      bits 0-23  rule slot (n_rules = the sentinel)         bit 24 DROP: the rule's action == ACL_RULE_ACTION_DROP
+ *      bit 25     the protocol range contains 6 (TCP)       bit 26 contains 17 (UDP)
+ *      bit 27     sip is a /32 (exact compare)              bit 28 dip is a /32
+ *      bit 29     NOHIT: the sentinel (hit -1; bit 24 = the default action is DROP)
+ *  compact record (4 words, 16 B, by slot; slot n_rules = the sentinel, matching every TCP / UDP key):
+ *      sip: prefix | 1 << (31 - len) for len 0..31 (the lowest set bit marks the prefix end), the address for a /32
+ *      dip: likewise;  sport_lo | dport_lo << 16;  (sport_hi - sport_lo) | (dport_hi - dport_lo) << 16
+ *      The address matches iff (key ^ word) has no bit set above the marker bit (every bit for a /32).
+ *  idtab (word 20 != 0): n_rules words, the rule index of each slot (when unused entries make slots != indices)
  */
 #ifndef PPE_IMAGE_H
 #define PPE_IMAGE_H
@@ -91,8 +110,10 @@
 #define PPE_IMG_W_MAXBDEPTH 18
 #define PPE_IMG_W_OFFCREC  19
 #define PPE_IMG_W_OFFIDTAB 20
+#define PPE_IMG_W_BLKLV    21
 
-#define PPE_BLK_WORDS 8u
+#define PPE_BLK_WORDS 8u           /* 2-level block */
+#define PPE_BLK3_WORDS 16u         /* 3-level block */
 #define PPE_BLK_LEAF 0x80000000u  /* exit word: a leaf payload (else a block index) */
 #define PPE_CX_SLOT   0x00ffffffu  /* compact leaf exit fields (v6) */
 #define PPE_CX_DROP   (1u << 24)

@@ -683,10 +683,12 @@ __device__ __forceinline__ uint32_t key_sel(uint32_t d, const uint32_t (&k)[5]) 
 // tree levels, so a deep walk through an L2-resident tree takes half the dependent round trips of a node walk.  Keys
 // come from registers; a lane stops reading at its leaf.  Returns, per tile, a node whose .z is the leaf payload in
 // the node format acl_leaf reads.
-template <int MODE, int IMGB, int MT>
+template <int MODE, int IMGB, int MT, int KL = 2>
 __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ gimg, const AclGeo &g,
                                                    const uint32_t (&key)[MT][5], const bool (&need)[MT],
                                                    uint4 (&nd)[MT]) {
+    constexpr uint32_t BB = KL == 2 ? 32u : 64u;  // block bytes
+    constexpr int NQ = (int)BB / 16;
     uint32_t blk[MT];
     bool done[MT];
 #pragma unroll
@@ -702,18 +704,18 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
     }
 #pragma unroll 1
     for (uint32_t it = 0; it < g.max_bdepth; ++it) {
-        uint4 lo[MT], hi[MT];
+        uint4 q[MT][NQ];
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
             if (!done[t]) {
                 if (MODE != IMG_GLOBAL && blk[t] < g.lds_blocks) {
-                    const uint32_t la = IMGB + g.blk_lds + 32u * blk[t];
-                    lo[t] = lds_u128(la);
-                    hi[t] = lds_u128(la + 16u);
+                    const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
+#pragma unroll
+                    for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
                 } else {
-                    const uint32_t ga = 4u * g.off_blocks + 32u * blk[t];
-                    lo[t] = gld<uint4>(gimg, ga);
-                    hi[t] = gld<uint4>(gimg, ga + 16u);
+                    const uint32_t ga = 4u * g.off_blocks + BB * blk[t];
+#pragma unroll
+                    for (int j = 0; j < NQ; ++j) q[t][j] = gld<uint4>(gimg, ga + 16u * j);
                 }
             }
         }
@@ -721,12 +723,30 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
             if (!done[t]) {
-                // position 0 → b0; position 1 + b0 → b1; exit 2 b0 + b1 (a leaf position passes through: thr ~0)
-                const bool b0 = key_sel(lo[t].w & 15u, key[t]) > lo[t].x;
-                const uint32_t t1 = b0 ? lo[t].z : lo[t].y;
-                const uint32_t k1 = (lo[t].w >> (b0 ? 8u : 4u)) & 15u;
-                const bool b1 = key_sel(k1, key[t]) > t1;
-                const uint32_t x = b0 ? (b1 ? hi[t].w : hi[t].z) : (b1 ? hi[t].y : hi[t].x);
+                uint32_t x;
+                if constexpr (KL == 2) {
+                    // position 0 → b0; position 1 + b0 → b1; exit 2 b0 + b1 (a leaf position passes through: thr ~0)
+                    const uint4 lo = q[t][0], hi = q[t][NQ - 1];
+                    const bool b0 = key_sel(lo.w & 15u, key[t]) > lo.x;
+                    const uint32_t t1 = b0 ? lo.z : lo.y;
+                    const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
+                    const bool b1 = key_sel(k1, key[t]) > t1;
+                    x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
+                } else {
+                    // 3 levels: thresholds w0..w6 (a, b.xyz), key slots b.w, exits c, d; position 1 + b0, then
+                    // 3 + 2 b0 + b1; exit 4 b0 + 2 b1 + b2
+                    const uint4 a = q[t][0], b = q[t][1], c = q[t][2 % NQ], d = q[t][3 % NQ];
+                    const uint32_t sl = b.w;
+                    const bool b0 = key_sel(sl & 15u, key[t]) > a.x;
+                    const uint32_t t1 = b0 ? a.z : a.y;
+                    const uint32_t k1 = (sl >> (b0 ? 8u : 4u)) & 15u;
+                    const bool b1 = key_sel(k1, key[t]) > t1;
+                    const uint32_t t2 = b0 ? (b1 ? b.z : b.y) : (b1 ? b.x : a.w);
+                    const uint32_t k2 = (sl >> (4u * (3u + 2u * (uint32_t)b0 + (uint32_t)b1))) & 15u;
+                    const bool b2 = key_sel(k2, key[t]) > t2;
+                    const uint4 ex = b0 ? d : c;
+                    x = b1 ? (b2 ? ex.w : ex.z) : (b2 ? ex.y : ex.x);
+                }
                 if (x & PPE_BLK_LEAF) {
                     done[t] = true;
                     // leaf payload in node form: slot / sentinel, or first | count << 24 for leaf lists
@@ -890,8 +910,16 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
                     // (staged block levels in LDS, the rest and the rule records from L2)
 #define PF_MULTI 3  // split / global images: each wave loads, decodes and walks PPE_MT tiles together (acl_walk_blocks_mt),
                     // 4 waves/SIMD with 128 VGPRs, one 1024-thread workgroup per CU and its whole LDS for the image
+#define PF_MULTI3 6  // PF_MULTI over an image of 3-level blocks (image word PPE_IMG_W_BLKLV == 3)
+#define PF_SBLK3 7   // PF_SBLK over 3-level blocks
 #ifndef PPE_MT
 #define PPE_MT 4
+#endif
+#ifndef PPE_MT3  // tiles per wave of the PF_MULTI3 kernel (a 64-B block per lane and tile in flight)
+#define PPE_MT3 3
+#endif
+#ifndef PPE_MT3_WAVES
+#define PPE_MT3_WAVES 4
 #endif
 #ifndef PPE_MT_WAVES  // waves per SIMD the PF_MULTI kernel is compiled for (VGPR budget 512 / this)
 #define PPE_MT_WAVES 4
@@ -904,12 +932,14 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
 // list, no tile counts, no tuple: ppe_kargs.part_layout), so the output checks are compile-time and the kernel holds
 // fewer scalars (C1 step -2..4 %, C4 -3.5 %: fewer SGPR spills to VGPR lanes)
 template <int MODE, int PF, int BLOCK, bool FLOW, bool PART = false>
-__global__ __launch_bounds__(BLOCK, (PF == PF_MULTI && !FLOW) ? PPE_MT_WAVES : PPE_WAVES_PER_EU)
+__global__ __launch_bounds__(BLOCK, ((PF == PF_MULTI || PF == PF_MULTI3) && !FLOW)
+                                        ? (PF == PF_MULTI3 ? PPE_MT3_WAVES : PPE_MT_WAVES) : PPE_WAVES_PER_EU)
 void ppe_classify_kernel(ppe_kargs a) {
-    constexpr int MT = (PF == PF_MULTI && !FLOW) ? PPE_MT : 1;
+    constexpr int MT = FLOW ? 1 : PF == PF_MULTI ? PPE_MT : PF == PF_MULTI3 ? PPE_MT3 : 1;
+    constexpr int KL = (PF == PF_MULTI3 || PF == PF_SBLK3) ? 3 : 2;  // block levels of the image's block section
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     // single-tile walks over a whole-LDS image use its 2-level blocks with the keys in registers (no key slots)
-    constexpr bool STB = (PPE_ST_BLOCKS && MT == 1 && MODE == IMG_LDS) || PF == PF_SBLK;
+    constexpr bool STB = (PPE_ST_BLOCKS && MT == 1 && MODE == IMG_LDS) || PF == PF_SBLK || PF == PF_SBLK3;
     using L = Lds<BLOCK, MT == 1 && !STB>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
     uint32_t *lcnt = bins + PPE_NBINS;       // [32] per-reason counters of this workgroup
@@ -968,7 +998,8 @@ void ppe_classify_kernel(ppe_kargs a) {
     };
     auto load_tile = [&](uint32_t t) { load_at(B.hdr, B.len, B.n, B.stride, t); };
     // first window in flight during the image staging
-    bool have = (PF == PF_HOIST || PF == PF_SBLK) && wave_live && wtile < ((B.n + 63u) >> 6);  // (PF_MULTI: at the loop top)
+    bool have = (PF == PF_HOIST || PF == PF_SBLK || PF == PF_SBLK3) && wave_live &&
+                wtile < ((B.n + 63u) >> 6);  // (PF_MULTI: at the loop top)
     if (have) load_tile(wtile);
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
@@ -1086,7 +1117,7 @@ void ppe_classify_kernel(ppe_kargs a) {
                 const uint32_t key[1][5] = {{k.sip, k.dip, k.sport, k.dport, k.proto}};
                 const bool need[1] = {true};
                 uint4 nd[1];
-                acl_walk_blocks_mt<MODE, L::IMGB, 1>(a.img, geo, key, need, nd);
+                acl_walk_blocks_mt<MODE, L::IMGB, 1, KL>(a.img, geo, key, need, nd);
                 if (geo.off_crec) {
                     bool drop;
                     acl_leaf_compact<L::IMGB>(a.img, geo, nd[0].z, k.sip, k.dip, k.sport, k.dport, k.proto == 6u,
@@ -1151,7 +1182,7 @@ void ppe_classify_kernel(ppe_kargs a) {
                     key[t][4] = k[t].proto;
                 }
                 uint4 nd[MT];
-                acl_walk_blocks_mt<MODE, L::IMGB, MT>(a.img, geo, key, need, nd);
+                acl_walk_blocks_mt<MODE, L::IMGB, MT, KL>(a.img, geo, key, need, nd);
 #pragma unroll
                 for (int t = 0; t < MT; ++t) {
                     const uint32_t tile = t0 + t;
@@ -1691,6 +1722,8 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block) 
         if (pipe == PF_NONE) PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__); \
         if (pipe == PF_MULTI) PPE_DISPATCH_B(FN, M, PF_MULTI, __VA_ARGS__); \
         if (pipe == PF_SBLK) return FN<M, PF_SBLK, 1024>(__VA_ARGS__);   \
+        if (pipe == PF_MULTI3) return FN<M, PF_MULTI3, 1024>(__VA_ARGS__); \
+        if (pipe == PF_SBLK3) return FN<M, PF_SBLK3, 1024>(__VA_ARGS__);   \
         PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__);                \
     } while (0)
 #define PPE_DISPATCH(FN, ...)                                        \
@@ -1732,7 +1765,8 @@ extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, in
 // LDS of a workgroup besides the staged image: the per-wave key slots of node walks and the counter bins.  Block
 // walks (the multi-tile kernel; the single-tile kernel over a whole-LDS image) keep the keys in registers.
 extern "C" uint32_t ppe_classify_fixed_lds(int block, int pipe, int mode) {
-    const bool blocks = pipe == PF_MULTI || pipe == PF_SBLK || (PPE_ST_BLOCKS && mode == IMG_LDS);
+    const bool blocks = pipe == PF_MULTI || pipe == PF_SBLK || pipe == PF_MULTI3 || pipe == PF_SBLK3 ||
+                        (PPE_ST_BLOCKS && mode == IMG_LDS);
     return (blocks ? 0u : (uint32_t)(block / 64) * KEY_WAVE_BYTES) + PPE_LDS_FIXED;
 }
 

@@ -228,3 +228,26 @@ def test_compact_leaves_edge_cases(monkeypatch, compact):
         # every protocol kind and prefix kind is hit
         hit = lin["acl_hit"][lin["acl_hit"] >= 0]
         assert len(np.unique(pr[hit])) >= 4 and (r["sip_mask"][hit] == 32).any() and (r["sip_mask"][hit] == 0).any()
+
+
+@pytest.mark.parametrize("levels", ["2", "3"])
+@pytest.mark.parametrize("nrules,resid,binth", [(256, 0.0, 1), (2048, 0.0, 1), (300, 0.3, 1), (1024, 0.0, 4)])
+def test_block_levels_equal_linear(monkeypatch, levels, nrules, resid, binth):
+    """2- and 3-level blocks (image word 21; 64-B blocks of 7 thresholds, their key slots and 8 exits) walk to the
+    same leaves as the node tree: compact leaves, leaf lists (binth 4) and residual rules, jump root on."""
+    monkeypatch.setenv("PPE_BLOCK_LEVELS", levels)
+    rules = synth.make_rules(nrules, seed=nrules + 7, resid_frac=resid, any_ip_frac=0.1)
+    pk = synth.make_packets(6000, rules, seed=12, kind="imix", stride=128, malformed_frac=0.02, with_ts=True)
+    img, st, lin = compare(rules, None, pk, binth=binth)
+    assert int(img[21]) == int(levels)
+    bw = 8 if levels == "2" else 16
+    assert int(img[17]) % bw == 0 and (lin["acl_hit"] >= 0).sum() > 500
+
+
+def test_large_rule_sets_get_three_level_blocks():
+    """A rule set whose 2-level walk would not be LDS-resident (C3: 65,536 rules) gets 3-level blocks; C4 (4,096
+    rules) keeps 2-level blocks and fits the CU's LDS whole with its compact records."""
+    img3, _ = abi.build_image(synth.make_rules(65536))
+    img2, _ = abi.build_image(synth.make_rules(4096))
+    assert int(img3[21]) == 3 and int(img2[21]) == 2
+    assert (len(img2) - int(img2[15])) * 4 <= 158 * 1024

@@ -264,10 +264,33 @@ def test_c3_64k_rules_vs_oracle(eng):
     old = eng.tuning()
     try:
         eng.tuning(pipeline=5)
-        assert eng.launch_info()["fetch"] == "sblk"
+        assert eng.launch_info()["fetch"] == "sblk3"  # 64k rules: 3-level blocks
         assert_same(gpu_classify(eng, pk["hdr"], pk["len"]), ref)
     finally:
         eng.tuning(**old)
+
+
+@pytest.mark.parametrize("nrules", [256, 4096])
+@pytest.mark.parametrize("pipeline", [0, 5])
+def test_three_level_blocks_forced(eng, monkeypatch, nrules, pipeline):
+    """3-level (64-B) blocks forced on rule sets that would get 2-level ones (PPE_BLOCK_LEVELS=3): the PF_MULTI3
+    kernel (default pipeline) and PF_SBLK3 (pipeline 5), IMIX with malformed packets, against the linear oracle."""
+    monkeypatch.setenv("PPE_BLOCK_LEVELS", "3")
+    rules = synth.make_rules(nrules, seed=500 + nrules)
+    pk = synth.make_packets(65_536, rules, seed=501, kind="imix", stride=128, malformed_frac=0.05)
+    st = eng.commit(rules, default_action=1)
+    old = eng.tuning()
+    try:
+        eng.tuning(pipeline=pipeline)
+        assert eng.launch_info()["fetch"] == ("multi3" if pipeline == 0 else "sblk3")
+        res = gpu_classify(eng, pk["hdr"], pk["len"])
+    finally:
+        eng.tuning(**old)
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    assert_same(res, ref)
+    check_compaction(res, len(pk["len"]))
+    assert st["n_rules"] == nrules
 
 
 def test_residual_rules_with_timestamps(eng):
