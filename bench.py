@@ -334,7 +334,7 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
 def traffic_per_packet(name):
     """HBM bytes per packet of this config's launch from the committed rocprofv3 profile (tools/collect_traffic.py
     output: FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE, calibrated), or None."""
-    files = sorted((ROOT / "profiles").glob(f"r2*_traffic_{name}.json"))
+    files = sorted((ROOT / "profiles").glob(f"r[0-9]*_traffic_{name}.json"))
     if not files:
         return None
     tj = json.load(open(files[-1]))

@@ -32,10 +32,6 @@
 
 namespace {
 
-// LDS bytes a 1024-thread multi-tile workgroup has for the block section and compact records (160 KiB less the
-// counter bins and the staging round-up): beyond it the image gets 3-level blocks
-constexpr uint32_t kBlock2LdsBudget = 158u * 1024u;
-
 struct Rule {
     uint32_t lo[PPE_NDIMS], hi[PPE_NDIMS];
     uint32_t id;
@@ -449,14 +445,15 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         }
         return (uint32_t)bnode.size();
     };
-    // K = 3 when the 2-level walk (block jump table, blocks, compact records) would not be LDS-resident: the L2 part
-    // of the walk then takes one round trip per three levels instead of two (C3: lockstep group steps with an L2
-    // read 4.6 -> 2.4, tools/block_levels.py).  PPE_BLOCK_LEVELS=2|3 forces it (tests, A/B).
+    // K = 2 by default.  3-level blocks take one L2 round trip per three levels instead of two (C3: lockstep group
+    // steps with an L2 read 4.6 -> 2.4, tools/block_levels.py), but measured slower on C3 (step 32.4 us per 1M with
+    // 2-level blocks, 33.9 / 36.4 with 3-level blocks at 4 / 3 tiles per wave: gpurun_out/r3c): the
+    // 64-B block in flight per lane and tile costs the registers that would hold more tiles.  PPE_BLOCK_LEVELS=3
+    // selects them (tests, A/B).
     const char *bl = std::getenv("PPE_BLOCK_LEVELS");
     const int force_k = bl && *bl ? std::atoi(bl) : 0;
     uint32_t n_blocks = build_blocks(2);
-    if (force_k == 3 || (force_k != 2 && 4.0 * n_jump + 32.0 * n_blocks + (compact ? 16.0 * (n_slots + 1) : 0.0) >
-                                             (double)kBlock2LdsBudget)) {
+    if (force_k == 3) {
         KL = 3;
         n_blocks = build_blocks(3);
     }

@@ -650,14 +650,18 @@ __device__ __forceinline__ void acl_leaf(const uint32_t *__restrict__ gimg, cons
 
 // Compact leaf (image v6, ppe_image.h): `x` = the leaf exit of the block walk (slot and the candidate's flags).  One
 // 16-B record read (LDS when staged) and ~20 VALU: the address prefixes by their marker bits, the ports by packed
-// 16-bit spans, the protocol by the exit's TCP / UDP bits (only TCP / UDP packets reach the ACL here).
+// 16-bit spans, the protocol by the exit's TCP / UDP bits (only TCP / UDP packets reach the ACL here).  (Issuing
+// every tile's record read before the first check needs 4 more VGPRs per tile: spills at 128)
 template <int IMGB>
-__device__ __forceinline__ void acl_leaf_compact(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t x,
-                                                 uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport,
-                                                 bool tcp, int32_t &hit, bool &drop) {
+__device__ __forceinline__ uint4 crec_load(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t x) {
+    const uint32_t ro = 16u * (x & PPE_CX_SLOT);
+    return g.crec_lds != ~0u ? lds_u128(IMGB + g.crec_lds + ro) : gld<uint4>(gimg, 4u * g.off_crec + ro);
+}
+template <int IMGB>
+__device__ __forceinline__ void crec_check(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t x,
+                                           const uint4 r, uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport,
+                                           bool tcp, int32_t &hit, bool &drop) {
     const uint32_t slot = x & PPE_CX_SLOT;
-    const uint32_t ro = 16u * slot;
-    const uint4 r = g.crec_lds != ~0u ? lds_u128(IMGB + g.crec_lds + ro) : gld<uint4>(gimg, 4u * g.off_crec + ro);
     // (a /32 compares every bit; else the bits above the marker: ~((lowbit << 1) - 1), 0 for a /0)
     const uint32_t ms = (x & PPE_CX_S32) ? ~0u : ~(((r.x & (0u - r.x)) << 1) - 1u);
     const uint32_t md = (x & PPE_CX_D32) ? ~0u : ~(((r.y & (0u - r.y)) << 1) - 1u);
@@ -671,6 +675,12 @@ __device__ __forceinline__ void acl_leaf_compact(const uint32_t *__restrict__ gi
         id = g.idtab_lds != ~0u ? lds_u32(IMGB + g.idtab_lds + 4u * slot) : gld<uint32_t>(gimg, 4u * g.off_idtab + 4u * slot);
     hit = (m & !(x & PPE_CX_NOHIT)) ? (int32_t)id : -1;
     drop = m ? (x & PPE_CX_DROP) != 0u : g.default_action == ACL_RULE_ACTION_DROP;
+}
+template <int IMGB>
+__device__ __forceinline__ void acl_leaf_compact(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t x,
+                                                 uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport,
+                                                 bool tcp, int32_t &hit, bool &drop) {
+    crec_check<IMGB>(gimg, g, x, crec_load<IMGB>(gimg, g, x), sip, dip, sport, dport, tcp, hit, drop);
 }
 
 // 5-way key select by key slot (multi-tile walks keep the keys in registers)
@@ -1192,8 +1202,8 @@ void ppe_classify_kernel(ppe_kargs a) {
                     if (need[t]) {
                         bool drop;
                         if (geo.off_crec) {
-                            acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, k[t].sip, k[t].dip, k[t].sport, k[t].dport,
-                                                      k[t].proto == 6u, hit, drop);
+                            acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, k[t].sip, k[t].dip, k[t].sport,
+                                                      k[t].dport, k[t].proto == 6u, hit, drop);
                         } else {
                             uint32_t rule_act;
                             const MacFromWindow mac = {B.hdr, p, B.stride};

@@ -244,10 +244,9 @@ def test_block_levels_equal_linear(monkeypatch, levels, nrules, resid, binth):
     assert int(img[17]) % bw == 0 and (lin["acl_hit"] >= 0).sum() > 500
 
 
-def test_large_rule_sets_get_three_level_blocks():
-    """A rule set whose 2-level walk would not be LDS-resident (C3: 65,536 rules) gets 3-level blocks; C4 (4,096
-    rules) keeps 2-level blocks and fits the CU's LDS whole with its compact records."""
-    img3, _ = abi.build_image(synth.make_rules(65536))
+def test_default_block_levels_and_lds_fit():
+    """2-level blocks by default (3-level ones measured slower on C3); C4's block section with its compact
+    records (4,096 rules) fits a 1024-thread workgroup's LDS whole."""
     img2, _ = abi.build_image(synth.make_rules(4096))
-    assert int(img3[21]) == 3 and int(img2[21]) == 2
+    assert int(img2[21]) == 2
     assert (len(img2) - int(img2[15])) * 4 <= 158 * 1024

@@ -264,7 +264,7 @@ def test_c3_64k_rules_vs_oracle(eng):
     old = eng.tuning()
     try:
         eng.tuning(pipeline=5)
-        assert eng.launch_info()["fetch"] == "sblk3"  # 64k rules: 3-level blocks
+        assert eng.launch_info()["fetch"] == "sblk"
         assert_same(gpu_classify(eng, pk["hdr"], pk["len"]), ref)
     finally:
         eng.tuning(**old)
