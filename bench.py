@@ -973,7 +973,8 @@ def run_defrag(args, cfgd, dev, world, rank, dist, name=None, nested=False):
                        "fragments_per_gpu": n, "mean_frame_bytes": round(frame_bytes / n, 1),
                        "datagrams_per_batch": n_dgram, "parallelism": f"fcb-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": round(traffic_per_packet(name) * n) if traffic_per_packet(name) else None,
                          "kernel": "one ppe_defrag call (parse..assemble, 17 stream-ordered kernels)",
                          "call_avg_us": round(call_ms * 1e3, 3), "bytes_per_call": bytes_call},
             "cpu_baseline": cpu,

@@ -7,7 +7,8 @@
  *               hit, partition entry), one packet per lane, 64-packet tiles, a persistent grid over up to 32 batches
  *               in one launch (the ring launch of ppe_classify_batches)
  *   read-only   the same reads, one 4-B word written per 64-packet tile: separates the write mix from the row fetch
- *   copy        a plain 16-B-per-lane copy (the guide's float4 copy, MI355X_MICROARCH.md: 6.29 TB/s)
+ *   copy        a 16-B-per-lane copy, 4 loads in flight per lane (the guide's float4 copy, MI355X_MICROARCH.md:
+ *               6.29 TB/s)
  *
  * Each launch also measures the shader clock it ran at: wave 0 of workgroup 0 (resident for the whole persistent
  * launch) reads the shader-clock counter (s_memtime) and the 100-MHz real-time counter (s_memrealtime) at its start
@@ -83,13 +84,25 @@ __global__ __launch_bounds__(512) void calib_kernel(ppe_calib_args a) {
     clk_mark(a, 1);
 }
 
+// 4 independent 16-B loads in flight per lane before their stores (a one-load loop keeps too few bytes in flight
+// per CU to reach the HBM rate: 5.1-5.2 TB/s measured in gpurun_out/r3b)
 __global__ __launch_bounds__(512) void copy_kernel(const v4u *__restrict__ src, v4u *__restrict__ dst, size_t n16,
                                                    unsigned long long *clk) {
     if (clk && blockIdx.x == 0 && threadIdx.x == 0) {
         clk[0] = __builtin_amdgcn_s_memtime();
         clk[2] = __builtin_amdgcn_s_memrealtime();
     }
-    for (size_t i = (size_t)blockIdx.x * 512u + threadIdx.x; i < n16; i += (size_t)gridDim.x * 512u) dst[i] = src[i];
+    const size_t stride = (size_t)gridDim.x * 512u;
+    size_t i = (size_t)blockIdx.x * 512u + threadIdx.x;
+    for (; i + 3u * stride < n16; i += 4u * stride) {
+        const v4u a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + stride),
+                  c = __builtin_nontemporal_load(src + i + 2u * stride), d = __builtin_nontemporal_load(src + i + 3u * stride);
+        __builtin_nontemporal_store(a, dst + i);
+        __builtin_nontemporal_store(b, dst + i + stride);
+        __builtin_nontemporal_store(c, dst + i + 2u * stride);
+        __builtin_nontemporal_store(d, dst + i + 3u * stride);
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
     if (clk && blockIdx.x == 0 && threadIdx.x == 0) {
         clk[1] = __builtin_amdgcn_s_memtime();
         clk[3] = __builtin_amdgcn_s_memrealtime();

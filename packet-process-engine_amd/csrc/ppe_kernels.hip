@@ -49,6 +49,9 @@
 #ifndef PPE_TUPLE_SELECT
 #define PPE_TUPLE_SELECT 0
 #endif
+#ifndef PPE_REC_IN_WALK  // experiment: multi-tile walks read compact records inside the walk loop (acl_walk_blocks_mt)
+#define PPE_REC_IN_WALK 0
+#endif
 // (trace the wave's tile iterations PPE_TRACE_SKIP .. + 3: a skip > 0 samples the steady state of a long launch)
 #ifndef PPE_TRACE_SKIP
 #define PPE_TRACE_SKIP 0u
@@ -684,8 +687,11 @@ __device__ __forceinline__ void acl_leaf_compact(const uint32_t *__restrict__ gi
 }
 
 // 5-way key select by key slot (multi-tile walks keep the keys in registers)
-__device__ __forceinline__ uint32_t key_sel(uint32_t d, const uint32_t (&k)[5]) {
-    return d == 0u ? k[0] : d == 1u ? k[1] : d == 2u ? k[2] : d == 3u ? k[3] : d == 4u ? k[4] : 0u;
+// Block walks take the packed key {sip, dip, sport | dport << 16, meta} (meta: proto at bits 16-23; the multi-tile
+// kernel keeps the status and flags in its low bits), 4 registers per tile instead of 5 + the decode's copies.
+__device__ __forceinline__ uint32_t key_sel(uint32_t d, const uint32_t (&k)[4]) {
+    return d == 0u ? k[0] : d == 1u ? k[1] : d == 2u ? (k[2] & 0xffffu) : d == 3u ? (k[2] >> 16)
+         : d == 4u ? ((k[3] >> 16) & 0xffu) : 0u;
 }
 
 // Multi-tile walk over the image's 2-level blocks (PF_MULTI; ppe_image.h block section): the lanes of MT tiles walk
@@ -693,14 +699,16 @@ __device__ __forceinline__ uint32_t key_sel(uint32_t d, const uint32_t (&k)[5]) 
 // tree levels, so a deep walk through an L2-resident tree takes half the dependent round trips of a node walk.  Keys
 // come from registers; a lane stops reading at its leaf.  Returns, per tile, a node whose .z is the leaf payload in
 // the node format acl_leaf reads.
-template <int MODE, int IMGB, int MT, int KL = 2>
+// RECW (experiment, PPE_REC_IN_WALK): on a compact image a lane that reaches its leaf reads its 16-B record in the
+// walk's next step (rec[t]) while the other lanes keep walking, instead of after the walk, tile by tile.
+template <int MODE, int IMGB, int MT, int KL = 2, bool RECW = false>
 __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ gimg, const AclGeo &g,
-                                                   const uint32_t (&key)[MT][5], const bool (&need)[MT],
-                                                   uint4 (&nd)[MT]) {
+                                                   const uint32_t (&key)[MT][4], const bool (&need)[MT],
+                                                   uint4 (&nd)[MT], uint4 *rec = nullptr) {
     constexpr uint32_t BB = KL == 2 ? 32u : 64u;  // block bytes
     constexpr int NQ = (int)BB / 16;
     uint32_t blk[MT];
-    bool done[MT];
+    bool done[MT], recp[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
         blk[t] = 0u;  // single tree: root block 0
@@ -710,15 +718,18 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
             blk[t] = MODE != IMG_GLOBAL ? lds_u32(IMGB + g.bsec_lds + jo) : gld<uint32_t>(gimg, 4u * g.off_bsec + jo);
         }
         done[t] = !need[t];
+        recp[t] = false;
         nd[t] = make_uint4(PPE_LEAF_THR, 0u, 0u, 0u);
     }
 #pragma unroll 1
-    for (uint32_t it = 0; it < g.max_bdepth; ++it) {
+    for (uint32_t it = 0; it < g.max_bdepth + (RECW ? 1u : 0u); ++it) {
         uint4 q[MT][NQ];
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
+            if (RECW && recp[t]) q[t][0] = crec_load<IMGB>(gimg, g, nd[t].z);
             if (!done[t]) {
-                if (MODE != IMG_GLOBAL && blk[t] < g.lds_blocks) {
+                // (a whole-LDS image: every block is staged, no global-load path compiled in)
+                if (MODE == IMG_LDS || (MODE != IMG_GLOBAL && blk[t] < g.lds_blocks)) {
                     const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
 #pragma unroll
                     for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
@@ -732,6 +743,10 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
         bool pending = false;
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
+            if (RECW && recp[t]) {  // the record requested this step has arrived
+                rec[t] = q[t][0];
+                recp[t] = false;
+            }
             if (!done[t]) {
                 uint32_t x;
                 if constexpr (KL == 2) {
@@ -762,6 +777,10 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
                     // leaf payload in node form: slot / sentinel, or first | count << 24 for leaf lists
                     // (compact images: slot | flags, acl_leaf_compact)
                     nd[t].z = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF) : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
+                    if (RECW) {
+                        recp[t] = true;
+                        pending = true;
+                    }
                 } else {
                     blk[t] = x;
                     pending = true;
@@ -1124,7 +1143,7 @@ void ppe_classify_kernel(ppe_kargs a) {
             uint32_t rule_act;
             const MacFromWindow mac = {B.hdr, p, B.stride};
             if constexpr (STB) {
-                const uint32_t key[1][5] = {{k.sip, k.dip, k.sport, k.dport, k.proto}};
+                const uint32_t key[1][4] = {{k.sip, k.dip, k.sport | (k.dport << 16), k.proto << 16}};
                 const bool need[1] = {true};
                 uint4 nd[1];
                 acl_walk_blocks_mt<MODE, L::IMGB, 1, KL>(a.img, geo, key, need, nd);
@@ -1171,8 +1190,10 @@ void ppe_classify_kernel(ppe_kargs a) {
                     r3[t] = gld_win<uint32_t>(B.hdr, ro + 48u);
                     rl[t] = gld_win<uint32_t>(B.len, 4u * pc);
                 }
-                Dec k[MT];
-                uint32_t fh[MT], key[MT][5];
+                // per tile through the walk: the packed key (sip, dip, ports, meta = status | flags << 8 | proto
+                // << 16) and, for the tuple output only, payload length and TCP option word; the flow hash is
+                // computed after the walk (fewer live registers while the block reads are in flight)
+                uint32_t key[MT][4], kpay[MT], kopt[MT];
                 bool need[MT];
 #pragma unroll
                 for (int t = 0; t < MT; ++t) {
@@ -1181,40 +1202,58 @@ void ppe_classify_kernel(ppe_kargs a) {
                     if (valid) rx_bytes += rl[t];
                     const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
                                             r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
-                    k[t] = decode(w, rl[t], B.hdr, p, B.stride, a.syn_check);
-                    fh[t] = (k[t].flags & PPE_F_L4) ? flow_hashfn_l4(k[t].proto == 6u, k[t].sip, k[t].dip, k[t].sport,
-                                                                     k[t].dport) : 0u;
-                    need[t] = k[t].st == ST_ACL;
-                    key[t][0] = k[t].sip;
-                    key[t][1] = k[t].dip;
-                    key[t][2] = k[t].sport;
-                    key[t][3] = k[t].dport;
-                    key[t][4] = k[t].proto;
+                    const Dec d = decode(w, rl[t], B.hdr, p, B.stride, a.syn_check);
+                    need[t] = d.st == ST_ACL;
+                    key[t][0] = d.sip;
+                    key[t][1] = d.dip;
+                    key[t][2] = d.sport | (d.dport << 16);
+                    key[t][3] = d.st | (d.flags << 8) | (d.proto << 16);
+                    kpay[t] = d.paylen;
+                    kopt[t] = d.tcpopt;
                 }
                 uint4 nd[MT];
-                acl_walk_blocks_mt<MODE, L::IMGB, MT, KL>(a.img, geo, key, need, nd);
+                uint4 rec[MT];
+                if (PPE_REC_IN_WALK && geo.off_crec)
+                    acl_walk_blocks_mt<MODE, L::IMGB, MT, KL, true>(a.img, geo, key, need, nd, rec);
+                else
+                    acl_walk_blocks_mt<MODE, L::IMGB, MT, KL>(a.img, geo, key, need, nd);
 #pragma unroll
                 for (int t = 0; t < MT; ++t) {
                     const uint32_t tile = t0 + t;
                     if (tile >= ntiles) break;  // wave-uniform
                     const uint32_t p = (tile << 6) + lane;
+                    Dec k;
+                    k.sip = key[t][0];
+                    k.dip = key[t][1];
+                    k.sport = key[t][2] & 0xffffu;
+                    k.dport = key[t][2] >> 16;
+                    k.st = key[t][3] & 0xffu;
+                    k.flags = (key[t][3] >> 8) & 0xffu;
+                    k.proto = key[t][3] >> 16;
+                    k.paylen = kpay[t];
+                    k.tcpopt = kopt[t];
+                    const uint32_t fh = (k.flags & PPE_F_L4) ? flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport,
+                                                                               k.dport) : 0u;
                     int32_t hit = -1;
                     if (need[t]) {
                         bool drop;
-                        if (geo.off_crec) {
-                            acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, k[t].sip, k[t].dip, k[t].sport,
-                                                      k[t].dport, k[t].proto == 6u, hit, drop);
+                        if (PPE_REC_IN_WALK && geo.off_crec) {
+                            crec_check<L::IMGB>(a.img, geo, nd[t].z, rec[t], k.sip, k.dip, k.sport, k.dport,
+                                                k.proto == 6u, hit, drop);
+                        } else if (geo.off_crec) {
+                            acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, k.sip, k.dip, k.sport, k.dport,
+                                                      k.proto == 6u, hit, drop);
                         } else {
                             uint32_t rule_act;
                             const MacFromWindow mac = {B.hdr, p, B.stride};
-                            acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], k[t].sip, k[t].dip, k[t].sport, k[t].dport,
-                                                    k[t].proto, mac, B.ts, p, a.now, hit, rule_act);
+                            acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], k.sip, k.dip, k.sport, k.dport, k.proto, mac,
+                                                    B.ts, p, a.now, hit, rule_act);
                             drop = rule_act == ACL_RULE_ACTION_DROP;
                         }
-                        k[t].st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
-                        k[t].flags |= PPE_F_ACL;
+                        k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
+                        k.flags |= PPE_F_ACL;
                     }
-                    finish(tile, p, p < B.n, k[t], fh[t], hit, false);
+                    finish(tile, p, p < B.n, k, fh, hit, false);
                 }
             }
         }

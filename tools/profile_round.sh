@@ -17,7 +17,7 @@ if [ ! -f $O/cal_fetch/cal_counter_collection.csv ]; then
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/cal_write -o cal -- tools/calib/stream_calib 1048576 4 > $O/cal_write.log 2>&1 || exit 1
 fi
 for C in $CONFIGS; do
-  B="bench.py --config $C --configs= --warmup $K --steps $K --no-cpu-baseline --no-host-inclusive"
+  B="bench.py --config $C --configs= --stateful= --warmup $K --steps $K --no-cpu-baseline --no-host-inclusive"
   R="tools/ring_run.py --config $C --batches $K --launches 3"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$C -o k -- python3 $B > $O/kt_$C.log 2>&1 || exit 1
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch_$C -o k -- python3 $R > $O/fetch_$C.log 2>&1 || exit 1
@@ -28,7 +28,7 @@ for C in $CONFIGS; do
     --cal-fetch $O/cal_fetch/cal_counter_collection.csv --cal-write $O/cal_write/cal_counter_collection.csv \
     --n $((K * 1048576)) --read-per-pkt $RP --out $O/${T}_traffic_$C.json > $O/traffic_$C.log 2>&1 || exit 1
   python3 tools/pmc_summary.py $O/tcc_$C/k_counter_collection.csv --tiles $((K * 16384)) --min-us 50 > $O/tcc_$C.txt 2>&1
-  if [ $C = C1 ]; then
+  if [ $C = C1 ] || [ $C = C3 ] || [ $C = C4 ]; then
     timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES --kernel-trace --output-format csv -d $O/sq_$C -o k -- python3 $R > $O/sq_$C.log 2>&1 || exit 1
     python3 tools/pmc_summary.py $O/sq_$C/k_counter_collection.csv --tiles $((K * 16384)) --min-us 50 > $O/sq_$C.txt 2>&1
   fi
