@@ -271,7 +271,8 @@ def sample_clocks(busy):
 def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
     """Same-run memory ceilings beside the classify launch: the kernel's own traffic with no decode / ACL
     work (skeleton: 52 + 4 B read and four 4-B results written per packet, one persistent launch over the same
-    resident batches), the reads alone (read-only), and a 16-B-per-lane copy of 1 GiB; each with the shader clock it
+    resident batches; real_GBps counts the 64-B lines the 52 B fetch, 68 + 16 B), the reads alone (read-only, 68 B),
+    and a 16-B-per-lane copy of 1 GiB; each with the shader clock it
     ran at (in-kernel s_memtime over s_memrealtime), plus rocm-smi's sclk / mclk sampled under load."""
     import ctypes as C
     lib = C.CDLL(str(ROOT / "packet-process-engine_amd" / "libppe_calib.so"))
@@ -322,8 +323,8 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
     return {
         "skeleton": {"us_per_1M_packets": us_1m(skel_ms), "frac": round(alg * pk / (skel_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "real_GBps": round(84.0 * pk / (skel_ms / 1e3) / 1e9, 1), "sclk_mhz": skel_clk,
-                     "bytes_per_pkt": "52 + 4 read, 16 written (the kernel's own traffic)"},
-        "read_only": {"us_per_1M_packets": us_1m(ro_ms), "real_GBps": round(56.0 * pk / (ro_ms / 1e3) / 1e9, 1),
+                     "bytes_per_pkt": "52 + 4 read (68 B of HBM lines), 16 written (the kernel's own traffic)"},
+        "read_only": {"us_per_1M_packets": us_1m(ro_ms), "real_GBps": round(68.0 * pk / (ro_ms / 1e3) / 1e9, 1),
                       "frac_at_68B": round(68.0 * pk / (ro_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "sclk_mhz": ro_clk},
         "copy": {"GBps": round(2.0 * nbytes / (copy_ms / 1e3) / 1e9, 1), "bytes": nbytes, "sclk_mhz": copy_clk},
         "kernel_over_skeleton": round(skel_ms / (kern_avg_ms * nb * res.n / pk_launch), 4),

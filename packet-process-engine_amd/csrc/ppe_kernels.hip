@@ -52,6 +52,26 @@
 #ifndef PPE_REC_IN_WALK  // experiment: multi-tile walks read compact records inside the walk loop (acl_walk_blocks_mt)
 #define PPE_REC_IN_WALK 0
 #endif
+// PPE_MT_PF: the multi-tile kernel requests the next round's windows while it finishes the current one (software
+// pipeline, one round deep, across batch boundaries).  vmcnt retires loads in issue order, so the request goes where
+// no later global load of the round has to wait for it: before the walk when the whole image is in LDS (the walk and
+// the record check issue no global loads), else after the record checks (overlapping the hash, stores, compaction
+// and counters).  1 = whole-LDS images only, at PPE_MT_LDS tiles per wave (the next round's windows need the
+// registers of two more tiles: C2 / C4 step -4.5 / -3 % at 2 tiles against the round-2 loop at 4, 3 tiles with
+// prefetch -1 %, 4 spills; gpurun_out/r3h); 2 = every image (split images: C3 +3 %, experiment); 0 = the round-2
+// loop (load, decode, walk, finish) everywhere.
+#ifndef PPE_MT_PF
+#define PPE_MT_PF 1
+#endif
+#ifndef PPE_MT_LDS
+#define PPE_MT_LDS 2
+#endif
+// PPE_WALK_BL: a whole-LDS image's multi-tile block walk without per-tile branches: every lane reads a block each
+// step (a finished lane re-reads its last one) and the updates are selects, so the wave trades the per-tile exec-mask
+// bookkeeping (scalar instructions) for a few VALU selects
+#ifndef PPE_WALK_BL
+#define PPE_WALK_BL 0
+#endif
 // (trace the wave's tile iterations PPE_TRACE_SKIP .. + 3: a skip > 0 samples the steady state of a long launch)
 #ifndef PPE_TRACE_SKIP
 #define PPE_TRACE_SKIP 0u
@@ -721,6 +741,52 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
         recp[t] = false;
         nd[t] = make_uint4(PPE_LEAF_THR, 0u, 0u, 0u);
     }
+    if constexpr (PPE_WALK_BL && MODE == IMG_LDS && !RECW) {
+#pragma unroll 1
+        for (uint32_t it = 0; it < g.max_bdepth; ++it) {
+            uint4 q[MT][NQ];
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
+            }
+            bool pending = false;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                uint32_t x;
+                if constexpr (KL == 2) {
+                    const uint4 lo = q[t][0], hi = q[t][NQ - 1];
+                    const bool b0 = key_sel(lo.w & 15u, key[t]) > lo.x;
+                    const uint32_t t1 = b0 ? lo.z : lo.y;
+                    const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
+                    const bool b1 = key_sel(k1, key[t]) > t1;
+                    x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
+                } else {
+                    const uint4 a = q[t][0], b = q[t][1], c = q[t][2 % NQ], d = q[t][3 % NQ];
+                    const uint32_t sl = b.w;
+                    const bool b0 = key_sel(sl & 15u, key[t]) > a.x;
+                    const uint32_t t1 = b0 ? a.z : a.y;
+                    const uint32_t k1 = (sl >> (b0 ? 8u : 4u)) & 15u;
+                    const bool b1 = key_sel(k1, key[t]) > t1;
+                    const uint32_t t2 = b0 ? (b1 ? b.z : b.y) : (b1 ? b.x : a.w);
+                    const uint32_t k2 = (sl >> (4u * (3u + 2u * (uint32_t)b0 + (uint32_t)b1))) & 15u;
+                    const bool b2 = key_sel(k2, key[t]) > t2;
+                    const uint4 ex = b0 ? d : c;
+                    x = b1 ? (b2 ? ex.w : ex.z) : (b2 ? ex.y : ex.x);
+                }
+                const bool leaf = (x & PPE_BLK_LEAF) != 0u, act = !done[t];
+                const uint32_t pay = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF)
+                                                      : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
+                nd[t].z = (act & leaf) ? pay : nd[t].z;
+                blk[t] = (act & !leaf) ? x : blk[t];
+                pending = pending | (act & !leaf);
+                done[t] = done[t] | leaf;
+            }
+            if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
+        }
+        return;
+    }
 #pragma unroll 1
     for (uint32_t it = 0; it < g.max_bdepth + (RECW ? 1u : 0u); ++it) {
         uint4 q[MT][NQ];
@@ -964,7 +1030,11 @@ template <int MODE, int PF, int BLOCK, bool FLOW, bool PART = false>
 __global__ __launch_bounds__(BLOCK, ((PF == PF_MULTI || PF == PF_MULTI3) && !FLOW)
                                         ? (PF == PF_MULTI3 ? PPE_MT3_WAVES : PPE_MT_WAVES) : PPE_WAVES_PER_EU)
 void ppe_classify_kernel(ppe_kargs a) {
-    constexpr int MT = FLOW ? 1 : PF == PF_MULTI ? PPE_MT : PF == PF_MULTI3 ? PPE_MT3 : 1;
+    constexpr bool MT_PIPE = PF == PF_MULTI && !FLOW &&
+                             (PPE_MT_PF == 2 || (PPE_MT_PF == 1 && MODE == IMG_LDS));  // the pipelined round loop
+    constexpr int MT = FLOW ? 1
+                     : PF == PF_MULTI ? ((PPE_MT_PF == 1 && MODE == IMG_LDS) ? PPE_MT_LDS : PPE_MT)
+                     : PF == PF_MULTI3 ? PPE_MT3 : 1;
     constexpr int KL = (PF == PF_MULTI3 || PF == PF_SBLK3) ? 3 : 2;  // block levels of the image's block section
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     // single-tile walks over a whole-LDS image use its 2-level blocks with the keys in registers (no key slots)
@@ -1172,7 +1242,136 @@ void ppe_classify_kernel(ppe_kargs a) {
         finish(tile, p, valid, k, fh, hit, pend);
     };
 
-    if constexpr (MT > 1) {
+    if constexpr (MT > 1 && MT_PIPE) {
+        // PF_MULTI, pipelined: wave w takes rounds of MT tiles [MT w, MT w + MT), then + MT W, ... of its group's
+        // batches; round r + 1's windows are requested during round r (PPE_MT_PF above)
+        constexpr bool PF_EARLY = MODE == IMG_LDS;  // request before the walk (no global loads in walk / records)
+        uint4 r0[MT], r1[MT], r2[MT];
+        uint32_t r3[MT], rl[MT];
+        auto load_round = [&](const uint8_t *hdr, const uint32_t *lenp, uint32_t n, uint32_t stride, uint32_t t0) {
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const uint32_t pc = min(((t0 + t) << 6) + lane, n - 1u);
+                const uint32_t ro = pc * stride;
+                r0[t] = gld_win<uint4>(hdr, ro);
+                r1[t] = gld_win<uint4>(hdr, ro + 16u);
+                r2[t] = gld_win<uint4>(hdr, ro + 32u);
+                r3[t] = gld_win<uint32_t>(hdr, ro + 48u);
+                rl[t] = gld_win<uint32_t>(lenp, 4u * pc);
+            }
+        };
+        const uint32_t t_first = wtile * MT, t_step = stride_waves * MT;
+        // the first round: the group's first batch with a tile for this wave
+        uint32_t bi = grp, t0 = t_first;
+        bool live = wave_live;
+        while (live && t0 >= ((B.n + 63u) >> 6)) {
+            bi += ngroups;
+            live = bi < a.nbatch;
+            if (live) B = bdesc(bi);
+        }
+        if (live) load_round(B.hdr, B.len, B.n, B.stride, t0);
+        while (live) {
+            const uint32_t ntiles = (B.n + 63u) >> 6;
+            // decode: the packed key (sip, dip, ports, meta = status | flags << 8 | proto << 16) and, for the tuple
+            // output only, payload length and TCP option word
+            uint32_t key[MT][4], kpay[MT], kopt[MT];
+            bool need[MT];
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const uint32_t p = ((t0 + t) << 6) + lane;
+                if (p < B.n) rx_bytes += rl[t];
+                const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
+                                        r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
+                Dec d = decode(w, rl[t], B.hdr, p, B.stride, a.syn_check);
+                if ((PPE_ABLATE & 1) && d.st == ST_ACL) {
+                    d.st = PPE_ST_ACL_FW;
+                    d.flags |= PPE_F_ACL;
+                }
+                need[t] = d.st == ST_ACL;
+                key[t][0] = d.sip;
+                key[t][1] = d.dip;
+                key[t][2] = d.sport | (d.dport << 16);
+                key[t][3] = d.st | (d.flags << 8) | (d.proto << 16);
+                kpay[t] = d.paylen;
+                kopt[t] = d.tcpopt;
+            }
+            // the next round (scalar): this batch's next tiles, else the group's next batch with a tile for this wave
+            uint32_t nbi = bi, nt0 = t0 + t_step;
+            const uint8_t *nh = B.hdr;
+            const uint32_t *nl = B.len;
+            uint32_t nn = B.n, ns = B.stride;
+            bool nlive = true;
+            if (nt0 >= ntiles) {
+                nt0 = t_first;
+                for (;;) {
+                    nbi += ngroups;
+                    nlive = nbi < a.nbatch;
+                    if (!nlive) break;
+                    const ppe_bdesc D = bdesc(nbi);
+                    if (nt0 < ((D.n + 63u) >> 6)) {
+                        nh = D.hdr;
+                        nl = D.len;
+                        nn = D.n;
+                        ns = D.stride;
+                        break;
+                    }
+                }
+            }
+            if (PF_EARLY && nlive) load_round(nh, nl, nn, ns, nt0);
+            uint4 nd[MT];
+            acl_walk_blocks_mt<MODE, L::IMGB, MT, KL>(a.img, geo, key, need, nd);
+            int32_t hit[MT];
+            bool drop[MT];
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                hit[t] = -1;
+                drop[t] = false;
+                if (need[t]) {
+                    const uint32_t sip = key[t][0], dip = key[t][1], sport = key[t][2] & 0xffffu,
+                                   dport = key[t][2] >> 16, proto = key[t][3] >> 16;
+                    if (geo.off_crec) {
+                        acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, sip, dip, sport, dport, proto == 6u, hit[t],
+                                                  drop[t]);
+                    } else {
+                        uint32_t rule_act;
+                        const uint32_t p = ((t0 + t) << 6) + lane;
+                        const MacFromWindow mac = {B.hdr, p, B.stride};
+                        acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], sip, dip, sport, dport, proto, mac, B.ts, p, a.now,
+                                                hit[t], rule_act);
+                        drop[t] = rule_act == ACL_RULE_ACTION_DROP;
+                    }
+                }
+            }
+            if (!PF_EARLY && nlive) load_round(nh, nl, nn, ns, nt0);
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const uint32_t tile = t0 + t;
+                if (tile >= ntiles) break;  // wave-uniform
+                const uint32_t p = (tile << 6) + lane;
+                Dec k;
+                k.sip = key[t][0];
+                k.dip = key[t][1];
+                k.sport = key[t][2] & 0xffffu;
+                k.dport = key[t][2] >> 16;
+                k.st = key[t][3] & 0xffu;
+                k.flags = (key[t][3] >> 8) & 0xffu;
+                k.proto = key[t][3] >> 16;
+                k.paylen = kpay[t];
+                k.tcpopt = kopt[t];
+                const uint32_t fh = (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4))
+                                        ? flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport) : 0u;
+                if (need[t]) {
+                    k.st = drop[t] ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
+                    k.flags |= PPE_F_ACL;
+                }
+                finish(tile, p, p < B.n, k, fh, hit[t], false);
+            }
+            if (nlive && nbi != bi) B = bdesc(nbi);
+            bi = nbi;
+            t0 = nt0;
+            live = nlive;
+        }
+    } else if constexpr (MT > 1) {
         // PF_MULTI: wave w takes tiles [MT w, MT w + MT), then + MT W, ...; all MT windows are requested together
         for (uint32_t bi = grp; wave_live && bi < a.nbatch; bi += ngroups) {
             if (bi != grp) B = bdesc(bi);
@@ -1202,7 +1401,11 @@ void ppe_classify_kernel(ppe_kargs a) {
                     if (valid) rx_bytes += rl[t];
                     const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
                                             r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
-                    const Dec d = decode(w, rl[t], B.hdr, p, B.stride, a.syn_check);
+                    Dec d = decode(w, rl[t], B.hdr, p, B.stride, a.syn_check);
+                    if ((PPE_ABLATE & 1) && d.st == ST_ACL) {
+                        d.st = PPE_ST_ACL_FW;
+                        d.flags |= PPE_F_ACL;
+                    }
                     need[t] = d.st == ST_ACL;
                     key[t][0] = d.sip;
                     key[t][1] = d.dip;
@@ -1232,8 +1435,8 @@ void ppe_classify_kernel(ppe_kargs a) {
                     k.proto = key[t][3] >> 16;
                     k.paylen = kpay[t];
                     k.tcpopt = kopt[t];
-                    const uint32_t fh = (k.flags & PPE_F_L4) ? flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport,
-                                                                               k.dport) : 0u;
+                    const uint32_t fh = (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4))
+                                            ? flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport) : 0u;
                     int32_t hit = -1;
                     if (need[t]) {
                         bool drop;
