@@ -66,11 +66,13 @@
 #ifndef PPE_MT_LDS
 #define PPE_MT_LDS 2
 #endif
-// PPE_WALK_BL: a whole-LDS image's multi-tile block walk without per-tile branches: every lane reads a block each
-// step (a finished lane re-reads its last one) and the updates are selects, so the wave trades the per-tile exec-mask
-// bookkeeping (scalar instructions) for a few VALU selects
+// PPE_WALK_BL: a whole-LDS image's block walk without per-tile branches: every lane reads a block each step (a
+// finished lane its last one again) and the updates are selects, so the wave trades the per-tile exec-mask
+// bookkeeping (scalar instructions) for a few VALU selects (C2 / C4 step -2 / -2.6 %, gpurun_out/r3j).  The same on
+// split images, and a key select by bit tests instead of the equality chain, measured C3 +6.7 % (gpurun_out/r3m:
+// SALU 336 -> 159 but VALU 506 -> 702 per tile, gpurun_out/r3n), so they are not used.
 #ifndef PPE_WALK_BL
-#define PPE_WALK_BL 0
+#define PPE_WALK_BL 1
 #endif
 // (trace the wave's tile iterations PPE_TRACE_SKIP .. + 3: a skip > 0 samples the steady state of a long launch)
 #ifndef PPE_TRACE_SKIP
@@ -747,9 +749,21 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
             uint4 q[MT][NQ];
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
-                const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
+                if constexpr (MODE == IMG_LDS) {  // every lane reads (a finished one its last block again)
+                    const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
 #pragma unroll
-                for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
+                    for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
+                } else if (!done[t]) {  // (no global traffic for finished lanes)
+                    if (MODE != IMG_GLOBAL && blk[t] < g.lds_blocks) {
+                        const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
+#pragma unroll
+                        for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
+                    } else {
+                        const uint32_t ga = 4u * g.off_blocks + BB * blk[t];
+#pragma unroll
+                        for (int j = 0; j < NQ; ++j) q[t][j] = gld<uint4>(gimg, ga + 16u * j);
+                    }
+                }
             }
             bool pending = false;
 #pragma unroll
