@@ -58,7 +58,7 @@
 // the record check issue no global loads), else after the record checks (overlapping the hash, stores, compaction
 // and counters).  1 = whole-LDS images only, at PPE_MT_LDS tiles per wave (the next round's windows need the
 // registers of two more tiles: C2 / C4 step -4.5 / -3 % at 2 tiles against the round-2 loop at 4, 3 tiles with
-// prefetch -1 %, 4 spills; gpurun_out/r3h); 2 = every image (split images: C3 +3 %, experiment); 0 = the round-2
+// prefetch -1 %, 4 spills; profiles/r3_ab_runs.md r3h); 2 = every image (split images: C3 +3 %, experiment); 0 = the round-2
 // loop (load, decode, walk, finish) everywhere.
 #ifndef PPE_MT_PF
 #define PPE_MT_PF 1
@@ -68,9 +68,9 @@
 #endif
 // PPE_WALK_BL: a whole-LDS image's block walk without per-tile branches: every lane reads a block each step (a
 // finished lane its last one again) and the updates are selects, so the wave trades the per-tile exec-mask
-// bookkeeping (scalar instructions) for a few VALU selects (C2 / C4 step -2 / -2.6 %, gpurun_out/r3j).  The same on
-// split images, and a key select by bit tests instead of the equality chain, measured C3 +6.7 % (gpurun_out/r3m:
-// SALU 336 -> 159 but VALU 506 -> 702 per tile, gpurun_out/r3n), so they are not used.
+// bookkeeping (scalar instructions) for a few VALU selects (C2 / C4 step -2 / -2.6 %, profiles/r3_ab_runs.md r3j).  The same on
+// split images, and a key select by bit tests instead of the equality chain, measured C3 +6.7 % (profiles/r3_ab_runs.md r3m:
+// SALU 336 -> 159 but VALU 506 -> 702 per tile, profiles/r3_instruction_mix.md r3n), so they are not used.
 #ifndef PPE_WALK_BL
 #define PPE_WALK_BL 1
 #endif
