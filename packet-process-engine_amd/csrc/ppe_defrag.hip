@@ -9,16 +9,17 @@
  *              look the key up in the device FCB hash table (open addressing, linear probing);
  *   claim      fragments whose FCB does not exist claim a slot (CAS, key = the claiming fragment's parsed key) and
  *              record the lowest claiming index: that fragment is the one whose fcb_create runs;
- *   admit      creators in index order (per-tile ballot counts, one-workgroup scan) get FCB records while
- *              running + rank < fcb_max (fcb_create's fetch-and-add cap); the others fail, and with them every later
- *              fragment of their key in this batch, because the running count cannot fall inside a batch;
+ *   admit      creators in index order (per-tile ballot counts; each workgroup sums the counts before it) get FCB
+ *              records while running + rank < fcb_max (fcb_create's fetch-and-add cap); the others fail, and with
+ *              them every later fragment of their key in this batch, because the running count cannot fall inside
+ *              a batch;
  *   group      stable LSD radix sort of the fragments by FCB, keyed by the FCB's first fragment index in the batch
- *              (8-bit digits, wave multisplit ranks; 2 passes for 65,536 fragments), so each FCB's fragments are
- *              contiguous and in arrival order;
+ *              (8-bit digits, wave multisplit ranks, each scatter workgroup scanning the digit histogram itself; 2
+ *              passes for 65,536 fragments), so each FCB's fragments are contiguous and in arrival order;
  *   process    one lane per FCB runs the reference state machine over its fragments in order (chain ≤ cache_max
  *              entries, kept as a nibble list of store slots);
  *   stash      one wave per held fragment copies its frame into the FCB's store slot (PACKET_HW2SW, mbuf.c:117-156);
- *   place      completing fragments in index order get datagram indices (ballot counts + scan);
+ *   place      completing fragments in index order get datagram indices (ballot counts, summed per workgroup);
  *   assemble   one workgroup per datagram concatenates the chain (Frag_defrag_reasm, decode-defrag.c:222-289),
  *              patches ip_len / ip_off / the header checksum, and writes a classify-ready window + length.
  *
@@ -56,7 +57,7 @@ constexpr uint32_t kRecWords = 8;
 
 // control words (u64)
 enum { C_RUNNING = 0, C_NEW, C_DEL, C_FREE_TOP, C_DGRAMS, C_TEARDROP, C_TIMEOUT_DROP, C_NDGRAM, C_ST0 = 8,
-       C_ADMIT_BASE = C_ST0 + PPE_DF__COUNT, C_FREE_BASE, C_CREATORS, C_AGE_DROPPED, C_AGE_FREED, C_SCRATCH,
+       C_CREATORS = C_ST0 + PPE_DF__COUNT + 2, C_AGE_DROPPED, C_AGE_FREED, C_SCRATCH,
        C_WORDS = 24 };
 
 // parsed fragment record words (frec): sip, dip, id | proto << 16 | mf << 24, off | flen << 16, totlen,
@@ -252,64 +253,53 @@ __global__ void __launch_bounds__(kBlock) df_tile_count_kernel(DfArgs a) {
     if (__lane_id() == 0 && i < a.n) a.tcnt[i >> 6] = (uint32_t)__popcll(b);
 }
 
-// exclusive scan of cnt[0..m) in place by one workgroup of kScanT threads; total → *total
-__device__ void block_scan_inplace(uint32_t *cnt, uint32_t m, unsigned long long *total) {
-    __shared__ uint32_t wsum[kScanT / 64];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (uint32_t base = 0; base < m; base += kScanT) {
-        const uint32_t j = base + threadIdx.x;
-        const uint32_t v = j < m ? cnt[j] : 0u;
-        uint32_t x = v;   // inclusive wave scan
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if ((int)__lane_id() >= o) x += y;
-        }
-        const uint32_t w = threadIdx.x >> 6;
-        if (__lane_id() == 63) wsum[w] = x;
-        __syncthreads();
-        uint32_t before = carry;
-        for (uint32_t k = 0; k < w; ++k) before += wsum[k];
-        if (j < m) cnt[j] = before + x - v;
-        __syncthreads();
-        if (threadIdx.x == kScanT - 1) carry = before + x;
-        __syncthreads();
+// This workgroup's exclusive prefix of the tile counts: the sum of cnt[0, t0), and (total != nullptr) the sum of
+// cnt[0, tiles).  Every workgroup reads the whole (small: n / 64 words) count array from L2 itself, so the ranked
+// kernels need no separate scan launch.
+template <int T>
+__device__ uint32_t wg_tile_prefix(const uint32_t *cnt, uint32_t t0, uint32_t tiles, uint32_t *total) {
+    __shared__ uint32_t wsum[2][T / 64];
+    uint32_t before = 0, all = 0;
+    for (uint32_t k = threadIdx.x; k < tiles; k += T) {
+        const uint32_t v = cnt[k];
+        all += v;
+        before += k < t0 ? v : 0u;
     }
-    if (threadIdx.x == 0) *total = carry;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        before += __shfl_xor(before, o, 64);
+        all += __shfl_xor(all, o, 64);
+    }
+    if (__lane_id() == 0) {
+        wsum[0][threadIdx.x >> 6] = before;
+        wsum[1][threadIdx.x >> 6] = all;
+    }
+    __syncthreads();
+    uint32_t b = 0, t = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < T / 64; ++w) {
+        b += wsum[0][w];
+        t += wsum[1][w];
+    }
+    if (total) *total = t;
+    return b;
 }
 
-// creators: base values for the admission kernel, then the running count / free-stack top after it
-__global__ void __launch_bounds__(kScanT) df_scan_kernel(DfArgs a) {
-    const uint32_t tiles = (a.n + 63) / 64;
-    block_scan_inplace(a.tcnt, tiles, a.flag_mode == 0 ? a.ctl + C_CREATORS : a.ctl + C_NDGRAM);
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    if (a.flag_mode == 0) {
-        const unsigned long long run = a.ctl[C_RUNNING], creators = a.ctl[C_CREATORS];
-        const unsigned long long room = run < a.fcb_max ? a.fcb_max - run : 0ull;
-        const unsigned long long adm = creators < room ? creators : room;
-        a.ctl[C_ADMIT_BASE] = run;
-        a.ctl[C_FREE_BASE] = a.ctl[C_FREE_TOP];
-        a.ctl[C_RUNNING] = run + adm;
-        a.ctl[C_FREE_TOP] -= adm;
-        a.ctl[C_NEW] += adm;
-    } else {
-        a.ctl[C_DGRAMS] += a.ctl[C_NDGRAM];
-        if (a.n_dgram) *a.n_dgram = (uint32_t)a.ctl[C_NDGRAM];
-    }
-}
-
+// (the running count and free-stack top are read as they stood before this batch: the histogram pass of the sort,
+// which runs next, moves them past this batch's admissions)
 __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t t0 = blockIdx.x * (kBlock / 64), w = threadIdx.x >> 6;
+    uint32_t base = wg_tile_prefix<kBlock>(a.tcnt, t0, (a.n + 63) / 64, nullptr);
+    for (uint32_t k = 0; k < w; ++k) base += a.tcnt[t0 + k];   // the workgroup's earlier waves
     const bool f = df_flag(a, i);
     const uint64_t b = __builtin_amdgcn_ballot_w64(f);
     if (!f) return;
-    const uint32_t rank = a.tcnt[i >> 6] + (uint32_t)__popcll(b & lanemask_lt());
+    const uint32_t rank = base + (uint32_t)__popcll(b & lanemask_lt());
     const uint32_t s = a.fslot[i];
     // fcb_create (decode-defrag.c:74-81): fetch-and-add, fail when the previous count reached DEFRAG_FCB_MAX
-    if (a.ctl[C_ADMIT_BASE] + rank < a.fcb_max) {
-        const uint32_t r = a.freestk[a.ctl[C_FREE_BASE] - 1 - rank];
+    if (a.ctl[C_RUNNING] + rank < a.fcb_max) {
+        const uint32_t r = a.freestk[a.ctl[C_FREE_TOP] - 1 - rank];
         const uint32_t *fr = a.frec + (size_t)i * kFrecWords;
         uint32_t *k = a.tkey + (size_t)s * 4;
         k[0] = fr[0];
@@ -374,67 +364,66 @@ __global__ void __launch_bounds__(kSortBlock) df_sort_pass_kernel(DfArgs a) {
             for (uint32_t k = 0; k < kSortBlock / 64; ++k) t += cnt[k][dd];
             a.hist[dd * a.sort_blocks + blockIdx.x] = t;
         }
+        if (INIT && blockIdx.x == 0) {
+            // after the admission kernel: the creators of this batch (the tile counts it ranked) move the running
+            // count and the free-stack top (fcb_create's fetch-and-add, decode-defrag.c:74-81)
+            uint32_t creators = 0;
+            wg_tile_prefix<kSortBlock>(a.tcnt, 0u, (a.n + 63) / 64, &creators);
+            if (threadIdx.x == 0) {
+                const unsigned long long run = a.ctl[C_RUNNING];
+                const unsigned long long room = run < a.fcb_max ? a.fcb_max - run : 0ull;
+                const unsigned long long adm = creators < room ? creators : room;
+                a.ctl[C_CREATORS] = creators;
+                a.ctl[C_RUNNING] = run + adm;
+                a.ctl[C_FREE_TOP] -= adm;
+                a.ctl[C_NEW] += adm;
+            }
+        }
         return;
     }
+    // the digit bases of this workgroup from the histogram (every workgroup scans it itself; no scan launch):
+    // digit d starts after every smaller digit of all workgroups and digit d of the earlier workgroups.  Four
+    // threads per digit read its row of sort_blocks words.
+    __shared__ uint32_t dsum[256], dbase[256], wtot[4];
+    {
+        const uint32_t dd = threadIdx.x >> 2, qq = threadIdx.x & 3u;
+        const uint32_t chunk = (a.sort_blocks + 3u) / 4u, b0 = qq * chunk;
+        const uint32_t b1 = b0 + chunk < a.sort_blocks ? b0 + chunk : a.sort_blocks;
+        uint32_t col = 0, part = 0;
+        for (uint32_t bb = b0; bb < b1; ++bb) {
+            const uint32_t h = a.hist[dd * a.sort_blocks + bb];
+            col += h;
+            part += bb < blockIdx.x ? h : 0u;
+        }
+        col += __shfl_xor(col, 1, 64);
+        col += __shfl_xor(col, 2, 64);
+        part += __shfl_xor(part, 1, 64);
+        part += __shfl_xor(part, 2, 64);
+        if (qq == 0) dsum[dd] = col;
+        __syncthreads();
+        if (threadIdx.x < 256) {   // exclusive scan of the 256 digit totals (4 waves)
+            const uint32_t c = dsum[threadIdx.x];
+            uint32_t x = c;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if ((int)__lane_id() >= o) x += y;
+            }
+            dbase[threadIdx.x] = x - c;   // within the wave; the earlier waves' totals are added below
+            if (__lane_id() == 63) wtot[threadIdx.x >> 6] = x;
+        }
+        __syncthreads();
+        if (qq == 0) {
+            uint32_t carry = 0;
+            for (uint32_t k = 0; k < (dd >> 6); ++k) carry += wtot[k];
+            dbase[dd] += carry + part;
+        }
+        __syncthreads();
+    }
     if (!v) return;
-    uint32_t pos = a.hist[d * a.sort_blocks + blockIdx.x] + rank;
+    uint32_t pos = dbase[d] + rank;
     for (uint32_t k = 0; k < w; ++k) pos += cnt[k][d];
     a.skey[1][pos] = key;
     a.sval[1][pos] = a.sval[0][j];
-}
-
-// exclusive scan of the digit histogram (256 x sort_blocks words) by one workgroup: thread t owns the contiguous chunk
-// [t*c, (t+1)*c) (16-B loads and stores), so there is one block-wide scan instead of one per 1,024 words
-__global__ void __launch_bounds__(kScanT) df_hist_scan_kernel(DfArgs a) {
-    __shared__ uint32_t wsum[kScanT / 64];
-    const uint32_t m = 256u * a.sort_blocks;
-    const uint32_t c = (((m + kScanT - 1) / kScanT) + 3u) & ~3u;   // words per thread, a multiple of 4
-    const uint32_t b0 = threadIdx.x * c;
-    constexpr uint32_t kHold = 16;   // chunks of up to 64 words (max_batch <= 65,536) stay in registers
-    uint4 held[kHold];
-    const bool hold = c <= 4 * kHold;
-    uint32_t sum = 0;
-    if (hold) {
-#pragma unroll
-        for (uint32_t q = 0; q < kHold; ++q) {
-            const uint32_t k = b0 + 4 * q;
-            held[q] = (4 * q < c && k < m) ? *(const uint4 *)(a.hist + k) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < kHold; ++q) sum += held[q].x + held[q].y + held[q].z + held[q].w;
-    } else {
-        for (uint32_t k = b0; k < b0 + c && k < m; k += 4) {   // m = 256 * sort_blocks is a multiple of 4
-            const uint4 v = *(const uint4 *)(a.hist + k);
-            sum += v.x + v.y + v.z + v.w;
-        }
-    }
-    uint32_t x = sum;   // inclusive wave scan of the chunk sums
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if ((int)__lane_id() >= o) x += y;
-    }
-    const uint32_t w = threadIdx.x >> 6;
-    if (__lane_id() == 63) wsum[w] = x;
-    __syncthreads();
-    uint32_t run = x - sum;
-    for (uint32_t k = 0; k < w; ++k) run += wsum[k];
-    if (hold) {
-#pragma unroll
-        for (uint32_t q = 0; q < kHold; ++q) {
-            const uint32_t k = b0 + 4 * q;
-            const uint4 v = held[q];
-            if (4 * q < c && k < m)
-                *(uint4 *)(a.hist + k) = make_uint4(run, run + v.x, run + v.x + v.y, run + v.x + v.y + v.z);
-            run += v.x + v.y + v.z + v.w;
-        }
-        return;
-    }
-    for (uint32_t k = b0; k < b0 + c && k < m; k += 4) {
-        uint4 v = *(const uint4 *)(a.hist + k);
-        const uint4 e = make_uint4(run, run + v.x, run + v.x + v.y, run + v.x + v.y + v.z);
-        run += v.x + v.y + v.z + v.w;
-        *(uint4 *)(a.hist + k) = e;
-    }
 }
 
 // ---- the reference state machine, one lane per FCB --------------------------------------------------------------------
@@ -652,12 +641,21 @@ __global__ void __launch_bounds__(kBlock) df_stash_kernel(DfArgs a) {
 // ---- place: datagram index of each completing fragment, in index order ------------------------------------------------
 __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t t0 = blockIdx.x * (kBlock / 64), w = threadIdx.x >> 6;
+    uint32_t nd = 0;
+    uint32_t base = wg_tile_prefix<kBlock>(a.tcnt, t0, (a.n + 63) / 64, &nd);
+    for (uint32_t k = 0; k < w; ++k) base += a.tcnt[t0 + k];   // the workgroup's earlier waves
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // the datagram count (read by the assembly kernel, next)
+        a.ctl[C_NDGRAM] = nd;
+        a.ctl[C_DGRAMS] += nd;
+        if (a.n_dgram) *a.n_dgram = nd;
+    }
     const bool f = df_flag(a, i);
     const uint64_t b = __builtin_amdgcn_ballot_w64(f);
     if (i >= a.n) return;
     uint32_t j = kNone;
     if (f) {
-        j = a.tcnt[i >> 6] + (uint32_t)__popcll(b & lanemask_lt());
+        j = base + (uint32_t)__popcll(b & lanemask_lt());
         a.dgsrc[j] = i;
     }
     if (a.dgram_of) a.dgram_of[i] = j;
@@ -1030,7 +1028,6 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
     hipLaunchKernelGGL(df_claim_kernel, dim3(g), dim3(kBlock), 0, s, a);
     a.flag_mode = 0;
     hipLaunchKernelGGL(df_tile_count_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(df_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(df_admit_kernel, dim3(g), dim3(kBlock), 0, s, a);
     uint32_t passes = 1;   // sort keys are batch indices < n
     while (passes < 4 && (uint64_t)a.n > (1ull << (8 * passes))) ++passes;
@@ -1040,7 +1037,6 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
             hipLaunchKernelGGL((df_sort_pass_kernel<false, true>), dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
         else
             hipLaunchKernelGGL((df_sort_pass_kernel<false, false>), dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
-        hipLaunchKernelGGL(df_hist_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
         hipLaunchKernelGGL((df_sort_pass_kernel<true, false>), dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
         std::swap(a.skey[0], a.skey[1]);
         std::swap(a.sval[0], a.sval[1]);
@@ -1049,7 +1045,6 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
     hipLaunchKernelGGL(df_stash_kernel, dim3(blocks(a.n, kBlock / 64)), dim3(kBlock), 0, s, a);
     a.flag_mode = 1;
     hipLaunchKernelGGL(df_tile_count_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(df_scan_kernel, dim3(1), dim3(kScanT), 0, s, a);
     hipLaunchKernelGGL(df_place_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_assemble_kernel, dim3(blocks(a.n, kBlock / 64)), dim3(kBlock), 0, s, a);
     return launched(d, "ppe_defrag");
