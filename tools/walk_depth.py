@@ -30,7 +30,7 @@ def walk(img, keys):
     n = len(keys)
     jump = int(img[W_JUMP])
     off_bsec, off_blocks, max_bd = int(img[W_OFFBSEC]), int(img[W_OFFBLOCKS]), int(img[W_MAXBDEPTH])
-    blocks = img[off_blocks:].reshape(-1, 8)[: int(img[W_NBLOCKS])]
+    blocks = img[off_blocks: off_blocks + 8 * int(img[W_NBLOCKS])].reshape(-1, 8)
     kx = np.concatenate([keys.astype(np.uint64), np.zeros((n, 11), np.uint64)], axis=1)  # slots >= 5 read key 0
     if jump:
         dim, shift = jump & 0xFF, (jump >> 8) & 0xFF
