@@ -53,7 +53,7 @@ struct HostStage {
 // Device flow table (ppe_classify_flow) and what the host knows about it without synchronising.
 struct FlowArrays {
     uint32_t *keys = nullptr, *creator = nullptr;
-    unsigned long long *stats = nullptr, *packed = nullptr, *last = nullptr;
+    unsigned long long *stats = nullptr, *packed = nullptr;
 };
 struct FlowTable {
     uint32_t capacity = 0, max_batch = 0, nslots = 0;
@@ -1044,27 +1044,24 @@ static void flow_free_arrays(FlowArrays &a) {
     (void)hipFree(a.creator);
     (void)hipFree(a.stats);
     (void)hipFree(a.packed);
-    (void)hipFree(a.last);
     a = FlowArrays();
 }
 
 // allocate (if needed) and clear one slot-array set: every slot EMPTY with zero counters, no creator
 static int flow_clear_arrays(ppe_ctx *c, FlowArrays &a, uint32_t nslots, hipStream_t s) {
     if (!a.keys) {
-        if (hipMalloc(&a.keys, (size_t)nslots * 16u) != hipSuccess ||
+        if (hipMalloc(&a.keys, (size_t)nslots * 4u * PPE_FLOW_SLOT_WORDS) != hipSuccess ||
             hipMalloc(&a.creator, (size_t)nslots * 4u) != hipSuccess ||
             hipMalloc(&a.stats, (size_t)nslots * 32u) != hipSuccess ||
-            hipMalloc(&a.packed, (size_t)nslots * 16u) != hipSuccess ||
-            hipMalloc(&a.last, (size_t)nslots * 8u) != hipSuccess) {
+            hipMalloc(&a.packed, (size_t)nslots * 16u) != hipSuccess) {
             flow_free_arrays(a);
             return fail(c, PPE_ENOMEM, "flow table: out of device memory (%u slots)", nslots);
         }
     }
-    HIPCHK(c, hipMemsetAsync(a.keys, 0, (size_t)nslots * 16u, s));
+    HIPCHK(c, hipMemsetAsync(a.keys, 0, (size_t)nslots * 4u * PPE_FLOW_SLOT_WORDS, s));
     HIPCHK(c, hipMemsetAsync(a.creator, 0xff, (size_t)nslots * 4u, s));
     HIPCHK(c, hipMemsetAsync(a.stats, 0, (size_t)nslots * 32u, s));
     HIPCHK(c, hipMemsetAsync(a.packed, 0, (size_t)nslots * 16u, s));
-    HIPCHK(c, hipMemsetAsync(a.last, 0, (size_t)nslots * 8u, s));
     return PPE_OK;
 }
 
@@ -1081,14 +1078,13 @@ static ppe_flowdev flow_dev(const FlowTable &t, int which) {
     d.fold_bytes = t.fold_bytes;
     d.snap = t.snap_d;
     d.seq = t.batches;
-    d.last = a.last;
     d.creator = a.creator;
     d.ctl = t.ctl;
     d.rec = t.rec;
     d.tile_miss = t.tile_miss;
     d.tile_new = t.tile_new;
     d.rslot = t.rslot;
-    d.gmask = t.nslots / 4u - 1u;
+    d.gmask = t.nslots / PPE_FLOW_GROUP - 1u;
     d.capacity = t.capacity;
     return d;
 }
@@ -1336,28 +1332,27 @@ int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_
     HIPCHK(c, hipDeviceSynchronize());
     const FlowTable &t = *c->flow;
     const FlowArrays &a = t.arr[t.cur];
-    std::vector<uint32_t> keys((size_t)t.nslots * 4u);
+    constexpr uint32_t W = PPE_FLOW_SLOT_WORDS;
+    std::vector<uint32_t> keys((size_t)t.nslots * W);
     HIPCHK(c, hipMemcpy(keys.data(), a.keys, keys.size() * 4u, hipMemcpyDeviceToHost));
-    std::vector<unsigned long long> stats, packed, last;
+    std::vector<unsigned long long> stats, packed;
     if (entries && max) {
         stats.resize((size_t)t.nslots * 4u);
         packed.resize((size_t)t.nslots * 2u);
-        last.resize(t.nslots);
         HIPCHK(c, hipMemcpy(stats.data(), a.stats, stats.size() * 8u, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(packed.data(), a.packed, packed.size() * 8u, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(last.data(), a.last, last.size() * 8u, hipMemcpyDeviceToHost));
     }
     uint32_t k = 0;
     for (uint32_t s = 0; s < t.nslots; ++s) {
-        const uint32_t st = keys[4u * s + 3u];
+        const uint32_t *kw = &keys[(size_t)W * s], st = kw[3];
         if ((st & (PPE_FS_PEND | 0xffu)) != PPE_FS_LIVE(0u)) continue;
         if (entries && k < max) {
             ppe_flow_entry_t &e = entries[k];
             std::memset(&e, 0, sizeof e);
-            e.sip = keys[4u * s];
-            e.dip = keys[4u * s + 1u];
-            e.sport = (uint16_t)(keys[4u * s + 2u] & 0xffffu);
-            e.dport = (uint16_t)(keys[4u * s + 2u] >> 16);
+            e.sip = kw[0];
+            e.dip = kw[1];
+            e.sport = (uint16_t)(kw[2] & 0xffffu);
+            e.dport = (uint16_t)(kw[2] >> 16);
             e.protocol = (uint8_t)(st >> 8);
             e.slot = s;
             const unsigned long long bmask = (1ull << PPE_PK_SHIFT) - 1u, p0 = packed[2u * s], p1 = packed[2u * s + 1u];
@@ -1365,7 +1360,7 @@ int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_
             e.bytecnts2d = stats[4u * s + 1u] + (p0 & bmask);
             e.pktcntd2s = stats[4u * s + 2u] + (p1 >> PPE_PK_SHIFT);
             e.bytecntd2s = stats[4u * s + 3u] + (p1 & bmask);
-            e.last_seen = last[s];
+            e.last_seen = (uint64_t)kw[PPE_FLOW_LAST_WORD] | ((uint64_t)kw[PPE_FLOW_LAST_WORD + 1u] << 32);
         }
         ++k;
     }

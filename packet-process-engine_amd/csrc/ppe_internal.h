@@ -22,9 +22,15 @@ struct ppe_bdesc {
     uint32_t pad;
 };
 
-/* Device flow table (ppe_classify_flow; ppe_kernels.hip "flow table").  Open addressing over groups of 4 slots
- * (64 B of keys), linear probing from group flow_hash & gmask; a key lies before the first EMPTY slot of its probe
- * sequence (slots never return to EMPTY: deletions leave TOMBs, reclaimed by a rehash). */
+/* Device flow table (ppe_classify_flow; ppe_kernels.hip "flow table").  Open addressing over groups of
+ * PPE_FLOW_GROUP slots (one 64-B line segment of slot records), linear probing from group flow_hash & gmask; a key lies
+ * before the first EMPTY slot of its probe sequence (slots never return to EMPTY: deletions leave TOMBs, reclaimed by
+ * a rehash).  A slot record is 32 B, {sip, dip, sport | dport << 16, state, last-seen (u64), 0, 0}: the last-seen
+ * store of a found packet lands in the 64 B its probe has just brought into L2, instead of a random 8-B partial
+ * write of its own in a separate array. */
+#define PPE_FLOW_GROUP 2u       /* slots per probe group */
+#define PPE_FLOW_SLOT_WORDS 8u  /* u32 words per slot record */
+#define PPE_FLOW_LAST_WORD 4u   /* the record's last-seen time (u64, words 4-5) */
 #define PPE_FS_EMPTY 0u
 #define PPE_FS_TOMB 1u
 #define PPE_FS_LIVE(proto) (2u | ((proto) << 8))  /* key words valid */
@@ -37,11 +43,11 @@ enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_N
 #define PPE_PK_FOLD_PKTS (1ull << 23)          /* fold into `stats` once either field reaches half its range */
 #define PPE_PK_FOLD_BYTES (1ull << 39)
 struct ppe_flowdev {
-    uint32_t *keys;               /* nslots × {sip, dip, sport | dport << 16, state}, the creating packet's orientation */
+    uint32_t *keys;               /* nslots × {sip, dip, sport | dport << 16, state, last-seen (u64), 0, 0}: the key in
+                                     the creating packet's orientation                                                 */
     unsigned long long *packed;   /* nslots × {s2d, d2s}: packets << 40 | bytes, one atomic per packet (FlowUpdate)    */
     unsigned long long *stats;    /* nslots × {pkts s2d, bytes s2d, pkts d2s, bytes d2s}: folded from `packed` before a
                                      field can overflow; a flow's counters = stats + the packed fields               */
-    unsigned long long *last;     /* nslots × last-seen time                                                          */
     uint32_t *creator;            /* nslots: lowest index of the packets claiming the slot in this batch (| REVOKED)   */
     unsigned long long *ctl;      /* PPE_FCTL_* device counters                                                        */
     uint32_t *rec;                /* max_batch × {sip, dip, ports, proto | provisional status << 8} of pending packets */

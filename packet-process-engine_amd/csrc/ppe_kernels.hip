@@ -74,6 +74,13 @@
 #ifndef PPE_WALK_BL
 #define PPE_WALK_BL 1
 #endif
+// PPE_WALK_2PH: a split image's block walk in two phases.  The staged blocks are the breadth-first prefix of the
+// block forest, so a lane that leaves them never returns: phase 1 walks the LDS-resident levels without per-tile
+// branches (a lane outside them, or done, reads block 0 and keeps its state), phase 2 walks the rest from L2 with
+// one exec-masked global read per tile and step (no LDS / global branch pair per step).
+#ifndef PPE_WALK_2PH
+#define PPE_WALK_2PH 1
+#endif
 // (trace the wave's tile iterations PPE_TRACE_SKIP .. + 3: a skip > 0 samples the steady state of a long launch)
 #ifndef PPE_TRACE_SKIP
 #define PPE_TRACE_SKIP 0u
@@ -801,6 +808,75 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
         }
         return;
     }
+    if constexpr (PPE_WALK_2PH && MODE == IMG_SPLIT && KL == 2 && !RECW) {
+        // phase 1: the LDS-resident levels, branchless
+#pragma unroll 1
+        for (uint32_t it = 0; it < g.max_bdepth; ++it) {
+            uint4 q[MT][NQ];
+            bool inl[MT];
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                inl[t] = !done[t] & (blk[t] < g.lds_blocks);
+                const uint32_t la = IMGB + g.blk_lds + BB * (inl[t] ? blk[t] : 0u);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
+            }
+            bool pending = false;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const uint4 lo = q[t][0], hi = q[t][NQ - 1];
+                const bool b0 = key_sel(lo.w & 15u, key[t]) > lo.x;
+                const uint32_t t1 = b0 ? lo.z : lo.y;
+                const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
+                const bool b1 = key_sel(k1, key[t]) > t1;
+                const uint32_t x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
+                const bool leaf = (x & PPE_BLK_LEAF) != 0u;
+                const uint32_t pay = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF)
+                                                      : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
+                nd[t].z = (inl[t] & leaf) ? pay : nd[t].z;
+                blk[t] = (inl[t] & !leaf) ? x : blk[t];
+                done[t] = done[t] | (inl[t] & leaf);
+                pending = pending | (inl[t] & !leaf & (x < g.lds_blocks));
+            }
+            if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
+        }
+        // phase 2: the levels read from L2
+#pragma unroll 1
+        for (uint32_t it = 0; it < g.max_bdepth; ++it) {
+            bool pending = false;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) pending = pending | !done[t];
+            if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
+            uint4 q[MT][NQ];
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                if (!done[t]) {
+                    const uint32_t ga = 4u * g.off_blocks + BB * blk[t];
+#pragma unroll
+                    for (int j = 0; j < NQ; ++j) q[t][j] = gld<uint4>(gimg, ga + 16u * j);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                if (!done[t]) {
+                    const uint4 lo = q[t][0], hi = q[t][NQ - 1];
+                    const bool b0 = key_sel(lo.w & 15u, key[t]) > lo.x;
+                    const uint32_t t1 = b0 ? lo.z : lo.y;
+                    const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
+                    const bool b1 = key_sel(k1, key[t]) > t1;
+                    const uint32_t x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
+                    if (x & PPE_BLK_LEAF) {
+                        done[t] = true;
+                        nd[t].z = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF)
+                                                   : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
+                    } else {
+                        blk[t] = x;
+                    }
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll 1
     for (uint32_t it = 0; it < g.max_bdepth + (RECW ? 1u : 0u); ++it) {
         uint4 q[MT][NQ];
@@ -956,23 +1032,25 @@ __device__ __forceinline__ bool key_match(uint32_t ax, uint32_t ay, uint32_t az,
 }
 
 // FlowFind (flow.c:96-115) over the table as it stood at the start of the batch: the slot of the live flow of
-// this 5-tuple, or -1.  One 64-B group (4 slots) per probe step; stops at the first EMPTY slot.
+// this 5-tuple, or -1.  One 64-B group (PPE_FLOW_GROUP 32-B slot records, their key halves read) per probe step;
+// stops at the first EMPTY slot.
 __device__ __forceinline__ int32_t flow_find(const ppe_flowdev &f, uint32_t fh, uint32_t sip, uint32_t dip,
                                              uint32_t ports, uint32_t proto, uint32_t &fsip, uint32_t &fports) {
     const uint32_t live = PPE_FS_LIVE(proto);
-    const uint4 *keys = (const uint4 *)f.keys;
+    const uint4 *keys = (const uint4 *)f.keys;  // slot s's key half: keys[2 s]
+    constexpr uint32_t G = PPE_FLOW_GROUP;
     uint32_t g = fh & f.gmask;
 #pragma unroll 1
     for (uint32_t it = 0; it <= f.gmask; ++it) {
-        uint4 e[4];
+        uint4 e[G];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) e[j] = keys[4u * g + j];
+        for (uint32_t j = 0; j < G; ++j) e[j] = keys[2u * (G * g + j)];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (uint32_t j = 0; j < G; ++j) {
             if (e[j].w == live && key_match(e[j].x, e[j].y, e[j].z, sip, dip, ports)) {
                 fsip = e[j].x;
                 fports = e[j].z;
-                return (int32_t)(4u * g + j);
+                return (int32_t)(G * g + j);
             }
             if (e[j].w == PPE_FS_EMPTY) return -1;
         }
@@ -982,7 +1060,8 @@ __device__ __forceinline__ int32_t flow_find(const ppe_flowdev &f, uint32_t fh, 
 }
 
 // FlowGetPacketDirection (flow.c:248-269) + FlowUpdate (flow.c:163-178) + FLOW_UPDATE_TIMESTAMP: the packet's
-// direction flag; per-direction packet / byte counters by returnless atomics, last-seen time.
+// direction flag; per-direction packet / byte counters by one memory-side atomic, last-seen time into the slot record
+// (whose line the probe has just read).
 __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t s, uint32_t fsip, uint32_t fports,
                                                  uint32_t sip, uint32_t ports, uint32_t wire_len, uint64_t now) {
     const uint32_t sport = ports & 0xffffu, dport = ports >> 16, fsport = fports & 0xffffu;
@@ -1006,7 +1085,8 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
     }
     // every packet of the batch carries the same batch time (PPE_LAST_COND, experiment: store only when it differs)
     if (!(PPE_ABLATE & 32)) {
-        if (!PPE_LAST_COND || f.last[s] != now) f.last[s] = now;
+        unsigned long long *lp = (unsigned long long *)(f.keys + PPE_FLOW_SLOT_WORDS * (size_t)s + PPE_FLOW_LAST_WORD);
+        if (!PPE_LAST_COND || *lp != now) *lp = now;
     }
     return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
 }
@@ -1582,9 +1662,9 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_claim_kernel(ppe_flow_kargs a)
 #pragma unroll 1
         for (uint32_t it = 0; it <= a.f.gmask && !done; ++it) {
 #pragma unroll 1
-            for (uint32_t j = 0; j < 4u && !done; ++j) {
-                const uint32_t s = 4u * g + j;
-                uint32_t *sw = a.f.keys + 4ull * s + 3u;
+            for (uint32_t j = 0; j < PPE_FLOW_GROUP && !done; ++j) {
+                const uint32_t s = PPE_FLOW_GROUP * g + j;
+                uint32_t *sw = a.f.keys + (size_t)PPE_FLOW_SLOT_WORDS * s + 3u;
                 uint32_t st = __hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (st == PPE_FS_EMPTY) {
                     uint32_t expect = PPE_FS_EMPTY;
@@ -1623,9 +1703,9 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_resolve_kernel(ppe_flow_kargs 
 #pragma unroll 1
             for (uint32_t it = 0; it <= a.f.gmask && !stop; ++it) {
 #pragma unroll 1
-                for (uint32_t j = 0; j < 4u && !stop; ++j) {
-                    const uint32_t s = 4u * g + j;
-                    const uint32_t st = a.f.keys[4ull * s + 3u];
+                for (uint32_t j = 0; j < PPE_FLOW_GROUP && !stop; ++j) {
+                    const uint32_t s = PPE_FLOW_GROUP * g + j;
+                    const uint32_t st = a.f.keys[(size_t)PPE_FLOW_SLOT_WORDS * s + 3u];
                     if (st == PPE_FS_EMPTY) stop = true;
                     else if ((st & PPE_FS_PEND) && rec_match(rec[st & ~PPE_FS_PEND], r)) {
                         found = s;
@@ -1712,12 +1792,12 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
                     if (rev) {  // FlowAdd: pool empty (flow.c:124-129); the claimed slot becomes a tombstone
                         st = PPE_ST_FLOW_NOMEM;
                         is_rev = true;
-                        a.f.keys[4ull * s + 3u] = PPE_FS_TOMB;
+                        a.f.keys[(size_t)PPE_FLOW_SLOT_WORDS * s + 3u] = PPE_FS_TOMB;
                     } else {    // FlowAdd (flow.c:120-158), oriented as this packet, then FlowUpdate
                         st = PPE_ST_ACL_FW;
                         is_new = true;
                         flags |= PPE_F_NEWFLOW | flow_account(a.f, s, r.x, r.z, r.x, r.z, a.len[p], a.now);
-                        ((uint4 *)a.f.keys)[s] = make_uint4(r.x, r.y, r.z, PPE_FS_LIVE(r.w & 0xffu));
+                        ((uint4 *)a.f.keys)[2ull * s] = make_uint4(r.x, r.y, r.z, PPE_FS_LIVE(r.w & 0xffu));
                     }
                 } else if (p > c) {
                     if (rev) {
@@ -1765,15 +1845,16 @@ template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ppe_flow_age_kernel(ppe_flow_kargs a) {
     uint32_t del = 0;
     for (uint32_t s = blockIdx.x * BLOCK + threadIdx.x; s < a.nslots; s += gridDim.x * BLOCK) {
-        const uint32_t st = a.f.keys[4ull * s + 3u];
+        uint32_t *rw = a.f.keys + (size_t)PPE_FLOW_SLOT_WORDS * s;
+        const uint32_t st = rw[3];
         if ((st & (PPE_FS_PEND | 0xffu)) != PPE_FS_LIVE(0u)) continue;
-        const uint64_t l = a.f.last[s];
+        const uint64_t l = *(const unsigned long long *)(rw + PPE_FLOW_LAST_WORD);
         if (a.now > l && a.now - l > a.timeout) {
-            a.f.keys[4ull * s + 3u] = PPE_FS_TOMB;
+            rw[3] = PPE_FS_TOMB;
             ((uint4 *)a.f.stats)[2ull * s] = make_uint4(0u, 0u, 0u, 0u);
             ((uint4 *)a.f.stats)[2ull * s + 1u] = make_uint4(0u, 0u, 0u, 0u);
             ((uint4 *)a.f.packed)[s] = make_uint4(0u, 0u, 0u, 0u);
-            a.f.last[s] = 0;
+            *(unsigned long long *)(rw + PPE_FLOW_LAST_WORD) = 0ull;
             ++del;
         }
     }
@@ -1792,25 +1873,26 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_age_kernel(ppe_flow_kargs a) {
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ppe_flow_rehash_kernel(ppe_flow_kargs a) {
     for (uint32_t s = blockIdx.x * BLOCK + threadIdx.x; s < a.nslots; s += gridDim.x * BLOCK) {
-        const uint4 k = ((const uint4 *)a.f.keys)[s];
+        const uint4 k = ((const uint4 *)a.f.keys)[2ull * s], kl = ((const uint4 *)a.f.keys)[2ull * s + 1u];
         if ((k.w & (PPE_FS_PEND | 0xffu)) != PPE_FS_LIVE(0u)) continue;
         uint32_t g = key_hash(k.x, k.y, k.z, (k.w >> 8) & 0xffu) & a.dst.gmask;
         bool done = false;
 #pragma unroll 1
         for (uint32_t it = 0; it <= a.dst.gmask && !done; ++it) {
 #pragma unroll 1
-            for (uint32_t j = 0; j < 4u && !done; ++j) {
-                const uint32_t d = 4u * g + j;
+            for (uint32_t j = 0; j < PPE_FLOW_GROUP && !done; ++j) {
+                const uint32_t d = PPE_FLOW_GROUP * g + j;
+                uint32_t *dw = a.dst.keys + (size_t)PPE_FLOW_SLOT_WORDS * d;
                 uint32_t expect = PPE_FS_EMPTY;
-                if (__hip_atomic_compare_exchange_strong(a.dst.keys + 4ull * d + 3u, &expect, k.w, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    a.dst.keys[4ull * d] = k.x;
-                    a.dst.keys[4ull * d + 1u] = k.y;
-                    a.dst.keys[4ull * d + 2u] = k.z;
+                if (__hip_atomic_compare_exchange_strong(dw + 3u, &expect, k.w, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+                    dw[0] = k.x;
+                    dw[1] = k.y;
+                    dw[2] = k.z;
+                    ((uint4 *)dw)[1] = kl;  // last-seen
                     ((uint4 *)a.dst.stats)[2ull * d] = ((const uint4 *)a.f.stats)[2ull * s];
                     ((uint4 *)a.dst.stats)[2ull * d + 1u] = ((const uint4 *)a.f.stats)[2ull * s + 1u];
                     ((uint4 *)a.dst.packed)[d] = ((const uint4 *)a.f.packed)[s];
-                    a.dst.last[d] = a.f.last[s];
                     done = true;
                 }
             }
