@@ -21,7 +21,8 @@ verdict gather a consumer would add is timed apart (`gather`).
 
 `roofline`: the config's launch timed with its dispatch start/end timestamps (hipExtLaunchKernelGGL events on the
 launch stream); achieved = SURVEY.md 8(d)'s 80 algorithmic bytes per 64-B packet (68 read + 12 written; the kernel
-also writes a 4-B compacted-list entry, reported as `written_bytes_per_pkt`) x packets in the launch / its
+also writes a 1-B compacted-list entry (the compact partition list, ppe_result_t.part8), reported as
+`written_bytes_per_pkt`) x packets in the launch / its
 duration.  `traffic` = HBM bytes of the launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE profile of the
 same launch shape (per packet, scaled), when one exists.  `cpu_baseline` = the oracle's C restatement (tree-walk
 ACL) timed on this host's cores as pinned run-to-completion pthreads (rank 0, N = 1).
@@ -194,12 +195,13 @@ class Resident:
             if reps > 1:
                 hdr = hdr.repeat(reps, 1)[:n].contiguous()
                 lens = lens.repeat(reps)[:n].contiguous()
-            out = {k: torch.empty(n, dtype=torch.int32, device=dev)
-                   for k in ("verdict", "flow_hash", "acl_hit", "part_idx")}
+            out = {k: torch.empty(n, dtype=torch.int32, device=dev) for k in ("verdict", "flow_hash", "acl_hit")}
+            out["part8"] = torch.empty(n, dtype=torch.uint8, device=dev)
             bb = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, stride)
-            # the compacted FW / PUNT / DROP lists in the partition layout (one list, include/ppe_hip.h)
+            # the compacted FW / PUNT / DROP lists in the compact partition layout (one byte per packet: its offset
+            # in the tile and its action, include/ppe_hip.h ppe_result_t.part8)
             rr = abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(),
-                            out["part_idx"].data_ptr(), out["part_idx"].data_ptr(), None, None)
+                            None, None, None, None, out["part8"].data_ptr())
             self.bufs.append((hdr, lens, out, bb, rr))
         lens0 = self.host[0]["len"].astype(np.int64)
         self.read_bytes_per_pkt = float(np.minimum(lens0 & 0xFFFF, 64).mean() + 4.0) if stride == 64 else None
@@ -213,7 +215,7 @@ class Resident:
 
 def parity_sample(eng, res, rules, name):
     """Batch 0's outputs against the oracle on a sample: bit-exact verdict / flow hash / ACL hit (packets whose
-    headers reach past the window must be WINDOW_PUNT) and the partition list of those tiles."""
+    headers reach past the window must be WINDOW_PUNT) and the compact partition list of those tiles."""
     import pyoracle
     pk = res.host[0]
     m = min(res.n, 4096 if synth.CONFIGS[name]["rules"] > 10000 else 1 << 16)
@@ -227,8 +229,8 @@ def parity_sample(eng, res, rules, name):
     ok = ~far
     act = (got_v >> 8) & 0xFF
     order = np.argsort((np.arange(m) // 64) * 4 + np.array([0, 2, 1], np.int64)[act], kind="stable")
-    want_part = (order.astype(np.uint32) | (act[order] << 30)).astype(np.uint32)
-    got_p = out["part_idx"][:m].cpu().numpy().view(np.uint32)
+    want_part = ((order & 63) | (act[order] << 6)).astype(np.uint8)  # PPE_PART8_OFFSET / _ACTION
+    got_p = out["part8"][:m].cpu().numpy()
     return bool(np.array_equal(got_v[ok], ref["verdict"][ok]) and np.array_equal(got_h[ok], ref["flow_hash"][ok])
                 and np.array_equal(got_a[ok], ref["acl_hit"][ok]) and ((got_v[far] & 0xFF) == 18).all()
                 and np.array_equal(got_p, want_part)), m
@@ -287,7 +289,7 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
     for i in range(nb):
         hdr, lens, out = res.bufs[i][:3]
         a.b[i] = _CalibBatch(hdr.data_ptr(), lens.data_ptr(), out["verdict"].data_ptr(), out["flow_hash"].data_ptr(),
-                             out["acl_hit"].data_ptr(), out["part_idx"].data_ptr(), res.n, 0)
+                             out["acl_hit"].data_ptr(), out["part8"].data_ptr(), res.n, 0)
     a.nb, a.clk = nb, clk.data_ptr()
     pk = res.n * nb
 
@@ -295,7 +297,7 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
         c = clk.cpu().tolist()
         return round((c[1] - c[0]) / max(c[3] - c[2], 1) * 100.0, 0)
 
-    def stream_run(mode):
+    def stream_run(mode):  # (mode 2: the skeleton with the kernel's 1-B compact list entry)
         a.mode = mode
         ms, t = C.c_double(), []
         for _ in range(3):  # one warm launch, then the faster of two
@@ -304,7 +306,7 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
             t.append(ms.value)
         return min(t[1:]), sclk()
 
-    skel_ms, skel_clk = stream_run(0)
+    skel_ms, skel_clk = stream_run(2)
     ro_ms, ro_clk = stream_run(1)
     nbytes = 1 << 30
     src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -322,8 +324,9 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
     us_1m = lambda t: round(t * 1e3 / (pk / (1 << 20)), 3)  # noqa: E731
     return {
         "skeleton": {"us_per_1M_packets": us_1m(skel_ms), "frac": round(alg * pk / (skel_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                     "real_GBps": round(84.0 * pk / (skel_ms / 1e3) / 1e9, 1), "sclk_mhz": skel_clk,
-                     "bytes_per_pkt": "52 + 4 read (68 B of HBM lines), 16 written (the kernel's own traffic)"},
+                     "real_GBps": round(81.0 * pk / (skel_ms / 1e3) / 1e9, 1), "sclk_mhz": skel_clk,
+                     "bytes_per_pkt": "52 + 4 read (68 B of HBM lines), 13 written (the kernel's own traffic: three "
+                                      "4-B results and the 1-B compact list entry)"},
         "read_only": {"us_per_1M_packets": us_1m(ro_ms), "real_GBps": round(68.0 * pk / (ro_ms / 1e3) / 1e9, 1),
                       "frac_at_68B": round(68.0 * pk / (ro_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "sclk_mhz": ro_clk},
         "copy": {"GBps": round(2.0 * nbytes / (copy_ms / 1e3) / 1e9, 1), "bytes": nbytes, "sclk_mhz": copy_clk},
@@ -448,7 +451,7 @@ def measure_config(name, args, dev, world, rank, dist, primary):
                      "traffic": round(tpp * pk_launch) if tpp else None,
                      "kernel": "ppe_classify_kernel", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                      "launches_timed": launches, "packets_per_launch": int(pk_launch),
-                     "bytes_per_pkt": round(alg, 3), "written_bytes_per_pkt": 16.0,
+                     "bytes_per_pkt": round(alg, 3), "written_bytes_per_pkt": 13.0,
                      "us_per_1M_packets": round(kern_avg_ms * 1e3 / (pk_launch / (1 << 20)), 3)},
         "parity_sample_ok": parity, "parity_sample_packets": psample,
         "acl": {**{k: acl[k] for k in ("n_rules", "n_nodes", "max_depth", "blob_bytes", "lds_resident")},

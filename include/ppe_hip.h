@@ -36,7 +36,7 @@ extern "C" {
 
 /* 2: ppe_tuning_t grew to 20 B (batches_per_launch) and mbuf_t (ppe_decode.h) took the reference's field layout;
  * 3: ppe_tuple's word 3 carries the TCP window-scale option offset (bits 9-15) */
-#define PPE_ABI_VERSION 3
+#define PPE_ABI_VERSION 4
 
 /* error codes (negative return values) */
 #define PPE_OK       0
@@ -86,6 +86,8 @@ enum ppe_action { PPE_ACT_FW = 0, PPE_ACT_DROP = 1, PPE_ACT_PUNT = 2 };
 
 #define PPE_PART_INDEX(e)  ((e) & 0x3fffffffu)   /* partition-layout entry → packet index                */
 #define PPE_PART_ACTION(e) ((e) >> 30)           /* partition-layout entry → enum ppe_action             */
+#define PPE_PART8_OFFSET(e) ((e) & 63u)          /* compact entry (part8) → packet index - 64 × tile      */
+#define PPE_PART8_ACTION(e) ((e) >> 6)           /* compact entry (part8) → enum ppe_action               */
 
 #define PPE_VERDICT_STATUS(v) ((v) & 0xffu)
 #define PPE_VERDICT_ACTION(v) (((v) >> 8) & 0xffu)
@@ -133,6 +135,10 @@ typedef struct {
                                   index | action << 30 (PPE_PART_*), so no tile_cnt is needed to split them     */
     uint32_t *tile_cnt;        /* ceil(n/64) × (nfw | ndrop << 8 | npunt << 16)                                */
     uint32_t *tuple;           /* optional n × 4 words: sip, dip, sport|dport<<16, proto|vlan<<8|payload_len<<16 */
+    uint8_t  *part8;           /* optional n bytes: the PARTITION layout in compact form (with fw_idx, drop_idx
+                                  and tile_cnt NULL): slot [64t + i] of tile t holds the i-th entry of the
+                                  partition order above as (packet index - 64t) | action << 6 (PPE_PART8_*);
+                                  1 B written per packet instead of 4 (ABI version 4)                         */
 } ppe_result_t;
 
 typedef struct {

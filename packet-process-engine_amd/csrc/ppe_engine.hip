@@ -424,8 +424,15 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         d.tile_cnt = out[i].tile_cnt;
         d.tuple = out[i].tuple;
         d.idx_base = idx_base;
-        d.pad = 0;
-        part = part && d.verdict && d.fhash && d.hit && d.fw_idx && d.fw_idx == d.drop_idx && !d.tile_cnt && !d.tuple;
+        d.flags = 0;
+        if (out[i].part8) {
+            if (d.fw_idx || d.drop_idx || d.tile_cnt)
+                return fail(c, PPE_EINVAL, "part8 replaces fw_idx / drop_idx / tile_cnt (pass them NULL)");
+            d.tile_cnt = (uint32_t *)out[i].part8;  // (the kernel reads the compact list from the tile_cnt field)
+            d.flags = PPE_BD_PART8;
+        }
+        part = part && d.verdict && d.fhash && d.hit && !d.tuple &&
+               ((d.fw_idx && d.fw_idx == d.drop_idx && !d.tile_cnt) || d.flags == PPE_BD_PART8);
         tiles = std::max(tiles, (in[i].n + 63u) / 64u);
         tiles_total += (uint64_t)((in[i].n + 63u) / 64u);
     }
@@ -771,7 +778,7 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         bool ok = (b.hdr = (const uint8_t *)mapped_host(in->hdr)) && (b.len = (const uint32_t *)mapped_host(in->len));
         if (in->ts) ok = ok && (b.ts = (const uint64_t *)mapped_host(in->ts));
         uint32_t **outs[] = {&r.verdict, &r.flow_hash, (uint32_t **)&r.acl_hit, &r.fw_idx, &r.drop_idx, &r.tile_cnt,
-                             &r.tuple};
+                             &r.tuple, (uint32_t **)&r.part8};
         for (uint32_t **o : outs)
             if (ok && *o) ok = (*o = (uint32_t *)mapped_host(*o)) != nullptr;
         if (ok) {
@@ -821,6 +828,7 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         r.drop_idx = part ? h.fw : (out->drop_idx ? h.drop : nullptr);
         r.tile_cnt = out->tile_cnt ? h.tcnt : nullptr;
         r.tuple = out->tuple ? h.tuple : nullptr;
+        r.part8 = out->part8 ? (uint8_t *)h.fw : nullptr;  // (part8 excludes fw_idx: the staging list is free)
         rc = launch(c, &b, &r, 1, cfg, h.s, 1 + (int)(i % kHostStreams), base);
         if (rc != PPE_OK) return rc;
         if (out->verdict) HIPCHK(c, hipMemcpyAsync(out->verdict + base, h.verdict, (size_t)m * 4, d2h, h.s));
@@ -833,6 +841,7 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         if (out->fw_idx) HIPCHK(c, hipMemcpyAsync(out->fw_idx + base, h.fw, (size_t)m * 4, d2h, h.s));
         if (out->drop_idx && !part)
             HIPCHK(c, hipMemcpyAsync(out->drop_idx + base, h.drop, (size_t)m * 4, d2h, h.s));
+        if (out->part8) HIPCHK(c, hipMemcpyAsync(out->part8 + base, h.fw, (size_t)m, d2h, h.s));
     }
     for (auto &h : c->hs) HIPCHK(c, hipStreamSynchronize(h.s));
     return PPE_OK;
@@ -1250,6 +1259,7 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     k.fw_idx = out->fw_idx;
     k.drop_idx = out->drop_idx;
     k.tile_cnt = out->tile_cnt;
+    k.part8 = out->part8;
     k.n = in->n;
     k.unsup_fw = cfg ? cfg->unsupport_proto_action : 0u;
     k.now = cfg ? cfg->now_seconds : 0u;

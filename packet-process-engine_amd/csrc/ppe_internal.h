@@ -19,8 +19,9 @@ struct ppe_bdesc {
     uint32_t n;
     uint32_t stride;
     uint32_t idx_base;        /* added to the packet indices written to fw_idx / drop_idx */
-    uint32_t pad;
+    uint32_t flags;           /* PPE_BD_PART8: tile_cnt carries the compact partition list (ppe_result_t.part8) */
 };
+#define PPE_BD_PART8 1u
 
 /* Device flow table (ppe_classify_flow; ppe_kernels.hip "flow table").  Open addressing over groups of
  * PPE_FLOW_GROUP slots (one 64-B line segment of slot records), linear probing from group flow_hash & gmask; a key lies
@@ -70,6 +71,7 @@ struct ppe_flow_kargs {
     uint32_t *verdict;
     int32_t *hit;
     uint32_t *fw_idx, *drop_idx, *tile_cnt;
+    uint8_t *part8;               /* compact partition list (ppe_result_t.part8) */
     uint32_t n;
     uint32_t unsup_fw;
     uint64_t now;

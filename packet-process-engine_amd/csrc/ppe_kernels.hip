@@ -127,6 +127,9 @@ __device__ __forceinline__ uint4 lds_u128(uint32_t addr) {
 __device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) {
     *(__attribute__((address_space(3))) uint32_t *)(uintptr_t)addr = v;
 }
+__device__ __forceinline__ void lds_st8(uint32_t addr, uint32_t v) {
+    *(__attribute__((address_space(3))) uint8_t *)(uintptr_t)addr = (uint8_t)v;
+}
 // global accesses by 32-bit byte offset from a uniform base (the saddr form: no 64-bit address math per lane)
 // (explicitly global: a select between two output pointers must not degrade to a flat store, whose out-of-order
 // completion makes the compiler wait for vmcnt(0) at the next use of any load)
@@ -977,12 +980,14 @@ __device__ __forceinline__ uint64_t make_act_table(uint32_t unsup_fw) {
 }
 
 // Wave-ballot compaction of a 64-packet tile's FW / DROP indices into the tile's 64-slot segment of each list (or
-// the partition layout when fw_idx == drop_idx), plus the tile count.  Every lane of the wave calls it.
+// the partition layout when fw_idx == drop_idx, or its compact byte form part8), plus the tile count.  Every lane of
+// the wave calls it.
 // scr: a wave-private 256-B LDS scratch (byte address) or ~0u.  With scratch, the partition layout's permuted store
-// goes through LDS (each lane writes its slot, then reads slot `lane`), so the global store is in lane order.
+// goes through LDS (each lane writes its slot, then reads slot `lane`), so the global store is in lane order (part8:
+// 16 lanes store the tile's 64 entries as dwords).
 __device__ __forceinline__ void compact_tile(uint32_t *fw_idx, uint32_t *drop_idx, uint32_t *tile_cnt, uint32_t n,
                                              uint32_t idx_base, uint32_t tile, uint32_t lane, bool valid, uint32_t act,
-                                             uint32_t scr = ~0u) {
+                                             uint32_t scr = ~0u, uint8_t *part8 = nullptr) {
     const uint32_t p = (tile << 6) + lane;
     const bool is_fw = valid && act == PPE_ACT_FW;
     const bool is_drop = valid && act == PPE_ACT_DROP;
@@ -991,7 +996,20 @@ __device__ __forceinline__ void compact_tile(uint32_t *fw_idx, uint32_t *drop_id
     const uint32_t pfw = __builtin_amdgcn_mbcnt_hi((uint32_t)(bfw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bfw, 0u));
     const uint32_t pdr = __builtin_amdgcn_mbcnt_hi((uint32_t)(bdr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bdr, 0u));
     const uint32_t so = (tile << 8) + 4u * (is_fw ? pfw : pdr);  // byte offset in the tile's segment
-    if (fw_idx == drop_idx && fw_idx) {
+    if (part8) {
+        // the partition order, one byte per entry: the packet's offset in its tile and its action
+        const uint32_t nv = min(n - (tile << 6), 64u);
+        const uint32_t ndr = (uint32_t)__popcll(bdr), nfw = (uint32_t)__popcll(bfw);
+        const uint32_t slot = is_fw ? pfw : (is_drop ? nv - ndr + pdr : nfw + lane - pfw - pdr);
+        const uint32_t e = lane | (act << 6);
+        if (scr != ~0u && nv == 64u) {  // (LDS ops of one wave complete in order)
+            lds_st8(scr + slot, e);
+            const uint32_t v = lds_u32(scr + 4u * (lane & 15u));
+            if (lane < 16u) gst_nt<uint32_t>(part8, (tile << 6) + 4u * lane, v);
+        } else if (valid) {
+            gst_nt<uint8_t>(part8, (tile << 6) + slot, (uint8_t)e);
+        }
+    } else if (fw_idx == drop_idx && fw_idx) {
         // partition layout (one shared list): the tile's segment holds every packet of the tile, FW from the
         // front, DROP at the back, PUNT in between, each in ascending order, the action in bits 31:30 —
         // every slot written by one store instruction (whole-line writes, no tile count needed)
@@ -1263,9 +1281,13 @@ void ppe_classify_kernel(ppe_kargs a) {
             }
         }
         // ---- wave-ballot compaction of FW / DROP indices into this tile's 64-slot segment of each list ----
-        if (!(PPE_ABLATE & 4))
-            compact_tile(B.fw_idx, PART ? B.fw_idx : B.drop_idx, PART ? nullptr : B.tile_cnt, B.n, B.idx_base, tile, lane,
-                         valid, act, (PPE_CMP_LDS && MT == 1 && !STB) ? lanebase - 4u * lane + 256u * PPE_DIM_SIP : ~0u);
+        if (!(PPE_ABLATE & 4)) {
+            const bool p8 = (B.flags & PPE_BD_PART8) != 0u;  // (the compact list travels in the tile_cnt field)
+            compact_tile(p8 ? nullptr : B.fw_idx, p8 ? nullptr : (PART ? B.fw_idx : B.drop_idx),
+                         (PART || p8) ? nullptr : B.tile_cnt, B.n, B.idx_base, tile, lane, valid, act,
+                         (PPE_CMP_LDS && MT == 1 && !STB) ? lanebase - 4u * lane + 256u * PPE_DIM_SIP : ~0u,
+                         p8 ? (uint8_t *)B.tile_cnt : nullptr);
+        }
 
         // ---- per-reason counters: one LDS add per packet into its (status, flags) bin ----
         if (!(PPE_ABLATE & 2) && valid) atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
@@ -1814,7 +1836,7 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
             a.verdict[p] = st | (act << 8) | (flags << 16);
             atomicAdd(&bins[st | ((flags & 7u) << 5)], 1u);
         }
-        compact_tile(a.fw_idx, a.drop_idx, a.tile_cnt, a.n, 0u, t, w.lane, valid, act);
+        compact_tile(a.fw_idx, a.drop_idx, a.tile_cnt, a.n, 0u, t, w.lane, valid, act, ~0u, a.part8);
         created += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(is_new));
         revoked += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(is_rev));
     }

@@ -54,7 +54,8 @@ class Batch(C.Structure):
 
 class Result(C.Structure):
     _fields_ = [("verdict", C.c_void_p), ("flow_hash", C.c_void_p), ("acl_hit", C.c_void_p),
-                ("fw_idx", C.c_void_p), ("drop_idx", C.c_void_p), ("tile_cnt", C.c_void_p), ("tuple", C.c_void_p)]
+                ("fw_idx", C.c_void_p), ("drop_idx", C.c_void_p), ("tile_cnt", C.c_void_p), ("tuple", C.c_void_p),
+                ("part8", C.c_void_p)]  # compact partition list (ABI version 4)
 
 
 class Cfg(C.Structure):
@@ -202,7 +203,7 @@ EXPORTED_DATA = ["rule_list", "dp_acl_action_default", "gWstDepth", "gAvgDepth",
 _lib = None
 
 
-ABI_VERSION = 3  # include/ppe_hip.h PPE_ABI_VERSION
+ABI_VERSION = 4  # include/ppe_hip.h PPE_ABI_VERSION
 
 
 def load(path: str | os.PathLike | None = None) -> C.CDLL:

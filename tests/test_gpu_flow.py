@@ -12,7 +12,7 @@ import torch  # noqa: E402
 
 import pyoracle  # noqa: E402
 from ppe import Engine, abi, synth  # noqa: E402
-from test_gpu_parity import check_compaction, check_partition  # noqa: E402
+from test_gpu_parity import check_compaction, check_part8, check_partition  # noqa: E402
 
 DEV = torch.device("cuda:0")
 NOW = 1_000_000
@@ -22,12 +22,17 @@ def gpu_flow(eng, hdr, lens, now, syn_check=1, part=False):
     n = len(lens)
     th = torch.from_numpy(np.ascontiguousarray(hdr)).to(DEV)
     tl = torch.from_numpy(np.ascontiguousarray(lens, np.uint32).view(np.int32)).to(DEV)
-    names = ("verdict", "flow_hash", "acl_hit") + (("part_idx",) if part else ("fw_idx", "drop_idx", "tile_cnt"))
+    # part: False = separate FW / DROP lists + tile counts, True = the partition list, "8" = its compact form
+    names = ("verdict", "flow_hash", "acl_hit") + (
+        ("part8",) if part == "8" else ("part_idx",) if part else ("fw_idx", "drop_idx", "tile_cnt"))
     out = {k: torch.full(((n + 63) // 64,) if k == "tile_cnt" else (n,), -7, dtype=torch.int32, device=DEV)
            for k in names}
+    if part == "8":
+        out["part8"] = torch.full((n + 64,), 0xEE, dtype=torch.uint8, device=DEV)
     eng.classify_flow_torch(th, tl, out, cfg=eng.cfg(0, syn_check, now))
     torch.cuda.synchronize()
-    return {k: (v.cpu().numpy() if k == "acl_hit" else v.cpu().numpy().view(np.uint32)) for k, v in out.items()}
+    return {k: (v.cpu().numpy() if k in ("acl_hit", "part8") else v.cpu().numpy().view(np.uint32))
+            for k, v in out.items()}
 
 
 def table(d):
@@ -58,7 +63,9 @@ class Pair:
                 bad = np.nonzero(got[k] != ref[k])[0]
                 raise AssertionError(f"{k}: {len(bad)} mismatches, first {bad[:5].tolist()}: "
                                      f"gpu={got[k][bad[:5]].tolist()} ref={ref[k][bad[:5]].tolist()}")
-        if part:
+        if part == "8":
+            check_part8(got, len(lens))
+        elif part:
             check_partition(got, len(lens))
         else:
             check_compaction(got, len(lens))
@@ -97,7 +104,7 @@ def test_flow_batches_parity(eng, kind, stride):
             pk = synth.make_flow_packets(40000, rules, n_flows=6000, seed=100 + b if b < 2 else 100, kind=kind,
                                          stride=stride, malformed_frac=0.01)
             # batches 0 and 2 share the template seed, so batch 2 revisits batch 0's flows
-            got, _ = p.batch(pk["hdr"], pk["len"], NOW + b, part=(b % 2 == 1))
+            got, _ = p.batch(pk["hdr"], pk["len"], NOW + b, part=(False, True, False, "8")[b])
             p.same_table()
         v = got["verdict"]
         assert ((v >> 16) & abi.F_FLOW).any() and ((v >> 16) & abi.F_TOCLIENT).any()
@@ -129,7 +136,7 @@ def test_flow_pool_exhaustion(eng):
     try:
         for b in range(3):
             pk = synth.make_flow_packets(12000, rules, n_flows=2000, seed=200 + b, syn_frac=0.8)
-            got, ref = p.batch(pk["hdr"], pk["len"], NOW + b)
+            got, ref = p.batch(pk["hdr"], pk["len"], NOW + b, part="8" if b == 1 else False)
             p.same_table()
         assert ((ref["verdict"] & 0xFF) == abi.ST["FLOW_NOMEM"]).any()
         assert p.eng.counters()["flow_node_nomem"] > 0

@@ -36,6 +36,8 @@ def gpu_classify(eng, hdr, lens, ts=None, cfg=None, outs=OUTS):
     shapes = {"tile_cnt": ((n + 63) // 64,), "tuple": (n, 4)}
     out = {k: torch.full(shapes.get(k, (n,)), -7, dtype=torch.int32, device=DEV) if k in outs else None
            for k in OUTS + ("part_idx",)}
+    # (64 guard bytes past n: the compact list must not write beyond its n entries)
+    out["part8"] = torch.full((n + 64,), 0xEE, dtype=torch.uint8, device=DEV) if "part8" in outs else None
     eng.classify_torch(th, tl, out, cfg=cfg or eng.cfg(now_seconds=NOW), ts=tt)
     torch.cuda.synchronize()
     res = {}
@@ -43,7 +45,7 @@ def gpu_classify(eng, hdr, lens, ts=None, cfg=None, outs=OUTS):
         if v is None:
             continue
         a = v.cpu().numpy()
-        res[k] = a if k == "acl_hit" else a.view(np.uint32)
+        res[k] = a if k in ("acl_hit", "part8") else a.view(np.uint32)
     return res
 
 
@@ -82,6 +84,20 @@ def check_partition(res, n):
         pu = np.nonzero(act[lo:hi] == 2)[0] + lo
         want = np.concatenate([fw, pu | (2 << 30), dr | (1 << 30)]).astype(np.uint32)
         assert np.array_equal(part[lo:hi], want), t
+
+
+def part8_expected(verdict, n):
+    """The compact partition list (ppe_result_t.part8) a verdict array implies: per tile, the partition order above,
+    one byte per entry, (index - 64 t) | action << 6."""
+    act = ((verdict[:n] >> 8) & 0xFF).astype(np.int64)
+    order = np.argsort((np.arange(n) // 64) * 4 + np.array([0, 2, 1], np.int64)[act], kind="stable")
+    return ((order & 63) | (act[order] << 6)).astype(np.uint8)
+
+
+def check_part8(res, n):
+    assert np.array_equal(res["part8"][:n], part8_expected(res["verdict"], n))
+    if len(res["part8"]) == n + 64:  # gpu_classify's buffer: its guard bytes untouched
+        assert (res["part8"][n:] == 0xEE).all()
 
 
 # ---------------------------------------------------------------- fixtures frozen in tests/golden
@@ -136,6 +152,7 @@ def test_host_pinned_buffers(eng, monkeypatch, zerocopy):
     pl = torch.from_numpy(pk["len"].view(np.int32)).pin_memory()
     pt = torch.from_numpy(pk["ts"].view(np.int64)).pin_memory()
     out = {k: torch.full((n,), -7, dtype=torch.int32).pin_memory() for k in ("verdict", "flow_hash", "acl_hit", "part")}
+    p8 = torch.full((n,), 0xEE, dtype=torch.uint8).pin_memory()
     b = abi.Batch(ph.data_ptr(), pl.data_ptr(), pt.data_ptr(), n, 128)
     r = abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(),
                    out["part"].data_ptr(), out["part"].data_ptr(), None, None)
@@ -148,6 +165,11 @@ def test_host_pinned_buffers(eng, monkeypatch, zerocopy):
     assert np.array_equal(got["flow_hash"].view(np.uint32), ref["flow_hash"])
     assert np.array_equal(got["acl_hit"], ref["acl_hit"])
     check_partition({"verdict": got["verdict"].view(np.uint32), "part_idx": got["part"].view(np.uint32)}, n)
+    # the compact partition list through the same host path
+    r8 = abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(), None, None,
+                    None, None, p8.data_ptr())
+    assert eng.lib.ppe_classify_host(eng.ctx, C.byref(b), C.byref(r8), C.byref(cfg), 1 << 14) == 0
+    check_part8({"verdict": out["verdict"].numpy().view(np.uint32), "part8": p8.numpy()}, n)
 
 
 def test_flow_hash_matches_reference_tluhash(eng, ref_hash):
@@ -198,7 +220,7 @@ BENCH_SAMPLE = {"C1": 1 << 16, "C2": 1 << 16, "C3": 1 << 14, "C4": 1 << 16}
 @pytest.mark.parametrize("cfgname", ["C1", "C2", "C3", "C4"])
 def test_config_exact_workload_vs_oracle(eng, cfgname):
     """The exact bench workload of each BASELINE config (bench.py's Resident: the two generated 1M-packet batches of
-    rank 0 with the bench's seeds, the config's packet kind and rule count, 64-B windows, the partition-list layout),
+    rank 0 with the bench's seeds, the config's packet kind and rule count, 64-B windows, the compact partition list; descriptors 0 and 1 write the 4-B partition list instead, which must agree),
     through ppe_classify_batches as the bench calls it: 34 descriptors over the two batches (more than the 32 the
     kernel arguments hold: the device descriptor ring, batch groups running different batches at once), every
     descriptor with its own outputs.  The first BENCH_SAMPLE packets of each batch, and a strided sample of the rest,
@@ -216,11 +238,16 @@ def test_config_exact_workload_vs_oracle(eng, cfgname):
     outs, bats, ress = [], [], []
     for d in range(ndesc):
         th, tl = dev_in[d % 2]
-        o = {k: torch.full((n,), -7, dtype=torch.int32, device=DEV) for k in ("verdict", "flow_hash", "acl_hit", "part")}
+        o = {k: torch.full((n,), -7, dtype=torch.int32, device=DEV) for k in ("verdict", "flow_hash", "acl_hit")}
+        if d < 2:
+            o["part"] = torch.full((n,), -7, dtype=torch.int32, device=DEV)
+        else:
+            o["part8"] = torch.full((n,), 0xEE, dtype=torch.uint8, device=DEV)
         outs.append(o)
         bats.append(abi.Batch(th.data_ptr(), tl.data_ptr(), None, n, 64))
         ress.append(abi.Result(o["verdict"].data_ptr(), o["flow_hash"].data_ptr(), o["acl_hit"].data_ptr(),
-                               o["part"].data_ptr(), o["part"].data_ptr(), None, None))
+                               o["part"].data_ptr() if d < 2 else None, o["part"].data_ptr() if d < 2 else None,
+                               None, None, o["part8"].data_ptr() if d >= 2 else None))
     ins, rs = (abi.Batch * ndesc)(*bats), (abi.Result * ndesc)(*ress)
     cfg = eng.cfg(now_seconds=NOW)
     s = torch.cuda.current_stream(DEV)
@@ -233,9 +260,16 @@ def test_config_exact_workload_vs_oracle(eng, cfgname):
     for g, pk in enumerate(host):
         got = {k: outs[g][k].cpu().numpy() for k in outs[g]}
         got = {k: (v if k == "acl_hit" else v.view(np.uint32)) for k, v in got.items()}
+        got["part8"] = outs[g + 2]["part8"].cpu().numpy()
         for d in range(g + 2, ndesc, 2):  # every descriptor over this batch wrote the same outputs
-            for k in outs[d]:
+            for k in ("verdict", "flow_hash", "acl_hit"):
                 assert torch.equal(outs[d][k], outs[g][k]), (cfgname, d, k)
+            if d > g + 2:
+                assert torch.equal(outs[d]["part8"], outs[g + 2]["part8"]), (cfgname, d)
+        # the compact list is the 4-B partition list in one byte per entry, over the whole batch
+        p32 = got["part"]
+        assert np.array_equal(got["part8"], ((p32 & 63) | ((p32 >> 30) << 6)).astype(np.uint8)), cfgname
+        assert np.array_equal((p32 & 0x3FFFFFFF) >> 6, np.arange(n, dtype=np.uint32) >> 6), cfgname
         idx = np.concatenate([np.arange(m), np.arange(m, n, max(1, (n - m) // m))])
         ref = o.classify_batch(pk["hdr"][idx], pk["len"][idx], cfg=o.cfg(0, 1, NOW), nthreads=16)
         far = ref["reach"] > 64
@@ -245,6 +279,7 @@ def test_config_exact_workload_vs_oracle(eng, cfgname):
         assert ((got["verdict"][idx][far] & 0xFF) == ST["WINDOW_PUNT"]).all()
         assert (got["acl_hit"][idx] >= 0).sum() > len(idx) // 8  # the sample exercises rule hits, not just misses
         check_partition({"verdict": got["verdict"][:m], "part_idx": got["part"][:m]}, m)
+        check_part8(got, m)
 
 
 def test_c3_64k_rules_vs_oracle(eng):
@@ -337,6 +372,9 @@ def test_ragged_sizes(eng, n):
     part = gpu_classify(eng, pk["hdr"], pk["len"], outs=PART_OUTS)
     assert_same(part, ref)
     check_partition(part, n)
+    p8 = gpu_classify(eng, pk["hdr"], pk["len"], outs=("verdict", "flow_hash", "acl_hit", "part8"))
+    assert_same(p8, ref, keys=("verdict", "flow_hash", "acl_hit"))
+    check_part8(p8, n)  # (ragged last tile: byte stores, nothing past n)
 
 
 def test_argument_errors(eng):
@@ -354,6 +392,14 @@ def test_argument_errors(eng):
     assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(bad), None) == -22
     b = abi.Batch(buf.data_ptr(), lens.data_ptr(), None, 0, 64)  # empty batch is a no-op
     assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), None) == 0
+    # the compact partition list replaces fw_idx / drop_idx / tile_cnt: both at once is refused, nothing written
+    ob = torch.full((64,), 0x5A, dtype=torch.uint8, device=DEV)
+    b = abi.Batch(buf.data_ptr(), lens.data_ptr(), None, 16, 64)
+    for fw, tc in ((ob.data_ptr(), None), (None, ob.data_ptr())):
+        r8 = abi.Result(None, None, None, fw, fw, tc, None, ob.data_ptr())
+        assert lib.ppe_classify(eng.ctx, C.byref(b), C.byref(r8), C.byref(cfg), None) == -22
+    torch.cuda.synchronize()
+    assert (ob == 0x5A).all()
     t = abi.Tuning(block=300)
     assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
     for pl in (2, 6):  # the register / LDS-DMA prefetch variants are not built
@@ -739,5 +785,15 @@ def test_partition_layout_kernel_variant(eng, monkeypatch, nrules):
     gen = gpu_classify(eng, pk["hdr"], pk["len"], outs=outs)
     for k in ("verdict", "flow_hash", "acl_hit", "part_idx"):
         assert np.array_equal(gen[k], got[k]), k
+    # the compact partition list (ppe_result_t.part8): the PART kernel, the general kernel, and the general kernel
+    # with the tuple output beside it
+    monkeypatch.delenv("PPE_NO_PART")
+    for env, extra in ((None, ()), ("1", ()), (None, ("tuple",))):
+        if env:
+            monkeypatch.setenv("PPE_NO_PART", env)
+        g8 = gpu_classify(eng, pk["hdr"], pk["len"], outs=("verdict", "flow_hash", "acl_hit", "part8") + extra)
+        assert_same(g8, ref, keys=("verdict", "flow_hash", "acl_hit") + extra)
+        check_part8(g8, n)
+        monkeypatch.delenv("PPE_NO_PART", raising=False)
     st = ref["verdict"] & 0xFF
     assert (st == ST["FLOW_TCP_NO_SYN_FIRST"]).sum() > 10

@@ -81,7 +81,8 @@ def main():
         os.environ["PPE_GROUPS"] = kvs.pop("groups", "8")  # batch groups of waves (read at context creation)
         os.environ.update(venv)
         eng = Engine(0, lib=libs[path])
-        # outs=sep (default): separate FW / DROP lists + tile counts; outs=part: one partition list, no tile counts
+        # outs=sep (default): separate FW / DROP lists + tile counts; outs=part: one partition list, no tile counts;
+        # outs=part8: the compact partition list (1 B per packet, the bench's layout; ABI version >= 4)
         mode = kvs.pop("outs", "sep")
         # streams=N: consecutive launches round-robin over N streams (batch pipelining: a launch's ramp-up overlaps
         # the previous one's tail); each stream needs its own output buffers, so --nbufs must be a multiple of N
@@ -103,7 +104,10 @@ def main():
             ptrs = [o.data_ptr() for o in outs]
             if mode == "part":
                 ptrs[4], ptrs[5] = ptrs[3], None
-            rr = abi.Result(*ptrs, None)
+            if mode == "part8":
+                rr = abi.Result(ptrs[0], ptrs[1], ptrs[2], None, None, None, None, ptrs[3])
+            else:
+                rr = abi.Result(*ptrs, None)
             calls.append((bb, rr))
         strs = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nstr - 1)]
         variants.append(dict(name=name, eng=eng, calls=calls, kern=[], step=[], streams=strs, api=api, env=venv))

@@ -44,8 +44,8 @@ def main():
         lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
         outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
         bufs.append((abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, 64),
-                     abi.Result(outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(), outs[3].data_ptr(),
-                                outs[3].data_ptr(), None, None), hdr, lens, outs))
+                     abi.Result(outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(), None, None, None, None,
+                                outs[3].data_ptr()), hdr, lens, outs))  # the bench's layout: compact list
     cfg = Engine.cfg(now_seconds=1_700_000_000)
     sp = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     ins = (abi.Batch * a.batches)(*(bufs[i % a.nbufs][0] for i in range(a.batches)))
