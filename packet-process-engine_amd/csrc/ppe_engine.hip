@@ -1267,11 +1267,12 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     k.cslots = c->d_cslots;
     // grid-stride over the miss-tile list (usually short): a few workgroups per CU, not one per tile
     const uint32_t fg = std::min(flow_grid(c, (in->n + 63u) / 64u, PPE_FLOW_BLOCK_WAVES), c->n_cu * 2u);
-    // 2-5. claim, resolve, [revoke: only when the pool may overflow], finalize
+    // 2-4. claim, resolve, finalize (when the host's bound says the pool may overflow, finalize checks the exact
+    // counts and, on an overflow, its workgroup 0 revokes the creators past the pool's room first)
     const bool may_overflow = t.live_ub + in->n > t.capacity;
-    for (int kind : {PPE_FLOW_K_CLAIM, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_REVOKE, PPE_FLOW_K_FINALIZE}) {
-        if (kind == PPE_FLOW_K_REVOKE && !may_overflow) continue;
-        const int e = ppe_launch_flow(kind, &k, kind == PPE_FLOW_K_REVOKE ? 1u : fg, (void *)s);
+    k.revoke = may_overflow ? 1u : 0u;
+    for (int kind : {PPE_FLOW_K_CLAIM, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_FINALIZE}) {
+        const int e = ppe_launch_flow(kind, &k, fg, (void *)s);
         if (e != 0) return fail(c, PPE_EIO, "flow kernel %d launch failed: %s", kind, hipGetErrorString((hipError_t)e));
     }
     t.cum_n[t.batches % FlowTable::kSnapRing] = t.tot_n;

@@ -39,7 +39,9 @@ struct ppe_bdesc {
 #define PPE_FLOW_NONE 0xffffffffu
 #define PPE_FLOW_REVOKED 0x80000000u              /* creator word: pool exhausted, the claim is withdrawn */
 enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_NEW, PPE_FCTL_TOMBS,
-       PPE_FCTL_MISS0, PPE_FCTL_MISS1, /* tiles with pending packets, by batch parity */ PPE_FCTL_WORDS = 8 };
+       PPE_FCTL_MISS0, PPE_FCTL_MISS1, /* tiles with pending packets, by batch parity */
+       PPE_FCTL_REVOKED_SEQ,           /* finalize: workgroup 0's revoke published for batch seq + 1 */
+       PPE_FCTL_WORDS = 8 };
 #define PPE_PK_SHIFT 40u                       /* packed counter: packets in bits 63:40, bytes in 39:0 */
 #define PPE_PK_FOLD_PKTS (1ull << 23)          /* fold into `stats` once either field reaches half its range */
 #define PPE_PK_FOLD_BYTES (1ull << 39)
@@ -77,7 +79,7 @@ struct ppe_flow_kargs {
     uint64_t now;
     uint64_t timeout;             /* aging */
     uint32_t nslots;
-    uint32_t pad;
+    uint32_t revoke;              /* finalize: the host's bound says the pool may overflow (check, rank, revoke) */
     unsigned long long *cslots;   /* counter slots (one per workgroup) */
     struct ppe_flowdev dst;       /* rehash target */
 };
@@ -175,9 +177,9 @@ extern "C" {
  * 1 first tile's loads issued before the image staging (see ppe_kernels.hip) */
 int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, int flow,
                         void *stream, void *ev_start, void *ev_stop);
-/* flow-table phases after a flow-mode classify launch (stream order): claim, resolve, [revoke], finalize */
-enum { PPE_FLOW_K_CLAIM = 0, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_REVOKE, PPE_FLOW_K_FINALIZE, PPE_FLOW_K_AGE,
-       PPE_FLOW_K_REHASH };
+/* flow-table phases after a flow-mode classify launch (stream order): claim, resolve, finalize (+ revoke in its
+ * workgroup 0 when the pool overflows) */
+enum { PPE_FLOW_K_CLAIM = 0, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_FINALIZE, PPE_FLOW_K_AGE, PPE_FLOW_K_REHASH };
 int ppe_launch_flow(int kind, const struct ppe_flow_kargs *a, uint32_t grid, void *stream);
 #define PPE_FLOW_BLOCK 256      /* flow kernels' workgroup size */
 /* steering: 0 count, 1 scan (one workgroup), 2 scatter the permutation; rows: gather / scatter of fixed rows */

@@ -1636,8 +1636,8 @@ void ppe_classify_kernel(ppe_kargs a) {
 //   claim     pending would-be creators claim one slot per 5-tuple (CAS EMPTY → PEND | index, or join the claim of
 //             an equal key found on the probe path) and lower the slot's creator index (atomicMin);
 //   resolve   every pending packet finds its flow's claimed slot (rslot) and whether it is the creator;
-//   revoke    (only when the pool may overflow) ranks the creators in packet order and revokes those past the
-//             free count;
+//   revoke    (only when the pool overflows; finalize's workgroup 0, the others wait on its flag) ranks the
+//             creators in packet order and revokes those past the free count;
 //   finalize  final verdicts of the pending packets, flow creation and accounting, the tile's compaction and the
 //             pending packets' counters.
 
@@ -1748,21 +1748,20 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_resolve_kernel(ppe_flow_kargs 
                                __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One workgroup: if the batch's creators overflow the pool, rank them in packet order (tile counts, block scan)
-// and mark the ones past the free count revoked.
-__global__ __launch_bounds__(1024) void ppe_flow_revoke_kernel(ppe_flow_kargs a) {
-    __shared__ uint32_t part[1024];
-    const unsigned long long live = a.f.ctl[PPE_FCTL_LIVE], created = a.f.ctl[PPE_FCTL_BATCH_NEW];
-    if (live + created <= a.f.capacity) return;
-    const unsigned long long room = a.f.capacity > live ? a.f.capacity - live : 0ull;
+// Revoke (finalize's workgroup 0, when the batch's creators overflow the pool): rank the creators in packet order
+// (tile counts, block scan over the workgroup) and mark the ones past the free count revoked.  The creator words go
+// out as sc1 stores and the other workgroups read them with sc1 loads after the flag (MI355X_MICROARCH.md hand-off
+// forms; until round 3 this was a one-workgroup launch of its own between resolve and finalize).
+template <int BLOCK>
+__device__ __forceinline__ void flow_revoke(const ppe_flow_kargs &a, uint32_t *part, unsigned long long room) {
     const uint32_t tid = threadIdx.x, ntiles = (a.n + 63u) >> 6;
-    const uint32_t chunk = (ntiles + 1023u) / 1024u, lo = min(tid * chunk, ntiles), hi = min(lo + chunk, ntiles);
+    const uint32_t chunk = (ntiles + BLOCK - 1u) / BLOCK, lo = min(tid * chunk, ntiles), hi = min(lo + chunk, ntiles);
     uint32_t cnt = 0;
     for (uint32_t t = lo; t < hi; ++t)
         if (a.f.tile_miss[t]) cnt += (uint32_t)__popcll(a.f.tile_new[t]);
     part[tid] = cnt;
     __syncthreads();
-    for (uint32_t o = 1; o < 1024u; o <<= 1) {  // inclusive scan
+    for (uint32_t o = 1; o < (uint32_t)BLOCK; o <<= 1) {  // inclusive scan
         const uint32_t v = tid >= o ? part[tid - o] : 0u;
         __syncthreads();
         part[tid] += v;
@@ -1774,7 +1773,8 @@ __global__ __launch_bounds__(1024) void ppe_flow_revoke_kernel(ppe_flow_kargs a)
         for (; m; m &= m - 1ull, ++rank) {
             if (rank < room) continue;
             const uint32_t p = (t << 6) + (uint32_t)__builtin_ctzll(m);
-            a.f.creator[a.f.rslot[p]] = p | PPE_FLOW_REVOKED;
+            __hip_atomic_store(&a.f.creator[a.f.rslot[p]], p | PPE_FLOW_REVOKED, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -1783,10 +1783,46 @@ template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs a) {
     __shared__ uint32_t bins[PPE_NBINS];
     __shared__ uint32_t lcnt[32];
+    __shared__ uint32_t part[BLOCK];
+    __shared__ uint32_t rev_s;
+    __shared__ unsigned long long room_s;
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < PPE_NBINS; i += BLOCK) bins[i] = 0;
     if (tid < 32u) lcnt[tid] = 0;
+    // revoke: when the host's bound says the pool may overflow, every workgroup checks the exact counts; on an
+    // overflow workgroup 0 (dispatched first, so resident while the others wait) ranks and revokes, then publishes
+    // this batch's sequence number, which the others poll for (bounded) before reading any creator word
+    if (tid == 0) {
+        rev_s = 0u;
+        if (a.revoke) {
+            const unsigned long long live = __hip_atomic_load(&a.f.ctl[PPE_FCTL_LIVE], __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT),
+                                     cr = __hip_atomic_load(&a.f.ctl[PPE_FCTL_BATCH_NEW], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+            rev_s = live + cr > a.f.capacity ? 1u : 0u;
+            room_s = a.f.capacity > live ? a.f.capacity - live : 0ull;
+        }
+    }
     __syncthreads();
+    const bool rev = rev_s != 0u;
+    if (rev) {
+        if (blockIdx.x == 0) {
+            flow_revoke<BLOCK>(a, part, room_s);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0)
+                __hip_atomic_store(&a.f.ctl[PPE_FCTL_REVOKED_SEQ], a.f.seq + 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (tid == 0) {
+                for (uint32_t k = 0; k < (1u << 24) &&
+                                     __hip_atomic_load(&a.f.ctl[PPE_FCTL_REVOKED_SEQ], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) != a.f.seq + 1ull; ++k)
+                    __builtin_amdgcn_s_sleep(8);
+            }
+            __syncthreads();
+        }
+    }
     const TileWalk w = TileWalk::make<BLOCK>(a.f);
     const uint4 *rec = (const uint4 *)a.f.rec;
     const uint64_t act_table = make_act_table(a.unsup_fw);
@@ -1807,7 +1843,8 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
             uint32_t st = prov, flags = v >> 16;
             const uint32_t s = a.f.rslot[p];
             if (s != PPE_FLOW_NONE) {
-                const uint32_t cw = a.f.creator[s];
+                const uint32_t cw = rev ? __hip_atomic_load(&a.f.creator[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : a.f.creator[s];
                 const bool rev = (cw & PPE_FLOW_REVOKED) != 0u;
                 const uint32_t c = cw & ~PPE_FLOW_REVOKED;
                 if (p == c) {
@@ -2117,7 +2154,6 @@ extern "C" int ppe_launch_flow(int kind, const ppe_flow_kargs *a, uint32_t grid,
     switch (kind) {
         case PPE_FLOW_K_CLAIM: hipLaunchKernelGGL(ppe_flow_claim_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
         case PPE_FLOW_K_RESOLVE: hipLaunchKernelGGL(ppe_flow_resolve_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
-        case PPE_FLOW_K_REVOKE: hipLaunchKernelGGL(ppe_flow_revoke_kernel, dim3(1), dim3(1024), 0, s, *a); break;
         case PPE_FLOW_K_FINALIZE: hipLaunchKernelGGL(ppe_flow_finalize_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
         case PPE_FLOW_K_AGE: hipLaunchKernelGGL(ppe_flow_age_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
         case PPE_FLOW_K_REHASH: hipLaunchKernelGGL(ppe_flow_rehash_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
