@@ -182,6 +182,11 @@ template <class T> __device__ __forceinline__ void gst_nt(void *base, uint32_t o
 #ifndef PPE_CMP_LDS
 #define PPE_CMP_LDS 1
 #endif
+// PPE_CMP_LDS8: the compact (1-B) partition list through the same LDS permutation, stored as 16 dwords; 0: each lane
+// stores its entry byte at its slot (one 64-B byte-store instruction per tile; C1 ring step 16.76 -> 16.68 us, r4h)
+#ifndef PPE_CMP_LDS8
+#define PPE_CMP_LDS8 0
+#endif
 template <class T> __device__ __forceinline__ T gld_win(const void *base, uint32_t off) {
     typedef typename GType<T>::type G;
     if constexpr (PPE_NT_WIN != 0)
@@ -1002,7 +1007,7 @@ __device__ __forceinline__ void compact_tile(uint32_t *fw_idx, uint32_t *drop_id
         const uint32_t ndr = (uint32_t)__popcll(bdr), nfw = (uint32_t)__popcll(bfw);
         const uint32_t slot = is_fw ? pfw : (is_drop ? nv - ndr + pdr : nfw + lane - pfw - pdr);
         const uint32_t e = lane | (act << 6);
-        if (scr != ~0u && nv == 64u) {  // (LDS ops of one wave complete in order)
+        if (PPE_CMP_LDS8 && scr != ~0u && nv == 64u) {  // (LDS ops of one wave complete in order)
             lds_st8(scr + slot, e);
             const uint32_t v = lds_u32(scr + 4u * (lane & 15u));
             if (lane < 16u) gst_nt<uint32_t>(part8, (tile << 6) + 4u * lane, v);
