@@ -569,6 +569,8 @@ def run_stateless(args, dev, world, rank, dist):
         try:
             extra[name], _ = measure_config(name, args, dev, world, rank, dist, primary=False)
         except Exception as e:  # one config failing must not lose the headline line
+            import traceback
+            print(f"bench.py rank {rank}: nested {name} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
             extra[name] = {"error": str(e)[:300]}
     # the stateful paths: the flow table (FlowHandlePacket) and IPv4 reassembly
     # (Defrag), each with its own roofline and parity sample
@@ -577,6 +579,8 @@ def run_stateless(args, dev, world, rank, dist):
         try:
             extra[name] = fn(args, synth.CONFIGS[name], dev, world, rank, dist, name=name, nested=True)
         except Exception as e:
+            import traceback
+            print(f"bench.py rank {rank}: nested {name} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
             extra[name] = {"error": str(e)[:300]}
         torch.cuda.empty_cache()
 
@@ -634,7 +638,7 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     rules = synth.make_rules(cfgd["rules"])
     flows = cfgd["flows"]
     nbufs = args.nbufs or 8
-    eng = Engine(int(os.environ.get("LOCAL_RANK", "0")))
+    eng = Engine(dev.index)  # (the rank's device: cuda:0 for every rank under --shared-gpu)
     acl = eng.commit(rules, default_action=abi.ACL_RULE_ACTION_FW)
     # N = 1: one flow population.  N > 1: the ranks share one population and every batch is steered by flow hash
     # to the owning GPU (ppe.dist.steered_classify_flow: all-to-all over RCCL), so flows span ranks as on a NIC that
@@ -645,25 +649,30 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     # parity sample first: a fresh table, four 64k batches, against the oracle's sequential flow table
     parity = None
     if rank == 0:
-        import pyoracle
-        m = 1 << 16
-        eng.flow_create(2 * flows, m)
-        o = pyoracle.Oracle(rules, default_action=abi.ACL_RULE_ACTION_FW)
-        ft = pyoracle.OracleFlow(o, capacity=2 * flows)
-        ok = True
-        for b in range(4):
-            pk = synth.make_flow_packets(m, rules, flows // 16, seed=tseed + 31 * b, template_seed=tseed, stride=stride)
-            th = torch.from_numpy(pk["hdr"]).to(dev)
-            tl = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
-            out = {k: torch.empty(m, dtype=torch.int32, device=dev) for k in ("verdict", "flow_hash", "acl_hit")}
-            eng.classify_flow_torch(th, tl, out, cfg=eng.cfg(now_seconds=NOW + b))
-            ref = ft.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW + b))
-            torch.cuda.synchronize()
-            for k in ("verdict", "flow_hash", "acl_hit"):
-                g = out[k].cpu().numpy()
-                ok = ok and np.array_equal(g if k == "acl_hit" else g.view(np.uint32), ref[k])
-        parity = bool(ok and len(eng.flow_dump()) == ft.stats()["live"])
-        ft.close()
+        try:  # (rank 0 only, no collectives: an error here must not leave the other ranks in a barrier)
+            import pyoracle
+            m = 1 << 16
+            eng.flow_create(2 * flows, m)
+            o = pyoracle.Oracle(rules, default_action=abi.ACL_RULE_ACTION_FW)
+            ft = pyoracle.OracleFlow(o, capacity=2 * flows)
+            ok = True
+            for b in range(4):
+                pk = synth.make_flow_packets(m, rules, flows // 16, seed=tseed + 31 * b, template_seed=tseed, stride=stride)
+                th = torch.from_numpy(pk["hdr"]).to(dev)
+                tl = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
+                out = {k: torch.empty(m, dtype=torch.int32, device=dev) for k in ("verdict", "flow_hash", "acl_hit")}
+                eng.classify_flow_torch(th, tl, out, cfg=eng.cfg(now_seconds=NOW + b))
+                ref = ft.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW + b))
+                torch.cuda.synchronize()
+                for k in ("verdict", "flow_hash", "acl_hit"):
+                    g = out[k].cpu().numpy()
+                    ok = ok and np.array_equal(g if k == "acl_hit" else g.view(np.uint32), ref[k])
+            parity = bool(ok and len(eng.flow_dump()) == ft.stats()["live"])
+            ft.close()
+        except Exception as e:
+            import traceback
+            print(f"bench.py: {name} parity sample failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
+            parity = False
 
     eng.flow_create(2 * flows, 2 * n if steer else n)  # a steered batch may exceed n (uneven owners)
     bufs = []
@@ -846,37 +855,42 @@ def run_defrag(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     arena[:end] = a_full[:end]
     pos, variant = defrag_batch_variants(arena, off, lens, nvar)
 
-    eng = Engine(int(os.environ.get("LOCAL_RANK", "0")))
+    eng = Engine(dev.index)  # (the rank's device: cuda:0 for every rank under --shared-gpu)
     stream = torch.cuda.current_stream(dev)
     t_off = torch.from_numpy(off.view(np.int64)).to(dev)
     t_len = torch.from_numpy(lens.view(np.int32)).to(dev)
     t_ids = torch.arange(n, dtype=torch.int64, device=dev)
 
     # parity sample: batch variant 1 through a fresh table and the oracle's sequential Defrag
-    parity = None
+    parity, stats = None, None
     if rank == 0:
-        import pyoracle
-        g = Defrag(eng, fcb_max=1 << 16)
-        o = pyoracle.OracleDefrag(fcb_max=1 << 16)
-        a1 = variant(1)
-        out = g.alloc_out(n, hdr_stride)
-        g.run_torch(torch.from_numpy(a1).to(dev), t_off, t_len, out, NOW, ids=t_ids)
-        ref = o.batch(a1, off, lens, NOW, ids=np.arange(n, dtype=np.uint64))
-        torch.cuda.synchronize()
-        nd = ref["n_dgram"]
-        got_len = out["dgram_len"].cpu().numpy().view(np.uint32)
-        ok = (np.array_equal(out["status"].cpu().numpy().view(np.uint32), ref["status"]) and
-              int(out["n_dgram"].item()) == nd and np.array_equal(got_len, ref["dgram_len"]) and
-              np.array_equal(out["dgram_of"].cpu().numpy().view(np.uint32), ref["dgram_of"]))
-        gp = out["dgram_pkt"][:nd].cpu().numpy()
-        for j in range(nd):
-            m = int(ref["dgram_len"][j])
-            ok = ok and np.array_equal(gp[j, :m], ref["dgram_pkt"][j, :m])
-        parity = bool(ok)
-        stats = {k: int(v) for k, v in o.stats().items()}
-        del out, gp, ref
-        g.close()
-        o.close()
+        try:  # (rank 0 only, no collectives: an error here must not leave the other ranks in a barrier)
+            import pyoracle
+            g = Defrag(eng, fcb_max=1 << 16)
+            o = pyoracle.OracleDefrag(fcb_max=1 << 16)
+            a1 = variant(1)
+            out = g.alloc_out(n, hdr_stride)
+            g.run_torch(torch.from_numpy(a1).to(dev), t_off, t_len, out, NOW, ids=t_ids)
+            ref = o.batch(a1, off, lens, NOW, ids=np.arange(n, dtype=np.uint64))
+            torch.cuda.synchronize()
+            nd = ref["n_dgram"]
+            got_len = out["dgram_len"].cpu().numpy().view(np.uint32)
+            ok = (np.array_equal(out["status"].cpu().numpy().view(np.uint32), ref["status"]) and
+                  int(out["n_dgram"].item()) == nd and np.array_equal(got_len, ref["dgram_len"]) and
+                  np.array_equal(out["dgram_of"].cpu().numpy().view(np.uint32), ref["dgram_of"]))
+            gp = out["dgram_pkt"][:nd].cpu().numpy()
+            for j in range(nd):
+                m = int(ref["dgram_len"][j])
+                ok = ok and np.array_equal(gp[j, :m], ref["dgram_pkt"][j, :m])
+            parity = bool(ok)
+            stats = {k: int(v) for k, v in o.stats().items()}
+            del out, gp, ref
+            g.close()
+            o.close()
+        except Exception as e:
+            import traceback
+            print(f"bench.py: D1 parity sample failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
+            parity = False
 
     d = Defrag(eng, fcb_max=cfgd["fcb_max"])
     base = torch.from_numpy(arena).to(dev)
