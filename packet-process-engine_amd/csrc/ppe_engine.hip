@@ -488,7 +488,28 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     a.off_idtab = c->h_img[r][PPE_IMG_W_OFFIDTAB];
     a.crec_lds = plan.crec_lds;
     a.idtab_lds = plan.idtab_lds;
-    a.max_groups = c->max_groups;
+    // batch groups: the kernel splits its waves into min(batches, max_groups) groups, group g taking batches g, g + G,
+    // ...; when G does not divide the batch count the last round leaves groups idle (20 batches at G = 8: the last
+    // 4 run on half the grid; C3 / C4 ring step +12 %, profiles/r3_ab_runs.md r4l).  Take the power-of-two G up to the
+    // cap (or the batch count itself when smaller) with the least work-slot time, ceil(batches / G) x G batch slots
+    // weighted by the per-batch cost of G groups (1 group 1.10, 2 groups 1.02, more 1.00: C1 per-batch 20.2 / 18.7 /
+    // 18.3 us at 1 / 2 / >= 4 groups); ties go to the larger G.  20 batches -> 4 groups, 32 -> 8, 33 -> 2.
+    {
+        const uint32_t gmax = std::max(1u, std::min(c->max_groups, nb));
+        auto cost = [&](uint32_t g) {
+            return (double)((nb + g - 1u) / g * g) * (g == 1u ? 1.10 : g == 2u ? 1.02 : 1.0);
+        };
+        uint32_t best = gmax;
+        double cbest = cost(gmax);
+        for (uint32_t g = 1u << (31 - __builtin_clz(gmax)); g >= 1u; g >>= 1) {
+            if (g == gmax) continue;
+            if (cost(g) < cbest - 1e-9) {
+                best = g;
+                cbest = cost(g);
+            }
+        }
+        a.max_groups = best;
+    }
     a.max_depth = c->h_img[r][PPE_IMG_W_MAXDEPTH];
     a.max_leaf = c->h_img[r][PPE_IMG_W_MAXLEAF];
     a.root_ks = c->h_img[r][PPE_IMG_W_ROOTKS];
