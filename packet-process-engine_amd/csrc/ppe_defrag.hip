@@ -662,9 +662,15 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
 }
 
 // ---- assemble: one wave per datagram slot ----------------------------------------------------------------------
+// DF_AB (diagnostic builds only, wrong outputs): 1 = empty slots skip their zeroing, 2 = no window bytes, 4 = no
+// header checksum, 8 = datagram bytes not copied
+#ifndef DF_AB
+#define DF_AB 0
+#endif
 __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, uint32_t nd) {
     const uint32_t tid = __lane_id();
-    uint8_t *win = a.dgram_hdr ? a.dgram_hdr + (size_t)j * a.hdr_stride : nullptr;
+    uint8_t *win = (a.dgram_hdr && !(DF_AB & 2)) ? a.dgram_hdr + (size_t)j * a.hdr_stride : nullptr;
+    if ((DF_AB & 1) && j >= nd) return;
     if (j >= nd) {
         if (win && ((uintptr_t)win & 3u) == 0) {
             if (tid < a.hdr_stride / 4) ((uint32_t *)win)[tid] = 0u;
@@ -712,7 +718,7 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
     for (uint32_t p = 1; p < nlist; ++p) out_len += __shfl(cd0, p, 64) >> 16;
     // header patch (non-ICMP: ip_len = ihl*4 + total, ip_off = 0, checksum; ICMP: ip_off = 0)
     uint32_t w_iplen = ld_be16(hsrc + l2 + 2), w_csum = ld_be16(hsrc + l2 + 10);
-    if (!icmp) {
+    if (!icmp && !(DF_AB & 4)) {
         w_iplen = (ihl4 + total) & 0xffffu;
         // IPV4CalculateChecksum (decode-ipv4.h:117-163) over the patched header: words 0-4, 6-9, then the options
         uint32_t cs = ld_be16(hsrc + l2) + w_iplen + ld_be16(hsrc + l2 + 4) + 0u /* ip_off */ + ld_be16(hsrc + l2 + 8) +
@@ -736,7 +742,7 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
     };
     // the reassembled frame: segment 0 = the head frame, segment p = the last flen bytes of chain entry p
     // (ICMP: the head frame only; the reference sizes the buffer but copies nothing else)
-    uint8_t *full = a.dgram_pkt ? a.dgram_pkt + (size_t)j * a.reasm_buf : nullptr;
+    uint8_t *full = (a.dgram_pkt && !(DF_AB & 8)) ? a.dgram_pkt + (size_t)j * a.reasm_buf : nullptr;
     const uint32_t stride = a.hdr_stride;
     uint32_t dst0 = 0;
     // whole output dwords are assembled from two aligned source dwords (a funnel shift) and stored as dwords; the
