@@ -748,11 +748,14 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
     // whole output dwords are assembled from two aligned source dwords (a funnel shift) and stored as dwords; the
     // partial dwords at a segment's ends are stored bytewise (the neighbouring segment owns their other bytes)
     const bool wide = full && ((uintptr_t)full & 3u) == 0 && (a.reasm_buf & 3u) == 0;
+    // when the head frame covers the whole window, the window is the first `stride` bytes of the frame: its dwords
+    // are stored from the wide pass's registers (no byte pass of its own: one dependent round trip fewer)
+    const bool wfast = wide && win && ((uintptr_t)win & 3u) == 0 && head_tot >= stride && a.reasm_buf >= stride;
     for (uint32_t p = 0; p < (icmp ? 1u : nlist); ++p) {
         const uint32_t tot = __shfl(cd1, p, 64), flen = __shfl(cd0, p, 64) >> 16;
         const uint8_t *src = seg_base(p) + (p == 0 ? 0u : tot - flen);
         const uint32_t cnt = p == 0 ? tot : flen;
-        if (win && dst0 < stride) {
+        if (win && dst0 < stride && !wfast) {
             const uint32_t wl = cnt < stride - dst0 ? cnt : stride - dst0;
             for (uint32_t b = tid; b < wl; b += 64) win[dst0 + b] = (uint8_t)patched(dst0 + b, src[b]);
         }
@@ -785,6 +788,7 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
                             v = pv;
                         }
                         ((uint32_t *)full)[w] = v;
+                        if (wfast && p == 0 && w < stride / 4u) ((uint32_t *)win)[w] = v;
                     }
                 }
                 // head bytes [dst0, 4*wa) and tail bytes [4*we, end) (when the segment lies inside one dword, all)
