@@ -81,6 +81,10 @@
 #ifndef PPE_WALK_2PH
 #define PPE_WALK_2PH 1
 #endif
+// PPE_REC_PF: the split multi-tile round requests tile t + 1's compact record before tile t's record check
+#ifndef PPE_REC_PF
+#define PPE_REC_PF 1
+#endif
 // (trace the wave's tile iterations PPE_TRACE_SKIP .. + 3: a skip > 0 samples the steady state of a long launch)
 #ifndef PPE_TRACE_SKIP
 #define PPE_TRACE_SKIP 0u
@@ -1541,10 +1545,18 @@ void ppe_classify_kernel(ppe_kargs a) {
                     acl_walk_blocks_mt<MODE, L::IMGB, MT, KL, true>(a.img, geo, key, need, nd, rec);
                 else
                     acl_walk_blocks_mt<MODE, L::IMGB, MT, KL>(a.img, geo, key, need, nd);
+                // PPE_REC_PF (split compact images): tile t + 1's record is requested, by every lane (a lane with no
+                // leaf reads slot 0), before tile t's check, so the L2 round trips of the round's records overlap
+                // the tiles' finish work instead of one after another
+                constexpr bool RPF = PPE_REC_PF && MODE == IMG_SPLIT && !PPE_REC_IN_WALK;
+                uint4 rnext = make_uint4(0u, 0u, 0u, 0u);
+                if (RPF && geo.off_crec) rnext = crec_load<L::IMGB>(a.img, geo, nd[0].z);
 #pragma unroll
                 for (int t = 0; t < MT; ++t) {
                     const uint32_t tile = t0 + t;
                     if (tile >= ntiles) break;  // wave-uniform
+                    uint4 rcur = rnext;
+                    if (RPF && geo.off_crec && t + 1 < MT) rnext = crec_load<L::IMGB>(a.img, geo, nd[t + 1].z);
                     const uint32_t p = (tile << 6) + lane;
                     Dec k;
                     k.sip = key[t][0];
@@ -1563,6 +1575,9 @@ void ppe_classify_kernel(ppe_kargs a) {
                         bool drop;
                         if (PPE_REC_IN_WALK && geo.off_crec) {
                             crec_check<L::IMGB>(a.img, geo, nd[t].z, rec[t], k.sip, k.dip, k.sport, k.dport,
+                                                k.proto == 6u, hit, drop);
+                        } else if (RPF && geo.off_crec) {
+                            crec_check<L::IMGB>(a.img, geo, nd[t].z, rcur, k.sip, k.dip, k.sport, k.dport,
                                                 k.proto == 6u, hit, drop);
                         } else if (geo.off_crec) {
                             acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, k.sip, k.dip, k.sport, k.dport,
