@@ -1141,6 +1141,8 @@ static int flow_sync_counts(ppe_ctx *c, unsigned long long *ctl_out) {
     FlowTable &t = *c->flow;
     HIPCHK(c, hipDeviceSynchronize());
     HIPCHK(c, hipMemcpy(ctl_out, t.ctl, PPE_FCTL_WORDS * 8u, hipMemcpyDeviceToHost));
+    if (ctl_out[PPE_FCTL_ERR])
+        return fail(c, PPE_EIO, "flow table: %llu finalize workgroup(s) timed out waiting for the revoke", ctl_out[PPE_FCTL_ERR]);
     t.live_ub = ctl_out[PPE_FCTL_LIVE];
     t.tomb_ub = ctl_out[PPE_FCTL_TOMBS];
     t.snap_used = t.batches;  // (the device is idle: this is the state after every submitted batch)

@@ -41,7 +41,8 @@ struct ppe_bdesc {
 enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_NEW, PPE_FCTL_TOMBS,
        PPE_FCTL_MISS0, PPE_FCTL_MISS1, /* tiles with pending packets, by batch parity */
        PPE_FCTL_REVOKED_SEQ,           /* finalize: workgroup 0's revoke published for batch seq + 1 */
-       PPE_FCTL_WORDS = 8 };
+       PPE_FCTL_ERR,                   /* finalize: waits for the revoke flag that gave up (results not exact) */
+       PPE_FCTL_WORDS = 16 };
 #define PPE_PK_SHIFT 40u                       /* packed counter: packets in bits 63:40, bytes in 39:0 */
 #define PPE_PK_FOLD_PKTS (1ull << 23)          /* fold into `stats` once either field reaches half its range */
 #define PPE_PK_FOLD_BYTES (1ull << 39)

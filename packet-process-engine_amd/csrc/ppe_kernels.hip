@@ -1835,10 +1835,12 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
                                    __HIP_MEMORY_SCOPE_AGENT);
         } else {
             if (tid == 0) {
-                for (uint32_t k = 0; k < (1u << 24) &&
-                                     __hip_atomic_load(&a.f.ctl[PPE_FCTL_REVOKED_SEQ], __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT) != a.f.seq + 1ull; ++k)
+                uint32_t k = 0;
+                for (; k < (1u << 24) && __hip_atomic_load(&a.f.ctl[PPE_FCTL_REVOKED_SEQ], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) != a.f.seq + 1ull; ++k)
                     __builtin_amdgcn_s_sleep(8);
+                if (k == (1u << 24))  // (never seen; reported by the next synchronising flow call as an error)
+                    __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_ERR], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             __syncthreads();
         }
