@@ -81,6 +81,10 @@
 #ifndef PPE_WALK_2PH
 #define PPE_WALK_2PH 1
 #endif
+// PPE_WALK_CMP: the split walk's tail in one virtual tile (acl_walk_blocks_mt phase 2)
+#ifndef PPE_WALK_CMP
+#define PPE_WALK_CMP 1
+#endif
 // PPE_REC_PF: the split multi-tile round requests tile t + 1's compact record before tile t's record check
 #ifndef PPE_REC_PF
 #define PPE_REC_PF 1
@@ -853,12 +857,19 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
             if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
         }
         // phase 2: the levels read from L2
+        uint32_t it = 0;
 #pragma unroll 1
-        for (uint32_t it = 0; it < g.max_bdepth; ++it) {
+        for (; it < g.max_bdepth; ++it) {
             bool pending = false;
 #pragma unroll
             for (int t = 0; t < MT; ++t) pending = pending | !done[t];
             if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
+            if constexpr (PPE_WALK_CMP && MT > 1) {  // (the tail: see below)
+                uint32_t tot = 0;
+#pragma unroll
+                for (int t = 0; t < MT; ++t) tot += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(!done[t]));
+                if (tot <= 64u) break;
+            }
             uint4 q[MT][NQ];
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
@@ -885,6 +896,73 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
                         blk[t] = x;
                     }
                 }
+            }
+        }
+        if constexpr (PPE_WALK_CMP && MT > 1) {
+            // The tail (PPE_WALK_CMP): once the lanes still walking in all MT tiles fit one wave, they move into one
+            // virtual tile (ds_permute of the key and block index: lane l of tile t goes to lane P_t + its rank among
+            // tile t's walking lanes), which walks the remaining levels with one read per step instead of MT, and
+            // hands each lane its leaf back (ds_bpermute).  After the first L2 step about 7 % of C3's lanes walk on.
+            if (it >= g.max_bdepth) return;
+            uint64_t m[MT];
+            uint32_t P[MT + 1];
+            P[0] = 0u;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                m[t] = __builtin_amdgcn_ballot_w64(!done[t]);
+                P[t + 1] = P[t] + (uint32_t)__popcll(m[t]);
+            }
+            const uint32_t tot = P[MT];
+            if (tot == 0u) return;
+            const uint32_t lane = __lane_id();
+            uint32_t vkey[4], vblk = 0u, vpay = 0u, vt = 0u;
+#pragma unroll
+            for (int t = 1; t < MT; ++t) vt += lane >= P[t] ? 1u : 0u;  // the tile this virtual lane comes from
+#pragma unroll
+            for (int c = 0; c < 4; ++c) vkey[c] = 0u;
+            uint32_t dst[MT];
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[t] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[t], 0u));
+                // a lane that does not walk pushes outside tile t's range [P_t, P_t+1) (its value is not taken there)
+                const uint32_t outside = P[t + 1] < 64u ? P[t + 1] : (P[t] > 0u ? P[t] - 1u : 0u);
+                dst[t] = !done[t] ? P[t] + rank : outside;
+                const uint32_t a4 = dst[t] << 2;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_permute((int)a4, (int)key[t][c]);
+                    vkey[c] = vt == (uint32_t)t ? v : vkey[c];
+                }
+                const uint32_t vb = (uint32_t)__builtin_amdgcn_ds_permute((int)a4, (int)blk[t]);
+                vblk = vt == (uint32_t)t ? vb : vblk;
+            }
+            bool vdone = lane >= tot;
+#pragma unroll 1
+            for (; it < g.max_bdepth; ++it) {
+                if (__builtin_amdgcn_ballot_w64(!vdone) == 0) break;
+                if (!vdone) {
+                    const uint32_t ga = 4u * g.off_blocks + BB * vblk;
+                    uint4 q[NQ];
+#pragma unroll
+                    for (int j = 0; j < NQ; ++j) q[j] = gld<uint4>(gimg, ga + 16u * j);
+                    const uint4 lo = q[0], hi = q[NQ - 1];
+                    const bool b0 = key_sel(lo.w & 15u, vkey) > lo.x;
+                    const uint32_t t1 = b0 ? lo.z : lo.y;
+                    const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
+                    const bool b1 = key_sel(k1, vkey) > t1;
+                    const uint32_t x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
+                    if (x & PPE_BLK_LEAF) {
+                        vdone = true;
+                        vpay = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF) : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
+                    } else {
+                        vblk = x;
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {  // each walking lane takes its leaf back from its virtual lane
+                const uint32_t pay = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(dst[t] << 2), (int)vpay);
+                if (!done[t]) nd[t].z = pay;
             }
         }
         return;
