@@ -43,6 +43,10 @@ namespace {
 constexpr uint32_t kEmpty = 0u, kTomb = 1u, kLive = 2u, kPend = 0x80000000u;
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kBlock = 256;        // workgroup size of the per-fragment kernels
+#ifndef DF_SLOT_WAVES
+#define DF_SLOT_WAVES 4
+#endif
+constexpr uint32_t kSlotBlock = 64 * DF_SLOT_WAVES;   // workgroup size of the wave-per-item kernels (stash, assemble)
 constexpr uint32_t kScanT = 1024;       // one-workgroup scans
 constexpr uint32_t kSortBlock = 1024;   // radix sort: elements (= threads) per workgroup (64k-word histogram)
 
@@ -339,6 +343,9 @@ __global__ void __launch_bounds__(kSortBlock) df_sort_pass_kernel(DfArgs a) {
     __syncthreads();
     const uint32_t j = blockIdx.x * kSortBlock + threadIdx.x;
     const bool v = j < a.n;
+    // the first scatter pass runs after every reader of the admission counts: it clears the tile counts for the
+    // process kernel, which counts each tile's completing fragments into them (no second count launch)
+    if (SCATTER && a.shift == 0u && v && __lane_id() == 0) a.tcnt[j >> 6] = 0u;
     uint32_t key = 0u;
     if (INIT && v) {
         key = df_sort_key(a, j);
@@ -572,6 +579,8 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
             a.status[i] = out | (tear ? PPE_DF_TEARDROP : 0u);
             a.inserted[i] = ins;
             a.dgrec[i] = done;
+            // the place kernel's per-tile count of completing fragments (zeroed by the first scatter pass)
+            if (done != kNone) atomicAdd(a.tcnt + (i >> 6), 1u);
             st[out]++;
         }
         h[0] = flags | (last_in << 8) | (cache_num << 16) | (nlist << 24);
@@ -605,8 +614,8 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
 }
 
 // ---- stash: copy held frames into their FCB's store slot (PACKET_HW2SW) ----------------------------------------------
-__global__ void __launch_bounds__(kBlock) df_stash_kernel(DfArgs a) {
-    const uint32_t i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+__global__ void __launch_bounds__(kSlotBlock) df_stash_kernel(DfArgs a) {
+    const uint32_t i = blockIdx.x * (kSlotBlock / 64) + (threadIdx.x >> 6);
     if (i >= a.n) return;
     const uint32_t ins = a.inserted[i];
     if (ins == kNone) return;
@@ -818,8 +827,8 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
 }
 
 // one wave per slot (a fixed grid striding over the slots measured slower: 50 vs 40 µs for D1)
-__global__ void __launch_bounds__(kBlock) df_assemble_kernel(DfArgs a) {
-    const uint32_t j = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+__global__ void __launch_bounds__(kSlotBlock) df_assemble_kernel(DfArgs a) {
+    const uint32_t j = blockIdx.x * (kSlotBlock / 64) + (threadIdx.x >> 6);
     if (j < a.n) df_assemble_slot(a, j, (uint32_t)a.ctl[C_NDGRAM]);
 }
 
@@ -1052,11 +1061,10 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
         std::swap(a.sval[0], a.sval[1]);
     }
     hipLaunchKernelGGL(df_process_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(df_stash_kernel, dim3(blocks(a.n, kBlock / 64)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(df_stash_kernel, dim3(blocks(a.n, kSlotBlock / 64)), dim3(kSlotBlock), 0, s, a);
     a.flag_mode = 1;
-    hipLaunchKernelGGL(df_tile_count_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_place_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(df_assemble_kernel, dim3(blocks(a.n, kBlock / 64)), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(df_assemble_kernel, dim3(blocks(a.n, kSlotBlock / 64)), dim3(kSlotBlock), 0, s, a);
     return launched(d, "ppe_defrag");
 }
 
