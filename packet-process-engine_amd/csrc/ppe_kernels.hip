@@ -1215,6 +1215,9 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
 #ifndef PPE_MT3_WAVES
 #define PPE_MT3_WAVES 4
 #endif
+#ifndef PPE_FLOW_WAVES  // waves per SIMD the FLOW classify kernel is compiled for
+#define PPE_FLOW_WAVES 4   // 8 (the stateless kernels' value) measured 3 % slower per F1 batch: profiles/r3_ab_runs.md r4f
+#endif
 #ifndef PPE_MT_WAVES  // waves per SIMD the PF_MULTI kernel is compiled for (VGPR budget 512 / this)
 #define PPE_MT_WAVES 4
 #endif
@@ -1227,7 +1230,8 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
 // fewer scalars (C1 step -2..4 %, C4 -3.5 %: fewer SGPR spills to VGPR lanes)
 template <int MODE, int PF, int BLOCK, bool FLOW, bool PART = false>
 __global__ __launch_bounds__(BLOCK, ((PF == PF_MULTI || PF == PF_MULTI3) && !FLOW)
-                                        ? (PF == PF_MULTI3 ? PPE_MT3_WAVES : PPE_MT_WAVES) : PPE_WAVES_PER_EU)
+                                        ? (PF == PF_MULTI3 ? PPE_MT3_WAVES : PPE_MT_WAVES)
+                                        : (FLOW ? PPE_FLOW_WAVES : PPE_WAVES_PER_EU))
 void ppe_classify_kernel(ppe_kargs a) {
     constexpr bool MT_PIPE = PF == PF_MULTI && !FLOW &&
                              (PPE_MT_PF == 2 || (PPE_MT_PF == 1 && MODE == IMG_LDS));  // the pipelined round loop
