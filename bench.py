@@ -111,6 +111,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (all cores)")
+    ap.add_argument("--nested-cpu-seconds", type=float, default=3.0,
+                    help="CPU baseline sample length of each nested stateless config (all cores)")
+    ap.add_argument("--no-c0", action="store_true", help="skip the C0 plumbing config (10k x 64 B, 16 rules)")
     ap.add_argument("--dry-run", action="store_true", help="rank plumbing only (gloo, no GPU)")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, collectives over gloo "
@@ -370,6 +373,127 @@ def gpu_busy(dev, seconds=WARM_SECONDS):
     del x
 
 
+def cpu_baseline(pk, rules, image, seconds, what):
+    """The oracle's C restatement (the tree walk over the same classifier image: kind "port") on this host's cores:
+    all of them (nproc, OMP_NUM_THREADS-capped) as pinned run-to-completion shards (mainloop, main.c:422-425) for
+    `seconds` of passes over the batch, then one pinned thread for a quarter of that."""
+    import pyoracle
+    m = len(pk["len"])
+    o = pyoracle.Oracle(rules, default_action=1, image=image)
+    cores = host_cores()
+    ocfg = o.cfg(now_seconds=NOW)
+    o.pin(cores)
+    o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=len(cores), use_tree=True)
+    reps, tc = 0, time.perf_counter()
+    while time.perf_counter() - tc < seconds:
+        o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=len(cores), use_tree=True)
+        reps += 1
+    cpu_s = time.perf_counter() - tc
+    o.pin(cores[:1])
+    ones, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < seconds / 4:
+        o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=1, use_tree=True)
+        ones += 1
+    one_s = (time.perf_counter() - t1) / ones
+    o.pin([])
+    return {"value": m * reps / cpu_s / 1e6, "unit": "Mpps", "cores": len(cores), "kind": "port",
+            "sample": f"{reps} passes over a {m}-packet {what} batch ({m * reps} packets, {cpu_s:.1f} s), "
+                      f"{len(cores)} pinned pthreads (nproc of this host) as run-to-completion shards "
+                      f"(mainloop, main.c:422-425); 1 pinned thread: {m / one_s / 1e6:.2f} Mpps ({ones} passes)",
+            "single_thread_mpps": m / one_s / 1e6}
+
+
+def measure_c0(args, dev):
+    """C0 (BASELINE configs[0]): the reference's own plumbing case, 10k x 64-B IPv4/UDP packets and 16 rules on ONE
+    CPU thread: the oracle restatement on one pinned core (the reported baseline), and beside it the same batch as
+    one ppe_classify launch on the GPU (a 10k-packet launch is latency-bound: 157 tiles on 256 CUs), with the
+    whole batch checked against the oracle."""
+    import pyoracle
+    cfgd = synth.CONFIGS["C0"]
+    n = cfgd["n"]
+    rules = synth.make_rules(cfgd["rules"])
+    pk = synth.make_packets(n, rules, seed=synth.SEED + 3, kind=cfgd["kind"], stride=args.stride)
+    eng = Engine(dev.index)
+    try:
+        eng.commit(rules, default_action=1)
+        cfg = eng.cfg(now_seconds=NOW)
+        hdr = torch.from_numpy(pk["hdr"]).to(dev)
+        lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
+        out = {k: torch.empty(n, dtype=torch.int32, device=dev) for k in ("verdict", "flow_hash", "acl_hit")}
+        stream = torch.cuda.current_stream(dev)
+        warm_up(lambda: eng.classify_torch(hdr, lens, out, cfg=cfg))
+        reps = 200
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        for _ in range(reps):
+            eng.classify_torch(hdr, lens, out, cfg=cfg)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        gpu_ms = ev0.elapsed_time(ev1) / reps
+        o = pyoracle.Oracle(rules, default_action=1)
+        ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(now_seconds=NOW))
+        got = {k: v.cpu().numpy().view(np.uint32 if k != "acl_hit" else np.int32) for k, v in out.items()}
+        parity = all(np.array_equal(got[k], ref[k]) for k in got)
+        cpu = None
+        if not args.no_cpu_baseline:
+            o.set_image(eng.image())
+            cores = host_cores()
+            o.pin(cores[:1])
+            ocfg = o.cfg(now_seconds=NOW)
+            o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=1, use_tree=True)
+            passes, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < 2.0:
+                o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=1, use_tree=True)
+                passes += 1
+            cpu_s = time.perf_counter() - t0
+            o.pin([])
+            cpu = {"value": n * passes / cpu_s / 1e6, "unit": "Mpps", "cores": 1, "kind": "port",
+                   "sample": f"{passes} passes over the {n}-packet C0 batch on one pinned thread ({cpu_s:.1f} s)"}
+        return {"workload": f"C0: {n} x 64B IPv4/UDP packets, {cfgd['rules']} five-tuple ACL rules (the reference's "
+                            f"CPU plumbing config)", "value": round(n / (gpu_ms / 1e3) / 1e6, 2), "unit": "Mpps",
+                "ms_per_batch": round(gpu_ms, 5), "timing": f"GPU: {reps} back-to-back single-batch launches",
+                "parity_ok": parity, "parity_packets": n, "cpu_baseline": cpu}
+    finally:
+        eng.close()
+
+
+def acl_lookup_latency(eng, pk, rules, calls=300):
+    """DP_Acl_Lookup's latency (flow.c:232: one call per flow miss on the reference's hot path): host-pointer lookups
+    through the C ABI call DP_Acl_Lookup / DP_Acl_Lookup_Burst make (ppe_acl_lookup_host), 1 and 64 tuples per call,
+    median and 99th percentile over `calls` back-to-back calls timed around the ctypes call (its ~1 us included);
+    the 64 answers are checked against the oracle's linear first match."""
+    import ctypes as C
+    import pyoracle
+    from ppe import abi
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"][:64], pk["len"][:64], cfg=o.cfg(now_seconds=NOW))
+    tup = np.ascontiguousarray(ref["tuple"][:64])
+    tup[:, 3] &= 0xFF  # {sip, dip, sport | dport << 16, proto}
+    hit = np.zeros(64, np.int32)
+    act = np.zeros(64, np.uint32)
+    out = {}
+    for k in (1, 64):
+        t = abi.Tuples(tup.ctypes.data, None, None, k)
+        fn, cargs = eng.lib.ppe_acl_lookup_host, (eng.ctx, C.byref(t), hit.ctypes.data, act.ctypes.data, NOW)
+        for _ in range(20):
+            fn(*cargs)
+        ts = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            rc = fn(*cargs)
+            ts.append(time.perf_counter() - t0)
+            if rc:
+                raise RuntimeError(f"ppe_acl_lookup_host: {rc}")
+        out[f"lookup_us_{k}"] = round(float(np.median(ts)) * 1e6, 2)
+        out[f"lookup_us_{k}_p99"] = round(float(np.percentile(ts, 99)) * 1e6, 2)
+    z = np.zeros(6, np.uint8)
+    want = [o.lib.oracle_acl_linear(int(a), int(b), int(c) & 0xFFFF, int(c) >> 16, int(d), z.ctypes.data,
+                                    z.ctypes.data, NOW, None) for a, b, c, d in tup]
+    out["lookup_ok"] = bool(np.array_equal(hit, np.array(want, np.int32)))
+    return out
+
+
 def measure_config(name, args, dev, world, rank, dist, primary):
     """One stateless config: resident batches, K batches in one call, roofline launch, parity sample."""
     from ppe import abi
@@ -463,6 +587,8 @@ def measure_config(name, args, dev, world, rank, dist, primary):
             out["roofline"]["ceiling"] = ceiling(res, args, dev, kern_avg_ms, pk_launch, alg)
         except Exception as e:  # the ceiling is context, never worth losing the line over
             out["roofline"]["ceiling"] = {"error": str(e)[:200]}
+    if not primary and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(res.host[0], rules, eng.image(), args.nested_cpu_seconds, name)
     ctx = dict(eng=eng, res=res, rules=rules, cfg=cfg, n=n, my_ms=my_ms)
     if not primary:
         eng.close()
@@ -499,6 +625,26 @@ def run_stateless(args, dev, world, rank, dist):
             gather = {"ms_per_batch": round(g_ms, 4), "bytes_per_rank": 12 * n,
                       "collective": "all_gather (gloo, shared-GPU rehearsal)" if args.shared_gpu else "all_gather (RCCL)",
                       "value_with_gather": round(n * world / ((my_ms / args.steps + g_ms) / 1e3) / 1e6, 2)}
+            # the per-reason counters summed over ranks (dp_show_pkt_stat's sum over cores, dp_cmd.c:844; SURVEY.md
+            # 8(e)): ppe/dist.py allreduce_counters on the engine's 32 counters, device-resident on RCCL
+            from ppe.dist import allreduce_counters
+            from ppe.abi import COUNTERS
+            cdict = eng.counters()
+            cvec = np.array([cdict[k] for k in COUNTERS], np.int64)
+            cdev = None if args.shared_gpu else dev
+            cs = []
+            for _ in range(6):
+                dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                summed = allreduce_counters(dist, cvec, device=cdev)
+                cs.append(time.perf_counter() - t0)
+            ct = torch.tensor([float(np.median(cs[1:])) * 1e3], dtype=torch.float64, device=dev)
+            dist.all_reduce(ct, op=dist.ReduceOp.MAX)
+            gather["counters_allreduce"] = {
+                "ms": round(float(ct.item()), 4), "words": int(len(cvec)),
+                "pkts_all_ranks": int(summed[COUNTERS.index("pkts")]),
+                "collective": "all_reduce (gloo)" if args.shared_gpu else "all_reduce (RCCL)"}
         except Exception as e:  # a failed side measurement must not lose the throughput line
             gather = {"error": str(e)[:200]}
 
@@ -508,6 +654,13 @@ def run_stateless(args, dev, world, rank, dist):
         tc0 = time.perf_counter()
         eng.commit(rules, default_action=1)
         commit_ms.append((time.perf_counter() - tc0) * 1e3)
+
+    lookup = None
+    if rank == 0:
+        try:
+            lookup = acl_lookup_latency(eng, res.host[0], rules)
+        except Exception as e:
+            lookup = {"error": str(e)[:200]}
 
     # host-inclusive rate (pinned host buffers: the kernel reads / writes them across PCIe), rank 0 at N = 1
     host_mpps = None
@@ -534,36 +687,17 @@ def run_stateless(args, dev, world, rank, dist):
     # this host's cores (nproc) as pinned run-to-completion shards, then one pinned thread
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import pyoracle
-        pk = res.host[0]
-        m = len(pk["len"])
-        o = pyoracle.Oracle(rules, default_action=1, image=eng.image())
-        cores = host_cores()
-        ocfg = o.cfg(now_seconds=NOW)
-        o.pin(cores)
-        o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=len(cores), use_tree=True)
-        reps, tc = 0, time.perf_counter()
-        while time.perf_counter() - tc < args.cpu_seconds:
-            o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=len(cores), use_tree=True)
-            reps += 1
-        cpu_s = time.perf_counter() - tc
-        o.pin(cores[:1])
-        ones, t1 = 0, time.perf_counter()
-        while time.perf_counter() - t1 < args.cpu_seconds / 4:
-            o.classify_batch(pk["hdr"], pk["len"], cfg=ocfg, nthreads=1, use_tree=True)
-            ones += 1
-        one_s = (time.perf_counter() - t1) / ones
-        o.pin([])
-        cpu = {"value": m * reps / cpu_s / 1e6, "unit": "Mpps", "cores": len(cores), "kind": "port",
-               "sample": f"{reps} passes over a {m}-packet {args.config} batch ({m * reps} packets, {cpu_s:.1f} s), "
-                         f"{len(cores)} pinned pthreads (nproc of this host) as run-to-completion shards "
-                         f"(mainloop, main.c:422-425); 1 pinned thread: {m / one_s / 1e6:.2f} Mpps ({ones} passes)",
-               "single_thread_mpps": m / one_s / 1e6}
+        cpu = cpu_baseline(res.host[0], rules, eng.image(), args.cpu_seconds, args.config)
 
     eng.close()
     del res
     torch.cuda.empty_cache()
     extra = {}
+    if rank == 0 and world == 1 and args.n == 0 and not args.no_c0:
+        try:
+            extra["C0"] = measure_c0(args, dev)
+        except Exception as e:
+            extra["C0"] = {"error": str(e)[:300]}
     names = [c for c in args.configs.split(",") if c and c != args.config] if args.n == 0 else []
     for name in names:
         try:
@@ -600,7 +734,7 @@ def run_stateless(args, dev, world, rank, dist):
             "host_inclusive_mpps": round(host_mpps, 2) if host_mpps else None,
             "parity_sample_ok": line_cfg["parity_sample_ok"],
             "ranks_reported": dist.get_world_size() if dist is not None else 1,
-            "acl": {**line_cfg["acl"], "commit_ms": round(float(np.median(commit_ms)), 3)},
+            "acl": {**line_cfg["acl"], "commit_ms": round(float(np.median(commit_ms)), 3), **(lookup or {})},
             "launch": line_cfg["launch"],
             "configs": extra,
         }

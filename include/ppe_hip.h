@@ -35,8 +35,9 @@ extern "C" {
 #endif
 
 /* 2: ppe_tuning_t grew to 20 B (batches_per_launch) and mbuf_t (ppe_decode.h) took the reference's field layout;
- * 3: ppe_tuple's word 3 carries the TCP window-scale option offset (bits 9-15) */
-#define PPE_ABI_VERSION 4
+ * 3: ppe_tuple's word 3 carries the TCP window-scale option offset (bits 9-15); 4: ppe_result_t.part8;
+ * 5: the tuple carries a fragment's Defrag fields and the option-past-the-window bit; strides 64..256 */
+#define PPE_ABI_VERSION 5
 
 /* error codes (negative return values) */
 #define PPE_OK       0
@@ -89,6 +90,12 @@ enum ppe_action { PPE_ACT_FW = 0, PPE_ACT_DROP = 1, PPE_ACT_PUNT = 2 };
 #define PPE_PART8_OFFSET(e) ((e) & 63u)          /* compact entry (part8) → packet index - 64 × tile      */
 #define PPE_PART8_ACTION(e) ((e) >> 6)           /* compact entry (part8) → enum ppe_action               */
 
+/* tuple word 3: the window-scale option DecodeTCPOptions records (decode-tcp.c:61-70), as its byte offset from the
+ * TCP header (0 = none); OPT_PAST: none was found before the option parse needed a byte past the header window
+ * (stride), so the answer needs a wider window (the reference reads the whole option space) */
+#define PPE_TUPLE_WS(w3)      (((w3) >> 9) & 63u)
+#define PPE_TUPLE_OPT_PAST    (1u << 15)
+
 #define PPE_VERDICT_STATUS(v) ((v) & 0xffu)
 #define PPE_VERDICT_ACTION(v) (((v) >> 8) & 0xffu)
 #define PPE_VERDICT_FLAGS(v)  ((v) >> 16)
@@ -119,7 +126,10 @@ typedef struct {
     const uint32_t *len;       /* n × wire length (mbuf->pkt_totallen; truncated to 16 bits like Decode())      */
     const uint64_t *ts;        /* optional n × seconds since 1970 (mbuf->timestamp); NULL → cfg->now_seconds    */
     uint32_t        n;
-    uint32_t        stride;    /* 64 or 128                                                                     */
+    uint32_t        stride;    /* a multiple of 16 from 64 to 256: 64 holds every header of a 64-B packet without
+                                  VLAN / IPv4 / TCP options; 144 every byte the reference's decoders read
+                                  (Ethernet 14 + VLAN 4 + IPv4 60 + TCP 60), so no WINDOW_PUNT and no
+                                  PPE_TUPLE_OPT_PAST can occur                                                   */
 } ppe_batch_t;
 
 /* ---- batch output (SoA; any pointer may be NULL to skip that output) ---- */
@@ -134,7 +144,12 @@ typedef struct {
                                   front, DROP ascending at the back, PUNT ascending in between; each entry is
                                   index | action << 30 (PPE_PART_*), so no tile_cnt is needed to split them     */
     uint32_t *tile_cnt;        /* ceil(n/64) × (nfw | ndrop << 8 | npunt << 16)                                */
-    uint32_t *tuple;           /* optional n × 4 words: sip, dip, sport|dport<<16, proto|vlan<<8|payload_len<<16 */
+    uint32_t *tuple;           /* optional n × 4 words, what the reference's decoders record in the mbuf:
+                                  [0] sip [1] dip (0 unless the IPv4 checks passed, decode-ipv4.c:62-63)
+                                  [2] sport | dport << 16 (PPE_F_L4), or for a fragment (status FRAG /
+                                      FRAG_LEN_ERR) defrag_id | frag_offset << 16 (decode-ipv4.c:107-108)
+                                  [3] proto | vlan << 8 | PPE_TUPLE_WS | PPE_TUPLE_OPT_PAST | payload_len << 16
+                                      (a fragment: frag_len << 16, decode-ipv4.c:109)                            */
     uint8_t  *part8;           /* optional n bytes: the PARTITION layout in compact form (with fw_idx, drop_idx
                                   and tile_cnt NULL): slot [64t + i] of tile t holds the i-th entry of the
                                   partition order above as (packet index - 64t) | action << 6 (PPE_PART8_*);

@@ -399,6 +399,7 @@ static void flow_handle_packet(omb_t *m) {
             f->byted2s += m->totallen;
         }
     }
+    r->mset |= ORACLE_M_FLOW;    /* PKT_TO_SERVER / PKT_TO_CLIENT, PKT_HAS_FLOW: flow.c:294-307 */
     cnt(m, PPE_C_FLOW_PROC_OK);  /* flow.c:309 */
     out_fw(m);                   /* SELF_TEST, flow.c:376-377 */
 }
@@ -459,6 +460,8 @@ static int decode_udp(omb_t *m, const uint8_t *pkt, uint16_t len) {
         set_status(m, PPE_ST_UDP_HEADER_ERR);
         return DEC_DROP;
     }
+    m->r->mset |= ORACLE_M_L4H;  /* transport_header, decode-udp.c:24 */
+    m->r->l4off = (uint32_t)(pkt - m->frame);
     const uint32_t uh_len = rd16(m, pkt + 4);
     if (len < uh_len || len != uh_len) {
         cnt(m, PPE_C_UDP_PKTLEN_ERR);
@@ -468,24 +471,35 @@ static int decode_udp(omb_t *m, const uint8_t *pkt, uint16_t len) {
     m->r->sport = rd16(m, pkt);
     m->r->dport = rd16(m, pkt + 2);
     m->r->paylen = (uint16_t)(len - 8);
+    m->r->mset |= ORACLE_M_L4;   /* sport, dport, payload, payload_len: decode-udp.c:38-45 */
+    m->r->payoff = m->r->l4off + 8u;
     cnt(m, PPE_C_UDP_RX_OK);
     flow_handle_packet(m);
     return DEC_OK;
 }
 
 /* dataplane/src/decode/decode-tcp.c:18-131 — only the window-scale option is recorded (:61-70: the first valid one,
- * a duplicate is ignored), as its byte offset from the TCP header `th`; no verdict effect */
+ * a duplicate is ignored), as its byte offset from the TCP header `th`; no verdict effect.  The reference reads the
+ * whole option space (it lies inside the packet: hlen <= len, :149); here the frame holds `avail` bytes, so a parse
+ * that needs a byte past them before it has found the option records opt_past (what the kernel reports as
+ * PPE_TUPLE_OPT_PAST for a narrower header window).  The first valid option is final, so the parse stops there. */
 static void decode_tcp_options(omb_t *m, const uint8_t *th, const uint8_t *pkt, uint16_t len) {
     uint16_t plen = len;
     while (plen) {
         const uint32_t off = (uint32_t)(pkt - m->frame);
-        const uint8_t t = off < m->avail ? pkt[0] : 0;
+        if (off >= m->avail) { m->r->opt_past = 1; return; }
+        const uint8_t t = pkt[0];
         if (t == 0) break;          /* EOL */
         if (t == 1) { pkt++; plen--; continue; }  /* NOP */
         if (plen < 2) break;
-        const uint8_t ol = off + 1 < m->avail ? pkt[1] : 0;
-        if (ol > plen || ol < 2) return;
-        if (t == 3 && ol == 3 && !m->r->tcp_ws) m->r->tcp_ws = (uint32_t)(pkt - th);
+        if (off + 1 >= m->avail) { m->r->opt_past = 1; return; }
+        const uint8_t ol = pkt[1];
+        if (ol > plen || ol < 2) return;  /* invalid length: return -1 (:43-46) */
+        if (t == 3 && ol == 3) {    /* m->tcpvars.ws = &m->TCP_OPTS[0] (:63-70) */
+            m->r->tcp_ws = (uint32_t)(pkt - th);
+            m->r->mset |= ORACLE_M_WS;
+            return;
+        }
         pkt += ol;
         plen = (uint16_t)(plen - ol);
     }
@@ -498,6 +512,8 @@ static int decode_tcp(omb_t *m, const uint8_t *pkt, uint16_t len) {
         set_status(m, PPE_ST_TCP_HEADER_ERR);
         return DEC_DROP;
     }
+    m->r->mset |= ORACLE_M_L4H;  /* transport_header, decode-tcp.c:146 */
+    m->r->l4off = (uint32_t)(pkt - m->frame);
     const uint8_t hlen = (uint8_t)((rd8(m, pkt + 12) >> 4) << 2);
     if (len < hlen) {
         cnt(m, PPE_C_TCP_PKTLEN_ERR);
@@ -516,6 +532,8 @@ static int decode_tcp(omb_t *m, const uint8_t *pkt, uint16_t len) {
     m->r->sport = rd16(m, pkt);
     m->r->dport = rd16(m, pkt + 2);
     m->r->paylen = (uint16_t)(len - hlen);
+    m->r->mset |= ORACLE_M_L4;   /* sport, dport, payload, payload_len: decode-tcp.c:179-187 */
+    m->r->payoff = m->r->l4off + hlen;
     cnt(m, PPE_C_TCP_RX_OK);
     flow_handle_packet(m);
     return DEC_OK;
@@ -535,6 +553,8 @@ static int decode_ipv4(omb_t *m, const uint8_t *pkt, uint16_t len) {
         set_status(m, PPE_ST_IPV4_VERSION_ERR);
         return DEC_DROP;
     }
+    r->mset |= ORACLE_M_L3;       /* network_header, decode-ipv4.c:42 */
+    r->l3off = (uint32_t)(pkt - m->frame);
     const uint32_t hl = (verhl & 0x0f) << 2;
     if (hl < 20) {
         cnt(m, PPE_C_IPV4_HEADERLEN_ERR);
@@ -550,10 +570,15 @@ static int decode_ipv4(omb_t *m, const uint8_t *pkt, uint16_t len) {
     r->sip = rd32(m, pkt + 12);
     r->dip = rd32(m, pkt + 16);
     r->proto = rd8(m, pkt + 9);
+    r->mset |= ORACLE_M_IP;       /* ipv4.sip / dip, proto: decode-ipv4.c:62-63, 97 */
     const uint32_t ip_off = rd16(m, pkt + 6);
     if (((ip_off & 0x1fff) > 0 || ((ip_off & 0x2000) >> 13) == 1) && r->proto != 89) {
         r->flags |= PPE_F_FRAG;
         const uint16_t frag_len = (uint16_t)(len - hl);
+        r->mset |= ORACLE_M_FRAG;  /* decode-ipv4.c:106-109 */
+        r->frag_id = rd16(m, pkt + 4);
+        r->frag_off = (uint16_t)((ip_off & 0x1fff) << 3);
+        r->frag_len = frag_len;
         if (frag_len == 0) {
             cnt(m, PPE_C_FRAG_FRAGLEN_ERR);
             set_status(m, PPE_ST_FRAG_LEN_ERR);
@@ -601,6 +626,7 @@ static int decode_vlan(omb_t *m, const uint8_t *pkt, uint16_t len) {
     const uint32_t proto = rd16(m, pkt + 2);
     m->vlan_idx = 1;
     m->r->flags |= PPE_F_VLAN;
+    m->r->mset |= ORACLE_M_VLAN;  /* vlanh, vlan_idx: decode-vlan.c:41, 46 */
     switch (proto) {
         case 0x0800:
             cnt(m, PPE_C_VLAN_RX_OK);
@@ -636,6 +662,7 @@ static int decode_ethernet(omb_t *m, const uint8_t *pkt, uint16_t len) {
         set_status(m, PPE_ST_L2_HEADER_ERR);
         return DEC_DROP;
     }
+    m->r->mset |= ORACLE_M_ETH;   /* ethh, eth_dst, eth_src: decode-ethernet.c:57, 71-72 */
     switch (rd16(m, pkt + 12)) {
         case 0x0800:
             cnt(m, PPE_C_L2_RX_OK);
@@ -710,9 +737,11 @@ static void *run_shard(void *arg) {
         if (s->tuple) {
             s->tuple[4 * (size_t)i + 0] = r.sip;
             s->tuple[4 * (size_t)i + 1] = r.dip;
-            s->tuple[4 * (size_t)i + 2] = r.sport | (r.dport << 16);
+            /* ppe_hip.h ppe_result_t.tuple (ABI 5): a fragment's word 2 / length field carry its Defrag fields */
+            const int fr = (r.mset & ORACLE_M_FRAG) != 0;
+            s->tuple[4 * (size_t)i + 2] = fr ? (r.frag_id | (r.frag_off << 16)) : (r.sport | (r.dport << 16));
             s->tuple[4 * (size_t)i + 3] = r.proto | (((r.flags & PPE_F_VLAN) ? 1u : 0u) << 8) | (r.tcp_ws << 9) |
-                                          (r.paylen << 16);
+                                          (r.opt_past ? PPE_TUPLE_OPT_PAST : 0u) | ((fr ? r.frag_len : r.paylen) << 16);
         }
         for (int c = 0; c < 32; c++)
             if (r.counters & (1u << c)) s->counters[c]++;

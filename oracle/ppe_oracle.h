@@ -41,7 +41,25 @@ typedef struct {
     uint32_t reach;      /* 1 + highest frame byte offset the verdict depends on */
     uint32_t tcp_ws;     /* byte offset (from the TCP header) of the window-scale option DecodeTCPOptions recorded
                             (m->tcpvars.ws, decode-tcp.c:61-70), 0 = none; no verdict effect */
+    /* the mbuf fields the reference's decoders write (dataplane/src/include/mbuf.h:23-87), for Decode()'s parity */
+    uint32_t mset;       /* ORACLE_M_* bits: which of them this packet's decode wrote */
+    uint32_t l3off, l4off, payoff;  /* frame offsets of network_header, transport_header, payload */
+    uint32_t frag_id, frag_off, frag_len;  /* defrag_id, frag_offset, frag_len (decode-ipv4.c:107-109) */
+    uint32_t opt_past;   /* 1: no window-scale option was found before the option parse needed a byte past the
+                            available window (the reference reads the whole option space; ppe_hip.h
+                            PPE_TUPLE_OPT_PAST) */
 } oracle_result_t;
+
+/* oracle_result_t.mset: mbuf fields written, with the reference line that writes them */
+#define ORACLE_M_ETH   0x001u  /* ethh, eth_dst, eth_src            decode-ethernet.c:57,71-72 */
+#define ORACLE_M_VLAN  0x002u  /* vlanh, vlan_idx = 1               decode-vlan.c:41,46 */
+#define ORACLE_M_L3    0x004u  /* network_header                    decode-ipv4.c:42 */
+#define ORACLE_M_IP    0x008u  /* ipv4.sip, ipv4.dip, proto         decode-ipv4.c:62-63,97 */
+#define ORACLE_M_FRAG  0x010u  /* defrag_id, frag_offset, frag_len  decode-ipv4.c:107-109 */
+#define ORACLE_M_L4H   0x020u  /* transport_header                  decode-udp.c:24, decode-tcp.c:146 */
+#define ORACLE_M_L4    0x040u  /* sport, dport, payload, payload_len decode-udp.c:38-45, decode-tcp.c:179-187 */
+#define ORACLE_M_WS    0x080u  /* tcpvars.ws = &TCP_OPTS[0]         decode-tcp.c:63-70 */
+#define ORACLE_M_FLOW  0x100u  /* flags |= PKT_TO_SERVER|CLIENT, PKT_HAS_FLOW (flow.c:294-307: the flow exists) */
 
 /* rule set used by oracle_classify (pointer kept; caller owns the memory) */
 void oracle_set_rules(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,

@@ -21,7 +21,13 @@ class OResult(C.Structure):
     _fields_ = [("status", C.c_uint32), ("action", C.c_uint32), ("flags", C.c_uint32), ("flow_hash", C.c_uint32),
                 ("acl_hit", C.c_int32), ("sip", C.c_uint32), ("dip", C.c_uint32), ("sport", C.c_uint32),
                 ("dport", C.c_uint32), ("proto", C.c_uint32), ("paylen", C.c_uint32), ("counters", C.c_uint32),
-                ("reach", C.c_uint32), ("tcp_ws", C.c_uint32)]
+                ("reach", C.c_uint32), ("tcp_ws", C.c_uint32), ("mset", C.c_uint32), ("l3off", C.c_uint32),
+                ("l4off", C.c_uint32), ("payoff", C.c_uint32), ("frag_id", C.c_uint32), ("frag_off", C.c_uint32),
+                ("frag_len", C.c_uint32), ("opt_past", C.c_uint32)]
+
+
+# OResult.mset: the mbuf fields the reference's decoders wrote (oracle/ppe_oracle.h ORACLE_M_*)
+M_ETH, M_VLAN, M_L3, M_IP, M_FRAG, M_L4H, M_L4, M_WS, M_FLOW = (1 << i for i in range(9))
 
 
 _lib = None

@@ -467,8 +467,9 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     for (uint32_t sl = 0; sl < n_slots; ++sl) holes |= R[sl].id != sl;
     const uint32_t off_crec = compact ? off_blocks + (uint32_t)bwords.size() : 0u;
     const uint32_t off_idtab = compact && holes ? off_crec + PPE_CREC_WORDS * (n_slots + 1u) : 0u;
+    // (the index table has an entry for the sentinel slot too: crec_check reads idtab[slot] for every leaf)
     const uint32_t total = !compact ? off_blocks + (uint32_t)bwords.size()
-                           : off_idtab ? off_idtab + ((n_slots + 3u) & ~3u)
+                           : off_idtab ? off_idtab + ((n_slots + 1u + 3u) & ~3u)
                                        : off_crec + PPE_CREC_WORDS * (n_slots + 1u);
 
     uint32_t *img = (uint32_t *)std::calloc(total, sizeof(uint32_t));
@@ -513,8 +514,10 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
             o[2] = r.lo[PPE_DIM_SPORT] | (r.lo[PPE_DIM_DPORT] << 16);
             o[3] = (r.hi[PPE_DIM_SPORT] - r.lo[PPE_DIM_SPORT]) | ((r.hi[PPE_DIM_DPORT] - r.lo[PPE_DIM_DPORT]) << 16);
         }
-        if (off_idtab)
+        if (off_idtab) {
             for (uint32_t sl = 0; sl < n_slots; ++sl) img[off_idtab + sl] = R[sl].id;
+            img[off_idtab + n_slots] = 0xffffffffu;  // the sentinel (its hit is -1 by its NOHIT flag)
+        }
     }
     auto node_byte = [&](uint32_t k) { return 4u * off_nodes + 16u * k; };
     for (uint32_t k = 0; k < n_nodes; ++k) {

@@ -168,10 +168,16 @@ static void mbuf_tuple(const mbuf_t *m, uint32_t *tw, uint32_t *mw) {
 int DP_Acl_Lookup_Burst(mbuf_t **m, uint32_t n, int *actions) {
     if (!m) return PPE_EINVAL;
     if (n == 0) return PPE_OK;
-    uint32_t *tw = (uint32_t *)malloc((size_t)n * 16), *mw = (uint32_t *)malloc((size_t)n * 16);
-    uint64_t *ts = (uint64_t *)malloc((size_t)n * 8);
-    int32_t *hit = (int32_t *)malloc((size_t)n * 4);
-    uint32_t *act = (uint32_t *)malloc((size_t)n * 4);
+    /* a short burst (DP_Acl_Lookup's one flow miss, flow.c:232) stays on the stack: no allocation per call */
+    enum { kStack = 64 };
+    uint32_t s_tw[4 * kStack], s_mw[4 * kStack], s_act[kStack];
+    uint64_t s_ts[kStack];
+    int32_t s_hit[kStack];
+    const int heap = n > kStack;
+    uint32_t *tw = heap ? (uint32_t *)malloc((size_t)n * 16) : s_tw, *mw = heap ? (uint32_t *)malloc((size_t)n * 16) : s_mw;
+    uint64_t *ts = heap ? (uint64_t *)malloc((size_t)n * 8) : s_ts;
+    int32_t *hit = heap ? (int32_t *)malloc((size_t)n * 4) : s_hit;
+    uint32_t *act = heap ? (uint32_t *)malloc((size_t)n * 4) : s_act;
     int rc = PPE_ENOMEM;
     if (tw && mw && ts && hit && act) {
         for (uint32_t i = 0; i < n; i++) {
@@ -188,11 +194,13 @@ int DP_Acl_Lookup_Burst(mbuf_t **m, uint32_t n, int *actions) {
                 if (actions) actions[i] = act[i] == ACL_RULE_ACTION_DROP ? ACL_RULE_ACTION_DROP : ACL_RULE_ACTION_FW;
             }
     }
-    free(tw);
-    free(mw);
-    free(ts);
-    free(hit);
-    free(act);
+    if (heap) {
+        free(tw);
+        free(mw);
+        free(ts);
+        free(hit);
+        free(act);
+    }
     return rc;
 }
 
@@ -205,8 +213,9 @@ int DP_Acl_Lookup(mbuf_t *m) {
 /* ---- Decode burst ----
  * One burst per thread (the reference decodes on the core that received the packet, main.c:301).  The GPU step of a
  * flush is serialised per process (one engine context, thread-compatible); the output hooks run after it with no
- * lock held. */
-#define PPE_COMPAT_STRIDE 128u
+ * lock held.  The header window holds every byte the reference's decoders read (Ethernet 14 + VLAN 4 + IPv4 60 +
+ * TCP 60 = 138 B): no packet PUNTs for its window and every TCP option is parsed (ppe_hip.h ppe_batch_t.stride). */
+#define PPE_COMPAT_STRIDE 144u
 typedef struct {
     mbuf_t **m;
     uint32_t n, alloc;
@@ -272,6 +281,72 @@ static int logged_drop(uint32_t st) {
     }
 }
 
+/* The mbuf fields the reference's decoders write, exactly on the packets where they write them, from the kernel's
+ * outputs for the packet (verdict, tuple) and its length.  Which layer wrote what follows from the terminal status:
+ * the decoders run in order and each writes its fields once its own checks have passed.  Header pointers are the
+ * packet's own addresses at the offsets the decoders use (IPV4_GET_HLEN / TCP_GET_HLEN read the same header bytes
+ * the reference reads); no field is derived by re-decoding the packet here.  The stateless path has no flow object:
+ * m->flow stays as it was (FlowHandlePacket sets it to the flow item, flow.c:306). */
+static void fill_mbuf(mbuf_t *m, uint32_t v, uint32_t fhash, int32_t hit, const uint32_t *tu) {
+    const uint32_t st = PPE_VERDICT_STATUS(v), fl = PPE_VERDICT_FLAGS(v);
+    uint8_t *pkt = (uint8_t *)m->pkt_ptr;
+    m->ppe_verdict = v;
+    m->ppe_flow_hash = fhash;
+    m->ppe_acl_hit = hit;
+    if (!pkt || st == PPE_ST_L2_HEADER_ERR) return;  /* DecodeEthernet failed before writing anything */
+    /* DecodeEthernet: decode-ethernet.c:57, 71-72 */
+    m->ethh = pkt;
+    memcpy(m->eth_dst, pkt, 6);
+    memcpy(m->eth_src, pkt + 6, 6);
+    if (fl & PPE_F_VLAN) {  /* DecodeVLAN passed its checks: decode-vlan.c:41, 46 */
+        m->vlanh = pkt + 14;
+        m->vlan_idx = 1;
+    }
+    if (st == PPE_ST_L2_UNSUPPORT || st == PPE_ST_VLAN_HEADER_ERR || st == PPE_ST_VLAN_LAYER_EXCEED ||
+        st == PPE_ST_VLAN_UNSUPPORT)
+        return;  /* never reached DecodeIPV4 */
+    /* DecodeIPV4Packet: network_header once len >= 20 and the version is 4 (decode-ipv4.c:30-42): an
+     * IPV4_HEADER_ERR is either check order's first failure (len < 20) or the header length (after :42) */
+    const uint32_t l3off = 14u + ((fl & PPE_F_VLAN) ? 4u : 0u);
+    const uint32_t l3len = ((m->pkt_totallen & 0xffffu) - l3off) & 0xffffu;
+    if (st == PPE_ST_IPV4_VERSION_ERR || (st == PPE_ST_IPV4_HEADER_ERR && l3len < 20u)) return;
+    uint8_t *l3 = pkt + l3off;
+    m->network_header = l3;
+    if (st == PPE_ST_IPV4_HEADER_ERR || st == PPE_ST_IPV4_LEN_ERR) return;
+    /* every IPv4 check passed: decode-ipv4.c:62-63, 97 */
+    m->ipv4.sip = tu[0];
+    m->ipv4.dip = tu[1];
+    m->proto = (uint8_t)tu[3];
+    if (st == PPE_ST_FRAG || st == PPE_ST_FRAG_LEN_ERR) {  /* decode-ipv4.c:106-109 (Defrag reads them) */
+        m->defrag_id = (uint16_t)tu[2];
+        m->frag_offset = (uint16_t)(tu[2] >> 16);
+        m->frag_len = (uint16_t)(tu[3] >> 16);
+        return;
+    }
+    const int tcp = m->proto == 6u;
+    if (st == PPE_ST_IPV4_UNSUPPORT || st == PPE_ST_UDP_HEADER_ERR || st == PPE_ST_TCP_HEADER_ERR) return;
+    /* the L4 decoder's first length check passed: decode-udp.c:24, decode-tcp.c:146 */
+    uint8_t *l4 = l3 + (l3[0] & 0x0fu) * 4u;
+    m->transport_header = l4;
+    if (!(fl & PPE_F_L4)) return;  /* UDP_LEN_ERR / TCP_LEN_ERR */
+    /* decode-udp.c:38-45, decode-tcp.c:175-187 */
+    m->sport = (uint16_t)tu[2];
+    m->dport = (uint16_t)(tu[2] >> 16);
+    m->payload_len = (uint16_t)(tu[3] >> 16);
+    m->payload = l4 + (tcp ? (uint32_t)(l4[12] >> 4) * 4u : 8u);
+    const uint32_t ws = PPE_TUPLE_WS(tu[3]);
+    if (tcp && ws) {  /* DecodeTCPOptions' window-scale record (decode-tcp.c:61-70), found by the kernel */
+        uint8_t *o = l4 + ws;
+        m->tcpvars.tcp_opts[0].type = o[0];
+        m->tcpvars.tcp_opts[0].len = o[1];
+        m->tcpvars.tcp_opts[0].data = o + 2;
+        m->tcpvars.ws = &m->tcpvars.tcp_opts[0];
+    }
+    /* FlowHandlePacket found or created the flow (ACL passed): flow.c:294-307.  Every packet of the stateless path
+     * is its flow's first, and FlowAdd orients the flow as that packet, so the direction is to-server. */
+    if (st == PPE_ST_ACL_FW) m->flags |= PKT_TO_SERVER | PKT_HAS_FLOW;
+}
+
 /* Classify `n` mbufs on the GPU (serialised) and fill their parse fields; returns PPE_OK or a PPE_E* code. */
 static int classify_mbufs(mbuf_t **mb, uint32_t n) {
     uint8_t *hdr = (uint8_t *)burst_alloc((size_t)n * PPE_COMPAT_STRIDE, 16);
@@ -300,48 +375,8 @@ static int classify_mbufs(mbuf_t **mb, uint32_t n) {
         pthread_mutex_lock(&g_ctx_lock);
         rc = g_ctx ? ppe_classify_host(g_ctx, &b, &r, &cfg, 0) : PPE_ENODEV;
         pthread_mutex_unlock(&g_ctx_lock);
-        if (rc == PPE_OK) {
-            for (uint32_t i = 0; i < n; i++) {
-                mbuf_t *m = mb[i];
-                const uint32_t v = verdict[i], fl = PPE_VERDICT_FLAGS(v);
-                uint8_t *pkt = (uint8_t *)m->pkt_ptr;
-                m->ppe_verdict = v;
-                m->ppe_flow_hash = fh[i];
-                m->ppe_acl_hit = hit[i];
-                m->vlan_idx = (fl & PPE_F_VLAN) ? 1 : 0;
-                if (pkt && m->pkt_totallen >= 14) {
-                    memcpy(m->eth_dst, pkt, 6);
-                    memcpy(m->eth_src, pkt + 6, 6);
-                    m->ethh = pkt;
-                    if (m->vlan_idx) m->vlanh = pkt + 14;
-                }
-                m->ipv4.sip = tuple[4 * i];
-                m->ipv4.dip = tuple[4 * i + 1];
-                m->proto = (uint8_t)tuple[4 * i + 3];
-                if (fl & PPE_F_L4) {
-                    m->sport = (uint16_t)tuple[4 * i + 2];
-                    m->dport = (uint16_t)(tuple[4 * i + 2] >> 16);
-                    m->payload_len = (uint16_t)(tuple[4 * i + 3] >> 16);
-                    m->flags |= PKT_HAS_FLOW;
-                    if (pkt) {  /* the header pointers DecodeIPV4 / DecodeTCP|UDP set (decode-ipv4.c:42, :131-157) */
-                        uint8_t *l3 = pkt + 14 + (m->vlan_idx ? 4 : 0);
-                        m->network_header = l3;
-                        m->transport_header = l3 + (l3[0] & 0x0fu) * 4u;
-                        /* DecodeTCPOptions' window-scale record (decode-tcp.c:61-70), found by the kernel: its offset
-                         * from the TCP header in bits 9-15 of the tuple */
-                        const uint32_t ws = (tuple[4 * i + 3] >> 9) & 0x7fu;
-                        if ((fl & PPE_F_TCP) && ws) {
-                            uint8_t *o = (uint8_t *)m->transport_header + ws;
-                            m->tcpvars.tcp_opts[0].type = o[0];
-                            m->tcpvars.tcp_opts[0].len = o[1];
-                            m->tcpvars.tcp_opts[0].data = o + 2;
-                            m->tcpvars.ws = &m->tcpvars.tcp_opts[0];
-                        }
-                    }
-                }
-                if (fl & PPE_F_FRAG) m->flags |= PKT_IP_FRAG;
-            }
-        }
+        if (rc == PPE_OK)
+            for (uint32_t i = 0; i < n; i++) fill_mbuf(mb[i], verdict[i], fh[i], hit[i], tuple + 4 * (size_t)i);
     }
     free(hdr);
     free(len);

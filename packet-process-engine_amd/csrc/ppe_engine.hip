@@ -50,6 +50,17 @@ struct HostStage {
     uint32_t cap = 0, stride = 0;
 };
 
+// Per-context staging of the host-pointer ACL lookup (DP_Acl_Lookup, one call per flow miss on the reference's hot
+// path, flow.c:232): pinned, device-mapped host memory the lookup kernel reads its tuples from and writes its results
+// to across PCIe (no hipMalloc, no copies, no device-wide synchronisation per call), its own stream and a spin wait
+// on that stream only.
+struct LookupStage {
+    hipStream_t s = nullptr;
+    uint8_t *h = nullptr;   // host view: tuples (16 B) | macs (16 B) | ts (8 B) | hit (4 B) | action (4 B), per entry
+    uint8_t *d = nullptr;   // the same memory as the device sees it
+    uint32_t cap = 0;       // entries
+};
+
 // Device flow table (ppe_classify_flow) and what the host knows about it without synchronising.
 struct FlowArrays {
     uint32_t *keys = nullptr, *creator = nullptr;
@@ -128,6 +139,7 @@ struct ppe_ctx {
     // / 8 / 32 groups 20.2 / 18.7 / 18.3 / 18.3 / 19.1 us (one run, tools/ab_bench.py)
     uint32_t max_groups = 8;
     FlowTable *flow = nullptr;  // ppe_flow_create
+    LookupStage lk;             // ppe_acl_lookup_host
     uint32_t *d_steer = nullptr;  // ppe_steer_partition: per-tile owner counts / offsets
     size_t steer_cap = 0;
     unsigned long long *trace = nullptr;  // ppe_debug_trace
@@ -331,19 +343,35 @@ uint32_t blocks_per_cu(ppe_ctx *c, const StagePlan &p) {
     return r;
 }
 
-// a launch on stream s reads image slot r: an event (one per slot and stream) is recorded behind it, so a rewrite
-// of the slot waits for exactly the launches that read it (the event outlives the stream if the caller frees it)
-int note_image_reader(ppe_ctx *c, int r, hipStream_t s) {
+// A launch on stream s reads slot r of an image or descriptor ring: an event (one per slot and stream) is recorded
+// behind it, so a rewrite of the slot waits for exactly the launches that read it (the event outlives the stream if
+// the caller frees it).  Events of other streams whose launches have completed are dropped once the list grows, so a
+// caller that uses a new stream per call does not make the list (and every later rewrite's wait) grow without bound.
+int note_reader(ppe_ctx *c, std::vector<std::pair<hipStream_t, hipEvent_t>> &readers, hipStream_t s) {
+    constexpr size_t kPruneAt = 8;
+    if (readers.size() >= kPruneAt) {
+        size_t k = 0;
+        for (size_t i = 0; i < readers.size(); ++i) {
+            auto &x = readers[i];
+            if (x.first != s && hipEventQuery(x.second) == hipSuccess) {
+                (void)hipEventDestroy(x.second);
+                continue;
+            }
+            readers[k++] = x;
+        }
+        readers.resize(k);
+    }
     hipEvent_t ev = nullptr;
-    for (auto &x : c->img_readers[r])
+    for (auto &x : readers)
         if (x.first == s) ev = x.second;
     if (!ev) {
         HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        c->img_readers[r].emplace_back(s, ev);
+        readers.emplace_back(s, ev);
     }
     HIPCHK(c, hipEventRecord(ev, s));
     return PPE_OK;
 }
+int note_image_reader(ppe_ctx *c, int r, hipStream_t s) { return note_reader(c, c->img_readers[r], s); }
 
 int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const ppe_acl_stats_t *st) {
     // The back image may still be read by launches queued before the previous swap.  Wait for exactly those (the
@@ -448,7 +476,11 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         if (rslot < 0) {
             rslot = c->ring_next;
             c->ring_next ^= 1;
-            for (auto &x : c->ring_readers[rslot]) HIPCHK(c, hipEventSynchronize(x.second));  // its last readers
+            for (auto &x : c->ring_readers[rslot]) {  // its last readers (then their events are done with)
+                HIPCHK(c, hipEventSynchronize(x.second));
+                HIPCHK(c, hipEventDestroy(x.second));
+            }
+            c->ring_readers[rslot].clear();
             std::memcpy(c->h_ring[rslot], rd.data(), bytes);
             c->ring_n[rslot] = nb;
             HIPCHK(c, hipMemcpyAsync(c->d_ring[rslot], c->h_ring[rslot], bytes, hipMemcpyHostToDevice, s));
@@ -549,14 +581,8 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
                             (void *)e1);
     if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
     if (use_ring) {  // every launch that reads the slot: a later rewrite waits for the last of them on each stream
-        hipEvent_t ev = nullptr;
-        for (auto &x : c->ring_readers[rslot])
-            if (x.first == s) ev = x.second;
-        if (!ev) {
-            HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            c->ring_readers[rslot].emplace_back(s, ev);
-        }
-        HIPCHK(c, hipEventRecord(ev, s));
+        const int rc2 = note_reader(c, c->ring_readers[rslot], s);
+        if (rc2 != PPE_OK) return rc2;
     }
     return note_image_reader(c, r, s);
 }
@@ -571,7 +597,8 @@ int check_batch(ppe_ctx *c, const ppe_batch_t *in, const ppe_cfg_t *cfg) {
     if (!in) return fail(c, PPE_EINVAL, "null batch");
     if (in->n == 0) return PPE_OK;
     if (!in->hdr || !in->len) return fail(c, PPE_EINVAL, "hdr/len required");
-    if (in->stride != 64 && in->stride != 128) return fail(c, PPE_EINVAL, "stride must be 64 or 128");
+    if (in->stride < 64 || in->stride > 256 || in->stride % 16u)
+        return fail(c, PPE_EINVAL, "stride must be a multiple of 16 from 64 to 256");
     // byte offsets inside the kernel are 32-bit, and partition-list entries keep the action in bits 31:30
     if ((uint64_t)in->n * in->stride >= (1ull << 31)) return fail(c, PPE_EINVAL, "batch too large (n * stride >= 2^31)");
     if (((uintptr_t)in->hdr & 15u) != 0) return fail(c, PPE_EINVAL, "hdr must be 16-byte aligned");
@@ -657,6 +684,8 @@ int ppe_ctx_destroy(ppe_ctx_t *c) {
     for (hipEvent_t e : c->pipe_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->flow) ppe_flow_destroy(c);
+    if (c->lk.s) (void)hipStreamDestroy(c->lk.s);
+    if (c->lk.h) (void)hipHostFree(c->lk.h);
     if (c->d_steer) (void)hipFree(c->d_steer);
     for (auto &h : c->hs) {
         if (h.s) (void)hipStreamDestroy(h.s);
@@ -876,7 +905,9 @@ int ppe_acl_lookup(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint32_t 
     HIPCHK(c, hipSetDevice(c->device));
     const int r = c->running;
     const uint32_t words = c->h_img[r][PPE_IMG_W_OFFBSEC];  // the binary walk's part of the image (no blocks)
-    const bool lds = (size_t)words * 4u + 1024u <= PPE_LDS_IMG_MAX;
+    // staging the image into each workgroup's LDS pays off over many tuples; a few (one flow miss's lookup) walk it
+    // from L2 / HBM in one workgroup
+    const bool lds = (size_t)words * 4u + 1024u <= PPE_LDS_IMG_MAX && in->n >= 4096u;
     ppe_tuple_kargs a;
     std::memset(&a, 0, sizeof a);
     a.tuple = in->tuple;
@@ -901,33 +932,40 @@ int ppe_acl_lookup_host(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint
     if (!c || !in) return PPE_EINVAL;
     if (in->n == 0) return PPE_OK;
     if (!in->tuple) return fail(c, PPE_EINVAL, "tuple required");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, use_device(c));
+    LookupStage &L = c->lk;
     const size_t n = in->n;
-    uint8_t *buf = nullptr;
-    const size_t bytes = n * 16 + (in->macs ? n * 16 : 0) + (in->ts ? n * 8 : 0) + n * 8;
-    HIPCHK(c, hipMalloc(&buf, bytes));
-    uint32_t *dt = (uint32_t *)buf;
-    uint8_t *p = buf + n * 16;
-    uint32_t *dm = nullptr;
-    uint64_t *dts = nullptr;
-    if (in->macs) { dm = (uint32_t *)p; p += n * 16; }
-    if (in->ts) { dts = (uint64_t *)p; p += n * 8; }
-    int32_t *dh = (int32_t *)p;
-    uint32_t *da = (uint32_t *)(p + n * 4);
-    int rc = PPE_OK;
-    if (hipMemcpy(dt, in->tuple, n * 16, hipMemcpyHostToDevice) != hipSuccess ||
-        (dm && hipMemcpy(dm, in->macs, n * 16, hipMemcpyHostToDevice) != hipSuccess) ||
-        (dts && hipMemcpy(dts, in->ts, n * 8, hipMemcpyHostToDevice) != hipSuccess))
-        rc = fail(c, PPE_EIO, "tuple upload failed");
-    if (rc == PPE_OK) {
-        ppe_tuples_t d = {dt, dm, dts, in->n};
-        rc = ppe_acl_lookup(c, &d, dh, da, now_seconds, nullptr);
+    if (!L.s) HIPCHK(c, hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
+    if (n > L.cap) {  // grown (with headroom) only when a larger burst arrives; the first call allocates
+        const uint32_t cap = (uint32_t)std::max<size_t>({n, (size_t)L.cap * 2u, 1024u});
+        HIPCHK(c, hipStreamSynchronize(L.s));
+        if (L.h) HIPCHK(c, hipHostFree(L.h));
+        L.h = L.d = nullptr;
+        L.cap = 0;
+        HIPCHK(c, hipHostMalloc((void **)&L.h, (size_t)cap * 48u, hipHostMallocMapped));
+        HIPCHK(c, hipHostGetDevicePointer((void **)&L.d, L.h, 0));
+        L.cap = cap;
     }
-    if (rc == PPE_OK && hipDeviceSynchronize() != hipSuccess) rc = fail(c, PPE_EIO, "acl kernel failed");
-    if (rc == PPE_OK && hit && hipMemcpy(hit, dh, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = PPE_EIO;
-    if (rc == PPE_OK && action && hipMemcpy(action, da, n * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = PPE_EIO;
-    (void)hipFree(buf);
-    return rc;
+    const size_t cap = L.cap;
+    uint8_t *ht = L.h, *hm = L.h + cap * 16, *hts = L.h + cap * 32, *hh = L.h + cap * 40, *ha = L.h + cap * 44;
+    std::memcpy(ht, in->tuple, n * 16);
+    if (in->macs) std::memcpy(hm, in->macs, n * 16);
+    if (in->ts) std::memcpy(hts, in->ts, n * 8);
+    uint8_t *d = L.d;
+    ppe_tuples_t dv = {(const uint32_t *)d, in->macs ? (const uint32_t *)(d + cap * 16) : nullptr,
+                       in->ts ? (const uint64_t *)(d + cap * 32) : nullptr, in->n};
+    int rc = ppe_acl_lookup(c, &dv, (int32_t *)(d + cap * 40), (uint32_t *)(d + cap * 44), now_seconds, L.s);
+    if (rc != PPE_OK) return rc;
+    // spin on this stream alone (a lookup is a few microseconds; a blocking wait would add the wake-up), then block
+    hipError_t q = hipErrorNotReady;
+    const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(2);
+    while ((q = hipStreamQuery(L.s)) == hipErrorNotReady && std::chrono::steady_clock::now() < until)
+        __builtin_ia32_pause();
+    if (q == hipErrorNotReady) q = hipStreamSynchronize(L.s);
+    if (q != hipSuccess) return fail(c, PPE_EIO, "acl lookup kernel failed: %s", hipGetErrorString(q));
+    if (hit) std::memcpy(hit, hh, n * 4);
+    if (action) std::memcpy(action, ha, n * 4);
+    return PPE_OK;
 }
 
 void *ppe_dev_alloc(ppe_ctx_t *c, size_t bytes) {
@@ -1141,8 +1179,13 @@ static int flow_sync_counts(ppe_ctx *c, unsigned long long *ctl_out) {
     FlowTable &t = *c->flow;
     HIPCHK(c, hipDeviceSynchronize());
     HIPCHK(c, hipMemcpy(ctl_out, t.ctl, PPE_FCTL_WORDS * 8u, hipMemcpyDeviceToHost));
-    if (ctl_out[PPE_FCTL_ERR])
+    if (ctl_out[PPE_FCTL_ERR]) {
+        // reported once: the word is cleared, so only this call fails (the batches it covers may be inexact; the
+        // table itself stays usable)
+        HIPCHK(c, hipMemset(t.ctl + PPE_FCTL_ERR, 0, 8u));
+        HIPCHK(c, hipDeviceSynchronize());
         return fail(c, PPE_EIO, "flow table: %llu finalize workgroup(s) timed out waiting for the revoke", ctl_out[PPE_FCTL_ERR]);
+    }
     t.live_ub = ctl_out[PPE_FCTL_LIVE];
     t.tomb_ub = ctl_out[PPE_FCTL_TOMBS];
     t.snap_used = t.batches;  // (the device is idle: this is the state after every submitted batch)

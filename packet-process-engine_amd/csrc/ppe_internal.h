@@ -42,6 +42,9 @@ enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_N
        PPE_FCTL_MISS0, PPE_FCTL_MISS1, /* tiles with pending packets, by batch parity */
        PPE_FCTL_REVOKED_SEQ,           /* finalize: workgroup 0's revoke published for batch seq + 1 */
        PPE_FCTL_ERR,                   /* finalize: waits for the revoke flag that gave up (results not exact) */
+       PPE_FCTL_LIVE_AT_BATCH,         /* LIVE as the batch's classify launch started: every finalize workgroup takes
+                                          its overflow decision from this word, which nothing changes during finalize
+                                          (LIVE itself grows as finalize workgroups finish) */
        PPE_FCTL_WORDS = 16 };
 #define PPE_PK_SHIFT 40u                       /* packed counter: packets in bits 63:40, bytes in 39:0 */
 #define PPE_PK_FOLD_PKTS (1ull << 23)          /* fold into `stats` once either field reaches half its range */

@@ -286,14 +286,20 @@ __device__ __forceinline__ uint64_t ld_u64_sync(const uint64_t *q) {
 
 // DecodeTCPOptions (dataplane/src/decode/decode-tcp.c:18-131) over a TCP header's options in the window `row`:
 // opt = Dec.tcpopt.  Returns the byte offset of the first valid window-scale option (type 3, length 3) from the TCP
-// header, what the reference records as m->tcpvars.ws (:61-70, a duplicate is ignored), or 0.  Bytes past the
-// window or the wire length read as 0 (an EOL), like the oracle's.  Rare path (tuple output only): dword loads
-// with their own wait.
+// header, what the reference records as m->tcpvars.ws (:61-70, a duplicate is ignored), or 0; | PPE_TUPLE_OPT_PAST
+// >> 9 when no such option was found before the parse needed a byte past the header window (the reference reads
+// the whole option space, which lies inside the packet: hlen <= l4len, decode-tcp.c:149; the answer for such a
+// packet needs a wider window, e.g. Decode's 144 B).  A recorded option is final (the first one counts), so the parse
+// stops there.  Rare path (tuple output only): dword loads with their own wait.
 __device__ __forceinline__ uint32_t tcp_ws_offset(const uint8_t *row, uint32_t opt) {
     const uint32_t th = opt & 0xffu, avail = opt >> 16;
-    uint32_t plen = (opt >> 8) & 0xffu, pos = th + 20u, ws = 0, dwi = ~0u, dw = 0;
+    uint32_t plen = (opt >> 8) & 0xffu, pos = th + 20u, dwi = ~0u, dw = 0;
+    bool past = false;
     auto byte_at = [&](uint32_t b) -> uint32_t {
-        if (b >= avail) return 0u;
+        if (b >= avail) {  // (option bytes lie below the wire length: past the window)
+            past = true;
+            return 0u;
+        }
         if ((b >> 2) != dwi) {
             dwi = b >> 2;
             dw = ld_u32_sync((const uint32_t *)row + dwi);
@@ -303,7 +309,7 @@ __device__ __forceinline__ uint32_t tcp_ws_offset(const uint8_t *row, uint32_t o
 #pragma unroll 1
     while (plen) {
         const uint32_t t = byte_at(pos);
-        if (t == 0u) break;  // EOL
+        if (t == 0u) break;  // EOL (or past the window)
         if (t == 1u) {       // NOP
             ++pos;
             --plen;
@@ -311,12 +317,12 @@ __device__ __forceinline__ uint32_t tcp_ws_offset(const uint8_t *row, uint32_t o
         }
         if (plen < 2u) break;
         const uint32_t ol = byte_at(pos + 1u);
-        if (ol > plen || ol < 2u) break;  // invalid length: return -1 (the option already recorded stays)
-        if (t == 3u && ol == 3u && ws == 0u) ws = pos - th;
+        if (past || ol > plen || ol < 2u) break;  // invalid length: return -1 (the option already recorded stays)
+        if (t == 3u && ol == 3u) return pos - th;
         pos += ol;
         plen -= ol;
     }
-    return ws;
+    return past ? (PPE_TUPLE_OPT_PAST >> 9) : 0u;
 }
 
 // Where a residual MAC rule gets the packet's MACs: re-read from the header window (classify kernel: rare path, keeps
@@ -384,6 +390,9 @@ struct Dec {
 // chosen by applying the checks in REVERSE order of the reference's control flow, so the first failing check
 // (the one the reference returns on) wins.  w[0..12] = first 52 bytes (little-endian dwords); hdr / p = the packet's
 // window in global memory (read only for L4 headers behind IPv4 options).
+// TUP (kernels that may write the tuple output): a fragment's sport / dport / paylen carry what DecodeIPV4 records
+// for Defrag instead (decode-ipv4.c:106-109): ip_id, the fragment offset in bytes and frag_len (ppe_hip.h tuple).
+template <bool TUP = true>
 __device__ __forceinline__ Dec decode(const uint32_t (&w)[13], uint32_t len32, const uint8_t *hdr, uint32_t p,
                                       uint32_t stride, uint32_t syn_check) {
     Dec k;
@@ -490,6 +499,12 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[13], uint32_t len32, c
     k.sport = sport & l4m;
     k.dport = dport & l4m;
     k.paylen = (is_tcp ? l4len - thl : l4len - 8u) & l4m;
+    if constexpr (TUP) {  // fragments (status FRAG / FRAG_LEN_ERR): defrag_id, frag_offset, frag_len
+        const uint32_t fm = (ip_ok & frag) ? ~0u : 0u;
+        k.sport |= be16_hi(D[1]) & fm;                       // ip_id, L3+4
+        k.dport |= ((ipoff & 0x1fffu) << 3) & fm;            // IPV4_GET_IPOFFSET << 3, uint16
+        k.paylen |= ((l3len - hlen) & 0xffffu) & fm;         // len - ihl, uint16
+    }
 #endif
     return k;
 }
@@ -1318,8 +1333,13 @@ void ppe_classify_kernel(ppe_kargs a) {
     // this batch's creator count, summed by the resolve kernel (which runs after this one)
     if (FLOW && blockIdx.x == 0 && tid == 0) {
         a.flow.ctl[PPE_FCTL_BATCH_NEW] = 0;
-        // the table state after the previous batches, for the host's bounds (zero-copy, no stream stall)
-        a.flow.snap[1] = __hip_atomic_load(&a.flow.ctl[PPE_FCTL_LIVE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the table state after the previous batches, for the host's bounds (zero-copy, no stream stall); LIVE is
+        // stable here (the previous batch's finalize has completed, this batch's has not started), so it is also
+        // the finalize kernel's overflow reference
+        const unsigned long long live0 =
+            __hip_atomic_load(&a.flow.ctl[PPE_FCTL_LIVE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.flow.ctl[PPE_FCTL_LIVE_AT_BATCH] = live0;
+        a.flow.snap[1] = live0;
         a.flow.snap[2] = __hip_atomic_load(&a.flow.ctl[PPE_FCTL_TOMBS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __threadfence_system();
         __hip_atomic_store(&a.flow.snap[0], a.flow.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1391,7 +1411,7 @@ void ppe_classify_kernel(ppe_kargs a) {
         const uint32_t p = (tile << 6) + lane;
         const bool valid = p < B.n;
         if (!(PPE_ABLATE & 2) && valid) rx_bytes += wlen;
-        Dec k = decode(w, wlen, B.hdr, p, B.stride, a.syn_check);
+        Dec k = decode<!PART>(w, wlen, B.hdr, p, B.stride, a.syn_check);
 
         uint32_t fh = 0;
         int32_t hit = -1;
@@ -1489,7 +1509,7 @@ void ppe_classify_kernel(ppe_kargs a) {
                 if (p < B.n) rx_bytes += rl[t];
                 const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
                                         r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
-                Dec d = decode(w, rl[t], B.hdr, p, B.stride, a.syn_check);
+                Dec d = decode<!PART>(w, rl[t], B.hdr, p, B.stride, a.syn_check);
                 if ((PPE_ABLATE & 1) && d.st == ST_ACL) {
                     d.st = PPE_ST_ACL_FW;
                     d.flags |= PPE_F_ACL;
@@ -1608,7 +1628,7 @@ void ppe_classify_kernel(ppe_kargs a) {
                     if (valid) rx_bytes += rl[t];
                     const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
                                             r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
-                    Dec d = decode(w, rl[t], B.hdr, p, B.stride, a.syn_check);
+                    Dec d = decode<!PART>(w, rl[t], B.hdr, p, B.stride, a.syn_check);
                     if ((PPE_ABLATE & 1) && d.st == ST_ACL) {
                         d.st = PPE_ST_ACL_FW;
                         d.flags |= PPE_F_ACL;
@@ -1893,11 +1913,14 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
     if (tid < 32u) lcnt[tid] = 0;
     // revoke: when the host's bound says the pool may overflow, every workgroup checks the exact counts; on an
     // overflow workgroup 0 (dispatched first, so resident while the others wait) ranks and revokes, then publishes
-    // this batch's sequence number, which the others poll for (bounded) before reading any creator word
+    // this batch's sequence number, which the others poll for (bounded) before reading any creator word.  The
+    // decision and the room come from words no finalize workgroup changes (LIVE_AT_BATCH, written by this batch's
+    // classify launch; BATCH_NEW, summed by the resolve launch), so a workgroup dispatched after others have finished
+    // and added their creations to LIVE decides exactly as workgroup 0 did.
     if (tid == 0) {
         rev_s = 0u;
         if (a.revoke) {
-            const unsigned long long live = __hip_atomic_load(&a.f.ctl[PPE_FCTL_LIVE], __ATOMIC_RELAXED,
+            const unsigned long long live = __hip_atomic_load(&a.f.ctl[PPE_FCTL_LIVE_AT_BATCH], __ATOMIC_RELAXED,
                                                               __HIP_MEMORY_SCOPE_AGENT),
                                      cr = __hip_atomic_load(&a.f.ctl[PPE_FCTL_BATCH_NEW], __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT);
@@ -1909,13 +1932,19 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
     const bool rev = rev_s != 0u;
     if (rev) {
         if (blockIdx.x == 0) {
+            // producer (MI355X_MICROARCH.md, inter-workgroup visibility): every storing wave drains, workgroup
+            // barrier, one lane's agent release, then the flag
             flow_revoke<BLOCK>(a, part, room_s);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid == 0)
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(&a.f.ctl[PPE_FCTL_REVOKED_SEQ], a.f.seq + 1ull, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+            }
         } else {
+            // consumer: one relaxed poll, one agent acquire, its wait, then the workgroup barrier
             if (tid == 0) {
                 uint32_t k = 0;
                 for (; k < (1u << 24) && __hip_atomic_load(&a.f.ctl[PPE_FCTL_REVOKED_SEQ], __ATOMIC_RELAXED,
@@ -1923,6 +1952,8 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
                     __builtin_amdgcn_s_sleep(8);
                 if (k == (1u << 24))  // (never seen; reported by the next synchronising flow call as an error)
                     __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_ERR], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             __syncthreads();
         }

@@ -173,6 +173,7 @@ class Mbuf(C.Structure):
 
 
 MBUF_MAGIC_NUM = 0xAB00AB00
+TUPLE_OPT_PAST = 1 << 15  # include/ppe_hip.h PPE_TUPLE_OPT_PAST (tuple word 3)
 
 
 # every symbol include/*.h declares (checked by tests/test_abi.py)
@@ -203,7 +204,7 @@ EXPORTED_DATA = ["rule_list", "dp_acl_action_default", "gWstDepth", "gAvgDepth",
 _lib = None
 
 
-ABI_VERSION = 4  # include/ppe_hip.h PPE_ABI_VERSION
+ABI_VERSION = 5  # include/ppe_hip.h PPE_ABI_VERSION
 
 
 def load(path: str | os.PathLike | None = None) -> C.CDLL:

@@ -25,7 +25,7 @@ def header_functions():
 
 def test_library_loads():
     lib = abi.load()
-    assert lib.ppe_abi_version() == abi.ABI_VERSION == 4
+    assert lib.ppe_abi_version() == abi.ABI_VERSION == 5
 
 
 def test_every_declared_function_is_exported():

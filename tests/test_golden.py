@@ -11,6 +11,11 @@ def test_oracle_vs_golden(golden):
         r = o.classify_batch(g["hdr"], g["len"], ts=g["ts"], cfg=cfg)
         for k in ("verdict", "flow_hash", "acl_hit", "tuple", "reach"):
             assert np.array_equal(r[k], g[f"{tag}_{k}"]), (tag, k)
+        # the ABI 5 tuple differs from the frozen v1 one only in the fragments' Defrag fields (conftest.tuple_abi5)
+        st = r["verdict"] & 0xFF
+        fr = (st == 10) | (st == 11)
+        assert fr.sum() > 20
+        assert np.array_equal(g[f"{tag}_tuple"][~fr], g[f"{tag}_tuple_v1"][~fr])
         # per-reason counters as frozen; slot 31 (rx_bytes, added after the fixtures) is the sum of wire lengths
         assert np.array_equal(r["counters"][:31], g[f"{tag}_counters"][:31]), tag
         assert int(r["counters"][31]) == int(g["len"].astype(np.uint64).sum())

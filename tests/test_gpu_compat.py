@@ -47,7 +47,7 @@ def test_rule_store_commit_decode_hooks():
     pk = synth.make_packets(5000, rules, seed=91, kind="imix", stride=128, malformed_frac=0.1, with_ts=True)
     n = len(pk["len"])
     frames = [bytes(pk["hdr"][i][: min(int(pk["len"][i]) & 0xFFFF, 128)]) for i in range(n)]
-    bufs = [C.create_string_buffer(f, max(len(f), 1)) for f in frames]
+    bufs = [C.create_string_buffer(f, max(len(f), 144)) for f in frames]  # (Decode reads up to 144 B)
     mbufs = (Mbuf * n)()
     for i in range(n):
         mbufs[i].pkt_ptr = C.cast(bufs[i], C.c_void_p)
@@ -122,7 +122,7 @@ def test_decode_from_several_threads():
     assert lib.DP_Acl_Rule_Commit() == 0
     pk = synth.make_packets(8000, rules, seed=96, kind="imix", stride=128, malformed_frac=0.05)
     n = len(pk["len"])
-    bufs = [C.create_string_buffer(bytes(pk["hdr"][i][: min(int(pk["len"][i]) & 0xFFFF, 128)]), 128)
+    bufs = [C.create_string_buffer(bytes(pk["hdr"][i][: min(int(pk["len"][i]) & 0xFFFF, 128)]), 144)
             for i in range(n)]
     mbufs = (Mbuf * n)()
     for i in range(n):
