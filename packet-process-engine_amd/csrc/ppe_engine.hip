@@ -33,7 +33,7 @@ constexpr int kPipeStreams = 2;
 // before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering (next tile's window, or
 // only its first 16 B, requested before the current tile is processed) and an LDS-DMA next-tile pipeline were
 // measured slower and are not built.
-constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3, kPfSblk = 5, kPfMulti3 = 6, kPfSblk3 = 7;
+constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3, kPfSblk = 5, kPfMulti3 = 6, kPfSblk3 = 7, kPfPc = 8;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 // ppe_classify_batches: batches per launch.  0 = every batch of the call in one persistent launch (descriptor ring in
 // device memory): the launch ramp and tail are paid once per call instead of once per batch
@@ -178,7 +178,7 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl == 1 || pl == 3 || pl == 4 || pl == 5 ? (uint32_t)pl : 0u;
+    t.pipeline = pl == 1 || pl == 3 || pl == 4 || pl == 5 || pl == 6 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     t.batches_per_launch = (uint32_t)std::max(0, std::min(env_int("PPE_BATCHES_PER_LAUNCH", (int)kBatchesPerLaunch),
                                                           PPE_MAX_RING));
@@ -254,6 +254,10 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
             p.pipe = k3 ? kPfMulti3 : kPfMulti;
             p.block = 1024u;
         }
+        if (!single && !k3 && c->tune.pipeline == 6) {  // PF_PC over a global image
+            p.pipe = kPfPc;
+            p.block = 1024u;
+        }
         return p;
     }
     // the whole image in LDS: the smallest workgroup (most copies per CU) whose share holds it.  A single-tile kernel
@@ -282,7 +286,12 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
         mt_plan(80u * 1024u > fixed ? 80u * 1024u - fixed : 0u);
         return p;
     }
-    if (!single && (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && (lds_bytes > budget || k3) && !c->tune.block))) {
+    // PF_PC (tuning pipeline 6, and the default for split images unless PPE_PC=0): the multi-tile walk with producer
+    // and consumer waves, its LDS tile queue taken from the image budget
+    const bool pc = !single && !k3 &&
+                    (c->tune.pipeline == 6 || (c->tune.pipeline == 0 && !c->tune.block && env_int("PPE_PC", 0) != 0));
+    if (!single && (c->tune.pipeline == 3 || c->tune.pipeline == 6 ||
+                    (c->tune.pipeline == 0 && (lds_bytes > budget || k3) && !c->tune.block))) {
         p.pipe = k3 ? kPfMulti3 : kPfMulti;
         // tuning knobs (A/B only): workgroup size and the LDS bytes each workgroup may take (default: all of it, one
         // workgroup per CU); less LDS lets more workgroups share a CU (the 3-level kernel is built for 1024 only)
@@ -292,6 +301,11 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
         const uint32_t cap = (uint32_t)std::min(160 * 1024, std::max(8 * 1024, env_int("PPE_MT_LDS", 160 * 1024)));
         budget = cap > fixed ? cap - fixed : 0u;
         mt_plan(budget);
+        if (pc && (p.mode == 2 || c->tune.pipeline == 6)) {  // split images (C3), or forced
+            p = StagePlan{0, kPfPc, 1024u, 0, 0, 0, 0, 0, 0, 0};
+            const uint32_t pfixed = ppe_classify_fixed_lds(1024, kPfPc, 2) + 1024u;
+            mt_plan(cap > pfixed ? cap - pfixed : 0u);
+        }
         return p;
     }
     const uint32_t off_resid = img[PPE_IMG_W_OFFRESID], off_rules = img[PPE_IMG_W_OFFRULES];
@@ -1059,11 +1073,12 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 3 && t->pipeline != 4 && t->pipeline != 5)
+    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 3 && t->pipeline != 4 && t->pipeline != 5 &&
+        t->pipeline != 6)
         return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top), 3 (images that do "
                                    "not fit in LDS: 4 tiles per wave walked together) or 4 (first tile's loads before "
                                    "the image staging) or 5 (one tile per wave walking the image's blocks, for "
-                                   "split images)");
+                                   "split images) or 6 (3 with producer and consumer waves)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     if (t->batches_per_launch > PPE_MAX_RING) return fail(c, PPE_EINVAL, "batches_per_launch must be <= 4096");
     c->tune = *t;

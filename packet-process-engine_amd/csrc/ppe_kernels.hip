@@ -117,10 +117,12 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 #define KEY_WAVE_BYTES (KEY_SLOTS * 256u)  // 1536
 // KEYS = false: the multi-tile kernel (PF_MULTI) walks with the keys in registers and has no key slots, so its
 // image starts right after the counter bins (24 KB more image per CU at 1024 threads)
-template <int BLOCK, bool KEYS = true> struct Lds {
+// QB: the producer / consumer kernel's tile queue (PF_PC), between the counter bins and the image
+template <int BLOCK, bool KEYS = true, uint32_t QB = 0> struct Lds {
     static constexpr uint32_t KEYB = KEYS ? (BLOCK / 64) * KEY_WAVE_BYTES : 0u;
     static constexpr uint32_t BINS = KEYB;                   // 256 u32 bins, then 32 u32 counters
-    static constexpr uint32_t IMGB = KEYB + PPE_LDS_FIXED;   // 16-B aligned (1152 = 72 × 16)
+    static constexpr uint32_t QUEUE = KEYB + PPE_LDS_FIXED;  // 16-B aligned (1152 = 72 × 16)
+    static constexpr uint32_t IMGB = QUEUE + QB;
 };
 
 // LDS accesses by byte address (the compiler folds constant parts into the instruction offset)
@@ -137,6 +139,33 @@ __device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) {
 }
 __device__ __forceinline__ void lds_st8(uint32_t addr, uint32_t v) {
     *(__attribute__((address_space(3))) uint8_t *)(uintptr_t)addr = (uint8_t)v;
+}
+// LDS words shared between the waves of a workgroup (the PF_PC queue): a wave's LDS operations execute in issue
+// order, so a flag stored after `s_waitcnt lgkmcnt(0)` is seen only after the data stored before it, and data read
+// after the flag read returns is the data the flag publishes (volatile: the compiler keeps every access and its order)
+__device__ __forceinline__ uint32_t lds_vld(uint32_t addr) {
+    return *(volatile __attribute__((address_space(3))) uint32_t *)(uintptr_t)addr;
+}
+__device__ __forceinline__ void lds_vst(uint32_t addr, uint32_t v) {
+    *(volatile __attribute__((address_space(3))) uint32_t *)(uintptr_t)addr = v;
+}
+__device__ __forceinline__ uint32_t lds_add(uint32_t addr, uint32_t v) {
+    return __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t *)(uintptr_t)addr, v, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Wait (bounded) until the LDS word at addr equals want; false on timeout (a protocol bug must end the kernel, not hang
+// the GPU).  Every lane reads the same word (a broadcast), so the loop is wave-uniform.
+__device__ __forceinline__ bool lds_wait_eq(uint32_t addr, uint32_t want, uint32_t &polls) {
+#pragma unroll 1
+    for (uint32_t k = 0; k < (1u << 22); ++k) {
+        if (__builtin_amdgcn_readfirstlane(lds_vld(addr)) == want) {
+            asm volatile("" ::: "memory");
+            polls += k;
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
 }
 // global accesses by 32-bit byte offset from a uniform base (the saddr form: no 64-bit address math per lane)
 // (explicitly global: a select between two output pointers must not degrade to a flat store, whose out-of-order
@@ -1221,6 +1250,12 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
                     // 4 waves/SIMD with 128 VGPRs, one 1024-thread workgroup per CU and its whole LDS for the image
 #define PF_MULTI3 6  // PF_MULTI over an image of 3-level blocks (image word PPE_IMG_W_BLKLV == 3)
 #define PF_SBLK3 7   // PF_SBLK over 3-level blocks
+#define PF_PC 8      // PF_MULTI with its waves in two roles (split images, C3): producer waves stream the header
+                     // windows from HBM, decode and hash them, and hand tiles to consumer waves through an LDS queue;
+                     // consumer waves walk the image (LDS levels, then dependent L2 reads), check the records and
+                     // write the results.  A wave's s_waitcnt vmcnt retires its loads in issue order, so in one wave
+                     // a walk's L2 read would wait behind any HBM window load issued before it: split into roles,
+                     // the window stream never waits for a walk and no walk step waits for the window stream.
 #ifndef PPE_MT
 #define PPE_MT 4
 #endif
@@ -1236,6 +1271,33 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
 #ifndef PPE_MT_WAVES  // waves per SIMD the PF_MULTI kernel is compiled for (VGPR budget 512 / this)
 #define PPE_MT_WAVES 4
 #endif
+// PF_PC geometry: producer waves of the 16 in a 1024-thread workgroup, queue slots (tiles; deadlock freedom needs
+// >= 2 * PPE_MT, see the PF_PC loop), dwords per lane in a slot (key 4, flow hash, payload length, TCP option word)
+#ifndef PPE_PC_PROD
+#define PPE_PC_PROD 4
+#endif
+#ifndef PPE_PC_Q
+#define PPE_PC_Q 12
+#endif
+// diagnostic builds only (make variant NAME=pcstats VFLAGS=-DPPE_PC_STATS=1, tools/pc_stats.py): per role, the polls
+// spent waiting on the queue and the tiles handled, added into kargs.trace[0..7]
+#ifndef PPE_PC_STATS
+#define PPE_PC_STATS 0
+#endif
+// diagnostic builds only (make variant NAME=mttrace VFLAGS="-DPPE_MTTRACE=1 -DPPE_MTTRACE_SKIP=k", tools/trace_mt.py):
+// lane 0 of every wave of the multi-tile round loop writes s_memrealtime stamps of rounds k .. k + 4 to kargs.trace
+// (wave w at [32 w + 1 + 4 r + j]: j 0 round top, 1 decoded (window loads returned), 2 walked, 3 finished)
+#ifndef PPE_MTTRACE
+#define PPE_MTTRACE 0
+#endif
+#ifndef PPE_MTTRACE_SKIP
+#define PPE_MTTRACE_SKIP 8u
+#endif
+#define PC_W 7u
+#define PC_SLOT_BYTES (PC_W * 256u)
+#define PC_QBYTES (PPE_PC_Q * PC_SLOT_BYTES + 8u * PPE_PC_Q + 16u)  // slots, ready[Q] + free[Q], two tickets
+static_assert(PPE_PC_Q >= 2 * PPE_MT, "PF_PC queue: at least two ticket groups of slots");
+static_assert(PC_QBYTES % 16u == 0, "PF_PC queue keeps the image 16-B aligned");
 
 // FLOW: stateful flow-table mode (ppe_classify_flow, one batch): packets whose flow exists are accounted and
 // forwarded here; the rest are recorded for the claim / resolve / finalize kernels below, which complete their
@@ -1244,20 +1306,21 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
 // list, no tile counts, no tuple: ppe_kargs.part_layout), so the output checks are compile-time and the kernel holds
 // fewer scalars (C1 step -2..4 %, C4 -3.5 %: fewer SGPR spills to VGPR lanes)
 template <int MODE, int PF, int BLOCK, bool FLOW, bool PART = false>
-__global__ __launch_bounds__(BLOCK, ((PF == PF_MULTI || PF == PF_MULTI3) && !FLOW)
+__global__ __launch_bounds__(BLOCK, ((PF == PF_MULTI || PF == PF_MULTI3 || PF == PF_PC) && !FLOW)
                                         ? (PF == PF_MULTI3 ? PPE_MT3_WAVES : PPE_MT_WAVES)
                                         : (FLOW ? PPE_FLOW_WAVES : PPE_WAVES_PER_EU))
 void ppe_classify_kernel(ppe_kargs a) {
     constexpr bool MT_PIPE = PF == PF_MULTI && !FLOW &&
                              (PPE_MT_PF == 2 || (PPE_MT_PF == 1 && MODE == IMG_LDS));  // the pipelined round loop
+    constexpr bool PC = PF == PF_PC && !FLOW;
     constexpr int MT = FLOW ? 1
                      : PF == PF_MULTI ? ((PPE_MT_PF == 1 && MODE == IMG_LDS) ? PPE_MT_LDS : PPE_MT)
-                     : PF == PF_MULTI3 ? PPE_MT3 : 1;
+                     : PF == PF_MULTI3 ? PPE_MT3 : PC ? PPE_MT : 1;
     constexpr int KL = (PF == PF_MULTI3 || PF == PF_SBLK3) ? 3 : 2;  // block levels of the image's block section
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     // single-tile walks over a whole-LDS image use its 2-level blocks with the keys in registers (no key slots)
     constexpr bool STB = (PPE_ST_BLOCKS && MT == 1 && MODE == IMG_LDS) || PF == PF_SBLK || PF == PF_SBLK3;
-    using L = Lds<BLOCK, MT == 1 && !STB>;
+    using L = Lds<BLOCK, MT == 1 && !STB, PC ? PC_QBYTES : 0u>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
     uint32_t *lcnt = bins + PPE_NBINS;       // [32] per-reason counters of this workgroup
     const uint32_t tid = threadIdx.x;
@@ -1320,6 +1383,11 @@ void ppe_classify_kernel(ppe_kargs a) {
     if (have) load_tile(wtile);
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
+    if constexpr (PC) {  // the tile queue's flags: ready[s] = none, free[s] = s (slot s takes ticket s first), tickets 0
+        uint32_t *qf = smem + (L::QUEUE + PPE_PC_Q * PC_SLOT_BYTES) / 4u;
+        for (uint32_t i = tid; i < 2u * PPE_PC_Q + 2u; i += BLOCK)
+            qf[i] = i < PPE_PC_Q ? ~0u : (i < 2u * PPE_PC_Q ? i - PPE_PC_Q : 0u);
+    }
     const uint32_t lanebase = wv * KEY_WAVE_BYTES + 4u * lane;  // this lane's key slot 0 (LDS byte address)
     if (MT == 1 && !STB) lds_st32(lanebase + 256u * PPE_NODE_LEAF, 0u);  // the leaves' zero key
     if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img + a.stage_src, smem + L::IMGB / 4u, a.stage_words, tid);
@@ -1469,7 +1537,197 @@ void ppe_classify_kernel(ppe_kargs a) {
         finish(tile, p, valid, k, fh, hit, pend);
     };
 
-    if constexpr (MT > 1 && MT_PIPE) {
+    if constexpr (PC) {
+        // ---- PF_PC: the workgroup's tiles, batch after batch (workgroup wg takes tiles wg, wg + G, ... of every
+        // batch), are tickets handed out in groups of MT by two LDS counters, one per role.  Ticket u lives in queue
+        // slot u % Q: its producer waits until free[slot] == u (the consumer of u - Q has read the slot), fills it and
+        // sets ready[slot] = u; its consumer waits for that, takes the slot into registers and sets free[slot] = u + Q.
+        // No deadlock: the smallest ticket u not yet filled always proceeds.  Its producer holds the group [u', u' +
+        // MT) with u' <= u and waits only for the consumers of tickets below u' + MT - Q; each of those waits only for
+        // its own group, whose tickets lie below u' + 2 MT - Q <= u' <= u (Q >= 2 MT), all filled.  Every wait is
+        // bounded anyway (lds_wait_eq): a tile lost to a timeout gets verdict 0xffffffff, never a hang.
+        constexpr uint32_t Q = PPE_PC_Q;
+        const uint32_t qbase = L::QUEUE, qf = L::QUEUE + Q * PC_SLOT_BYTES;
+        const uint32_t rdy = qf, fre = qf + 4u * Q, tk_prod = qf + 8u * Q, tk_cons = tk_prod + 4u;
+        const uint32_t G = gridDim.x, wg = blockIdx.x;
+        // this wave's cursor over the batches: tickets [cbase, cbase + ccnt) are batch cb's (a wave's tickets only grow)
+        uint32_t cb = 0, cbase = 0;
+        auto cnt_of = [&](uint32_t n) -> uint32_t {
+            const uint32_t nt = (n + 63u) >> 6;
+            return nt > wg ? (nt - wg + G - 1u) / G : 0u;
+        };
+        uint32_t ccnt = cnt_of(bdesc(0).n);
+        auto locate = [&](uint32_t u, uint32_t &bi, uint32_t &tile) -> bool {
+            while (u >= cbase + ccnt) {
+                if (cb + 1u >= a.nbatch) return false;
+                cbase += ccnt;
+                ++cb;
+                ccnt = cnt_of(bdesc(cb).n);
+            }
+            bi = cb;
+            tile = wg + (u - cbase) * G;
+            return true;
+        };
+        uint32_t polls = 0, tiles_done = 0;
+        auto take = [&](uint32_t ctr) -> uint32_t {  // the wave's next ticket group
+            uint32_t u = 0;
+            if (lane == 0) u = lds_add(ctr, (uint32_t)MT);
+            return __builtin_amdgcn_readfirstlane(u);
+        };
+        if (wv < PPE_PC_PROD) {
+            // producer: MT tiles' windows in flight at once, then decode + hash each and hand it over
+#pragma unroll 1
+            for (;;) {
+                const uint32_t u0 = take(tk_prod);
+                uint32_t tbi[MT], tti[MT];
+                bool tv[MT];
+#pragma unroll
+                for (int t = 0; t < MT; ++t) tv[t] = locate(u0 + t, tbi[t], tti[t]);
+                if (!tv[0]) break;  // past the last batch (and so is every later ticket)
+                const uint8_t *th[MT];
+                const uint32_t *tl[MT];
+                uint32_t tn[MT], ts[MT];
+                uint4 r0[MT], r1[MT], r2[MT];
+                uint32_t r3[MT], rl[MT];
+#pragma unroll
+                for (int t = 0; t < MT; ++t) {
+                    if (!tv[t]) continue;
+                    const ppe_bdesc D = bdesc(tbi[t]);
+                    th[t] = D.hdr;
+                    tl[t] = D.len;
+                    tn[t] = D.n;
+                    ts[t] = D.stride;
+                    const uint32_t pc = min((tti[t] << 6) + lane, tn[t] - 1u);
+                    const uint32_t ro = pc * ts[t];
+                    r0[t] = gld_win<uint4>(th[t], ro);
+                    r1[t] = gld_win<uint4>(th[t], ro + 16u);
+                    r2[t] = gld_win<uint4>(th[t], ro + 32u);
+                    r3[t] = gld_win<uint32_t>(th[t], ro + 48u);
+                    rl[t] = gld_win<uint32_t>(tl[t], 4u * pc);
+                }
+#pragma unroll
+                for (int t = 0; t < MT; ++t) {
+                    if (!tv[t]) continue;
+                    const uint32_t p = (tti[t] << 6) + lane;
+                    if (p < tn[t]) rx_bytes += rl[t];
+                    const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
+                                            r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
+                    Dec d = decode<!PART>(w, rl[t], th[t], p, ts[t], a.syn_check);
+                    if ((PPE_ABLATE & 1) && d.st == ST_ACL) {
+                        d.st = PPE_ST_ACL_FW;
+                        d.flags |= PPE_F_ACL;
+                    }
+                    const uint32_t fh = (!(PPE_ABLATE & 8) && (d.flags & PPE_F_L4))
+                                            ? flow_hashfn_l4(d.proto == 6u, d.sip, d.dip, d.sport, d.dport) : 0u;
+                    const uint32_t u = u0 + (uint32_t)t, slot = u % Q;
+                    if (!lds_wait_eq(fre + 4u * slot, u, polls)) continue;  // (timeout: the consumer reports it)
+                    ++tiles_done;
+                    const uint32_t sb = qbase + slot * PC_SLOT_BYTES + 4u * lane;
+                    lds_st32(sb, d.sip);
+                    lds_st32(sb + 256u, d.dip);
+                    lds_st32(sb + 512u, d.sport | (d.dport << 16));
+                    lds_st32(sb + 768u, d.st | (d.flags << 8) | (d.proto << 16));
+                    lds_st32(sb + 1024u, fh);
+                    if (!PART) {
+                        lds_st32(sb + 1280u, d.paylen);
+                        lds_st32(sb + 1536u, d.tcpopt);
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lane == 0) lds_vst(rdy + 4u * slot, u);
+                }
+            }
+        } else {
+            // consumer: MT tiles walked in lockstep (acl_walk_blocks_mt), their records checked, results written
+            uint32_t curB = ~0u;
+#pragma unroll 1
+            for (;;) {
+                const uint32_t u0 = take(tk_cons);
+                uint32_t tbi[MT], tti[MT];
+                bool tv[MT], got[MT];
+#pragma unroll
+                for (int t = 0; t < MT; ++t) tv[t] = locate(u0 + t, tbi[t], tti[t]);
+                if (!tv[0]) break;
+                uint32_t key[MT][4], kfh[MT], kpay[MT], kopt[MT];
+                bool need[MT];
+#pragma unroll
+                for (int t = 0; t < MT; ++t) {
+                    const uint32_t u = u0 + (uint32_t)t, slot = u % Q;
+                    got[t] = tv[t] && lds_wait_eq(rdy + 4u * slot, u, polls);
+                    tiles_done += got[t] ? 1u : 0u;
+                    const uint32_t sb = qbase + (got[t] ? slot : 0u) * PC_SLOT_BYTES + 4u * lane;
+                    key[t][0] = got[t] ? lds_u32(sb) : 0u;
+                    key[t][1] = got[t] ? lds_u32(sb + 256u) : 0u;
+                    key[t][2] = got[t] ? lds_u32(sb + 512u) : 0u;
+                    key[t][3] = got[t] ? lds_u32(sb + 768u) : 0u;
+                    kfh[t] = got[t] ? lds_u32(sb + 1024u) : 0u;
+                    kpay[t] = (!PART && got[t]) ? lds_u32(sb + 1280u) : 0u;
+                    kopt[t] = (!PART && got[t]) ? lds_u32(sb + 1536u) : 0u;
+                    need[t] = got[t] && (key[t][3] & 0xffu) == ST_ACL;
+                }
+                // the slots go back to the producers once their words are in registers
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int t = 0; t < MT; ++t)
+                    if (got[t] && lane == 0) lds_vst(fre + 4u * ((u0 + (uint32_t)t) % Q), u0 + (uint32_t)t + Q);
+                uint4 nd[MT];
+                acl_walk_blocks_mt<MODE, L::IMGB, MT, KL>(a.img, geo, key, need, nd);
+                constexpr bool RPF = PPE_REC_PF && MODE == IMG_SPLIT;
+                uint4 rnext = make_uint4(0u, 0u, 0u, 0u);
+                if (RPF && geo.off_crec) rnext = crec_load<L::IMGB>(a.img, geo, nd[0].z);
+#pragma unroll
+                for (int t = 0; t < MT; ++t) {
+                    uint4 rcur = rnext;
+                    if (RPF && geo.off_crec && t + 1 < MT) rnext = crec_load<L::IMGB>(a.img, geo, nd[t + 1].z);
+                    if (!tv[t]) continue;
+                    if (tbi[t] != curB) {
+                        B = bdesc(tbi[t]);
+                        curB = tbi[t];
+                    }
+                    const uint32_t tile = tti[t], p = (tile << 6) + lane;
+                    if (!got[t]) {  // (queue timeout: the tile's packets are reported, not classified)
+                        if (p < B.n && B.verdict) B.verdict[p] = 0xffffffffu;
+                        continue;
+                    }
+                    Dec k;
+                    k.sip = key[t][0];
+                    k.dip = key[t][1];
+                    k.sport = key[t][2] & 0xffffu;
+                    k.dport = key[t][2] >> 16;
+                    k.st = key[t][3] & 0xffu;
+                    k.flags = (key[t][3] >> 8) & 0xffu;
+                    k.proto = key[t][3] >> 16;
+                    k.paylen = kpay[t];
+                    k.tcpopt = kopt[t];
+                    int32_t hit = -1;
+                    if (need[t]) {
+                        bool drop;
+                        if (RPF && geo.off_crec) {
+                            crec_check<L::IMGB>(a.img, geo, nd[t].z, rcur, k.sip, k.dip, k.sport, k.dport,
+                                                k.proto == 6u, hit, drop);
+                        } else if (geo.off_crec) {
+                            acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, k.sip, k.dip, k.sport, k.dport,
+                                                      k.proto == 6u, hit, drop);
+                        } else {
+                            uint32_t rule_act;
+                            const MacFromWindow mac = {B.hdr, p, B.stride};
+                            acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], k.sip, k.dip, k.sport, k.dport, k.proto, mac,
+                                                    B.ts, p, a.now, hit, rule_act);
+                            drop = rule_act == ACL_RULE_ACTION_DROP;
+                        }
+                        k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
+                        k.flags |= PPE_F_ACL;
+                    }
+                    finish(tile, p, p < B.n, k, kfh[t], hit, false);
+                }
+            }
+        }
+        if (PPE_PC_STATS && lane == 0 && a.trace) {
+            const uint32_t r = wv < PPE_PC_PROD ? 0u : 4u;
+            atomicAdd(&a.trace[r + 0], (unsigned long long)polls);
+            atomicAdd(&a.trace[r + 1], (unsigned long long)tiles_done);
+            atomicAdd(&a.trace[r + 2], 1ull);
+        }
+    } else if constexpr (MT > 1 && MT_PIPE) {
         // PF_MULTI, pipelined: wave w takes rounds of MT tiles [MT w, MT w + MT), then + MT W, ... of its group's
         // batches; round r + 1's windows are requested during round r (PPE_MT_PF above)
         constexpr bool PF_EARLY = MODE == IMG_LDS;  // request before the walk (no global loads in walk / records)
@@ -1600,10 +1858,16 @@ void ppe_classify_kernel(ppe_kargs a) {
         }
     } else if constexpr (MT > 1) {
         // PF_MULTI: wave w takes tiles [MT w, MT w + MT), then + MT W, ...; all MT windows are requested together
+        uint32_t rnd = 0;
+        auto mt_stamp = [&](uint32_t j) {
+            if (PPE_MTTRACE && lane == 0 && a.trace && rnd - PPE_MTTRACE_SKIP < 5u)
+                a.trace[(size_t)twave * 32u + 1u + 4u * (rnd - PPE_MTTRACE_SKIP) + j] = __builtin_amdgcn_s_memrealtime();
+        };
         for (uint32_t bi = grp; wave_live && bi < a.nbatch; bi += ngroups) {
             if (bi != grp) B = bdesc(bi);
             const uint32_t ntiles = (B.n + 63u) >> 6;
-            for (uint32_t t0 = wtile * MT; t0 < ntiles; t0 += stride_waves * MT) {
+            for (uint32_t t0 = wtile * MT; t0 < ntiles; t0 += stride_waves * MT, ++rnd) {
+                mt_stamp(0);
                 uint4 r0[MT], r1[MT], r2[MT];
                 uint32_t r3[MT], rl[MT];
 #pragma unroll
@@ -1641,6 +1905,10 @@ void ppe_classify_kernel(ppe_kargs a) {
                     kpay[t] = d.paylen;
                     kopt[t] = d.tcpopt;
                 }
+                if (PPE_MTTRACE) {
+                    asm volatile("" ::"v"(key[0][3]), "v"(key[MT - 1][3]));
+                    mt_stamp(1);
+                }
                 uint4 nd[MT];
                 uint4 rec[MT];
                 if (PPE_REC_IN_WALK && geo.off_crec)
@@ -1650,6 +1918,10 @@ void ppe_classify_kernel(ppe_kargs a) {
                 // PPE_REC_PF (split compact images): tile t + 1's record is requested, by every lane (a lane with no
                 // leaf reads slot 0), before tile t's check, so the L2 round trips of the round's records overlap
                 // the tiles' finish work instead of one after another
+                if (PPE_MTTRACE) {
+                    asm volatile("" ::"v"(nd[0].z), "v"(nd[MT - 1].z));
+                    mt_stamp(2);
+                }
                 constexpr bool RPF = PPE_REC_PF && MODE == IMG_SPLIT && !PPE_REC_IN_WALK;
                 uint4 rnext = make_uint4(0u, 0u, 0u, 0u);
                 if (RPF && geo.off_crec) rnext = crec_load<L::IMGB>(a.img, geo, nd[0].z);
@@ -1695,6 +1967,10 @@ void ppe_classify_kernel(ppe_kargs a) {
                         k.flags |= PPE_F_ACL;
                     }
                     finish(tile, p, p < B.n, k, fh, hit, false);
+                }
+                if (PPE_MTTRACE) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    mt_stamp(3);
                 }
             }
         }
@@ -2266,6 +2542,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block) 
         if (pipe == PF_SBLK) return FN<M, PF_SBLK, 1024>(__VA_ARGS__);   \
         if (pipe == PF_MULTI3) return FN<M, PF_MULTI3, 1024>(__VA_ARGS__); \
         if (pipe == PF_SBLK3) return FN<M, PF_SBLK3, 1024>(__VA_ARGS__);   \
+        if (pipe == PF_PC) return FN<M, PF_PC, 1024>(__VA_ARGS__);         \
         PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__);                \
     } while (0)
 #define PPE_DISPATCH(FN, ...)                                        \
@@ -2307,8 +2584,8 @@ extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, in
 // walks (the multi-tile kernel; the single-tile kernel over a whole-LDS image) keep the keys in registers.
 extern "C" uint32_t ppe_classify_fixed_lds(int block, int pipe, int mode) {
     const bool blocks = pipe == PF_MULTI || pipe == PF_SBLK || pipe == PF_MULTI3 || pipe == PF_SBLK3 ||
-                        (PPE_ST_BLOCKS && mode == IMG_LDS);
-    return (blocks ? 0u : (uint32_t)(block / 64) * KEY_WAVE_BYTES) + PPE_LDS_FIXED;
+                        pipe == PF_PC || (PPE_ST_BLOCKS && mode == IMG_LDS);
+    return (blocks ? 0u : (uint32_t)(block / 64) * KEY_WAVE_BYTES) + PPE_LDS_FIXED + (pipe == PF_PC ? PC_QBYTES : 0u);
 }
 
 // 1: the single-tile kernel walks the block section of a whole-LDS image (the engine stages the whole image)

@@ -295,12 +295,19 @@ def test_c3_64k_rules_vs_oracle(eng):
     # the compiler too, not only the walk: 16,384 packets against the linear first-match definition
     lin = o.classify_batch(pk["hdr"][:16384], pk["len"][:16384], cfg=o.cfg(0, 1, NOW), nthreads=16)
     assert_same({k: v[:16384] for k, v in res.items()}, lin)
-    # the single-tile block walk (pipeline 5): fewer block levels in LDS, the rest from L2
+    # the single-tile block walk (pipeline 5): fewer block levels in LDS, the rest from L2; the multi-tile walk with
+    # and without producer / consumer waves (pipelines 6 and 3), at several ticket-queue positions (ragged sizes)
     old = eng.tuning()
     try:
-        eng.tuning(pipeline=5)
-        assert eng.launch_info()["fetch"] == "sblk"
-        assert_same(gpu_classify(eng, pk["hdr"], pk["len"]), ref)
+        for pl, fetch in ((5, "sblk"), (6, "pc"), (3, "multi")):
+            eng.tuning(pipeline=pl)
+            assert eng.launch_info()["fetch"] == fetch and eng.launch_info()["image"] == "split"
+            assert_same(gpu_classify(eng, pk["hdr"], pk["len"]), ref)
+        eng.tuning(pipeline=6)
+        for m in (1, 63, 64, 65, 4097, 99_999):
+            r = gpu_classify(eng, pk["hdr"][:m], pk["len"][:m])
+            assert_same(r, {k: v[:m] for k, v in ref.items()})
+            check_compaction(r, m)
     finally:
         eng.tuning(**old)
 
@@ -403,7 +410,7 @@ def test_argument_errors(eng):
     assert (ob == 0x5A).all()
     t = abi.Tuning(block=300)
     assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
-    for pl in (2, 6):  # the register / LDS-DMA prefetch variants are not built
+    for pl in (2, 7, 8):  # the register / LDS-DMA prefetch variants are not built; 6 is PF_PC
         t = abi.Tuning(pipeline=pl)
         assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
 
@@ -411,7 +418,8 @@ def test_argument_errors(eng):
 TUNINGS = [dict(lds_image=0), dict(block=512), dict(block=1024), dict(block=256), dict(pipeline=1),
            dict(pipeline=4), dict(pipeline=1, block=256), dict(pipeline=1, block=512), dict(pipeline=1, lds_image=0),
            dict(pipeline=4, lds_image=0), dict(pipeline=4, block=1024), dict(blocks_per_cu=16), dict(blocks_per_cu=1),
-           dict(pipeline=3), dict(pipeline=3, lds_image=0), dict(pipeline=5), dict(pipeline=5, block=1024)]
+           dict(pipeline=3), dict(pipeline=3, lds_image=0), dict(pipeline=5), dict(pipeline=5, block=1024),
+           dict(pipeline=6), dict(pipeline=6, lds_image=0)]
 
 
 @pytest.mark.parametrize("tune", TUNINGS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))

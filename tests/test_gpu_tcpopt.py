@@ -89,8 +89,9 @@ def test_tcp_option_parse_vs_oracle(stride):
     past = (ref["tuple"][:, 3] & abi.TUPLE_OPT_PAST) != 0
     st = ref["verdict"] & 0xFF
     assert (ws[ok] > 0).sum() > 2000 and (ws[ok] == 0).sum() > 2000  # both outcomes well covered
-    # a 64-B window cuts many option spaces short before their window-scale option; 128 B only behind IPv4 options
-    assert past[ok].sum() > (1000 if stride == 64 else 20)
+    # a 64-B window cuts many option spaces short before their window-scale option (128 B holds these packets' options
+    # whole: IPv4 options here reach ihl 8 only; tests/test_gpu_mbuf.py covers 128-B windows cut short)
+    assert past[ok].sum() > 1000 if stride == 64 else not past.any()
     assert ((st[ok] == ST["ACL_FW"]) | (st[ok] == ST["ACL_DROP"]) | (st[ok] == ST["FLOW_TCP_NO_SYN_FIRST"])).mean() > 0.9
     assert ((got["verdict"].view(np.uint32)[far] & 0xFF) == ST["WINDOW_PUNT"]).all()
 
