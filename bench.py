@@ -750,13 +750,20 @@ def run_stateless(args, dev, world, rank, dist):
 FLOW_METRIC = "Mpps device-resident decode+flow-table+ACL classify (stateful FlowHandlePacket)"
 
 
-def flow_bytes(stride: int) -> float:
+def flow_owner_update() -> bool:
+    """The library's FlowUpdate mode (ppe_flow_create reads PPE_FLOW_OWNER the same way): owner-computed (default)
+    or one atomic per found packet inside the classify kernel."""
+    return os.environ.get("PPE_FLOW_OWNER", "1").strip() not in ("0", "")
+
+
+def flow_bytes(stride: int, owner: bool = False) -> float:
     """Algorithmic bytes per packet of the flow-mode classify kernel on the hit path: the stateless kernel's 84 B
-    (window + length read; verdict, hash, hit, partition entry written) plus the flow slot's 16-B key read, its
-    16-B direction counters read and written (two 8-B atomics) and the 8-B last-seen store, and the 8-B tile mask
-    per 64 packets."""
+    (window + length read; verdict, hash, hit, partition entry written), the flow slot's 16-B key read and the 8-B
+    tile mask per 64 packets, plus the FlowUpdate: in the kernel, the 16-B direction counters read and written (two
+    8-B atomics) and the 8-B last-seen store; owner-computed, the 8-B bucket entry the kernel writes
+    instead (the update kernel then touches each flow once per batch, outside this kernel's time)."""
     rd, wr = algorithmic_bytes(stride)
-    return rd + wr + 4.0 + 16.0 + 32.0 + 8.0 + 8.0 / 64.0
+    return rd + wr + 4.0 + 16.0 + (8.0 if owner else 32.0 + 8.0) + 8.0 / 64.0
 
 
 def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
@@ -882,8 +889,11 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
         my_ms = float(t.item())
     mpps = n * args.steps * world / (my_ms / 1e3) / 1e6
     kern_avg_ms = kern_ms / max(launches, 1)
-    bpp = flow_bytes(stride)
+    owner = flow_owner_update()
+    bpp = flow_bytes(stride, owner)
     achieved = bpp * n / (kern_avg_ms / 1e3) / 1e9
+    # the whole batch (classify, flow kernels, update) against the in-kernel definition's bytes: the batch roofline
+    batch_achieved = flow_bytes(stride) * n / (my_ms / args.steps / 1e3) / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not nested:
@@ -917,10 +927,14 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": round(tpp * n) if tpp else None,
-                         "kernel": "ppe_classify_kernel<FLOW> (FlowFind + accounting; misses resolved by the flow "
-                                   "kernels)",
+                         "kernel": "ppe_classify_kernel<FLOW> (FlowFind; found flows' updates "
+                                   + ("to the owners' buckets, applied by ppe_flow_update_kernel" if owner else
+                                      "by one atomic per packet") + "; misses resolved by the flow kernels)",
                          "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": bpp,
-                         "batch_avg_us": round(my_ms / args.steps * 1e3, 3)},
+                         "batch_avg_us": round(my_ms / args.steps * 1e3, 3),
+                         "batch_bytes_per_pkt": flow_bytes(stride),
+                         "batch_frac": round(batch_achieved / HBM_PEAK_GBPS, 4),
+                         "flow_update": "owner" if owner else "atomic"},
             "cpu_baseline": cpu,
             "parity_sample_ok": parity,
             "flow_table": info,

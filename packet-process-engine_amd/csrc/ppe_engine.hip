@@ -64,7 +64,7 @@ struct LookupStage {
 // Device flow table (ppe_classify_flow) and what the host knows about it without synchronising.
 struct FlowArrays {
     uint32_t *keys = nullptr, *creator = nullptr;
-    unsigned long long *stats = nullptr, *packed = nullptr;
+    unsigned long long *stats = nullptr;
 };
 struct FlowTable {
     uint32_t capacity = 0, max_batch = 0, nslots = 0;
@@ -73,6 +73,10 @@ struct FlowTable {
     unsigned long long *ctl = nullptr;
     uint32_t *rec = nullptr, *rslot = nullptr, *miss_tiles = nullptr;
     unsigned long long *tile_miss = nullptr, *tile_new = nullptr;
+    // owner-computed FlowUpdate (ppe_flow_update_kernel): bucket columns for upd_wgs classify workgroups
+    unsigned long long *upd = nullptr;
+    uint32_t *ucnt = nullptr;
+    uint32_t upd_wgs = 0, upd_osh = 0, upd_owners = 0, upd_hmask = PPE_UPD_HASH - 1u;
     uint64_t batches = 0;   // ppe_classify_flow calls (the parity selects the miss-tile counter)
     unsigned long long fold_pkts = PPE_PK_FOLD_PKTS, fold_bytes = PPE_PK_FOLD_BYTES;
     uint64_t live_ub = 0;   // upper bound of live flows: a snapshot's count + n per batch since
@@ -197,11 +201,13 @@ struct StagePlan {
     uint32_t crec_lds = ~0u, idtab_lds = ~0u;  // compact records / index table in LDS (byte offsets), ~0u = global
 };
 
-// LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves): 160 KiB shared, minus
-// the per-wave walk keys and counter bins, and the 1-KB rounding of the staged image
-uint32_t image_budget(uint32_t block, int mode) {
-    const uint32_t per_wg = (160u * 1024u) / (2048u / block);
-    const uint32_t fixed = ppe_classify_fixed_lds((int)block, kPfHoist, mode) + 1024u;
+// LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves; a flow-table launch:
+// the waves per CU its kernel is compiled for): 160 KiB shared, minus the per-wave walk keys and counter bins
+// (flow-table launches: and the owner-update buckets), and the 1-KB rounding of the staged image
+uint32_t image_budget(uint32_t block, int mode, bool flow = false) {
+    const uint32_t waves_cu = flow ? std::min(32u, std::max(block / 64u, 4u * ppe_flow_waves())) : 32u;
+    const uint32_t per_wg = (160u * 1024u) / std::max(1u, waves_cu / (block / 64u));
+    const uint32_t fixed = ppe_classify_fixed_lds((int)block, kPfHoist, mode) + 1024u + (flow ? ppe_flow_lds_extra() : 0u);
     return per_wg > fixed ? per_wg - fixed : 0u;
 }
 
@@ -267,13 +273,13 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
     const uint32_t lds_bytes = stb ? all_words * 4u : bytes;
     if (!c->tune.block) {
         for (uint32_t b : {256u, 512u, 1024u}) {
-            if (lds_bytes <= image_budget(b, 1)) {
+            if (lds_bytes <= image_budget(b, 1, single)) {
                 p.block = b;
                 break;
             }
         }
     }
-    uint32_t budget = image_budget(p.block, 1);
+    uint32_t budget = image_budget(p.block, 1, single);
     // PF_MULTI (tuning pipeline 3, and the default) for images that do not fit whole: 1024-thread workgroups, one
     // per CU, with the CU's whole LDS for the image prefix (C2 / C3 / C4 step 27.2 / 52.1 / 27.3 -> 23.6 / 42.8 /
     // 22.7 us)
@@ -323,7 +329,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
         p.stage_words = p.lds_words;
         return p;
     }
-    budget = image_budget(p.block, 2);  // node walks of a partly staged image keep their key slots
+    budget = image_budget(p.block, 2, single);  // node walks of a partly staged image keep their key slots
     if (off_resid * 4u <= budget) {  // nodes, leaf lists and rule records; residual records from global
         p.mode = 2;
         p.lds_words = off_resid;
@@ -343,15 +349,18 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
 
 // Resident workgroups per CU: the occupancy API's answer (register and LDS limits) unless the tuning fixes it.
 // The persistent grid is CUs × this, so no workgroup waits for a second round.
-uint32_t blocks_per_cu(ppe_ctx *c, const StagePlan &p) {
+uint32_t blocks_per_cu(ppe_ctx *c, const StagePlan &p, bool flow = false) {
     const uint32_t cap = kMaxBlocksPerCU * 256u / p.block;
     if (c->tune.blocks_per_cu) return std::max(1u, std::min(c->tune.blocks_per_cu, cap));  // may exceed residency
-    // the occupancy query costs microseconds of host time per call: cached per kernel variant and LDS size
+    // the occupancy query costs microseconds of host time per call: cached per kernel variant and LDS size (a
+    // flow-table launch: the flow variant's own occupancy, so its grid is resident in one round and each workgroup's
+    // owner-update buckets hold as many entries as it can)
     const uint64_t key = (uint64_t)p.stage_words | ((uint64_t)p.mode << 32) | ((uint64_t)p.pipe << 40) |
-                         ((uint64_t)p.block << 48);
+                         ((uint64_t)p.block << 48) | ((uint64_t)(flow ? 1u : 0u) << 63);
     for (const auto &e : c->occ_cache)
         if (e.first == key) return e.second;
-    const int occ = ppe_classify_occupancy(p.stage_words, p.mode, p.pipe, (int)p.block);
+    const int occ = flow ? ppe_classify_occupancy_flow(p.stage_words, p.mode, (int)p.block)
+                         : ppe_classify_occupancy(p.stage_words, p.mode, p.pipe, (int)p.block);
     const uint32_t r = occ > 0 ? std::min<uint32_t>((uint32_t)occ, cap) : 1u;
     c->occ_cache.emplace_back(key, r);
     return r;
@@ -513,7 +522,7 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     // enough workgroups for every tile of every batch (the kernel splits its waves into batch groups), at most
     // the resident grid
     const uint32_t want = (uint32_t)std::min<uint64_t>((tiles_total + wpb - 1) / wpb, 1u << 30);
-    const uint32_t maxg = c->n_cu * blocks_per_cu(c, plan);
+    const uint32_t maxg = c->n_cu * blocks_per_cu(c, plan, fl != nullptr);
     const uint32_t grid = std::max(1u, std::min(want, std::min(maxg, c->max_grid)));
     a.img = c->d_img[r];
     a.img_words = words;
@@ -1126,17 +1135,15 @@ static void flow_free_arrays(FlowArrays &a) {
     (void)hipFree(a.keys);
     (void)hipFree(a.creator);
     (void)hipFree(a.stats);
-    (void)hipFree(a.packed);
     a = FlowArrays();
 }
 
 // allocate (if needed) and clear one slot-array set: every slot EMPTY with zero counters, no creator
 static int flow_clear_arrays(ppe_ctx *c, FlowArrays &a, uint32_t nslots, hipStream_t s) {
-    if (!a.keys) {
+    if (!a.keys) {  // (the packed counters and last-seen times live in the slot records: `packed` views them)
         if (hipMalloc(&a.keys, (size_t)nslots * 4u * PPE_FLOW_SLOT_WORDS) != hipSuccess ||
             hipMalloc(&a.creator, (size_t)nslots * 4u) != hipSuccess ||
-            hipMalloc(&a.stats, (size_t)nslots * 32u) != hipSuccess ||
-            hipMalloc(&a.packed, (size_t)nslots * 16u) != hipSuccess) {
+            hipMalloc(&a.stats, (size_t)nslots * 32u) != hipSuccess) {
             flow_free_arrays(a);
             return fail(c, PPE_ENOMEM, "flow table: out of device memory (%u slots)", nslots);
         }
@@ -1144,7 +1151,6 @@ static int flow_clear_arrays(ppe_ctx *c, FlowArrays &a, uint32_t nslots, hipStre
     HIPCHK(c, hipMemsetAsync(a.keys, 0, (size_t)nslots * 4u * PPE_FLOW_SLOT_WORDS, s));
     HIPCHK(c, hipMemsetAsync(a.creator, 0xff, (size_t)nslots * 4u, s));
     HIPCHK(c, hipMemsetAsync(a.stats, 0, (size_t)nslots * 32u, s));
-    HIPCHK(c, hipMemsetAsync(a.packed, 0, (size_t)nslots * 16u, s));
     return PPE_OK;
 }
 
@@ -1154,7 +1160,7 @@ static ppe_flowdev flow_dev(const FlowTable &t, int which) {
     const FlowArrays &a = t.arr[which];
     d.keys = a.keys;
     d.stats = a.stats;
-    d.packed = a.packed;
+    d.packed = (unsigned long long *)(a.keys + 4);
     d.miss_tiles = t.miss_tiles;
     d.parity = (uint32_t)(t.batches & 1u);
     d.fold_pkts = t.fold_pkts;
@@ -1169,6 +1175,12 @@ static ppe_flowdev flow_dev(const FlowTable &t, int which) {
     d.rslot = t.rslot;
     d.gmask = t.nslots / PPE_FLOW_GROUP - 1u;
     d.capacity = t.capacity;
+    d.upd = t.upd;
+    d.ucnt = t.ucnt;
+    d.upd_wgs = t.upd_wgs;
+    d.upd_osh = t.upd_osh;
+    d.upd_owners = t.upd_owners;
+    d.upd_hmask = t.upd_hmask;
     return d;
 }
 
@@ -1248,6 +1260,8 @@ int ppe_flow_destroy(ppe_ctx_t *c) {
     (void)hipFree(t->miss_tiles);
     (void)hipFree(t->tile_miss);
     (void)hipFree(t->tile_new);
+    (void)hipFree(t->upd);
+    (void)hipFree(t->ucnt);
     delete t;
     c->flow = nullptr;
     return PPE_OK;
@@ -1283,6 +1297,22 @@ int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
         hipMalloc(&t->tile_new, (size_t)tiles * 8u) != hipSuccess)
         rc = fail(c, PPE_ENOMEM, "flow table: out of device memory");
     if (rc == PPE_OK && hipMemset(t->ctl, 0, PPE_FCTL_WORDS * 8u) != hipSuccess) rc = fail(c, PPE_EIO, "memset");
+    // owner-computed FlowUpdate: one bucket column per classify workgroup of a flow launch (at most 8 per CU and one
+    // per 4 tiles of the largest batch; a workgroup past the columns updates its found flows by atomics);
+    // PPE_FLOW_OWNER=0 turns it off (A/B)
+    if (rc == PPE_OK && env_int("PPE_FLOW_OWNER", 1) != 0) {
+        uint32_t owners = std::min<uint32_t>(PPE_UPD_OWNERS, ns), osh = 0;
+        while ((ns >> osh) > owners) ++osh;
+        t->upd_osh = osh;
+        t->upd_owners = ns >> osh;
+        t->upd_wgs = std::max(1u, std::min(c->n_cu * 8u, (tiles + 3u) / 4u));
+        // test hook: a smaller LDS hash, so the update kernel's full-hash path runs on small inputs (power of two)
+        const int hl = env_int("PPE_FLOW_UPD_HASH", 0);
+        if (hl > 0 && hl < (int)PPE_UPD_HASH && (hl & (hl - 1)) == 0) t->upd_hmask = (uint32_t)hl - 1u;
+        if (hipMalloc(&t->upd, (size_t)t->upd_owners * t->upd_wgs * PPE_UPD_CAP * 8u) != hipSuccess ||
+            hipMalloc(&t->ucnt, (size_t)t->upd_owners * t->upd_wgs * 4u) != hipSuccess)
+            rc = fail(c, PPE_ENOMEM, "flow table: out of device memory (update buckets)");
+    }
     if (rc == PPE_OK && (hipHostMalloc(&t->snap_h, 64, hipHostMallocMapped) != hipSuccess ||
                          hipHostGetDevicePointer((void **)&t->snap_d, t->snap_h, 0) != hipSuccess))
         rc = fail(c, PPE_ENOMEM, "flow table: pinned snapshot buffer");
@@ -1328,12 +1358,15 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     const hipStream_t s = (hipStream_t)stream;
     const ppe_flowdev d = flow_dev(t, t.cur);
     HIPCHK(c, hipEventRecord(t.pre_launch, s));
-    // 1. decode, hash, FlowFind; found flows are accounted and forwarded, the rest get syn_check + ACL
-    rc = launch(c, in, out, 1, cfg, s, 0, 0, &d);
+    // 1. decode, hash, FlowFind; found flows are forwarded and their updates logged to the owners' buckets, the
+    // rest get syn_check + ACL (would-be creators claim their slots)
+    uint32_t cgrid = 0;
+    rc = launch(c, in, out, 1, cfg, s, 0, 0, &d, &cgrid);
     if (rc != PPE_OK) return rc;
     ppe_flow_kargs k;
     std::memset(&k, 0, sizeof k);
     k.f = d;
+    k.f.upd_grid = cgrid;
     k.len = in->len;
     k.verdict = out->verdict;
     k.hit = out->acl_hit;
@@ -1348,12 +1381,14 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     k.cslots = c->d_cslots;
     // grid-stride over the miss-tile list (usually short): a few workgroups per CU, not one per tile
     const uint32_t fg = std::min(flow_grid(c, (in->n + 63u) / 64u, PPE_FLOW_BLOCK_WAVES), c->n_cu * 2u);
-    // 2-4. claim, resolve, finalize (when the host's bound says the pool may overflow, finalize checks the exact
-    // counts and, on an overflow, its workgroup 0 revokes the creators past the pool's room first)
+    // 2. finalize (when the host's bound says the pool may overflow, it checks the exact counts and, on an overflow,
+    // marks the creators and has its workgroup 0 revoke those past the pool's room first), then 3. the found flows'
+    // counters and last-seen times, one workgroup per owner (disjoint from the slots finalize touches)
     const bool may_overflow = t.live_ub + in->n > t.capacity;
     k.revoke = may_overflow ? 1u : 0u;
-    for (int kind : {PPE_FLOW_K_CLAIM, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_FINALIZE}) {
-        const int e = ppe_launch_flow(kind, &k, fg, (void *)s);
+    for (int kind : {PPE_FLOW_K_FINALIZE, PPE_FLOW_K_UPDATE}) {
+        if (kind == PPE_FLOW_K_UPDATE && !t.upd_wgs) continue;
+        const int e = ppe_launch_flow(kind, &k, kind == PPE_FLOW_K_UPDATE ? t.upd_owners : fg, (void *)s);
         if (e != 0) return fail(c, PPE_EIO, "flow kernel %d launch failed: %s", kind, hipGetErrorString((hipError_t)e));
     }
     t.cum_n[t.batches % FlowTable::kSnapRing] = t.tot_n;
@@ -1427,12 +1462,10 @@ int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_
     constexpr uint32_t W = PPE_FLOW_SLOT_WORDS;
     std::vector<uint32_t> keys((size_t)t.nslots * W);
     HIPCHK(c, hipMemcpy(keys.data(), a.keys, keys.size() * 4u, hipMemcpyDeviceToHost));
-    std::vector<unsigned long long> stats, packed;
+    std::vector<unsigned long long> stats;
     if (entries && max) {
         stats.resize((size_t)t.nslots * 4u);
-        packed.resize((size_t)t.nslots * 2u);
         HIPCHK(c, hipMemcpy(stats.data(), a.stats, stats.size() * 8u, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(packed.data(), a.packed, packed.size() * 8u, hipMemcpyDeviceToHost));
     }
     uint32_t k = 0;
     for (uint32_t s = 0; s < t.nslots; ++s) {
@@ -1447,12 +1480,14 @@ int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_
             e.dport = (uint16_t)(kw[2] >> 16);
             e.protocol = (uint8_t)(st >> 8);
             e.slot = s;
-            const unsigned long long bmask = (1ull << PPE_PK_SHIFT) - 1u, p0 = packed[2u * s], p1 = packed[2u * s + 1u];
+            unsigned long long pr[3];  // the record's packed counters and last-seen time (words 4-9)
+            std::memcpy(pr, kw + 4, sizeof pr);
+            const unsigned long long bmask = (1ull << PPE_PK_SHIFT) - 1u, p0 = pr[0], p1 = pr[1];
             e.pktcnts2d = stats[4u * s] + (p0 >> PPE_PK_SHIFT);
             e.bytecnts2d = stats[4u * s + 1u] + (p0 & bmask);
             e.pktcntd2s = stats[4u * s + 2u] + (p1 >> PPE_PK_SHIFT);
             e.bytecntd2s = stats[4u * s + 3u] + (p1 & bmask);
-            e.last_seen = (uint64_t)kw[PPE_FLOW_LAST_WORD] | ((uint64_t)kw[PPE_FLOW_LAST_WORD + 1u] << 32);
+            e.last_seen = pr[PPE_FLOW_REC_LAST];
         }
         ++k;
     }

@@ -26,12 +26,14 @@ struct ppe_bdesc {
 /* Device flow table (ppe_classify_flow; ppe_kernels.hip "flow table").  Open addressing over groups of
  * PPE_FLOW_GROUP slots (one 64-B line segment of slot records), linear probing from group flow_hash & gmask; a key lies
  * before the first EMPTY slot of its probe sequence (slots never return to EMPTY: deletions leave TOMBs, reclaimed by
- * a rehash).  A slot record is 32 B, {sip, dip, sport | dport << 16, state, last-seen (u64), 0, 0}: the last-seen
- * store of a found packet lands in the 64 B its probe has just brought into L2, instead of a random 8-B partial
- * write of its own in a separate array. */
+ * a rehash).  A slot record is 64 B: {sip, dip, sport | dport << 16, state}, then the packed counters of both
+ * directions and the last-seen time (`packed` points at them: u64 words 0-2 of each record's second 16 B), so a
+ * probe group of 2 slots is one 128-B line and the owner-computed update (ppe_flow_update_kernel) rewrites the line
+ * the probe read. */
 #define PPE_FLOW_GROUP 2u       /* slots per probe group */
-#define PPE_FLOW_SLOT_WORDS 8u  /* u32 words per slot record */
-#define PPE_FLOW_LAST_WORD 4u   /* the record's last-seen time (u64, words 4-5) */
+#define PPE_FLOW_SLOT_WORDS 16u /* u32 words per slot record */
+#define PPE_FLOW_REC_WORDS 8u   /* u64 stride of the counter records {s2d, d2s, last-seen, 0} (= the slot record) */
+#define PPE_FLOW_REC_LAST 2u    /* the counter record's last-seen time */
 #define PPE_FS_EMPTY 0u
 #define PPE_FS_TOMB 1u
 #define PPE_FS_LIVE(proto) (2u | ((proto) << 8))  /* key words valid */
@@ -45,14 +47,24 @@ enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_N
        PPE_FCTL_LIVE_AT_BATCH,         /* LIVE as the batch's classify launch started: every finalize workgroup takes
                                           its overflow decision from this word, which nothing changes during finalize
                                           (LIVE itself grows as finalize workgroups finish) */
+       PPE_FCTL_BATCH_NEW1,            /* BATCH_NEW of odd batches: the creators (slots claimed) the classify launch
+                                          counts, by batch parity; finalize reads its batch's and zeroes the next's */
+       PPE_FCTL_ARRIVE,                /* finalize, overflow batches: workgroups done marking their tiles' creators */
        PPE_FCTL_WORDS = 16 };
 #define PPE_PK_SHIFT 40u                       /* packed counter: packets in bits 63:40, bytes in 39:0 */
 #define PPE_PK_FOLD_PKTS (1ull << 23)          /* fold into `stats` once either field reaches half its range */
 #define PPE_PK_FOLD_BYTES (1ull << 39)
+/* Owner-computed FlowUpdate (ppe_flow_update_kernel): a found packet's counter update goes to a bucket of its slot's
+ * owner (one of at most PPE_UPD_OWNERS slot ranges) in its classify workgroup's column, instead of a memory-side
+ * atomic per packet; each owner's workgroup then sums its buckets in LDS and updates each touched slot once. */
+#define PPE_UPD_OWNERS 256u
+#define PPE_UPD_CAP 16u        /* entries per (owner, classify workgroup) bucket; a full bucket: the direct atomic */
+#define PPE_UPD_HASH 4096u     /* LDS hash entries of an owner workgroup (slots it accumulates; more: direct atomics) */
 struct ppe_flowdev {
     uint32_t *keys;               /* nslots × {sip, dip, sport | dport << 16, state, last-seen (u64), 0, 0}: the key in
                                      the creating packet's orientation                                                 */
-    unsigned long long *packed;   /* nslots × {s2d, d2s}: packets << 40 | bytes, one atomic per packet (FlowUpdate)    */
+    unsigned long long *packed;   /* keys + 4 words, stride PPE_FLOW_REC_WORDS: {s2d, d2s, last-seen, 0}, packets << 40
+                                     | bytes per direction (FlowUpdate) and the last-seen time, inside the slot record */
     unsigned long long *stats;    /* nslots × {pkts s2d, bytes s2d, pkts d2s, bytes d2s}: folded from `packed` before a
                                      field can overflow; a flow's counters = stats + the packed fields               */
     uint32_t *creator;            /* nslots: lowest index of the packets claiming the slot in this batch (| REVOKED)   */
@@ -68,6 +80,13 @@ struct ppe_flowdev {
     unsigned long long seq;       /* batches completed before this one                                                 */
     uint32_t gmask;               /* slot groups - 1                                                                   */
     uint32_t capacity;            /* flow pool size                                                                     */
+    unsigned long long *upd;      /* [owner][upd_wgs][PPE_UPD_CAP]: slot | (wire length | dir << 31) << 32             */
+    uint32_t *ucnt;               /* [upd_wgs][owner]: entries in each bucket (written by the classify launch)         */
+    uint32_t upd_wgs;             /* classify workgroups with a bucket column (0: every found packet's atomic inline)  */
+    uint32_t upd_osh;             /* owner of slot s = s >> upd_osh                                                      */
+    uint32_t upd_owners;          /* owners (nslots >> upd_osh)                                                          */
+    uint32_t upd_grid;            /* the update kernel: the batch's classify grid (bucket columns written)              */
+    uint32_t upd_hmask;           /* the update kernel's LDS hash entries - 1 (PPE_UPD_HASH - 1; lowered by tests)       */
 };
 
 /* flow-table kernels after the classify kernel (one batch) */
@@ -183,7 +202,7 @@ int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int 
                         void *stream, void *ev_start, void *ev_stop);
 /* flow-table phases after a flow-mode classify launch (stream order): claim, resolve, finalize (+ revoke in its
  * workgroup 0 when the pool overflows) */
-enum { PPE_FLOW_K_CLAIM = 0, PPE_FLOW_K_RESOLVE, PPE_FLOW_K_FINALIZE, PPE_FLOW_K_AGE, PPE_FLOW_K_REHASH };
+enum { PPE_FLOW_K_UPDATE = 0, PPE_FLOW_K_FINALIZE, PPE_FLOW_K_AGE, PPE_FLOW_K_REHASH };
 int ppe_launch_flow(int kind, const struct ppe_flow_kargs *a, uint32_t grid, void *stream);
 #define PPE_FLOW_BLOCK 256      /* flow kernels' workgroup size */
 /* steering: 0 count, 1 scan (one workgroup), 2 scatter the permutation; rows: gather / scatter of fixed rows */
@@ -191,7 +210,10 @@ int ppe_launch_steer(int phase, const struct ppe_steer_kargs *a, uint32_t grid, 
 int ppe_launch_rows(const struct ppe_rows_kargs *a, uint32_t grid, void *stream);
 #define PPE_FLOW_BLOCK_WAVES 4u /* waves (tiles in flight) per flow-kernel workgroup */
 int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, int block);
-uint32_t ppe_classify_fixed_lds(int block, int pipe, int mode);  /* key slots (node walks only) + counter bins */
+uint32_t ppe_classify_fixed_lds(int block, int pipe, int mode);
+uint32_t ppe_flow_lds_extra(void);  /* classify LDS of a flow-table launch beyond the stateless kernel's (buckets) */
+uint32_t ppe_flow_waves(void);      /* waves per SIMD of the flow-table classify kernel */
+int ppe_classify_occupancy_flow(uint32_t lds_words, int mode, int block);  /* key slots (node walks only) + counter bins */
 int ppe_classify_st_blocks(void);  /* 1: single-tile walks of a whole-LDS image use the block section */
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
 #ifdef __cplusplus

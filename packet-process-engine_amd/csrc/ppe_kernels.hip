@@ -1186,14 +1186,14 @@ __device__ __forceinline__ bool key_match(uint32_t ax, uint32_t ay, uint32_t az,
 __device__ __forceinline__ int32_t flow_find(const ppe_flowdev &f, uint32_t fh, uint32_t sip, uint32_t dip,
                                              uint32_t ports, uint32_t proto, uint32_t &fsip, uint32_t &fports) {
     const uint32_t live = PPE_FS_LIVE(proto);
-    const uint4 *keys = (const uint4 *)f.keys;  // slot s's key half: keys[2 s]
+    const uint4 *keys = (const uint4 *)f.keys;  // slot s's key: keys[(PPE_FLOW_SLOT_WORDS / 4) s]
     constexpr uint32_t G = PPE_FLOW_GROUP;
     uint32_t g = fh & f.gmask;
 #pragma unroll 1
     for (uint32_t it = 0; it <= f.gmask; ++it) {
         uint4 e[G];
 #pragma unroll
-        for (uint32_t j = 0; j < G; ++j) e[j] = keys[2u * (G * g + j)];
+        for (uint32_t j = 0; j < G; ++j) e[j] = keys[(PPE_FLOW_SLOT_WORDS / 4u) * (G * g + j)];
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
             if (e[j].w == live && key_match(e[j].x, e[j].y, e[j].z, sip, dip, ports)) {
@@ -1220,7 +1220,7 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
         // one memory-side atomic per packet: packets and bytes packed in one word.  The lane whose add takes a field
         // past half its range moves the whole word into the wide counters (exchange with 0, then add), so a field
         // never wraps and concurrent folds never count twice.
-        unsigned long long *pk = f.packed + 2ull * s + (d >> 1);
+        unsigned long long *pk = f.packed + (size_t)PPE_FLOW_REC_WORDS * s + (d >> 1);
         const unsigned long long inc = (1ull << PPE_PK_SHIFT) | (unsigned long long)wire_len;
         const unsigned long long nv =
             __hip_atomic_fetch_add(pk, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + inc;
@@ -1234,10 +1234,142 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
     }
     // every packet of the batch carries the same batch time (PPE_LAST_COND, experiment: store only when it differs)
     if (!(PPE_ABLATE & 32)) {
-        unsigned long long *lp = (unsigned long long *)(f.keys + PPE_FLOW_SLOT_WORDS * (size_t)s + PPE_FLOW_LAST_WORD);
+        unsigned long long *lp = f.packed + (size_t)PPE_FLOW_REC_WORDS * s + PPE_FLOW_REC_LAST;
         if (!PPE_LAST_COND || *lp != now) *lp = now;
     }
     return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
+}
+
+// PPE_UPD_NT (experiment): the owner update's stores (bucket entries, packed counters, last-seen times) with the
+// non-temporal policy, so fewer dirty lines wait in L2 for the write-back at the launch's end
+#ifndef PPE_UPD_NT
+#define PPE_UPD_NT 0
+#endif
+template <class T> __device__ __forceinline__ void upd_st(T *p, T v) {
+    if constexpr (PPE_UPD_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// PPE_UPD_LDS: the classify workgroup collects its bucket entries in LDS as 4-B entries {wire length (16 bits), dir,
+// slot within the owner (up to 15 bits)} and writes each bucket out as one 64-B segment at its end, instead of one
+// scattered 8-B store per found packet (tables of up to 2^23 slots; larger ones keep the 8-B global entries)
+#ifndef PPE_UPD_LDS
+#define PPE_UPD_LDS 1
+#endif
+__device__ __forceinline__ bool upd_small(const ppe_flowdev &f) { return PPE_UPD_LDS && f.upd_osh <= 15u; }
+
+// A found packet (classify launch): its direction flag, and its FlowUpdate as an entry in the bucket of its slot's
+// owner in this workgroup's column (ppe_flow_update_kernel applies it after the launch, with the last-seen time).
+// Without a column (update off, or a workgroup past the allocated columns) or with the bucket full: flow_account.
+__device__ __forceinline__ uint32_t flow_found(const ppe_flowdev &f, uint32_t *ucur, uint32_t *ubuf, uint32_t s,
+                                               uint32_t fsip, uint32_t fports, uint32_t sip, uint32_t ports,
+                                               uint32_t wire_len, uint64_t now) {
+    if (blockIdx.x < f.upd_wgs && wire_len < (upd_small(f) ? 0x10000u : 0x80000000u)) {
+        const uint32_t sport = ports & 0xffffu, dport = ports >> 16, fsport = fports & 0xffffu;
+        const bool to_server = sport != dport ? fsport == sport : fsip == sip;
+        const uint32_t d = sport == fsport ? 0u : 1u;
+        const uint32_t o = s >> f.upd_osh;
+        const uint32_t pos = atomicAdd(&ucur[o], 1u);
+        if (pos < PPE_UPD_CAP) {
+            if (upd_small(f))
+                ubuf[o * PPE_UPD_CAP + pos] = wire_len | (d << 16) | ((s & ((1u << f.upd_osh) - 1u)) << 17);
+            else
+                upd_st(f.upd + ((size_t)o * f.upd_wgs + blockIdx.x) * PPE_UPD_CAP + pos,
+                       (unsigned long long)s | ((unsigned long long)(wire_len | (d << 31)) << 32));
+            return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
+        }
+    }
+    return flow_account(f, s, fsip, fports, sip, ports, wire_len, now);
+}
+
+// the batch's creator counter (classify counts its claims into it; finalize reads it)
+__device__ __forceinline__ uint32_t fctl_new(uint32_t parity) {
+    return parity ? (uint32_t)PPE_FCTL_BATCH_NEW1 : (uint32_t)PPE_FCTL_BATCH_NEW;
+}
+
+__device__ __forceinline__ bool rec_match(const uint4 &q, const uint4 &r) {
+    return ((q.w ^ r.w) & 0xffu) == 0u && key_match(q.x, q.y, q.z, r.x, r.y, r.z);
+}
+// flow_hashfn of a record / key (TCP or UDP only reach the flow table); symmetric, so either orientation
+__device__ __forceinline__ uint32_t key_hash(uint32_t sip, uint32_t dip, uint32_t ports, uint32_t proto) {
+    return flow_hashfn_l4(proto == 6u, sip, dip, ports & 0xffffu, ports >> 16);
+}
+
+// A pending record read or written while other workgroups of the same launch may read it: agent-scope 8-B halves
+// (sc1: past this CU's L1, and the store out of the writer's XCD L2), MI355X_MICROARCH.md hand-off row 1 with the
+// claim's CAS as the per-record signal
+__device__ __forceinline__ void rec_store_shared(uint32_t *rec, uint32_t p, const uint4 &r) {
+    unsigned long long *q = (unsigned long long *)(rec + 4ull * p);
+    __hip_atomic_store(q, (unsigned long long)r.x | ((unsigned long long)r.y << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (unsigned long long)r.z | ((unsigned long long)r.w << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint4 rec_load_shared(const uint32_t *rec, uint32_t p) {
+    unsigned long long *q = (unsigned long long *)(rec + 4ull * p);
+    const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                             b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+
+// The claim of a would-be creator (pending, provisional ACL_FW), made by the classify launch as soon as the packet's
+// ACL result is known: the first EMPTY slot on the key's probe path becomes PEND | p (CAS), or the packet joins the
+// claim of an equal key met on the way; either way it lowers the slot's creator index (atomicMin).  The caller stored
+// the packet's record with rec_store_shared and waited for it (s_waitcnt vmcnt(0)) before the CAS publishes the index.
+// Concurrent FlowFind probes of the same launch may see a claimed slot as EMPTY or as PEND: both are "not live".
+// Returns the slot, or PPE_FLOW_NONE when the probe path holds no EMPTY slot (table full of live / tombstone slots).
+__device__ __forceinline__ uint32_t flow_claim(const ppe_flowdev &f, uint32_t p, const uint4 &r, bool &won) {
+    uint32_t g = key_hash(r.x, r.y, r.z, r.w & 0xffu) & f.gmask;
+#pragma unroll 1
+    for (uint32_t it = 0; it <= f.gmask; ++it) {
+#pragma unroll 1
+        for (uint32_t j = 0; j < PPE_FLOW_GROUP; ++j) {
+            const uint32_t s = PPE_FLOW_GROUP * g + j;
+            uint32_t *sw = f.keys + (size_t)PPE_FLOW_SLOT_WORDS * s + 3u;
+            uint32_t st = __hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (st == PPE_FS_EMPTY) {
+                uint32_t expect = PPE_FS_EMPTY;
+                if (__hip_atomic_compare_exchange_strong(sw, &expect, PPE_FS_PEND | p, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    atomicMin(&f.creator[s], p);
+                    won = true;  // one winning CAS per new flow: the batch's creator count
+                    return s;
+                }
+                st = expect;  // claimed meanwhile (by this flow or another)
+            }
+            if ((st & PPE_FS_PEND) && rec_match(rec_load_shared(f.rec, st & ~PPE_FS_PEND), r)) {
+                atomicMin(&f.creator[s], p);
+                return s;
+            }
+        }
+        g = (g + 1u) & f.gmask;
+    }
+    return PPE_FLOW_NONE;
+}
+
+// After the classify launch (every claim made): the slot claimed for a pending packet's flow, or PPE_FLOW_NONE.  The
+// finalize launch runs this while its creators turn their PEND slots LIVE (one 16-B store of key and state), so an
+// equal LIVE key is this batch's claim too (the packet missed the table as it stood before the batch).
+__device__ __forceinline__ uint32_t flow_find_claim(const ppe_flowdev &f, const uint4 &r) {
+    const uint4 *keys = (const uint4 *)f.keys;
+    const uint32_t live = PPE_FS_LIVE(r.w & 0xffu);
+    constexpr uint32_t G = PPE_FLOW_GROUP;
+    uint32_t g = key_hash(r.x, r.y, r.z, r.w & 0xffu) & f.gmask;
+#pragma unroll 1
+    for (uint32_t it = 0; it <= f.gmask; ++it) {
+        uint4 e[G];
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) e[j] = keys[(PPE_FLOW_SLOT_WORDS / 4u) * (G * g + j)];
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) {
+            if (e[j].w == PPE_FS_EMPTY) return PPE_FLOW_NONE;
+            if ((e[j].w & PPE_FS_PEND) ? rec_match(((const uint4 *)f.rec)[e[j].w & ~PPE_FS_PEND], r)
+                                       : (e[j].w == live && key_match(e[j].x, e[j].y, e[j].z, r.x, r.y, r.z)))
+                return G * g + j;
+        }
+        g = (g + 1u) & f.gmask;
+    }
+    return PPE_FLOW_NONE;
 }
 
 // PF: when a tile's window is fetched
@@ -1300,8 +1432,8 @@ static_assert(PPE_PC_Q >= 2 * PPE_MT, "PF_PC queue: at least two ticket groups o
 static_assert(PC_QBYTES % 16u == 0, "PF_PC queue keeps the image 16-B aligned");
 
 // FLOW: stateful flow-table mode (ppe_classify_flow, one batch): packets whose flow exists are accounted and
-// forwarded here; the rest are recorded for the claim / resolve / finalize kernels below, which complete their
-// tiles (verdict, compaction, counters).
+// forwarded here; the rest are recorded (and the would-be creators claim their slots) for the resolve / finalize
+// kernels below, which complete their tiles (verdict, compaction, counters).
 // PART: every batch of the launch has the throughput layout (verdict, flow hash and ACL hit written, one partition
 // list, no tile counts, no tuple: ppe_kargs.part_layout), so the output checks are compile-time and the kernel holds
 // fewer scalars (C1 step -2..4 %, C4 -3.5 %: fewer SGPR spills to VGPR lanes)
@@ -1320,9 +1452,12 @@ void ppe_classify_kernel(ppe_kargs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     // single-tile walks over a whole-LDS image use its 2-level blocks with the keys in registers (no key slots)
     constexpr bool STB = (PPE_ST_BLOCKS && MT == 1 && MODE == IMG_LDS) || PF == PF_SBLK || PF == PF_SBLK3;
-    using L = Lds<BLOCK, MT == 1 && !STB, PC ? PC_QBYTES : 0u>;
+    using L = Lds<BLOCK, MT == 1 && !STB,
+                  PC ? PC_QBYTES : FLOW ? 4u * PPE_UPD_OWNERS * (1u + (PPE_UPD_LDS ? PPE_UPD_CAP : 0u)) : 0u>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
     uint32_t *lcnt = bins + PPE_NBINS;       // [32] per-reason counters of this workgroup
+    uint32_t *ucur = smem + L::QUEUE / 4u;   // FLOW: [PPE_UPD_OWNERS] entries in this workgroup's owner buckets
+    uint32_t *ubuf = ucur + PPE_UPD_OWNERS;  // FLOW, PPE_UPD_LDS: [PPE_UPD_OWNERS][PPE_UPD_CAP] the buckets
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1383,6 +1518,8 @@ void ppe_classify_kernel(ppe_kargs a) {
     if (have) load_tile(wtile);
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
+    if constexpr (FLOW)
+        for (uint32_t i = tid; i < PPE_UPD_OWNERS; i += BLOCK) ucur[i] = 0;
     if constexpr (PC) {  // the tile queue's flags: ready[s] = none, free[s] = s (slot s takes ticket s first), tickets 0
         uint32_t *qf = smem + (L::QUEUE + PPE_PC_Q * PC_SLOT_BYTES) / 4u;
         for (uint32_t i = tid; i < 2u * PPE_PC_Q + 2u; i += BLOCK)
@@ -1398,9 +1535,8 @@ void ppe_classify_kernel(ppe_kargs a) {
                         a.off_bsec, a.off_blocks, a.max_bdepth, a.off_crec, a.off_idtab, a.crec_lds, a.idtab_lds};
 
     const uint64_t act_table = make_act_table(a.unsup_fw);
-    // this batch's creator count, summed by the resolve kernel (which runs after this one)
+    // (this batch's creator counter was zeroed by the previous batch's finalize launch)
     if (FLOW && blockIdx.x == 0 && tid == 0) {
-        a.flow.ctl[PPE_FCTL_BATCH_NEW] = 0;
         // the table state after the previous batches, for the host's bounds (zero-copy, no stream stall); LIVE is
         // stable here (the previous batch's finalize has completed, this batch's has not started), so it is also
         // the finalize kernel's overflow reference
@@ -1442,8 +1578,21 @@ void ppe_classify_kernel(ppe_kargs a) {
         }
 
         if (FLOW) {
-            // pending packets: key + provisional status (NO_SYN / ACL_DROP / ACL_FW = would create the flow)
-            if (pend) gst<uint4>(a.flow.rec, 16u * p, make_uint4(k.sip, k.dip, k.sport | (k.dport << 16), k.proto | (st << 8)));
+            // pending packets: key + provisional status (NO_SYN / ACL_DROP / ACL_FW = would create the flow); a would-be
+            // creator claims its flow's slot here (flow_claim), its record stored first for the joiners of its claim
+            const uint4 rq = make_uint4(k.sip, k.dip, k.sport | (k.dport << 16), k.proto | (st << 8));
+            const bool claim = pend && st == PPE_ST_ACL_FW;
+            if (claim) rec_store_shared(a.flow.rec, p, rq);
+            else if (pend) gst<uint4>(a.flow.rec, 16u * p, rq);
+            if (__builtin_amdgcn_ballot_w64(claim)) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                bool won = false;
+                if (claim) a.flow.rslot[p] = flow_claim(a.flow, p, rq, won);
+                const uint64_t wb = __builtin_amdgcn_ballot_w64(won);
+                if (lane == 0 && wb)
+                    __hip_atomic_fetch_add(&a.flow.ctl[fctl_new(a.flow.parity)], (unsigned long long)__popcll(wb),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             const uint64_t pm = __builtin_amdgcn_ballot_w64(pend);
             if (lane == 0) {
                 a.flow.tile_miss[tile] = pm;
@@ -1494,7 +1643,8 @@ void ppe_classify_kernel(ppe_kargs a) {
             uint32_t fsip = 0, fports = 0;
             const int32_t s = flow_find(a.flow, fh, k.sip, k.dip, ports, k.proto, fsip, fports);
             if (s >= 0) {  // found: STAT_ACL_FW without an ACL lookup, then FlowHandlePacket's accounting
-                if (valid) k.flags |= flow_account(a.flow, (uint32_t)s, fsip, fports, k.sip, ports, wlen, a.now);
+                if (valid)
+                    k.flags |= flow_found(a.flow, ucur, ubuf, (uint32_t)s, fsip, fports, k.sip, ports, wlen, a.now);
                 k.st = PPE_ST_ACL_FW;
             } else {
                 pend = valid;
@@ -2016,6 +2166,18 @@ void ppe_classify_kernel(ppe_kargs a) {
             for (uint32_t cb = bin_counters(b, act_table); cb; cb &= cb - 1u) atomicAdd(&lcnt[__builtin_ctz(cb)], c);
         }
     }
+    if (FLOW && blockIdx.x < a.flow.upd_wgs) {  // this workgroup's row of bucket counts, for the update kernel
+        for (uint32_t o = tid; o < a.flow.upd_owners; o += BLOCK)
+            a.flow.ucnt[(size_t)blockIdx.x * a.flow.upd_owners + o] = min(ucur[o], PPE_UPD_CAP);
+        if (upd_small(a.flow)) {  // the LDS buckets: 16 lanes write one bucket's 64 B
+            uint32_t *ub = (uint32_t *)a.flow.upd;
+            for (uint32_t i = tid; i < a.flow.upd_owners * PPE_UPD_CAP; i += BLOCK) {
+                const uint32_t o = i / PPE_UPD_CAP, e = i % PPE_UPD_CAP;
+                if (e < ucur[o])
+                    ub[((size_t)o * a.flow.upd_wgs + blockIdx.x) * PPE_UPD_CAP + e] = ubuf[i];
+            }
+        }
+    }
     __syncthreads();
     // this workgroup's own counter slot: a returnless add (uncontended; the wave does not wait on it)
     if (tid < PPE_C__COUNT && lcnt[tid])
@@ -2031,21 +2193,16 @@ void ppe_classify_kernel(ppe_kargs a) {
 // syn_check and the ACL (provisional status ACL_FW) creates the flow; the packets before it keep their own miss
 // verdict, the packets after it find the flow.  When the pool runs out, creators beyond the free count (in packet
 // order) fail with FLOW_NOMEM, and so do the later would-be creators of their flows.
-//   claim     pending would-be creators claim one slot per 5-tuple (CAS EMPTY → PEND | index, or join the claim of
-//             an equal key found on the probe path) and lower the slot's creator index (atomicMin);
-//   resolve   every pending packet finds its flow's claimed slot (rslot) and whether it is the creator;
-//   revoke    (only when the pool overflows; finalize's workgroup 0, the others wait on its flag) ranks the
-//             creators in packet order and revokes those past the free count;
-//   finalize  final verdicts of the pending packets, flow creation and accounting, the tile's compaction and the
-//             pending packets' counters.
+//   claim     (inside the classify launch, flow_claim) pending would-be creators claim one slot per 5-tuple (CAS
+//             EMPTY → PEND | index, or join the claim of an equal key found on the probe path) and lower the slot's
+//             creator index (atomicMin); the winning CASes are the batch's creator count;
+//   revoke    (finalize's prologue, only when the pool overflows) every workgroup marks its tiles' creators, then
+//             workgroup 0 ranks them in packet order and revokes those past the free count, the others waiting on
+//             its flag;
+//   finalize  per pending packet the flow's claimed slot (the claimer's own, else found, flow_find_claim), final
+//             verdicts, flow creation and accounting, the tile's compaction and the pending packets' counters;
+//   update    (ppe_flow_update_kernel, owner-computed) the found flows' counters and last-seen times.
 
-__device__ __forceinline__ bool rec_match(const uint4 &q, const uint4 &r) {
-    return ((q.w ^ r.w) & 0xffu) == 0u && key_match(q.x, q.y, q.z, r.x, r.y, r.z);
-}
-// flow_hashfn of a record / key (TCP or UDP only reach the flow table); symmetric, so either orientation
-__device__ __forceinline__ uint32_t key_hash(uint32_t sip, uint32_t dip, uint32_t ports, uint32_t proto) {
-    return flow_hashfn_l4(proto == 6u, sip, dip, ports & 0xffffu, ports >> 16);
-}
 
 struct TileWalk {  // persistent grid: wave gw of W takes the listed tiles gw, gw + W, ... (tiles with pending packets)
     uint32_t lane, gw, W, count;
@@ -2066,90 +2223,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void ppe_flow_claim_kernel(ppe_flow_kargs a) {
-    const TileWalk w = TileWalk::make<BLOCK>(a.f);
-    const uint4 *rec = (const uint4 *)a.f.rec;
-    for (uint32_t i = w.gw; i < w.count; i += w.W) {
-        const uint32_t t = a.f.miss_tiles[i];
-        const uint64_t mask = a.f.tile_miss[t];
-        if (!((mask >> w.lane) & 1ull)) continue;
-        const uint32_t p = (t << 6) + w.lane;
-        const uint4 r = rec[p];
-        if (((r.w >> 8) & 0xffu) != PPE_ST_ACL_FW) continue;  // only a packet that would create its flow claims
-        uint32_t g = key_hash(r.x, r.y, r.z, r.w & 0xffu) & a.f.gmask;
-        bool done = false;
-#pragma unroll 1
-        for (uint32_t it = 0; it <= a.f.gmask && !done; ++it) {
-#pragma unroll 1
-            for (uint32_t j = 0; j < PPE_FLOW_GROUP && !done; ++j) {
-                const uint32_t s = PPE_FLOW_GROUP * g + j;
-                uint32_t *sw = a.f.keys + (size_t)PPE_FLOW_SLOT_WORDS * s + 3u;
-                uint32_t st = __hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (st == PPE_FS_EMPTY) {
-                    uint32_t expect = PPE_FS_EMPTY;
-                    if (__hip_atomic_compare_exchange_strong(sw, &expect, PPE_FS_PEND | p, __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        atomicMin(&a.f.creator[s], p);
-                        done = true;
-                        break;
-                    }
-                    st = expect;  // claimed meanwhile (by this flow or another)
-                }
-                if ((st & PPE_FS_PEND) && rec_match(rec[st & ~PPE_FS_PEND], r)) {
-                    atomicMin(&a.f.creator[s], p);
-                    done = true;
-                }
-            }
-            g = (g + 1u) & a.f.gmask;
-        }
-    }
-}
-
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void ppe_flow_resolve_kernel(ppe_flow_kargs a) {
-    const TileWalk w = TileWalk::make<BLOCK>(a.f);
-    const uint4 *rec = (const uint4 *)a.f.rec;
-    uint32_t creators = 0;
-    for (uint32_t i = w.gw; i < w.count; i += w.W) {
-        const uint32_t t = a.f.miss_tiles[i];
-        const uint64_t mask = a.f.tile_miss[t];
-        const uint32_t p = (t << 6) + w.lane;
-        bool is_new = false;
-        if ((mask >> w.lane) & 1ull) {
-            const uint4 r = rec[p];
-            uint32_t g = key_hash(r.x, r.y, r.z, r.w & 0xffu) & a.f.gmask, found = PPE_FLOW_NONE;
-            bool stop = false;
-#pragma unroll 1
-            for (uint32_t it = 0; it <= a.f.gmask && !stop; ++it) {
-#pragma unroll 1
-                for (uint32_t j = 0; j < PPE_FLOW_GROUP && !stop; ++j) {
-                    const uint32_t s = PPE_FLOW_GROUP * g + j;
-                    const uint32_t st = a.f.keys[(size_t)PPE_FLOW_SLOT_WORDS * s + 3u];
-                    if (st == PPE_FS_EMPTY) stop = true;
-                    else if ((st & PPE_FS_PEND) && rec_match(rec[st & ~PPE_FS_PEND], r)) {
-                        found = s;
-                        stop = true;
-                    }
-                }
-                g = (g + 1u) & a.f.gmask;
-            }
-            a.f.rslot[p] = found;
-            is_new = found != PPE_FLOW_NONE && a.f.creator[found] == p;
-        }
-        const uint64_t bn = __builtin_amdgcn_ballot_w64(is_new);
-        if (w.lane == 0) a.f.tile_new[t] = bn;
-        creators += (uint32_t)__popcll(bn);
-    }
-    if (w.lane == 0 && creators)
-        __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_BATCH_NEW], (unsigned long long)creators, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Revoke (finalize's workgroup 0, when the batch's creators overflow the pool): rank the creators in packet order
-// (tile counts, block scan over the workgroup) and mark the ones past the free count revoked.  The creator words go
-// out as sc1 stores and the other workgroups read them with sc1 loads after the flag (MI355X_MICROARCH.md hand-off
-// forms; until round 3 this was a one-workgroup launch of its own between resolve and finalize).
+// (tile masks marked by every finalize workgroup, block scan over the workgroup) and mark the ones past the free
+// count revoked.  The creator words go out as sc1 stores and the other workgroups read them with sc1 loads after the
+// flag (MI355X_MICROARCH.md hand-off forms; until round 3 this was a one-workgroup launch of its own, until round 4
+// a resolve launch marked the creators).
 template <int BLOCK>
 __device__ __forceinline__ void flow_revoke(const ppe_flow_kargs &a, uint32_t *part, unsigned long long room) {
     const uint32_t tid = threadIdx.x, ntiles = (a.n + 63u) >> 6;
@@ -2188,26 +2266,66 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
     for (uint32_t i = tid; i < PPE_NBINS; i += BLOCK) bins[i] = 0;
     if (tid < 32u) lcnt[tid] = 0;
     // revoke: when the host's bound says the pool may overflow, every workgroup checks the exact counts; on an
-    // overflow workgroup 0 (dispatched first, so resident while the others wait) ranks and revokes, then publishes
-    // this batch's sequence number, which the others poll for (bounded) before reading any creator word.  The
-    // decision and the room come from words no finalize workgroup changes (LIVE_AT_BATCH, written by this batch's
-    // classify launch; BATCH_NEW, summed by the resolve launch), so a workgroup dispatched after others have finished
-    // and added their creations to LIVE decides exactly as workgroup 0 did.
+    // overflow every workgroup marks the creators of its miss tiles (tile_new) and arrives on a counter, workgroup 0
+    // (dispatched first) waits for all arrivals (the grid, at most two workgroups per CU, is resident), ranks and
+    // revokes, then publishes this batch's sequence number, which the others poll for (bounded) before reading any
+    // creator word.  The decision and the room come from words no finalize workgroup changes (LIVE_AT_BATCH, written
+    // by this batch's classify launch; the creator count, summed by it), so a workgroup dispatched after others have
+    // finished and added their creations to LIVE decides exactly as workgroup 0 did.
     if (tid == 0) {
         rev_s = 0u;
         if (a.revoke) {
             const unsigned long long live = __hip_atomic_load(&a.f.ctl[PPE_FCTL_LIVE_AT_BATCH], __ATOMIC_RELAXED,
                                                               __HIP_MEMORY_SCOPE_AGENT),
-                                     cr = __hip_atomic_load(&a.f.ctl[PPE_FCTL_BATCH_NEW], __ATOMIC_RELAXED,
+                                     cr = __hip_atomic_load(&a.f.ctl[fctl_new(a.f.parity)], __ATOMIC_RELAXED,
                                                             __HIP_MEMORY_SCOPE_AGENT);
             rev_s = live + cr > a.f.capacity ? 1u : 0u;
             room_s = a.f.capacity > live ? a.f.capacity - live : 0ull;
         }
+        // the next batch's creator counter (last used by the previous batch, whose kernels have all completed)
+        if (blockIdx.x == 0) a.f.ctl[fctl_new(a.f.parity ^ 1u)] = 0;
     }
     __syncthreads();
     const bool rev = rev_s != 0u;
     if (rev) {
+        {  // mark this workgroup's miss tiles' creators: the claimers (ACL_FW) whose index is their slot's creator
+            const TileWalk w = TileWalk::make<BLOCK>(a.f);
+            const uint4 *rec = (const uint4 *)a.f.rec;
+            for (uint32_t i = w.gw; i < w.count; i += w.W) {
+                const uint32_t t = a.f.miss_tiles[i];
+                const uint64_t mask = a.f.tile_miss[t];
+                const uint32_t p = (t << 6) + w.lane;
+                bool is_new = false;
+                if ((mask >> w.lane) & 1ull) {
+                    if (((rec[p].w >> 8) & 0xffu) == PPE_ST_ACL_FW) {
+                        const uint32_t sl = a.f.rslot[p];
+                        is_new = sl != PPE_FLOW_NONE && a.f.creator[sl] == p;
+                    }
+                }
+                const uint64_t bn = __builtin_amdgcn_ballot_w64(is_new);
+                if (w.lane == 0) a.f.tile_new[t] = bn;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_ARRIVE], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
         if (blockIdx.x == 0) {
+            if (tid == 0) {  // every workgroup's marks, then the counter back to 0 for the next overflow batch
+                uint32_t k = 0;
+                for (; k < (1u << 24) && __hip_atomic_load(&a.f.ctl[PPE_FCTL_ARRIVE], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) < gridDim.x; ++k)
+                    __builtin_amdgcn_s_sleep(8);
+                if (k == (1u << 24))
+                    __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_ERR], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&a.f.ctl[PPE_FCTL_ARRIVE], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
             // producer (MI355X_MICROARCH.md, inter-workgroup visibility): every storing wave drains, workgroup
             // barrier, one lane's agent release, then the flag
             flow_revoke<BLOCK>(a, part, room_s);
@@ -2252,7 +2370,9 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
             const uint4 r = rec[p];
             const uint32_t prov = (r.w >> 8) & 0xffu;
             uint32_t st = prov, flags = v >> 16;
-            const uint32_t s = a.f.rslot[p];
+            // the flow's claimed slot: the claimer's own (classify launch), else found here (a revoked claim's
+            // tombstone reads as "not found", which for a packet that did not claim gives the same verdict)
+            const uint32_t s = prov == PPE_ST_ACL_FW ? a.f.rslot[p] : flow_find_claim(a.f, r);
             if (s != PPE_FLOW_NONE) {
                 const uint32_t cw = rev ? __hip_atomic_load(&a.f.creator[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                         : a.f.creator[s];
@@ -2267,7 +2387,8 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
                         st = PPE_ST_ACL_FW;
                         is_new = true;
                         flags |= PPE_F_NEWFLOW | flow_account(a.f, s, r.x, r.z, r.x, r.z, a.len[p], a.now);
-                        ((uint4 *)a.f.keys)[2ull * s] = make_uint4(r.x, r.y, r.z, PPE_FS_LIVE(r.w & 0xffu));
+                        ((uint4 *)a.f.keys)[(size_t)(PPE_FLOW_SLOT_WORDS / 4u) * s] =
+                            make_uint4(r.x, r.y, r.z, PPE_FS_LIVE(r.w & 0xffu));
                     }
                 } else if (p > c) {
                     if (rev) {
@@ -2310,6 +2431,129 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// FlowUpdate + FLOW_UPDATE_TIMESTAMP of the found packets (flow.c:163-178), owner-computed: workgroup o owns the
+// slots [o << upd_osh, (o + 1) << upd_osh), reads its bucket of every classify workgroup's column, sums the entries
+// per (slot, direction) in an LDS hash, then updates each touched slot once: plain read-modify-write of the packed
+// counters (no other workgroup touches them in this launch; the finalize launch only touches slots claimed in this
+// batch, never a found flow's), the fold into the wide counters, the last-seen time.  One update per flow and
+// direction instead of one memory-side atomic and one last-seen store per packet.  A slot the full hash cannot take
+// is updated by the atomic path directly.
+// PPE_UPD_AB (diagnostic builds only, wrong outputs): 1 = no apply phase, 2 = no gather phase either
+#ifndef PPE_UPD_AB
+#define PPE_UPD_AB 0
+#endif
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ppe_flow_update_kernel(ppe_flow_kargs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t usm[];
+    constexpr uint32_t HC = PPE_UPD_HASH, HB = 12;  // HC = 2^HB
+    static_assert(HC == (1u << HB) && HC % BLOCK == 0, "hash geometry");
+    // per entry: slot + 1 (0 = empty), then per direction the packets (u32) and the bytes (u64, no field limit)
+    uint32_t *hkey = usm;                                             // [HC]
+    uint32_t *hpk = usm + HC;                                         // [2][HC]
+    unsigned long long *hby = (unsigned long long *)(usm + 3u * HC);  // [2][HC]
+    const ppe_flowdev &f = a.f;
+    const uint32_t o = blockIdx.x, tid = threadIdx.x;
+    const unsigned long long bmask = (1ull << PPE_PK_SHIFT) - 1u;
+    for (uint32_t i = tid; i < HC; i += BLOCK) {
+        hkey[i] = 0u;
+        hpk[i] = hpk[HC + i] = 0u;
+        hby[i] = hby[HC + i] = 0ull;
+    }
+    __syncthreads();
+    // a slot's update the direct way (the hash is full): flow_account's atomic and fold, the last-seen store
+    auto direct = [&](uint32_t s, uint32_t d, uint32_t len) {
+        unsigned long long *pk = f.packed + (size_t)PPE_FLOW_REC_WORDS * s + d;
+        const unsigned long long inc = (1ull << PPE_PK_SHIFT) | (unsigned long long)len;
+        const unsigned long long nv = __hip_atomic_fetch_add(pk, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + inc;
+        if ((nv >> PPE_PK_SHIFT) >= f.fold_pkts || (nv & bmask) >= f.fold_bytes) {
+            const unsigned long long x = __hip_atomic_exchange(pk, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned long long *wd = f.stats + 4ull * s + 2u * d;
+            __hip_atomic_fetch_add(wd, x >> PPE_PK_SHIFT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(wd + 1, x & bmask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        f.packed[(size_t)PPE_FLOW_REC_WORDS * s + PPE_FLOW_REC_LAST] = a.now;
+    };
+    const uint32_t ncol = (PPE_UPD_AB & 2) ? 0u : min(f.upd_grid, f.upd_wgs);
+    for (uint32_t w = tid; w < ncol; w += BLOCK) {
+        const uint32_t n = min(f.ucnt[(size_t)w * f.upd_owners + o], PPE_UPD_CAP);
+        // the bucket is one 64-B (4-B entries) or 128-B segment: every entry's load issued before any is used
+        const bool sm = upd_small(f);
+        const size_t bk = (size_t)o * f.upd_wgs + w;
+        const uint4 *e = sm ? (const uint4 *)((const uint32_t *)f.upd + bk * PPE_UPD_CAP)
+                            : (const uint4 *)(f.upd + bk * PPE_UPD_CAP);
+        uint4 v[PPE_UPD_CAP / 2];
+#pragma unroll
+        for (uint32_t q = 0; q < PPE_UPD_CAP / 2; ++q)
+            v[q] = (sm ? 4u * q : 2u * q) < n ? e[q] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (uint32_t i = 0; i < PPE_UPD_CAP; ++i) {
+            if (i >= n) continue;  // (not break: the loop must unroll, v[] stays in registers)
+            uint32_t s, d, len;
+            if (sm) {
+                const uint4 q = v[i >> 2];
+                const uint32_t x = (i & 3u) == 0u ? q.x : (i & 3u) == 1u ? q.y : (i & 3u) == 2u ? q.z : q.w;
+                s = (o << f.upd_osh) | (x >> 17);
+                d = (x >> 16) & 1u;
+                len = x & 0xffffu;
+            } else {
+                s = (i & 1u) ? v[i >> 1].z : v[i >> 1].x;
+                const uint32_t hi = (i & 1u) ? v[i >> 1].w : v[i >> 1].y;
+                d = hi >> 31;
+                len = hi & 0x7fffffffu;
+            }
+            uint32_t h = ((s * 0x9E3779B1u) >> (32 - HB)) & f.upd_hmask;
+            bool done = false;
+            for (uint32_t t = 0; t <= f.upd_hmask && !done; ++t) {
+                const uint32_t prev = atomicCAS(&hkey[h], 0u, s + 1u);
+                if (prev == 0u || prev == s + 1u) {
+                    atomicAdd(&hpk[d * HC + h], 1u);
+                    atomicAdd(&hby[d * HC + h], (unsigned long long)len);
+                    done = true;
+                } else {
+                    h = (h + 1u) & f.upd_hmask;
+                }
+            }
+            if (!done) direct(s, d, len);
+        }
+    }
+    __syncthreads();
+    if (PPE_UPD_AB) return;
+    // each touched slot once: both directions' packed words in one 16-B read-modify-write, then the last-seen time
+    constexpr uint32_t PER = HC / BLOCK;
+    uint32_t ks[PER];
+    ulonglong2 old[PER];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        ks[j] = hkey[tid + j * BLOCK];
+        old[j] = ks[j] ? *(const ulonglong2 *)(f.packed + (size_t)PPE_FLOW_REC_WORDS * (ks[j] - 1u))
+                       : make_ulonglong2(0ull, 0ull);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        if (!ks[j]) continue;
+        const uint32_t h = tid + j * BLOCK, s = ks[j] - 1u;
+        unsigned long long nw[2] = {old[j].x, old[j].y};
+#pragma unroll
+        for (uint32_t d = 0; d < 2u; ++d) {
+            const uint32_t np = hpk[d * HC + h];
+            if (!np) continue;
+            const unsigned long long p = (nw[d] >> PPE_PK_SHIFT) + np, b = (nw[d] & bmask) + hby[d * HC + h];
+            if (p >= f.fold_pkts || b >= f.fold_bytes) {  // the fold: into the wide counters, the packed word to 0
+                unsigned long long *wd = f.stats + 4ull * s + 2u * d;
+                wd[0] += p;
+                wd[1] += b;
+                nw[d] = 0ull;
+            } else {
+                nw[d] = (p << PPE_PK_SHIFT) | b;
+            }
+        }
+        // the whole 32-B record: both directions, the last-seen time (one line per flow)
+        ulonglong2 *rp = (ulonglong2 *)(f.packed + (size_t)PPE_FLOW_REC_WORDS * s);
+        upd_st(rp, make_ulonglong2(nw[0], nw[1]));
+        upd_st(rp + 1, make_ulonglong2((unsigned long long)a.now, 0ull));
+    }
+}
+
 // FlowTimeOut + FlowAgeTimeoutCB (flow.c:391-467): live flows idle for more than `timeout` become tombstones.
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ppe_flow_age_kernel(ppe_flow_kargs a) {
@@ -2318,13 +2562,13 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_age_kernel(ppe_flow_kargs a) {
         uint32_t *rw = a.f.keys + (size_t)PPE_FLOW_SLOT_WORDS * s;
         const uint32_t st = rw[3];
         if ((st & (PPE_FS_PEND | 0xffu)) != PPE_FS_LIVE(0u)) continue;
-        const uint64_t l = *(const unsigned long long *)(rw + PPE_FLOW_LAST_WORD);
+        const uint64_t l = a.f.packed[(size_t)PPE_FLOW_REC_WORDS * s + PPE_FLOW_REC_LAST];
         if (a.now > l && a.now - l > a.timeout) {
             rw[3] = PPE_FS_TOMB;
             ((uint4 *)a.f.stats)[2ull * s] = make_uint4(0u, 0u, 0u, 0u);
             ((uint4 *)a.f.stats)[2ull * s + 1u] = make_uint4(0u, 0u, 0u, 0u);
-            ((uint4 *)a.f.packed)[s] = make_uint4(0u, 0u, 0u, 0u);
-            *(unsigned long long *)(rw + PPE_FLOW_LAST_WORD) = 0ull;
+            ((uint4 *)a.f.packed)[(size_t)(PPE_FLOW_REC_WORDS / 2u) * s] = make_uint4(0u, 0u, 0u, 0u);
+            ((uint4 *)a.f.packed)[(size_t)(PPE_FLOW_REC_WORDS / 2u) * s + 1u] = make_uint4(0u, 0u, 0u, 0u);
             ++del;
         }
     }
@@ -2343,7 +2587,7 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_age_kernel(ppe_flow_kargs a) {
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ppe_flow_rehash_kernel(ppe_flow_kargs a) {
     for (uint32_t s = blockIdx.x * BLOCK + threadIdx.x; s < a.nslots; s += gridDim.x * BLOCK) {
-        const uint4 k = ((const uint4 *)a.f.keys)[2ull * s], kl = ((const uint4 *)a.f.keys)[2ull * s + 1u];
+        const uint4 k = ((const uint4 *)a.f.keys)[(size_t)(PPE_FLOW_SLOT_WORDS / 4u) * s];
         if ((k.w & (PPE_FS_PEND | 0xffu)) != PPE_FS_LIVE(0u)) continue;
         uint32_t g = key_hash(k.x, k.y, k.z, (k.w >> 8) & 0xffu) & a.dst.gmask;
         bool done = false;
@@ -2359,10 +2603,12 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_rehash_kernel(ppe_flow_kargs a
                     dw[0] = k.x;
                     dw[1] = k.y;
                     dw[2] = k.z;
-                    ((uint4 *)dw)[1] = kl;  // last-seen
                     ((uint4 *)a.dst.stats)[2ull * d] = ((const uint4 *)a.f.stats)[2ull * s];
                     ((uint4 *)a.dst.stats)[2ull * d + 1u] = ((const uint4 *)a.f.stats)[2ull * s + 1u];
-                    ((uint4 *)a.dst.packed)[d] = ((const uint4 *)a.f.packed)[s];
+                    ((uint4 *)a.dst.packed)[(size_t)(PPE_FLOW_REC_WORDS / 2u) * d] =
+                        ((const uint4 *)a.f.packed)[(size_t)(PPE_FLOW_REC_WORDS / 2u) * s];
+                    ((uint4 *)a.dst.packed)[(size_t)(PPE_FLOW_REC_WORDS / 2u) * d + 1u] =
+                        ((const uint4 *)a.f.packed)[(size_t)(PPE_FLOW_REC_WORDS / 2u) * s + 1u];
                     done = true;
                 }
             }
@@ -2516,15 +2762,17 @@ static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t
 }
 
 template <int M, int P, int B>
-static int occ_t(size_t shmem) {
+static int occ_t(size_t shmem, bool flow = false) {
     int nb = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, P, B, false>, B, shmem) ==
-                   hipSuccess
-               ? nb : -1;
+    const hipError_t e =
+        flow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, PF_HOIST, B, true>, B, shmem)
+             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, P, B, false>, B, shmem);
+    return e == hipSuccess ? nb : -1;
 }
 
-static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block) {
-    const size_t base = ppe_classify_fixed_lds(block, pipe, mode);  // key slots (node walks) + counter bins
+static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block, bool flow = false) {
+    // key slots (node walks) + counter bins (+ flow-table launches: the owner-update bucket cursors)
+    const size_t base = ppe_classify_fixed_lds(block, pipe, mode) + (flow ? ppe_flow_lds_extra() : 0u);
     if (mode == IMG_GLOBAL) return base;
     return base + (((size_t)lds_words * 4u + 1023u) & ~(size_t)1023u);
 }
@@ -2554,7 +2802,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block) 
 
 extern "C" int ppe_launch_classify(const ppe_kargs *a, uint32_t grid, int mode, int pipe, int block, int flow,
                                    void *stream, void *ev_start, void *ev_stop) {
-    const size_t shmem = classify_shmem(a->stage_words, mode, pipe, block);
+    const size_t shmem = classify_shmem(a->stage_words, mode, pipe, block, flow != 0);
     hipStream_t s = (hipStream_t)stream;
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     PPE_DISPATCH(launch_t, a, grid, shmem, s, e0, e1, flow);
@@ -2564,8 +2812,9 @@ extern "C" int ppe_launch_flow(int kind, const ppe_flow_kargs *a, uint32_t grid,
     const hipStream_t s = (hipStream_t)stream;
     const dim3 g(grid), b(PPE_FLOW_BLOCK);
     switch (kind) {
-        case PPE_FLOW_K_CLAIM: hipLaunchKernelGGL(ppe_flow_claim_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
-        case PPE_FLOW_K_RESOLVE: hipLaunchKernelGGL(ppe_flow_resolve_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
+        case PPE_FLOW_K_UPDATE:
+            hipLaunchKernelGGL(ppe_flow_update_kernel<1024>, g, dim3(1024), PPE_UPD_HASH * 28u, s, *a);
+            break;
         case PPE_FLOW_K_FINALIZE: hipLaunchKernelGGL(ppe_flow_finalize_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
         case PPE_FLOW_K_AGE: hipLaunchKernelGGL(ppe_flow_age_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
         case PPE_FLOW_K_REHASH: hipLaunchKernelGGL(ppe_flow_rehash_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
@@ -2579,6 +2828,19 @@ extern "C" int ppe_classify_occupancy(uint32_t lds_words, int mode, int pipe, in
     const size_t shmem = classify_shmem(lds_words, mode, pipe, block);
     PPE_DISPATCH(occ_t, shmem);
 }
+// the same for the flow-table variant (its own waves per SIMD and LDS)
+extern "C" int ppe_classify_occupancy_flow(uint32_t lds_words, int mode, int block) {
+    const int pipe = PF_HOIST;
+    const size_t shmem = classify_shmem(lds_words, mode, pipe, block, true);
+    PPE_DISPATCH(occ_t, shmem, true);
+}
+
+// classify LDS of a flow-table launch beyond the stateless kernel's: the owner-update bucket cursors (and buckets)
+extern "C" uint32_t ppe_flow_lds_extra() {
+    return 4u * PPE_UPD_OWNERS + (PPE_UPD_LDS ? 4u * PPE_UPD_OWNERS * PPE_UPD_CAP : 0u);
+}
+// waves per SIMD the flow-table classify kernel is compiled for (its LDS share per workgroup)
+extern "C" uint32_t ppe_flow_waves() { return PPE_FLOW_WAVES; }
 
 // LDS of a workgroup besides the staged image: the per-wave key slots of node walks and the counter bins.  Block
 // walks (the multi-tile kernel; the single-tile kernel over a whole-LDS image) keep the keys in registers.

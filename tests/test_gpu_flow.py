@@ -164,14 +164,20 @@ def test_flow_aging_and_rehash(eng):
         p.close()
 
 
-def test_flow_counter_folding(monkeypatch):
+@pytest.mark.parametrize("capacity,uhash", [(10000, 0), (1 << 17, 0), (10000, 1)])
+def test_flow_counter_folding(monkeypatch, capacity, uhash):
     """The packed per-flow counters fold into the wide ones when a field passes its threshold (lowered here to a few
-    packets / bytes so every flow folds many times); totals stay exact under concurrent folds."""
+    packets / bytes so every flow folds many times); totals stay exact under concurrent folds.  The small pool makes
+    every batch a possible overflow (finalize checks the exact counts), the large one never.  uhash: the update
+    kernel's LDS hash cut to one entry, so every flow after the first of its owner takes the full-hash path (direct
+    atomics)."""
     monkeypatch.setenv("PPE_FLOW_FOLD_PKTS", "3")
     monkeypatch.setenv("PPE_FLOW_FOLD_BYTES", "500")
+    if uhash:
+        monkeypatch.setenv("PPE_FLOW_UPD_HASH", str(uhash))
     e = Engine(0)
     rules = synth.make_rules(16, seed=24)
-    p = Pair(e, rules, capacity=10000, max_batch=1 << 15, default_action=0)
+    p = Pair(e, rules, capacity=capacity, max_batch=1 << 15, default_action=0)
     try:
         for b in range(3):
             pk = synth.make_flow_packets(30000, rules, n_flows=300, seed=400 + b, template_seed=400, syn_frac=0.9)

@@ -1,0 +1,19 @@
+# round 4: F1 without the resolve launch (claims and creator count in classify, finalize marks creators on overflow)
+# + owner-computed FlowUpdate (libppe_hip_owner.so): flow tests both update modes, kernel trace, F1 A/B vs product
+set -o pipefail
+O=gpurun_out/${1:-r4f}
+mkdir -p $O
+L=packet-process-engine_amd
+NEW=$L/libppe_hip_owner.so
+PPE_LIB=$NEW timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_flow.py \
+  tests/test_gpu_steer.py > $O/pytest_flow_owner.txt 2>&1 || exit 1
+PPE_LIB=$NEW PPE_FLOW_OWNER=0 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+  tests/test_gpu_flow.py > $O/pytest_flow_atomic.txt 2>&1 || exit 1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+PPE_LIB=$NEW timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_owner -o k -- \
+  python3 bench.py --config F1 --steps 16 --warmup 4 --no-cpu-baseline > $O/kt_owner.log 2>&1 || exit 1
+for i in 1 2; do
+  PPE_LIB=$L/libppe_hip.so timeout -k 10 200 python bench.py --config F1 --no-cpu-baseline > $O/f1_base_$i.json 2> $O/f1_base_$i.err || exit 1
+  PPE_LIB=$NEW PPE_FLOW_OWNER=0 timeout -k 10 200 python bench.py --config F1 --no-cpu-baseline > $O/f1_atomic_$i.json 2> $O/f1_atomic_$i.err || exit 1
+  PPE_LIB=$NEW timeout -k 10 200 python bench.py --config F1 --no-cpu-baseline > $O/f1_owner_$i.json 2> $O/f1_owner_$i.err || exit 1
+done
