@@ -9,6 +9,7 @@
  *   - HIP-event kernel timing, and the pipelined host-buffer path (H2D → classify → D2H on 3 streams).
  */
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
@@ -90,6 +91,7 @@ struct FlowTable {
     // recorded on the stream right before each batch's classify launch: once it completes, that launch is the next
     // thing the stream runs, and its snapshot follows within microseconds (blocking-sync: the host sleeps on it)
     hipEvent_t pre_launch = nullptr;
+    bool use_event = true;
     // ring over the last kSnapRing batches: packets submitted before batch b (of batches that may revoke: _rev)
     static constexpr uint32_t kSnapRing = 4096;
     std::vector<uint64_t> cum_n, cum_rev;
@@ -1280,6 +1282,7 @@ int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
     c->flow = t;
     t->capacity = capacity;
     t->max_batch = max_batch;
+    t->use_event = env_int("PPE_FLOW_EVENT", 0) != 0;
     // test hook: lower fold thresholds so the fold path runs on small inputs (values <= the defaults only)
     const int fp = env_int("PPE_FLOW_FOLD_PKTS", 0), fb = env_int("PPE_FLOW_FOLD_BYTES", 0);
     if (fp > 0 && (unsigned long long)fp < t->fold_pkts) t->fold_pkts = (unsigned long long)fp;
@@ -1343,13 +1346,15 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         // The tombstone bound counts every packet of every batch since the snapshot as a possible revocation, so with
         // the host several batches ahead it passes the rehash threshold long before the table does.  Wait (bounded)
         // for the latest submitted batch's classify launch to publish its snapshot — one batch stays in flight, the
-        // queue does not drain — and decide on that tighter bound before synchronising.  The host sleeps on the
-        // event recorded just before that launch (no busy spin), then polls briefly, pausing, for the
-        // snapshot the launch's first workgroup writes as it starts.
-        HIPCHK(c, hipEventSynchronize(t.pre_launch));
+        // queue does not drain — and decide on that tighter bound before synchronising.  The host polls the snapshot
+        // the launch's first workgroup writes as it starts, yielding its core between polls (sched_yield: no busy
+        // spin), at most 20 ms.  Until round 4 it first slept on an event recorded before each classify
+        // launch; that marker cost the stream a 6-us gap per batch (PPE_FLOW_EVENT=1 restores it, for A/B).
+        if (t.use_event) HIPCHK(c, hipEventSynchronize(t.pre_launch));
         const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
         while (t.snap_used + 1u < t.batches && std::chrono::steady_clock::now() < until) {
-            __builtin_ia32_pause();
+            if (t.use_event) __builtin_ia32_pause();
+            else sched_yield();
             flow_apply_snapshot(t);
         }
     }
@@ -1357,7 +1362,7 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     if (rc != PPE_OK) return rc;
     const hipStream_t s = (hipStream_t)stream;
     const ppe_flowdev d = flow_dev(t, t.cur);
-    HIPCHK(c, hipEventRecord(t.pre_launch, s));
+    if (t.use_event) HIPCHK(c, hipEventRecord(t.pre_launch, s));
     // 1. decode, hash, FlowFind; found flows are forwarded and their updates logged to the owners' buckets, the
     // rest get syn_check + ACL (would-be creators claim their slots)
     uint32_t cgrid = 0;
@@ -1379,17 +1384,18 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     k.now = cfg ? cfg->now_seconds : 0u;
     k.nslots = t.nslots;
     k.cslots = c->d_cslots;
-    // grid-stride over the miss-tile list (usually short): a few workgroups per CU, not one per tile
-    const uint32_t fg = std::min(flow_grid(c, (in->n + 63u) / 64u, PPE_FLOW_BLOCK_WAVES), c->n_cu * 2u);
-    // 2. finalize (when the host's bound says the pool may overflow, it checks the exact counts and, on an overflow,
-    // marks the creators and has its workgroup 0 revoke those past the pool's room first), then 3. the found flows'
-    // counters and last-seen times, one workgroup per owner (disjoint from the slots finalize touches)
+    // 2. the post-classify launch: finalize (grid-stride over the miss-tile list, usually short: at most one
+    // workgroup per CU) and, beside it, the found flows' counters and last-seen times, one workgroup per owner
+    // (disjoint from the slots finalize touches).  When the host's bound says the pool may overflow, finalize checks
+    // the exact counts and, on an overflow, marks the creators and has its workgroup 0 revoke those past the pool's
+    // room first.
+    const uint32_t fg = std::min(flow_grid(c, (in->n + 63u) / 64u, PPE_FLOW_POST_BLOCK / 64u), c->n_cu);
     const bool may_overflow = t.live_ub + in->n > t.capacity;
     k.revoke = may_overflow ? 1u : 0u;
-    for (int kind : {PPE_FLOW_K_FINALIZE, PPE_FLOW_K_UPDATE}) {
-        if (kind == PPE_FLOW_K_UPDATE && !t.upd_wgs) continue;
-        const int e = ppe_launch_flow(kind, &k, kind == PPE_FLOW_K_UPDATE ? t.upd_owners : fg, (void *)s);
-        if (e != 0) return fail(c, PPE_EIO, "flow kernel %d launch failed: %s", kind, hipGetErrorString((hipError_t)e));
+    k.fin_wgs = fg;
+    {
+        const int e = ppe_launch_flow(PPE_FLOW_K_POST, &k, fg + (t.upd_wgs ? t.upd_owners : 0u), (void *)s);
+        if (e != 0) return fail(c, PPE_EIO, "flow post-classify launch failed: %s", hipGetErrorString((hipError_t)e));
     }
     t.cum_n[t.batches % FlowTable::kSnapRing] = t.tot_n;
     t.cum_rev[t.batches % FlowTable::kSnapRing] = t.tot_rev;

@@ -59,7 +59,8 @@ enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_N
  * atomic per packet; each owner's workgroup then sums its buckets in LDS and updates each touched slot once. */
 #define PPE_UPD_OWNERS 256u
 #define PPE_UPD_CAP 16u        /* entries per (owner, classify workgroup) bucket; a full bucket: the direct atomic */
-#define PPE_UPD_HASH 4096u     /* LDS hash entries of an owner workgroup (slots it accumulates; more: direct atomics) */
+#define PPE_UPD_HASH 2048u     /* LDS hash entries of an owner workgroup (slots it accumulates; more: direct atomics) */
+#define PPE_FLOW_POST_BLOCK 512 /* workgroup size of the post-classify launch (finalize + update) */
 struct ppe_flowdev {
     uint32_t *keys;               /* nslots × {sip, dip, sport | dport << 16, state, last-seen (u64), 0, 0}: the key in
                                      the creating packet's orientation                                                 */
@@ -103,6 +104,7 @@ struct ppe_flow_kargs {
     uint64_t timeout;             /* aging */
     uint32_t nslots;
     uint32_t revoke;              /* finalize: the host's bound says the pool may overflow (check, rank, revoke) */
+    uint32_t fin_wgs;             /* post-classify launch: workgroups [0, fin_wgs) finalize, the next upd_owners update */
     unsigned long long *cslots;   /* counter slots (one per workgroup) */
     struct ppe_flowdev dst;       /* rehash target */
 };
@@ -202,7 +204,7 @@ int ppe_launch_classify(const struct ppe_kargs *a, uint32_t grid, int mode, int 
                         void *stream, void *ev_start, void *ev_stop);
 /* flow-table phases after a flow-mode classify launch (stream order): claim, resolve, finalize (+ revoke in its
  * workgroup 0 when the pool overflows) */
-enum { PPE_FLOW_K_UPDATE = 0, PPE_FLOW_K_FINALIZE, PPE_FLOW_K_AGE, PPE_FLOW_K_REHASH };
+enum { PPE_FLOW_K_POST = 0, PPE_FLOW_K_AGE, PPE_FLOW_K_REHASH };
 int ppe_launch_flow(int kind, const struct ppe_flow_kargs *a, uint32_t grid, void *stream);
 #define PPE_FLOW_BLOCK 256      /* flow kernels' workgroup size */
 /* steering: 0 count, 1 scan (one workgroup), 2 scatter the permutation; rows: gather / scatter of fixed rows */

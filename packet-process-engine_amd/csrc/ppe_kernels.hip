@@ -2206,11 +2206,11 @@ void ppe_classify_kernel(ppe_kargs a) {
 
 struct TileWalk {  // persistent grid: wave gw of W takes the listed tiles gw, gw + W, ... (tiles with pending packets)
     uint32_t lane, gw, W, count;
-    template <int BLOCK> __device__ __forceinline__ static TileWalk make(const ppe_flowdev &f) {
+    template <int BLOCK> __device__ __forceinline__ static TileWalk make(const ppe_flowdev &f, uint32_t nwg) {
         TileWalk t;
         t.lane = threadIdx.x & 63u;
         t.gw = blockIdx.x * (BLOCK / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        t.W = gridDim.x * (BLOCK / 64);
+        t.W = nwg * (BLOCK / 64);
         t.count = (uint32_t)__hip_atomic_load(&f.ctl[PPE_FCTL_MISS0 + f.parity], __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
         return t;
@@ -2255,8 +2255,9 @@ __device__ __forceinline__ void flow_revoke(const ppe_flow_kargs &a, uint32_t *p
     }
 }
 
+// finalize, on the first nwg workgroups of the post-classify launch (ppe_flow_post_kernel)
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs a) {
+__device__ __forceinline__ void flow_finalize_wg(const ppe_flow_kargs &a, uint32_t nwg) {
     __shared__ uint32_t bins[PPE_NBINS];
     __shared__ uint32_t lcnt[32];
     __shared__ uint32_t part[BLOCK];
@@ -2289,7 +2290,7 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
     const bool rev = rev_s != 0u;
     if (rev) {
         {  // mark this workgroup's miss tiles' creators: the claimers (ACL_FW) whose index is their slot's creator
-            const TileWalk w = TileWalk::make<BLOCK>(a.f);
+            const TileWalk w = TileWalk::make<BLOCK>(a.f, nwg);
             const uint4 *rec = (const uint4 *)a.f.rec;
             for (uint32_t i = w.gw; i < w.count; i += w.W) {
                 const uint32_t t = a.f.miss_tiles[i];
@@ -2317,7 +2318,7 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
             if (tid == 0) {  // every workgroup's marks, then the counter back to 0 for the next overflow batch
                 uint32_t k = 0;
                 for (; k < (1u << 24) && __hip_atomic_load(&a.f.ctl[PPE_FCTL_ARRIVE], __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT) < gridDim.x; ++k)
+                                                           __HIP_MEMORY_SCOPE_AGENT) < nwg; ++k)
                     __builtin_amdgcn_s_sleep(8);
                 if (k == (1u << 24))
                     __hip_atomic_fetch_add(&a.f.ctl[PPE_FCTL_ERR], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2352,7 +2353,7 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
             __syncthreads();
         }
     }
-    const TileWalk w = TileWalk::make<BLOCK>(a.f);
+    const TileWalk w = TileWalk::make<BLOCK>(a.f, nwg);
     const uint4 *rec = (const uint4 *)a.f.rec;
     const uint64_t act_table = make_act_table(a.unsup_fw);
     uint32_t created = 0, revoked = 0;
@@ -2442,17 +2443,17 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_finalize_kernel(ppe_flow_kargs
 #ifndef PPE_UPD_AB
 #define PPE_UPD_AB 0
 #endif
+// (owner o's workgroup of the post-classify launch, ppe_flow_post_kernel; usm: its PPE_UPD_HASH * 28 B of LDS)
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void ppe_flow_update_kernel(ppe_flow_kargs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t usm[];
-    constexpr uint32_t HC = PPE_UPD_HASH, HB = 12;  // HC = 2^HB
+__device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t o, uint32_t *usm) {
+    constexpr uint32_t HC = PPE_UPD_HASH, HB = __builtin_ctz(PPE_UPD_HASH);  // HC = 2^HB
     static_assert(HC == (1u << HB) && HC % BLOCK == 0, "hash geometry");
     // per entry: slot + 1 (0 = empty), then per direction the packets (u32) and the bytes (u64, no field limit)
     uint32_t *hkey = usm;                                             // [HC]
     uint32_t *hpk = usm + HC;                                         // [2][HC]
     unsigned long long *hby = (unsigned long long *)(usm + 3u * HC);  // [2][HC]
     const ppe_flowdev &f = a.f;
-    const uint32_t o = blockIdx.x, tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x;
     const unsigned long long bmask = (1ull << PPE_PK_SHIFT) - 1u;
     for (uint32_t i = tid; i < HC; i += BLOCK) {
         hkey[i] = 0u;
@@ -2481,10 +2482,11 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_update_kernel(ppe_flow_kargs a
         const size_t bk = (size_t)o * f.upd_wgs + w;
         const uint4 *e = sm ? (const uint4 *)((const uint32_t *)f.upd + bk * PPE_UPD_CAP)
                             : (const uint4 *)(f.upd + bk * PPE_UPD_CAP);
+        // (the segment's loads do not wait for the count: a 4-B-entry bucket is read whole, 64 B, with it)
         uint4 v[PPE_UPD_CAP / 2];
 #pragma unroll
         for (uint32_t q = 0; q < PPE_UPD_CAP / 2; ++q)
-            v[q] = (sm ? 4u * q : 2u * q) < n ? e[q] : make_uint4(0u, 0u, 0u, 0u);
+            v[q] = (sm ? q < PPE_UPD_CAP / 4u : 2u * q < n) ? e[q] : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (uint32_t i = 0; i < PPE_UPD_CAP; ++i) {
             if (i >= n) continue;  // (not break: the loop must unroll, v[] stays in registers)
@@ -2552,6 +2554,16 @@ __global__ __launch_bounds__(BLOCK) void ppe_flow_update_kernel(ppe_flow_kargs a
         upd_st(rp, make_ulonglong2(nw[0], nw[1]));
         upd_st(rp + 1, make_ulonglong2((unsigned long long)a.now, 0ull));
     }
+}
+
+// The launch after a flow-mode classify launch: finalize on workgroups [0, fin_wgs) and the owner-computed update on
+// the next upd_owners workgroups, side by side (they touch disjoint slots: finalize the ones claimed in this batch,
+// the update the found flows'), so the update's memory traffic overlaps finalize's dependent chains.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ppe_flow_post_kernel(ppe_flow_kargs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t usm[];
+    if (blockIdx.x < a.fin_wgs) flow_finalize_wg<BLOCK>(a, a.fin_wgs);
+    else flow_update_wg<BLOCK>(a, blockIdx.x - a.fin_wgs, usm);
 }
 
 // FlowTimeOut + FlowAgeTimeoutCB (flow.c:391-467): live flows idle for more than `timeout` become tombstones.
@@ -2812,10 +2824,10 @@ extern "C" int ppe_launch_flow(int kind, const ppe_flow_kargs *a, uint32_t grid,
     const hipStream_t s = (hipStream_t)stream;
     const dim3 g(grid), b(PPE_FLOW_BLOCK);
     switch (kind) {
-        case PPE_FLOW_K_UPDATE:
-            hipLaunchKernelGGL(ppe_flow_update_kernel<1024>, g, dim3(1024), PPE_UPD_HASH * 28u, s, *a);
+        case PPE_FLOW_K_POST:
+            hipLaunchKernelGGL(ppe_flow_post_kernel<PPE_FLOW_POST_BLOCK>, g, dim3(PPE_FLOW_POST_BLOCK),
+                               a->f.upd_wgs ? PPE_UPD_HASH * 28u : 0u, s, *a);
             break;
-        case PPE_FLOW_K_FINALIZE: hipLaunchKernelGGL(ppe_flow_finalize_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
         case PPE_FLOW_K_AGE: hipLaunchKernelGGL(ppe_flow_age_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
         case PPE_FLOW_K_REHASH: hipLaunchKernelGGL(ppe_flow_rehash_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
         default: return (int)hipErrorInvalidValue;
