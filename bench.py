@@ -928,7 +928,7 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": round(tpp * n) if tpp else None,
                          "kernel": "ppe_classify_kernel<FLOW> (FlowFind; found flows' updates "
-                                   + ("to the owners' buckets, applied by ppe_flow_update_kernel" if owner else
+                                   + ("to the owners' buckets, applied beside finalize by ppe_flow_post_kernel" if owner else
                                       "by one atomic per packet") + "; misses resolved by the flow kernels)",
                          "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": bpp,
                          "batch_avg_us": round(my_ms / args.steps * 1e3, 3),
