@@ -74,7 +74,7 @@ struct FlowTable {
     unsigned long long *ctl = nullptr;
     uint32_t *rec = nullptr, *rslot = nullptr, *miss_tiles = nullptr;
     unsigned long long *tile_miss = nullptr, *tile_new = nullptr;
-    // owner-computed FlowUpdate (ppe_flow_update_kernel): bucket columns for upd_wgs classify workgroups
+    // owner-computed FlowUpdate (flow_update_wg in ppe_flow_post_kernel): bucket columns for upd_wgs classify workgroups
     unsigned long long *upd = nullptr;
     uint32_t *ucnt = nullptr;
     uint32_t upd_wgs = 0, upd_osh = 0, upd_owners = 0, upd_hmask = PPE_UPD_HASH - 1u;

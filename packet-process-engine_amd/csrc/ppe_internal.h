@@ -28,7 +28,7 @@ struct ppe_bdesc {
  * before the first EMPTY slot of its probe sequence (slots never return to EMPTY: deletions leave TOMBs, reclaimed by
  * a rehash).  A slot record is 64 B: {sip, dip, sport | dport << 16, state}, then the packed counters of both
  * directions and the last-seen time (`packed` points at them: u64 words 0-2 of each record's second 16 B), so a
- * probe group of 2 slots is one 128-B line and the owner-computed update (ppe_flow_update_kernel) rewrites the line
+ * probe group of 2 slots is one 128-B line and the owner-computed update (flow_update_wg) rewrites the line
  * the probe read. */
 #define PPE_FLOW_GROUP 2u       /* slots per probe group */
 #define PPE_FLOW_SLOT_WORDS 16u /* u32 words per slot record */
@@ -54,7 +54,7 @@ enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_N
 #define PPE_PK_SHIFT 40u                       /* packed counter: packets in bits 63:40, bytes in 39:0 */
 #define PPE_PK_FOLD_PKTS (1ull << 23)          /* fold into `stats` once either field reaches half its range */
 #define PPE_PK_FOLD_BYTES (1ull << 39)
-/* Owner-computed FlowUpdate (ppe_flow_update_kernel): a found packet's counter update goes to a bucket of its slot's
+/* Owner-computed FlowUpdate (flow_update_wg, ppe_flow_post_kernel): a found packet's counter update goes to a bucket of its slot's
  * owner (one of at most PPE_UPD_OWNERS slot ranges) in its classify workgroup's column, instead of a memory-side
  * atomic per packet; each owner's workgroup then sums its buckets in LDS and updates each touched slot once. */
 #define PPE_UPD_OWNERS 256u

@@ -1259,7 +1259,7 @@ template <class T> __device__ __forceinline__ void upd_st(T *p, T v) {
 __device__ __forceinline__ bool upd_small(const ppe_flowdev &f) { return PPE_UPD_LDS && f.upd_osh <= 15u; }
 
 // A found packet (classify launch): its direction flag, and its FlowUpdate as an entry in the bucket of its slot's
-// owner in this workgroup's column (ppe_flow_update_kernel applies it after the launch, with the last-seen time).
+// owner in this workgroup's column (flow_update_wg applies it in the next launch, with the last-seen time).
 // Without a column (update off, or a workgroup past the allocated columns) or with the bucket full: flow_account.
 __device__ __forceinline__ uint32_t flow_found(const ppe_flowdev &f, uint32_t *ucur, uint32_t *ubuf, uint32_t s,
                                                uint32_t fsip, uint32_t fports, uint32_t sip, uint32_t ports,
@@ -2201,7 +2201,8 @@ void ppe_classify_kernel(ppe_kargs a) {
 //             its flag;
 //   finalize  per pending packet the flow's claimed slot (the claimer's own, else found, flow_find_claim), final
 //             verdicts, flow creation and accounting, the tile's compaction and the pending packets' counters;
-//   update    (ppe_flow_update_kernel, owner-computed) the found flows' counters and last-seen times.
+//   update    (flow_update_wg, beside finalize in the same launch; owner-computed) the found flows' counters and
+//             last-seen times.
 
 
 struct TileWalk {  // persistent grid: wave gw of W takes the listed tiles gw, gw + W, ... (tiles with pending packets)

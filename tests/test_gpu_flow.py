@@ -128,6 +128,22 @@ def test_flow_large_rule_set(eng):
         p.close()
 
 
+def test_flow_large_table_global_buckets(eng):
+    """A table of more than 2^23 slots (capacity 2^22): the owner update's bucket entries no longer fit 4 B (slot
+    within the owner past 15 bits), so the classify kernel writes 8-B entries to global memory instead of staging
+    them in LDS; results and the table stay equal to the oracle's."""
+    rules = synth.make_rules(64, seed=27)
+    p = Pair(eng, rules, capacity=1 << 22, max_batch=1 << 15, default_action=0)
+    try:
+        for b in range(3):
+            pk = synth.make_flow_packets(20000, rules, n_flows=3000, seed=500 + b, template_seed=500, stride=64,
+                                         malformed_frac=0.01)
+            p.batch(pk["hdr"], pk["len"], NOW + b, part=(b == 1))
+        p.same_table()
+    finally:
+        p.close()
+
+
 def test_flow_pool_exhaustion(eng):
     """More new flows than the pool holds, within one batch and across batches: the creators past the free count
     (in packet order) fail with FLOW_NOMEM, exactly as one core running the batch in order."""
