@@ -1141,7 +1141,7 @@ def run_defrag(args, cfgd, dev, world, rank, dist, name=None, nested=False):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": round(traffic_per_packet(name) * n) if traffic_per_packet(name) else None,
-                         "kernel": "one ppe_defrag call (parse..assemble, 13 stream-ordered kernels)",
+                         "kernel": "one ppe_defrag call (parse..assemble, 10 stream-ordered kernels)",
                          "call_avg_us": round(call_ms * 1e3, 3), "bytes_per_call": bytes_call},
             "cpu_baseline": cpu,
             "parity_sample_ok": parity,

@@ -7,9 +7,9 @@
  *
  *   parse      one lane per fragment: re-derive the fields DecodeIPV4 stored in the mbuf (decode-ipv4.c:216-222) and
  *              look the key up in the device FCB hash table (open addressing, linear probing);
- *   claim      fragments whose FCB does not exist claim a slot (CAS, key = the claiming fragment's parsed key) and
- *              record the lowest claiming index: that fragment is the one whose fcb_create runs;
- *   admit      creators in index order (per-tile ballot counts; each workgroup sums the counts before it) get FCB
+ *   claim      (the parse launch) fragments whose FCB does not exist claim a slot (CAS, key = the claiming fragment's
+ *              parsed key) and record the lowest claiming index: that fragment is the one whose fcb_create runs;
+ *   admit      creators in index order (ballot counts, a look-back over the workgroups in one launch) get FCB
  *              records while running + rank < fcb_max (fcb_create's fetch-and-add cap); the others fail, and with
  *              them every later fragment of their key in this batch, because the running count cannot fall inside
  *              a batch;
@@ -18,10 +18,12 @@
  *              passes for 65,536 fragments), so each FCB's fragments are contiguous and in arrival order;
  *   process    one lane per FCB runs the reference state machine over its fragments in order (chain ≤ cache_max
  *              entries, kept as a nibble list of store slots);
+ *   place      completing fragments in index order get datagram indices (ballot counts, summed per workgroup)
+ *              and write their datagram's assembly plan;
  *   stash      one wave per held fragment copies its frame into the FCB's store slot (PACKET_HW2SW, mbuf.c:117-156);
- *   place      completing fragments in index order get datagram indices (ballot counts, summed per workgroup);
- *   assemble   one workgroup per datagram concatenates the chain (Frag_defrag_reasm, decode-defrag.c:222-289),
- *              patches ip_len / ip_off / the header checksum, and writes a classify-ready window + length.
+ *   assemble   (the stash's launch) one wave per datagram concatenates the chain (Frag_defrag_reasm,
+ *              decode-defrag.c:222-289) from the plan the place kernel wrote for it, patches ip_len / ip_off / the
+ *              header checksum, and writes a classify-ready window + length.
  *
  * Aging (Frag_defrag_timeout, decode-defrag.c:490-551) is one workgroup: free completed / idle FCBs, then rebuild
  * the hash table from the live records (which also clears the tombstones left by failed claims).
@@ -97,10 +99,12 @@ struct DfArgs {
     unsigned long long *ctl;
     uint32_t fcb_max, cache_max, frag_buf, reasm_buf, sstride;
     // batch scratch
-    uint32_t *frec, *fslot, *inserted, *dgrec, *dgsrc, *tcnt;
+    uint32_t *frec, *fslot, *inserted, *dgrec, *tcnt;
+    uint32_t *plan;                      // assembly plan: min(max_batch, fcb_max) × cache_max entries of 8 words
     uint32_t *skey[2], *sval[2], *hist;
     uint32_t shift, sort_blocks;         // radix pass: digit shift, workgroups
-    uint32_t flag_mode;                  // tile counts: 0 creators, 1 completing fragments
+    unsigned long long *look;            // admission: per-workgroup look-back words (epoch << 32 | flags | count)
+    uint32_t epoch, nlook;               // this call's tag (never 0) and the look-back array's length
     uint64_t *dropped;                   // age: ids of dropped fragments
     uint32_t max_dropped;
 };
@@ -172,17 +176,12 @@ __global__ void __launch_bounds__(kBlock) df_parse_kernel(DfArgs a) {
     (void)dummy;
     uint32_t *fr = a.frec + (size_t)i * kFrecWords;
     const uint32_t h = key_hash(sip, dip, idp & 0xffffu);
-    fr[0] = sip;
-    fr[1] = dip;
-    fr[2] = idp;
-    fr[3] = offf;
-    fr[4] = tot;
-    fr[5] = l2 | (ihl4 << 8);
-    fr[6] = h;
-    fr[7] = valid;
     uint32_t slot = kNone;
     if (valid) {
-        // FragFind (decode-defrag.c:124-146): ip4_frag_match compares id, sip, dip (not the protocol)
+        // FragFind (decode-defrag.c:124-146): ip4_frag_match compares id, sip, dip (not the protocol).  Claims of this
+        // launch make slots PEND only (never LIVE), so a plain probe of the table as it stood before the batch finds
+        // exactly what the reference's FragFind finds; a stale EMPTY only sends the fragment to the claim, which
+        // re-reads every slot by CAS.
         uint32_t s = h & a.smask;
         for (uint32_t probe = 0; probe <= a.smask; ++probe, s = (s + 1) & a.smask) {
             const uint32_t st = a.tstate[s];
@@ -196,25 +195,33 @@ __global__ void __launch_bounds__(kBlock) df_parse_kernel(DfArgs a) {
             }
         }
     }
-    a.fslot[i] = valid ? slot : (kNone - 1);   // kNone: create; kNone − 1: not a fragment
-}
-
-// ---- claim: a slot per new key, lowest claiming index recorded ------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) df_claim_kernel(DfArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    const uint32_t fs = a.fslot[i];
-    if (fs < kNone - 1) {   // found in the table: the FCB's first fragment in this batch is its group key
-        atomicMin(a.creator + fs, i);
+    const bool claim = valid && slot == kNone;
+    if (claim) {
+        // the key words other lanes of this launch compare when they meet this fragment's PEND claim: written through
+        // to memory (agent scope) and waited for before the CAS that publishes the index
+        unsigned long long *q = (unsigned long long *)fr;
+        __hip_atomic_store(q, (unsigned long long)sip | ((unsigned long long)dip << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, (unsigned long long)idp | ((unsigned long long)offf << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *(uint4 *)fr = make_uint4(sip, dip, idp, offf);
+    }
+    *(uint4 *)(fr + 4) = make_uint4(tot, l2 | (ihl4 << 8), h, valid);
+    if (!claim) {
+        // found in the table: the FCB's first fragment in this batch is its group key
+        if (valid) atomicMin(a.creator + slot, i);
+        a.fslot[i] = valid ? slot : (kNone - 1);   // kNone − 1: not a fragment
         return;
     }
-    if (fs != kNone) return;
-    const uint32_t *fr = a.frec + (size_t)i * kFrecWords;
-    const uint32_t sip = fr[0], dip = fr[1], id = fr[2] & 0xffffu;
-    uint32_t s = fr[6] & a.smask;
-    // terminates: slots >= 2 (fcb_max + max_batch) > live + pending, and EMPTY / TOMB slots are claimable
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // claim: a slot per new key, lowest claiming index recorded.  Terminates: slots >= 2 (fcb_max + max_batch) >
+    // live + pending, and EMPTY / TOMB slots are claimable.  The first CAS of each slot expects EMPTY (the common
+    // case) and doubles as its load: a failed CAS returns the slot's state.
+    const uint32_t id = idp & 0xffffu;
+    uint32_t s = h & a.smask;
     for (;;) {
-        uint32_t st = __hip_atomic_load(a.tstate + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t st = kEmpty;
         for (;;) {
             if (st == kEmpty || st == kTomb) {
                 const uint32_t old = atomicCAS(a.tstate + s, st, kPend | i);
@@ -227,8 +234,11 @@ __global__ void __launch_bounds__(kBlock) df_claim_kernel(DfArgs a) {
                 continue;
             }
             if (st & kPend) {
-                const uint32_t *fc = a.frec + (size_t)(st & ~kPend) * kFrecWords;
-                if (fc[0] == sip && fc[1] == dip && (fc[2] & 0xffffu) == id) {
+                // join an equal key's claim: its key words, read past this XCD's L2
+                const unsigned long long *q = (const unsigned long long *)(a.frec + (size_t)(st & ~kPend) * kFrecWords);
+                const unsigned long long k01 = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                         k23 = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)k01 == sip && (uint32_t)(k01 >> 32) == dip && ((uint32_t)k23 & 0xffffu) == id) {
                     atomicMin(a.creator + s, i);
                     a.fslot[i] = s;
                     return;
@@ -241,20 +251,12 @@ __global__ void __launch_bounds__(kBlock) df_claim_kernel(DfArgs a) {
 }
 
 // ---- per-tile ballot counts of a flag, one-workgroup scan, ranked placement ------------------------------------------
-__device__ __forceinline__ bool df_flag(const DfArgs &a, uint32_t i) {
+// a creator: the fragment whose claim (or join) recorded the lowest index on its still-pending slot
+__device__ __forceinline__ bool df_creator(const DfArgs &a, uint32_t i) {
     if (i >= a.n) return false;
-    if (a.flag_mode == 0) {
-        const uint32_t s = a.fslot[i];
-        if (s >= kNone - 1) return false;
-        return (a.tstate[s] & kPend) && a.creator[s] == i;
-    }
-    return a.dgrec[i] != kNone;
-}
-
-__global__ void __launch_bounds__(kBlock) df_tile_count_kernel(DfArgs a) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t b = __builtin_amdgcn_ballot_w64(df_flag(a, i));
-    if (__lane_id() == 0 && i < a.n) a.tcnt[i >> 6] = (uint32_t)__popcll(b);
+    const uint32_t s = a.fslot[i];
+    if (s >= kNone - 1) return false;
+    return (a.tstate[s] & kPend) && a.creator[s] == i;
 }
 
 // This workgroup's exclusive prefix of the tile counts: the sum of cnt[0, t0), and (total != nullptr) the sum of
@@ -289,15 +291,60 @@ __device__ uint32_t wg_tile_prefix(const uint32_t *cnt, uint32_t t0, uint32_t ti
     return b;
 }
 
-// (the running count and free-stack top are read as they stood before this batch: the histogram pass of the sort,
-// which runs next, moves them past this batch's admissions)
+// The creators' ranks come from a look-back over the workgroups in index order (one launch: the workgroups are
+// dispatched in index order and all resident, so every wait is on an earlier, running one).  Workgroup b publishes
+// its count as an aggregate, adds its predecessors' words back to the first inclusive one, then publishes its
+// inclusive prefix.  Words carry the call's epoch, so the array needs no clearing between calls.  The per-tile counts
+// are kept for the sort's first pass (the running-count update).  The running count and free-stack top are read as
+// they stood before this batch: that histogram pass, which runs next, moves them past this batch's admissions.
 __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
+    __shared__ uint32_t wc[kBlock / 64], wbase;
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t t0 = blockIdx.x * (kBlock / 64), w = threadIdx.x >> 6;
-    uint32_t base = wg_tile_prefix<kBlock>(a.tcnt, t0, (a.n + 63) / 64, nullptr);
-    for (uint32_t k = 0; k < w; ++k) base += a.tcnt[t0 + k];   // the workgroup's earlier waves
-    const bool f = df_flag(a, i);
+    const uint32_t w = threadIdx.x >> 6;
+    const bool f = df_creator(a, i);
     const uint64_t b = __builtin_amdgcn_ballot_w64(f);
+    if (__lane_id() == 0) {
+        wc[w] = (uint32_t)__popcll(b);
+        if (i < a.n) a.tcnt[i >> 6] = (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    if (w == 0) {
+        // wave 0 looks back 64 predecessors per round (one load each, all in flight together): the nearest inclusive
+        // word ends the walk; a window with an unpublished word before it is read again
+        constexpr unsigned long long kAgg = 1ull << 30, kIncl = 1ull << 31, kCount = kAgg - 1;
+        const unsigned long long tag = (unsigned long long)a.epoch << 32;
+        const uint32_t lane = __lane_id();
+        uint32_t agg = 0;
+        for (uint32_t k = 0; k < kBlock / 64; ++k) agg += wc[k];
+        if (lane == 0)
+            __hip_atomic_store(a.look + blockIdx.x, tag | kAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t excl = 0;
+        for (int end = (int)blockIdx.x; end > 0;) {
+            const int p = end - 1 - (int)lane;   // lane 0: the nearest predecessor
+            const unsigned long long v =
+                p >= 0 ? __hip_atomic_load(a.look + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag | kIncl;
+            const bool ready = (v >> 32) == a.epoch;
+            const uint64_t incl = __builtin_amdgcn_ballot_w64(ready && (v & kIncl));
+            const uint64_t wait = __builtin_amdgcn_ballot_w64(!ready);
+            const uint32_t fi = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;   // the nearest inclusive lane
+            const uint64_t upto = fi < 63 ? (2ull << fi) - 1ull : ~0ull;          // lanes [0, fi]
+            if (wait & upto) continue;   // a predecessor before it has not published yet
+            uint32_t c = lane <= fi ? (uint32_t)(v & kCount) : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+            excl += c;
+            if (incl) break;
+            end -= 64;
+        }
+        if (lane == 0) {
+            __hip_atomic_store(a.look + blockIdx.x, tag | kIncl | (excl + agg), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            wbase = excl;
+        }
+    }
+    __syncthreads();
+    uint32_t base = wbase;
+    for (uint32_t k = 0; k < w; ++k) base += wc[k];   // the workgroup's earlier waves
     if (!f) return;
     const uint32_t rank = base + (uint32_t)__popcll(b & lanemask_lt());
     const uint32_t s = a.fslot[i];
@@ -351,6 +398,15 @@ __global__ void __launch_bounds__(kSortBlock) df_sort_pass_kernel(DfArgs a) {
         key = df_sort_key(a, j);
         a.skey[0][j] = key;
         a.sval[0][j] = j;
+        // the process kernel's view of the fragment, in its parsed record's last two words (the hash and the valid
+        // flag are dead after the claim): word 6 = its FCB record (kNone: none), word 7 = its table slot (kNone: not
+        // a fragment).  The group head then reaches its FCB header in one load instead of three dependent ones.
+        const uint32_t s = a.fslot[j];
+        const bool rec = s < kNone - 1 && a.tstate[s] == kLive;
+        uint2 w67;
+        w67.x = rec ? a.tkey[(size_t)s * 4 + 3] : kNone;
+        w67.y = s < kNone - 1 ? s : kNone;
+        *(uint2 *)(a.frec + (size_t)j * kFrecWords + 6) = w67;
     } else if (v) {
         key = a.skey[0][j];
     }
@@ -440,156 +496,205 @@ __device__ __forceinline__ uint32_t chain_at(uint64_t order, uint32_t pos) { ret
 // LDS round trips instead of global ones.  Private per lane ([slot][lane]: no bank conflicts), no barrier.
 // cidx: batch index + 1 of the fragment each chain slot received in this batch (0: an earlier batch).  When the FCB
 // completes, these go to descriptor word 3 and the fragments are not stashed: the assembly reads them from the input.
+// The lane's loads come in three dependent rounds, not one per chain step: (1) the sorted keys and indices of the
+// next kWin positions (contiguous) and the neighbour's key; (2) the head's parsed record, which carries its FCB record
+// and table slot (df_sort_pass_kernel INIT), and the window's parsed records and ids; (3) the FCB header (and, for an
+// FCB from an earlier batch, its chain descriptors).  A segment longer than the window refills one position per step.
+constexpr uint32_t kWin = 16;
 __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint32_t (*cdesc)[kBlock],
                                                uint32_t (*cidx)[kBlock], uint32_t *st, uint32_t &teardrop) {
     const uint32_t tl = threadIdx.x;
     const uint32_t *key = a.skey[0];
+    const uint32_t *val = a.sval[0];
     const uint32_t g = key[j];
-    if (j > 0 && key[j - 1] == g) return;   // not the head of its FCB's segment
-    const uint32_t i0 = a.sval[0][j];
-    const uint32_t s0 = a.fslot[i0];
-    const bool rec = s0 < kNone - 1 && a.tstate[s0] == kLive;
-    if (s0 < kNone - 1) a.creator[s0] = kNone;   // the group key has been used: reset for the next batch
-    if (!rec) {   // a fragment without a record (no FCB, or not a fragment): a singleton group
-        const uint32_t i = i0;
-        const bool frag = a.frec[(size_t)i * kFrecWords + 7] != 0;
-        const uint32_t s = frag ? PPE_DF_FCB_FULL : PPE_DF_NOT_FRAG;
-        a.status[i] = s;
-        a.inserted[i] = kNone;
-        a.dgrec[i] = kNone;
+    const uint32_t kprev = j > 0 ? key[j - 1] : ~g;
+    uint32_t kq[kWin], iq[kWin];
+#pragma unroll
+    for (uint32_t u = 1; u < kWin; ++u) {
+        const bool in = j + u < a.n;
+        kq[u] = in ? key[j + u] : ~g;
+        iq[u] = in ? val[j + u] : 0u;
+    }
+    if (kprev == g) return;   // not the head of its FCB's segment
+    // a group's key is the batch index of its first fragment (df_sort_key), which the stable sort puts first
+    iq[0] = g;
+    uint32_t m = 1;           // valid window entries [0, m): keys equal g are contiguous
+#pragma unroll
+    for (uint32_t u = 1; u < kWin; ++u) m += kq[u] == g ? 1u : 0u;
+    bool more = m == kWin;    // the segment may continue past the window
+    uint32_t qn = j + kWin;   // the next sorted position to read into the window
+    uint4 fa[kWin];
+    uint2 fb[kWin];
+    uint64_t fid[kWin];
+    const uint4 h67 = *(const uint4 *)(a.frec + (size_t)g * kFrecWords + 4);
+    fa[0] = *(const uint4 *)(a.frec + (size_t)g * kFrecWords);
+    fb[0] = make_uint2(h67.x, h67.y);
+    fid[0] = a.id ? a.id[g] : (uint64_t)g;
+#pragma unroll
+    for (uint32_t u = 1; u < kWin; ++u) {
+        if (u < m) {
+            fa[u] = *(const uint4 *)(a.frec + (size_t)iq[u] * kFrecWords);
+            fb[u] = *(const uint2 *)(a.frec + (size_t)iq[u] * kFrecWords + 4);
+            fid[u] = a.id ? a.id[iq[u]] : (uint64_t)iq[u];
+        }
+    }
+    const uint32_t r = h67.z, s0 = h67.w;
+    if (s0 != kNone) a.creator[s0] = kNone;   // the group key has been used: reset for the next batch
+    if (r == kNone) {   // a fragment without a record (no FCB, or not a fragment): a singleton group
+        const uint32_t s = s0 != kNone ? PPE_DF_FCB_FULL : PPE_DF_NOT_FRAG;
+        a.status[g] = s;
+        a.inserted[g] = kNone;
+        a.dgrec[g] = kNone;
         st[s]++;
         return;
-    } else {
-        const uint32_t r = a.tkey[(size_t)s0 * 4 + 3];
-        uint32_t *h = a.rhdr + (size_t)r * kRecWords;
-        uint32_t flags = h[0] & 0xffu, last_in = (h[0] >> 8) & 0xffu, cache_num = (h[0] >> 16) & 0xffu,
-                 nlist = h[0] >> 24;
-        int total = (int)h[1], meat = (int)h[2];
-        uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
-        const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
-        uint32_t *descw = a.rdesc + (size_t)r * a.cache_max * 4;
-        for (uint32_t k = 0; k < cache_num && k < 16; ++k) {
-            cdesc[k][tl] = desc[k * 4];
+    }
+    uint32_t *h = a.rhdr + (size_t)r * kRecWords;
+    const uint4 h03 = *(const uint4 *)h;
+    const uint2 h45 = *(const uint2 *)(h + 4);
+    uint32_t flags = h03.x & 0xffu, last_in = (h03.x >> 8) & 0xffu, cache_num = (h03.x >> 16) & 0xffu,
+             nlist = h03.x >> 24;
+    int total = (int)h03.y, meat = (int)h03.z;
+    uint64_t order = (uint64_t)h45.x | ((uint64_t)h45.y << 32);
+    uint32_t *descw = a.rdesc + (size_t)r * a.cache_max * 4;
+    // descriptor word 2 of chain position 0 (l2 | ihl*4 << 8 | proto << 16): the completion's buffer check
+    uint32_t hd0 = 0;
+    if (cache_num) {   // an FCB from an earlier batch: its chain descriptors, one round of loads
+        uint32_t cw[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) cw[k] = k < cache_num ? descw[k * 4] : 0u;
+        if (nlist) hd0 = descw[chain_at(order, 0) * 4 + 2];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            cdesc[k][tl] = cw[k];
             cidx[k][tl] = 0;
         }
-        // the segment's fragments in order; the next one's index and record words are requested before the
-        // current one is processed (the chain is a serial dependence, the loads need not be)
-        uint32_t i_nx = i0;
-        uint4 f0_nx = *(const uint4 *)(a.frec + (size_t)i_nx * kFrecWords);
-        uint2 f1_nx = *(const uint2 *)(a.frec + (size_t)i_nx * kFrecWords + 4);
-        for (uint32_t q = j; q < a.n && key[q] == g; ++q) {
-            const uint32_t i = i_nx;
-            const uint32_t fr[6] = {f0_nx.x, f0_nx.y, f0_nx.z, f0_nx.w, f1_nx.x, f1_nx.y};
-            if (q + 1 < a.n && key[q + 1] == g) {
-                i_nx = a.sval[0][q + 1];
-                f0_nx = *(const uint4 *)(a.frec + (size_t)i_nx * kFrecWords);
-                f1_nx = *(const uint2 *)(a.frec + (size_t)i_nx * kFrecWords + 4);
-            }
-            uint32_t out = PPE_DF_CACHED, ins = kNone, done = kNone;
-            bool tear = false;
-            // FragFind / fcb_create refresh the FCB's timestamp (decode-defrag.c:139, 472); a.rts[r] = now below
-            if (fr[4] > a.frag_buf) {
-                out = PPE_DF_HW2SW_ERR;                    // PACKET_HW2SW (decode-defrag.c:415-420)
-            } else if (flags & kRecDelete) {
-                out = PPE_DF_DELETED;                      // decode-defrag.c:422-427 (no counter)
-            } else if (cache_num >= a.cache_max) {
-                out = PPE_DF_CACHE_FULL;                   // decode-defrag.c:429-437
-            } else {
-                // Frag_defrag_process (decode-defrag.c:292-406)
-                const int offset = (int)(fr[3] & 0xffffu);
-                const int flen = (int)(fr[3] >> 16);
-                const int end = offset + flen;
-                const bool mf = (fr[2] >> 24) & 1u;
-                bool err = false;
-                if (!mf) {
-                    if (end < total || (last_in & kLastIn)) err = true;
-                    else {
-                        last_in |= kLastIn;
-                        total = end;
-                    }
-                } else if (end > total) {
-                    if (last_in & kLastIn) err = true;
-                    else total = end;
-                }
-                uint32_t pos = nlist;       // insert before chain position pos
-                if (!err) {
-                    int prev = -1, next = -1;
-                    if (nlist == 0 || (int)(cdesc[chain_at(order, nlist - 1)][tl] & 0xffffu) < offset) {
-                        prev = nlist ? (int)chain_at(order, nlist - 1) : -1;
-                    } else {
-                        // the reference's scan compares the chained fragment's frag_len with the new offset
-                        // (decode-defrag.c:344-349)
-                        for (pos = 0; pos < nlist; ++pos) {
-                            const uint32_t k = chain_at(order, pos);
-                            if ((int)(cdesc[k][tl] >> 16) >= offset) {
-                                next = (int)k;
-                                break;
-                            }
-                            prev = (int)k;
-                        }
-                    }
-                    if (prev >= 0) {
-                        const uint32_t pd = cdesc[prev][tl];
-                        if ((int)(pd & 0xffffu) + (int)(pd >> 16) - offset > 0) err = tear = true;
-                    }
-                    if (!err && next >= 0 && (int)(cdesc[next][tl] & 0xffffu) - end < 0) err = tear = true;
-                }
-                if (err) {
-                    out = PPE_DF_DEFRAG_ERR;
-                    teardrop += tear ? 1u : 0u;
-                } else {
-                    const uint32_t k = cache_num;      // store slot: the fragment's arrival rank in this FCB
-                    descw[k * 4 + 0] = fr[3];
-                    cdesc[k][tl] = fr[3];
-                    descw[k * 4 + 1] = fr[4];
-                    descw[k * 4 + 2] = fr[5] | ((fr[2] >> 16) & 0xffu) << 16;
-                    descw[k * 4 + 3] = 0;
-                    cidx[k][tl] = i + 1;
-                    a.rid[(size_t)r * a.cache_max + k] = a.id ? a.id[i] : (uint64_t)i;
-                    const uint64_t lo = order & ((1ull << (4 * pos)) - 1ull);
-                    const uint64_t hi = pos + 1 < 16 ? (order >> (4 * pos)) << (4 * (pos + 1)) : 0ull;
-                    order = lo | ((uint64_t)k << (4 * pos)) | hi;
-                    nlist++;
-                    cache_num++;
-                    meat += flen;
-                    if (offset == 0) last_in |= kFirstIn;
-                    ins = (r << 8) | k;
-                    if (last_in == (kFirstIn | kLastIn) && meat == total) {
-                        // Frag_defrag_reasm / Frag_defrag_setup: the buffer is total + L2 + ihl*4 bytes of an 8 KB
-                        // slice (ICMP: 1000 bytes, always available)
-                        const uint32_t hd = desc[chain_at(order, 0) * 4 + 2];
-                        const uint32_t need = (uint32_t)total + (hd & 0xffu) + ((hd >> 8) & 0xffu);
-                        if (((hd >> 16) & 0xffu) != 1u && need > a.reasm_buf) {
-                            out = PPE_DF_SETUP_ERR;
-                        } else {
-                            out = PPE_DF_REASM;
-                            flags |= kRecComplete | kRecDelete;
-                            done = r;
-                            // this batch's fragments of the datagram are read from the input, not stashed
-                            for (uint32_t kk = 0; kk < cache_num; ++kk) {
-                                const uint32_t x = cidx[kk][tl];
-                                descw[kk * 4 + 3] = x;
-                                if (x && x - 1 != i) a.inserted[x - 1] = kNone;
-                            }
-                            ins = kNone;
-                        }
-                    }
-                }
-            }
-            a.status[i] = out | (tear ? PPE_DF_TEARDROP : 0u);
-            a.inserted[i] = ins;
-            a.dgrec[i] = done;
-            // the place kernel's per-tile count of completing fragments (zeroed by the first scatter pass)
-            if (done != kNone) atomicAdd(a.tcnt + (i >> 6), 1u);
-            st[out]++;
-        }
-        h[0] = flags | (last_in << 8) | (cache_num << 16) | (nlist << 24);
-        h[1] = (uint32_t)total;
-        h[2] = (uint32_t)meat;
-        h[4] = (uint32_t)order;
-        h[5] = (uint32_t)(order >> 32);
-        a.rts[r] = a.now;
     }
+    // the segment's fragments in order
+    while (m) {
+        const uint32_t i = iq[0];
+        const uint32_t fr[6] = {fa[0].x, fa[0].y, fa[0].z, fa[0].w, fb[0].x, fb[0].y};
+        const uint64_t fragid = fid[0];
+#pragma unroll
+        for (uint32_t u = 0; u + 1 < kWin; ++u) {
+            iq[u] = iq[u + 1];
+            fa[u] = fa[u + 1];
+            fb[u] = fb[u + 1];
+            fid[u] = fid[u + 1];
+        }
+        --m;
+        if (more) {   // refill the window's last position (segments longer than kWin only)
+            more = false;
+            if (qn < a.n && key[qn] == g) {
+                const uint32_t x = val[qn];
+                iq[kWin - 1] = x;
+                fa[kWin - 1] = *(const uint4 *)(a.frec + (size_t)x * kFrecWords);
+                fb[kWin - 1] = *(const uint2 *)(a.frec + (size_t)x * kFrecWords + 4);
+                fid[kWin - 1] = a.id ? a.id[x] : (uint64_t)x;
+                ++m;
+                ++qn;
+                more = true;
+            }
+        }
+        uint32_t out = PPE_DF_CACHED, ins = kNone, done = kNone;
+        bool tear = false;
+        // FragFind / fcb_create refresh the FCB's timestamp (decode-defrag.c:139, 472); a.rts[r] = now below
+        if (fr[4] > a.frag_buf) {
+            out = PPE_DF_HW2SW_ERR;                    // PACKET_HW2SW (decode-defrag.c:415-420)
+        } else if (flags & kRecDelete) {
+            out = PPE_DF_DELETED;                      // decode-defrag.c:422-427 (no counter)
+        } else if (cache_num >= a.cache_max) {
+            out = PPE_DF_CACHE_FULL;                   // decode-defrag.c:429-437
+        } else {
+            // Frag_defrag_process (decode-defrag.c:292-406)
+            const int offset = (int)(fr[3] & 0xffffu);
+            const int flen = (int)(fr[3] >> 16);
+            const int end = offset + flen;
+            const bool mf = (fr[2] >> 24) & 1u;
+            bool err = false;
+            if (!mf) {
+                if (end < total || (last_in & kLastIn)) err = true;
+                else {
+                    last_in |= kLastIn;
+                    total = end;
+                }
+            } else if (end > total) {
+                if (last_in & kLastIn) err = true;
+                else total = end;
+            }
+            uint32_t pos = nlist;       // insert before chain position pos
+            if (!err) {
+                int prev = -1, next = -1;
+                if (nlist == 0 || (int)(cdesc[chain_at(order, nlist - 1)][tl] & 0xffffu) < offset) {
+                    prev = nlist ? (int)chain_at(order, nlist - 1) : -1;
+                } else {
+                    // the reference's scan compares the chained fragment's frag_len with the new offset
+                    // (decode-defrag.c:344-349)
+                    for (pos = 0; pos < nlist; ++pos) {
+                        const uint32_t k = chain_at(order, pos);
+                        if ((int)(cdesc[k][tl] >> 16) >= offset) {
+                            next = (int)k;
+                            break;
+                        }
+                        prev = (int)k;
+                    }
+                }
+                if (prev >= 0) {
+                    const uint32_t pd = cdesc[prev][tl];
+                    if ((int)(pd & 0xffffu) + (int)(pd >> 16) - offset > 0) err = tear = true;
+                }
+                if (!err && next >= 0 && (int)(cdesc[next][tl] & 0xffffu) - end < 0) err = tear = true;
+            }
+            if (err) {
+                out = PPE_DF_DEFRAG_ERR;
+                teardrop += tear ? 1u : 0u;
+            } else {
+                const uint32_t k = cache_num;      // store slot: the fragment's arrival rank in this FCB
+                const uint32_t w2 = fr[5] | ((fr[2] >> 16) & 0xffu) << 16;
+                *(uint4 *)(descw + k * 4) = make_uint4(fr[3], fr[4], w2, 0u);
+                cdesc[k][tl] = fr[3];
+                cidx[k][tl] = i + 1;
+                a.rid[(size_t)r * a.cache_max + k] = fragid;
+                if (pos == 0) hd0 = w2;
+                const uint64_t lo = order & ((1ull << (4 * pos)) - 1ull);
+                const uint64_t hi = pos + 1 < 16 ? (order >> (4 * pos)) << (4 * (pos + 1)) : 0ull;
+                order = lo | ((uint64_t)k << (4 * pos)) | hi;
+                nlist++;
+                cache_num++;
+                meat += flen;
+                if (offset == 0) last_in |= kFirstIn;
+                ins = (r << 8) | k;
+                if (last_in == (kFirstIn | kLastIn) && meat == total) {
+                    // Frag_defrag_reasm / Frag_defrag_setup: the buffer is total + L2 + ihl*4 bytes of an 8 KB
+                    // slice (ICMP: 1000 bytes, always available)
+                    const uint32_t need = (uint32_t)total + (hd0 & 0xffu) + ((hd0 >> 8) & 0xffu);
+                    if (((hd0 >> 16) & 0xffu) != 1u && need > a.reasm_buf) {
+                        out = PPE_DF_SETUP_ERR;
+                    } else {
+                        out = PPE_DF_REASM;
+                        flags |= kRecComplete | kRecDelete;
+                        done = r;
+                        // this batch's fragments of the datagram are read from the input, not stashed
+                        for (uint32_t kk = 0; kk < cache_num; ++kk) {
+                            const uint32_t x = cidx[kk][tl];
+                            descw[kk * 4 + 3] = x;
+                            if (x && x - 1 != i) a.inserted[x - 1] = kNone;
+                        }
+                        ins = kNone;
+                    }
+                }
+            }
+        }
+        a.status[i] = out | (tear ? PPE_DF_TEARDROP : 0u);
+        a.inserted[i] = ins;
+        a.dgrec[i] = done;
+        // the place kernel's per-tile count of completing fragments (zeroed by the first scatter pass)
+        if (done != kNone) atomicAdd(a.tcnt + (i >> 6), 1u);
+        st[out]++;
+    }
+    *(uint4 *)h = make_uint4(flags | (last_in << 8) | (cache_num << 16) | (nlist << 24), (uint32_t)total,
+                             (uint32_t)meat, h03.w);
+    *(uint2 *)(h + 4) = make_uint2((uint32_t)order, (uint32_t)(order >> 32));
+    a.rts[r] = a.now;
 }
 
 __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
@@ -613,10 +718,8 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
                   (unsigned long long)wg[threadIdx.x]);
 }
 
-// ---- stash: copy held frames into their FCB's store slot (PACKET_HW2SW) ----------------------------------------------
-__global__ void __launch_bounds__(kSlotBlock) df_stash_kernel(DfArgs a) {
-    const uint32_t i = blockIdx.x * (kSlotBlock / 64) + (threadIdx.x >> 6);
-    if (i >= a.n) return;
+// ---- stash: copy held frames into their FCB's store slot (PACKET_HW2SW; run in the assembly launch) ------------------
+__device__ __forceinline__ void df_stash_one(const DfArgs &a, uint32_t i) {
     const uint32_t ins = a.inserted[i];
     if (ins == kNone) return;
     const uint32_t r = ins >> 8, k = ins & 0xffu;
@@ -659,13 +762,49 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
         a.ctl[C_DGRAMS] += nd;
         if (a.n_dgram) *a.n_dgram = nd;
     }
-    const bool f = df_flag(a, i);
+    const uint32_t r = i < a.n ? a.dgrec[i] : kNone;
+    const bool f = r != kNone;
     const uint64_t b = __builtin_amdgcn_ballot_w64(f);
     if (i >= a.n) return;
     uint32_t j = kNone;
     if (f) {
         j = base + (uint32_t)__popcll(b & lanemask_lt());
-        a.dgsrc[j] = i;
+        // datagram j's assembly plan: its chain in chain order, entry p = {descriptor words 0-2, total | nlist << 24,
+        // frame base address, fragment id}.  The FCB header → descriptors → frame offsets chain is walked here, one
+        // lane per datagram, so each assembly wave starts from one read (j < min(n, fcb_max): one record each).
+        const uint32_t *h = a.rhdr + (size_t)r * kRecWords;
+        const uint4 h03 = *(const uint4 *)h;
+        const uint2 h45 = *(const uint2 *)(h + 4);
+        const uint32_t nlist = h03.x >> 24, hw = h03.y | (nlist << 24);
+        const uint64_t order = (uint64_t)h45.x | ((uint64_t)h45.y << 32);
+        const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
+        uint4 dd[16];
+        uint64_t id[16], fb[16];
+#pragma unroll
+        for (uint32_t p = 0; p < 16; ++p) {
+            if (p < nlist) {
+                const uint32_t kk = chain_at(order, p);
+                dd[p] = *(const uint4 *)(desc + kk * 4);
+                id[p] = a.rid[(size_t)r * a.cache_max + kk];
+            }
+        }
+#pragma unroll
+        for (uint32_t p = 0; p < 16; ++p) {
+            if (p < nlist) {
+                const uint32_t kk = chain_at(order, p);
+                fb[p] = dd[p].w ? (uint64_t)(uintptr_t)(a.pkt + a.off[dd[p].w - 1])
+                                : (uint64_t)(uintptr_t)(a.store + ((size_t)r * a.cache_max + kk) * a.sstride);
+            }
+        }
+        uint32_t *pe = a.plan + (size_t)j * a.cache_max * 8;
+#pragma unroll
+        for (uint32_t p = 0; p < 16; ++p) {
+            if (p < nlist) {
+                *(uint4 *)(pe + p * 8) = make_uint4(dd[p].x, dd[p].y, dd[p].z, hw);
+                *(uint4 *)(pe + p * 8 + 4) =
+                    make_uint4((uint32_t)fb[p], (uint32_t)(fb[p] >> 32), (uint32_t)id[p], (uint32_t)(id[p] >> 32));
+            }
+        }
     }
     if (a.dgram_of) a.dgram_of[i] = j;
 }
@@ -675,6 +814,9 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
 // header checksum, 8 = datagram bytes not copied
 #ifndef DF_AB
 #define DF_AB 0
+#endif
+#ifndef DF_COPY_U
+#define DF_COPY_U 8
 #endif
 __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, uint32_t nd) {
     const uint32_t tid = __lane_id();
@@ -691,28 +833,20 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
             for (uint32_t k = tid; k < a.cache_max; k += 64) a.dgram_frags[(size_t)j * a.cache_max + k] = ~0ull;
         return;
     }
-    const uint32_t i = a.dgsrc[j];
-    const uint32_t r = a.dgrec[i];
-    const uint32_t *h = a.rhdr + (size_t)r * kRecWords;
-    const uint32_t nlist = h[0] >> 24;
-    const uint32_t total = h[1];
-    const uint64_t order = (uint64_t)h[4] | ((uint64_t)h[5] << 32);
-    const uint32_t *desc = a.rdesc + (size_t)r * a.cache_max * 4;
-    // lane p holds chain entry p's descriptor words 0 (offset | frag_len << 16), 1 (frame length), 2 (l2 | ihl*4 << 8
-    // | proto << 16): one round of loads for the whole chain, read below with lane broadcasts
-    // and the base of its frame: the input frame when the fragment arrived in this batch (word 3 = index + 1), else
-    // its store slot
-    uint32_t cd0 = 0, cd1 = 0, cd2 = 0;
-    uintptr_t cbase = 0;
-    if (tid < nlist) {
-        const uint32_t kk = chain_at(order, tid);
-        cd0 = desc[kk * 4];
-        cd1 = desc[kk * 4 + 1];
-        cd2 = desc[kk * 4 + 2];
-        const uint32_t cd3 = desc[kk * 4 + 3];
-        cbase = cd3 ? (uintptr_t)(a.pkt + a.off[cd3 - 1])
-                    : (uintptr_t)(a.store + ((size_t)r * a.cache_max + kk) * a.sstride);
+    // lane p holds chain entry p of the plan (df_place_kernel): descriptor words 0 (offset | frag_len << 16), 1 (frame
+    // length), 2 (l2 | ihl*4 << 8 | proto << 16), the frame's base (the input frame when the fragment arrived in
+    // this batch, else its store slot) and its id: one read for the whole chain, used below by lane broadcasts
+    uint4 e0 = make_uint4(0u, 0u, 0u, 0u), e1 = e0;
+    if (tid < a.cache_max) {
+        const uint32_t *pe = a.plan + ((size_t)j * a.cache_max + tid) * 8;
+        e0 = *(const uint4 *)pe;
+        e1 = *(const uint4 *)(pe + 4);
     }
+    const uint32_t hw = __shfl(e0.w, 0, 64);
+    const uint32_t nlist = hw >> 24, total = hw & 0xffffffu;
+    const bool live = tid < nlist;
+    const uint32_t cd0 = live ? e0.x : 0u, cd1 = live ? e0.y : 0u, cd2 = live ? e0.z : 0u;
+    const uintptr_t cbase = live ? (uintptr_t)(((uint64_t)e1.y << 32) | e1.x) : 0;
     auto seg_base = [&](uint32_t p) -> const uint8_t * {
         const uint32_t lo = __shfl((uint32_t)cbase, p, 64), hi = __shfl((uint32_t)((uint64_t)cbase >> 32), p, 64);
         return (const uint8_t *)(((uint64_t)hi << 32) | lo);
@@ -776,20 +910,27 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
                 const uintptr_t s0 = (uintptr_t)(src + (4u * wa - dst0));
                 const uint32_t sh = (uint32_t)(s0 & 3u) * 8u;
                 const uint32_t *ap = (const uint32_t *)(s0 & ~(uintptr_t)3);   // source dword of output dword wa
-                constexpr uint32_t U = 4;   // 1 KB of output per pass, every load issued before the stores
+                // DF_COPY_U dwords per lane per pass, every load issued before the stores; each source dword is
+                // loaded once: the funnel partner of dword w is dword w + 1, the next lane's (lane 63: the next
+                // row's lane 0, or for the last row one more dword)
+                constexpr uint32_t U = DF_COPY_U;
                 for (uint32_t base = wa; base < we; base += 64 * U) {
-                    uint32_t lo[U], hi[U];
+                    uint32_t lo[U];
 #pragma unroll
                     for (uint32_t u = 0; u < U; ++u) {
                         const uint32_t w = base + u * 64 + tid;
-                        lo[u] = w < we ? ap[w - wa] : 0u;
-                        hi[u] = (w < we && sh) ? ap[w - wa + 1] : 0u;
+                        lo[u] = (w < we || (w == we && sh)) ? ap[w - wa] : 0u;
                     }
+                    const uint32_t wn = base + 64 * U;   // the dword after the pass (lane 63's last partner)
+                    const uint32_t nx = (sh && wn <= we) ? ap[wn - wa] : 0u;
 #pragma unroll
                     for (uint32_t u = 0; u < U; ++u) {
                         const uint32_t w = base + u * 64 + tid;
+                        uint32_t hi = __shfl_down(lo[u], 1, 64);
+                        const uint32_t hn = u + 1 < U ? __shfl(lo[u + 1 < U ? u + 1 : u], 0, 64) : nx;
+                        if (tid == 63) hi = hn;
                         if (w >= we) continue;
-                        uint32_t v = sh ? (lo[u] >> sh) | (hi[u] << (32u - sh)) : lo[u];
+                        uint32_t v = sh ? (lo[u] >> sh) | (hi << (32u - sh)) : lo[u];
                         if (4u * w + 3u >= l2 && 4u * w < l2 + 12u) {
                             uint32_t pv = 0;
                             for (uint32_t q = 0; q < 4; ++q)
@@ -820,16 +961,27 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
     if (win)
         for (uint32_t b = dst0 + tid; b < stride; b += 64) win[b] = 0;
     if (tid == 0 && a.dgram_len) a.dgram_len[j] = out_len;
-    if (a.dgram_frags)
-        for (uint32_t p = tid; p < a.cache_max; p += 64)
-            a.dgram_frags[(size_t)j * a.cache_max + p] =
-                p < nlist ? a.rid[(size_t)r * a.cache_max + chain_at(order, p)] : ~0ull;
+    if (a.dgram_frags && tid < a.cache_max)
+        a.dgram_frags[(size_t)j * a.cache_max + tid] = live ? (((uint64_t)e1.w << 32) | e1.z) : ~0ull;
 }
 
-// one wave per slot (a fixed grid striding over the slots measured slower: 50 vs 40 µs for D1)
-__global__ void __launch_bounds__(kSlotBlock) df_assemble_kernel(DfArgs a) {
-    const uint32_t j = blockIdx.x * (kSlotBlock / 64) + (threadIdx.x >> 6);
-    if (j < a.n) df_assemble_slot(a, j, (uint32_t)a.ctl[C_NDGRAM]);
+// one wave per batch position w: the stash of fragment w, then datagram slot w (a fixed grid striding over the slots
+// measured slower: 50 vs 40 µs for D1).  The two are independent (the stash writes the store slots of fragments
+// held past this batch; the assembly reads this batch's fragments from the input and earlier batches' from their
+// store slots), so they share one launch.
+#ifndef DF_ASM_WAVES
+#define DF_ASM_WAVES 0   // > 0: the compiler is held to this many waves per SIMD (A/B builds)
+#endif
+#if DF_ASM_WAVES > 0
+__global__ void __launch_bounds__(kSlotBlock) __attribute__((amdgpu_waves_per_eu(DF_ASM_WAVES, DF_ASM_WAVES)))
+#else
+__global__ void __launch_bounds__(kSlotBlock)
+#endif
+df_assemble_kernel(DfArgs a) {
+    const uint32_t w = blockIdx.x * (kSlotBlock / 64) + (threadIdx.x >> 6);
+    if (w >= a.n) return;
+    df_stash_one(a, w);
+    df_assemble_slot(a, w, (uint32_t)a.ctl[C_NDGRAM]);
 }
 
 // ---- aging + table rebuild (one workgroup) ----------------------------------------------------------------------------
@@ -898,6 +1050,7 @@ __global__ void df_init_kernel(DfArgs a) {
         a.rhdr[(size_t)t * kRecWords] = 0;
     }
     if (t < C_WORDS) a.ctl[t] = t == C_FREE_TOP ? a.fcb_max : 0ull;
+    if (t < a.nlook) a.look[t] = 0ull;
 }
 
 }  // namespace
@@ -910,6 +1063,7 @@ struct ppe_defrag_table {
     void *allocs[24] = {};
     int nalloc = 0;
     unsigned long long *h_ctl = nullptr;   // pinned
+    uint32_t epoch = 0;                    // admission look-back tag of the last call
     char err[256] = {0};
 };
 
@@ -983,10 +1137,12 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
               dalloc(d, &a.rid, (size_t)c.fcb_max * c.cache_max) &&
               dalloc(d, &a.store, (size_t)c.fcb_max * c.cache_max * d->sstride + 64) && dalloc(d, &a.freestk, c.fcb_max) &&
               dalloc(d, &a.ctl, C_WORDS) && dalloc(d, &a.frec, (size_t)mb * kFrecWords) && dalloc(d, &a.fslot, mb) &&
-              dalloc(d, &a.inserted, mb) && dalloc(d, &a.dgrec, mb) && dalloc(d, &a.dgsrc, mb) &&
+              dalloc(d, &a.inserted, mb) && dalloc(d, &a.dgrec, mb) &&
+              dalloc(d, &a.plan, (size_t)std::min(mb, c.fcb_max) * c.cache_max * 8) &&
               dalloc(d, &a.tcnt, blocks(mb, 64)) && dalloc(d, &a.skey[0], mb) && dalloc(d, &a.sval[0], mb) &&
               dalloc(d, &a.skey[1], mb) && dalloc(d, &a.sval[1], mb) && dalloc(d, &a.hist, (size_t)256 * sb) &&
-              dalloc(d, &a.dropped, (size_t)c.fcb_max * c.cache_max);
+              dalloc(d, &a.dropped, (size_t)c.fcb_max * c.cache_max) &&
+              dalloc(d, &a.look, blocks(mb, kBlock));
     if (ok && hipHostMalloc((void **)&d->h_ctl, C_WORDS * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
         ok = false;
     if (!ok) {
@@ -994,7 +1150,8 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
         return PPE_ENOMEM;
     }
     a.max_dropped = c.fcb_max * c.cache_max;
-    const uint32_t span = std::max(ns, std::max(c.fcb_max, (uint32_t)C_WORDS));
+    a.nlook = blocks(mb, kBlock);
+    const uint32_t span = std::max(std::max(ns, a.nlook), std::max(c.fcb_max, (uint32_t)C_WORDS));
     hipLaunchKernelGGL(df_init_kernel, dim3(blocks(span, 256)), dim3(256), 0, 0, a);
     if (hipDeviceSynchronize() != hipSuccess) {
         ppe_defrag_destroy(d);
@@ -1044,9 +1201,8 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
     const uint32_t g = blocks(a.n, kBlock);
     a.sort_blocks = blocks(a.n, kSortBlock);
     hipLaunchKernelGGL(df_parse_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(df_claim_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    a.flag_mode = 0;
-    hipLaunchKernelGGL(df_tile_count_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    if (++d->epoch == 0) d->epoch = 1;   // (0 is the cleared array's tag)
+    a.epoch = d->epoch;
     hipLaunchKernelGGL(df_admit_kernel, dim3(g), dim3(kBlock), 0, s, a);
     uint32_t passes = 1;   // sort keys are batch indices < n
     while (passes < 4 && (uint64_t)a.n > (1ull << (8 * passes))) ++passes;
@@ -1061,8 +1217,6 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
         std::swap(a.sval[0], a.sval[1]);
     }
     hipLaunchKernelGGL(df_process_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    hipLaunchKernelGGL(df_stash_kernel, dim3(blocks(a.n, kSlotBlock / 64)), dim3(kSlotBlock), 0, s, a);
-    a.flag_mode = 1;
     hipLaunchKernelGGL(df_place_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_assemble_kernel, dim3(blocks(a.n, kSlotBlock / 64)), dim3(kSlotBlock), 0, s, a);
     return launched(d, "ppe_defrag");

@@ -2,7 +2,6 @@
 # profile sets of the stateless configs and of the stateful rows:  bash tools/gpu_r4final.sh TAG
 set -o pipefail
 T=$1
-bash tools/gpu_r4o.sh r4o   # (the D1 stride / prefetch A/B first: short, variant libraries only)
 bash tools/gpu_final.sh $T && \
 timeout -k 10 600 bash tools/profile_round.sh $T "C1 C2 C3 C4" > gpurun_out/$T/profile_round.log 2>&1 && \
 timeout -k 10 300 bash tools/profile_stateful.sh $T > gpurun_out/$T/profile_stateful.log 2>&1
