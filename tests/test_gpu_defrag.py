@@ -120,6 +120,53 @@ def test_cache_max_16_and_big_buffers(eng):
     replay(eng, a, o, l, 2048, cache_max=16, reasm_buf_bytes=16384, timeout=5)
 
 
+@pytest.mark.parametrize("fcb_max", [1 << 20, 1000])
+def test_large_batch_lookback(eng, fcb_max):
+    """One 524,288-fragment batch: 2,048 admission workgroups, more than the GPU holds at once beside the other
+    work, so the look-back ranking the creators crosses workgroups that start late.  With fcb_max 1000 the batch's
+    ~170k creators overflow the pool and exactly the first 1,000 in index order may get FCBs: any rank error shows in
+    the statuses.  Status, datagram index, count, lengths and fragment ids against the oracle (bytes: the other
+    tests)."""
+    import bench
+    a1, o1, l1 = synth.make_fragment_stream(int(65536 / 3.1) + 64, seed=31)
+    n1 = 65536
+    off1, len1 = o1[:n1].copy(), l1[:n1].copy()
+    end = int(off1[-1]) + int(len1[-1])
+    base = np.zeros(end + 64, np.uint8)
+    base[:end] = a1[:end]
+    _, variant = bench.defrag_batch_variants(base, off1, len1, 8)
+    copies = 8
+    arena_all = np.concatenate([variant(v + 1) for v in range(copies)])
+    off = np.concatenate([off1 + np.uint64(v * len(base)) for v in range(copies)])
+    lens = np.tile(len1, copies)
+    n = len(lens)
+    ids = np.arange(n, dtype=np.uint64) * 5 + 3
+    g = Defrag(eng, fcb_max=fcb_max, max_batch=n)
+    o = pyoracle.OracleDefrag(fcb_max=fcb_max)
+    try:
+        ref = o.batch(arena_all, off, lens, NOW, ids=ids, full=False)
+        out = g.alloc_out(n, 128, full=False)
+        g.run_torch(torch.from_numpy(arena_all).to(DEV),
+                    torch.from_numpy(off.view(np.int64)).to(DEV),
+                    torch.from_numpy(lens.view(np.int32)).to(DEV), out, NOW,
+                    ids=torch.from_numpy(ids.view(np.int64)).to(DEV))
+        torch.cuda.synchronize()
+        st = out["status"].cpu().numpy().view(np.uint32)
+        bad = np.nonzero(st != ref["status"])[0]
+        assert len(bad) == 0, f"status: {len(bad)} mismatches, first {bad[:6].tolist()}"
+        nd = ref["n_dgram"]
+        assert int(out["n_dgram"].item()) == nd
+        assert np.array_equal(out["dgram_of"].cpu().numpy().view(np.uint32), ref["dgram_of"])
+        assert np.array_equal(out["dgram_len"].cpu().numpy().view(np.uint32), ref["dgram_len"])
+        assert np.array_equal(out["dgram_frags"].cpu().numpy().view(np.uint64)[:nd], ref["dgram_frags"][:nd])
+        gi, os_ = g.info(), o.stats()
+        for k, v in os_.items():
+            assert gi[k] == v, (k, gi[k], v)
+    finally:
+        g.close()
+        o.close()
+
+
 def test_window_64(eng):
     a, o, l = synth.make_fragment_stream(600, seed=11)
     p = DfPair(eng, stride=64)
