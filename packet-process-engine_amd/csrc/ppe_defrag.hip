@@ -500,7 +500,10 @@ __device__ __forceinline__ uint32_t chain_at(uint64_t order, uint32_t pos) { ret
 // next kWin positions (contiguous) and the neighbour's key; (2) the head's parsed record, which carries its FCB record
 // and table slot (df_sort_pass_kernel INIT), and the window's parsed records and ids; (3) the FCB header (and, for an
 // FCB from an earlier batch, its chain descriptors).  A segment longer than the window refills one position per step.
-constexpr uint32_t kWin = 16;
+#ifndef DF_PROC_WIN
+#define DF_PROC_WIN 16
+#endif
+constexpr uint32_t kWin = DF_PROC_WIN;
 __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint32_t (*cdesc)[kBlock],
                                                uint32_t (*cidx)[kBlock], uint32_t *st, uint32_t &teardrop) {
     const uint32_t tl = threadIdx.x;
@@ -523,29 +526,22 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
     for (uint32_t u = 1; u < kWin; ++u) m += kq[u] == g ? 1u : 0u;
     bool more = m == kWin;    // the segment may continue past the window
     uint32_t qn = j + kWin;   // the next sorted position to read into the window
-    uint4 fa[kWin];
-    uint2 fb[kWin];
-    uint64_t fid[kWin];
-    const uint4 h67 = *(const uint4 *)(a.frec + (size_t)g * kFrecWords + 4);
-    fa[0] = *(const uint4 *)(a.frec + (size_t)g * kFrecWords);
-    fb[0] = make_uint2(h67.x, h67.y);
-    fid[0] = a.id ? a.id[g] : (uint64_t)g;
+    // the window's parsed-record words 2-5 (id | proto | mf, offset | frag_len, frame length, l2 | ihl*4): the state
+    // machine reads nothing else of a fragment (its id goes to the FCB's id list in the stash / place kernels)
+    uint4 fw[kWin];
+    const uint2 h67 = *(const uint2 *)(a.frec + (size_t)g * kFrecWords + 6);
+    fw[0] = *(const uint4 *)(a.frec + (size_t)g * kFrecWords + 2);
 #pragma unroll
-    for (uint32_t u = 1; u < kWin; ++u) {
-        if (u < m) {
-            fa[u] = *(const uint4 *)(a.frec + (size_t)iq[u] * kFrecWords);
-            fb[u] = *(const uint2 *)(a.frec + (size_t)iq[u] * kFrecWords + 4);
-            fid[u] = a.id ? a.id[iq[u]] : (uint64_t)iq[u];
-        }
-    }
-    const uint32_t r = h67.z, s0 = h67.w;
+    for (uint32_t u = 1; u < kWin; ++u)
+        if (u < m) fw[u] = *(const uint4 *)(a.frec + (size_t)iq[u] * kFrecWords + 2);
+    const uint32_t r = h67.x, s0 = h67.y;
     if (s0 != kNone) a.creator[s0] = kNone;   // the group key has been used: reset for the next batch
     if (r == kNone) {   // a fragment without a record (no FCB, or not a fragment): a singleton group
         const uint32_t s = s0 != kNone ? PPE_DF_FCB_FULL : PPE_DF_NOT_FRAG;
         a.status[g] = s;
         a.inserted[g] = kNone;
         a.dgrec[g] = kNone;
-        st[s]++;
+        atomicAdd(st + s, 1u);   // (LDS: the workgroup's status counts)
         return;
     }
     uint32_t *h = a.rhdr + (size_t)r * kRecWords;
@@ -569,32 +565,10 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
             cidx[k][tl] = 0;
         }
     }
-    // the segment's fragments in order
-    while (m) {
-        const uint32_t i = iq[0];
-        const uint32_t fr[6] = {fa[0].x, fa[0].y, fa[0].z, fa[0].w, fb[0].x, fb[0].y};
-        const uint64_t fragid = fid[0];
-#pragma unroll
-        for (uint32_t u = 0; u + 1 < kWin; ++u) {
-            iq[u] = iq[u + 1];
-            fa[u] = fa[u + 1];
-            fb[u] = fb[u + 1];
-            fid[u] = fid[u + 1];
-        }
-        --m;
-        if (more) {   // refill the window's last position (segments longer than kWin only)
-            more = false;
-            if (qn < a.n && key[qn] == g) {
-                const uint32_t x = val[qn];
-                iq[kWin - 1] = x;
-                fa[kWin - 1] = *(const uint4 *)(a.frec + (size_t)x * kFrecWords);
-                fb[kWin - 1] = *(const uint2 *)(a.frec + (size_t)x * kFrecWords + 4);
-                fid[kWin - 1] = a.id ? a.id[x] : (uint64_t)x;
-                ++m;
-                ++qn;
-                more = true;
-            }
-        }
+    // the segment's fragments in order: the window's entries by static index (the step is inlined once per window
+    // position, so no register array is shifted or indexed per lane), then a longer segment's rest one by one
+    auto step = [&](const uint32_t i, const uint4 w) {
+        const uint32_t fr[6] = {0u, 0u, w.x, w.y, w.z, w.w};   // (words 0-1 unused here)
         uint32_t out = PPE_DF_CACHED, ins = kNone, done = kNone;
         bool tear = false;
         // FragFind / fcb_create refresh the FCB's timestamp (decode-defrag.c:139, 472); a.rts[r] = now below
@@ -653,7 +627,6 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
                 *(uint4 *)(descw + k * 4) = make_uint4(fr[3], fr[4], w2, 0u);
                 cdesc[k][tl] = fr[3];
                 cidx[k][tl] = i + 1;
-                a.rid[(size_t)r * a.cache_max + k] = fragid;
                 if (pos == 0) hd0 = w2;
                 const uint64_t lo = order & ((1ull << (4 * pos)) - 1ull);
                 const uint64_t hi = pos + 1 < 16 ? (order >> (4 * pos)) << (4 * (pos + 1)) : 0ull;
@@ -689,7 +662,14 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
         a.dgrec[i] = done;
         // the place kernel's per-tile count of completing fragments (zeroed by the first scatter pass)
         if (done != kNone) atomicAdd(a.tcnt + (i >> 6), 1u);
-        st[out]++;
+        atomicAdd(st + out, 1u);
+    };
+#pragma unroll
+    for (uint32_t u = 0; u < kWin; ++u)
+        if (u < m) step(iq[u], fw[u]);
+    for (uint32_t q = qn; more && q < a.n && key[q] == g; ++q) {
+        const uint32_t x = val[q];
+        step(x, *(const uint4 *)(a.frec + (size_t)x * kFrecWords + 2));
     }
     *(uint4 *)h = make_uint4(flags | (last_in << 8) | (cache_num << 16) | (nlist << 24), (uint32_t)total,
                              (uint32_t)meat, h03.w);
@@ -703,14 +683,12 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
     __shared__ uint32_t wg[PPE_DF__COUNT + 1];   // per-status counts + teardrops of this workgroup
     if (threadIdx.x <= PPE_DF__COUNT) wg[threadIdx.x] = 0;
     __syncthreads();
-    uint32_t st[PPE_DF__COUNT] = {}, teardrop = 0;
+    uint32_t teardrop = 0;
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    if (j < a.n) df_process_one(a, j, cdesc, cidx, st, teardrop);
-    // LDS atomics, then one global atomic per counter per workgroup: per-lane global atomics on the same few
-    // words serialise in one L2 channel (they were most of this kernel's time)
-#pragma unroll
-    for (int s = 0; s < PPE_DF__COUNT; ++s)
-        if (st[s]) atomicAdd(&wg[s], st[s]);
+    // per-fragment LDS atomics into the workgroup's status counts (one instruction each, nothing waits on them), then
+    // one global atomic per counter per workgroup: per-lane global atomics on the same few words serialise in one L2
+    // channel (they were most of this kernel's time)
+    if (j < a.n) df_process_one(a, j, cdesc, cidx, wg, teardrop);
     if (teardrop) atomicAdd(&wg[PPE_DF__COUNT], teardrop);
     __syncthreads();
     if (threadIdx.x <= PPE_DF__COUNT && wg[threadIdx.x])
@@ -727,6 +705,8 @@ __device__ __forceinline__ void df_stash_one(const DfArgs &a, uint32_t i) {
     uint8_t *dst = a.store + ((size_t)r * a.cache_max + k) * a.sstride;
     const uint32_t tot = a.len[i];
     const uint32_t lane = __lane_id();
+    // the held fragment's id, kept with its store slot (the FCB's id list: later datagram plans and aging read it)
+    if (lane == 0) a.rid[(size_t)r * a.cache_max + k] = a.id ? a.id[i] : (uint64_t)i;
     if (((uintptr_t)src & 3u) == 0) {
         // all of a pass's loads are issued before its stores (2 KB per pass: one pass for a frag_buf frame)
         constexpr uint32_t U = 8;
@@ -762,6 +742,27 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
         a.ctl[C_DGRAMS] += nd;
         if (a.n_dgram) *a.n_dgram = nd;
     }
+    {
+        // the slots of this workgroup's range past the datagram count: zero window, length 0, ~0 id row (the ABI's
+        // "every output written"), as whole-workgroup coalesced stores instead of one assembly wave per slot
+        const uint32_t s0 = max(nd, blockIdx.x * kBlock), s1 = min(a.n, (blockIdx.x + 1) * kBlock);
+        if (s0 < s1) {
+            if (a.dgram_hdr) {
+                const size_t lo = (size_t)s0 * a.hdr_stride, hi = (size_t)s1 * a.hdr_stride;
+                if (((uintptr_t)a.dgram_hdr & 15u) == 0 && (a.hdr_stride & 15u) == 0) {
+                    for (size_t o = lo + 16u * threadIdx.x; o < hi; o += 16u * kBlock)
+                        *(uint4 *)(a.dgram_hdr + o) = make_uint4(0u, 0u, 0u, 0u);
+                } else {
+                    for (size_t o = lo + threadIdx.x; o < hi; o += kBlock) a.dgram_hdr[o] = 0;
+                }
+            }
+            if (a.dgram_len)
+                for (uint32_t t = s0 + threadIdx.x; t < s1; t += kBlock) a.dgram_len[t] = 0;
+            if (a.dgram_frags)
+                for (size_t e = (size_t)s0 * a.cache_max + threadIdx.x; e < (size_t)s1 * a.cache_max; e += kBlock)
+                    a.dgram_frags[e] = ~0ull;
+        }
+    }
     const uint32_t r = i < a.n ? a.dgrec[i] : kNone;
     const bool f = r != kNone;
     const uint64_t b = __builtin_amdgcn_ballot_w64(f);
@@ -785,15 +786,18 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
             if (p < nlist) {
                 const uint32_t kk = chain_at(order, p);
                 dd[p] = *(const uint4 *)(desc + kk * 4);
-                id[p] = a.rid[(size_t)r * a.cache_max + kk];
             }
         }
 #pragma unroll
         for (uint32_t p = 0; p < 16; ++p) {
             if (p < nlist) {
                 const uint32_t kk = chain_at(order, p);
-                fb[p] = dd[p].w ? (uint64_t)(uintptr_t)(a.pkt + a.off[dd[p].w - 1])
-                                : (uint64_t)(uintptr_t)(a.store + ((size_t)r * a.cache_max + kk) * a.sstride);
+                // this batch's fragments (word 3 = index + 1): the input frame and id; earlier ones: the store slot
+                // and the id the stash kept
+                const uint32_t x = dd[p].w;
+                fb[p] = x ? (uint64_t)(uintptr_t)(a.pkt + a.off[x - 1])
+                          : (uint64_t)(uintptr_t)(a.store + ((size_t)r * a.cache_max + kk) * a.sstride);
+                id[p] = x ? (a.id ? a.id[x - 1] : (uint64_t)(x - 1)) : a.rid[(size_t)r * a.cache_max + kk];
             }
         }
         uint32_t *pe = a.plan + (size_t)j * a.cache_max * 8;
@@ -810,8 +814,8 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
 }
 
 // ---- assemble: one wave per datagram slot ----------------------------------------------------------------------
-// DF_AB (diagnostic builds only, wrong outputs): 1 = empty slots skip their zeroing, 2 = no window bytes, 4 = no
-// header checksum, 8 = datagram bytes not copied
+// DF_AB (diagnostic builds only, wrong outputs): 2 = no window bytes, 4 = no header checksum, 8 = datagram bytes not
+// copied
 #ifndef DF_AB
 #define DF_AB 0
 #endif
@@ -821,18 +825,7 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
 __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, uint32_t nd) {
     const uint32_t tid = __lane_id();
     uint8_t *win = (a.dgram_hdr && !(DF_AB & 2)) ? a.dgram_hdr + (size_t)j * a.hdr_stride : nullptr;
-    if ((DF_AB & 1) && j >= nd) return;
-    if (j >= nd) {
-        if (win && ((uintptr_t)win & 3u) == 0) {
-            if (tid < a.hdr_stride / 4) ((uint32_t *)win)[tid] = 0u;
-        } else if (win) {
-            for (uint32_t b = tid; b < a.hdr_stride; b += 64) win[b] = 0;
-        }
-        if (tid == 0 && a.dgram_len) a.dgram_len[j] = 0;
-        if (a.dgram_frags)
-            for (uint32_t k = tid; k < a.cache_max; k += 64) a.dgram_frags[(size_t)j * a.cache_max + k] = ~0ull;
-        return;
-    }
+    if (j >= nd) return;   // an empty slot: the place kernel wrote its window, length and id row
     // lane p holds chain entry p of the plan (df_place_kernel): descriptor words 0 (offset | frag_len << 16), 1 (frame
     // length), 2 (l2 | ihl*4 << 8 | proto << 16), the frame's base (the input frame when the fragment arrived in
     // this batch, else its store slot) and its id: one read for the whole chain, used below by lane broadcasts
