@@ -63,8 +63,9 @@ constexpr uint32_t kRecWords = 8;
 
 // control words (u64)
 enum { C_RUNNING = 0, C_NEW, C_DEL, C_FREE_TOP, C_DGRAMS, C_TEARDROP, C_TIMEOUT_DROP, C_NDGRAM, C_ST0 = 8,
-       C_CREATORS = C_ST0 + PPE_DF__COUNT + 2, C_AGE_DROPPED, C_AGE_FREED, C_SCRATCH,
+       C_CREATORS = C_ST0 + PPE_DF__COUNT + 2, C_AGE_DROPPED, C_AGE_FREED, C_SCRATCH, C_LOOK_ERR,
        C_WORDS = 24 };
+static_assert(C_LOOK_ERR < C_WORDS, "control words");
 
 // parsed fragment record words (frec): sip, dip, id | proto << 16 | mf << 24, off | flen << 16, totlen,
 // l2 | ihl4 << 8, hash, valid
@@ -318,7 +319,7 @@ __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
         for (uint32_t k = 0; k < kBlock / 64; ++k) agg += wc[k];
         if (lane == 0)
             __hip_atomic_store(a.look + blockIdx.x, tag | kAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t excl = 0;
+        uint32_t excl = 0, spins = 0;
         for (int end = (int)blockIdx.x; end > 0;) {
             const int p = end - 1 - (int)lane;   // lane 0: the nearest predecessor
             const unsigned long long v =
@@ -328,7 +329,16 @@ __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
             const uint64_t wait = __builtin_amdgcn_ballot_w64(!ready);
             const uint32_t fi = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;   // the nearest inclusive lane
             const uint64_t upto = fi < 63 ? (2ull << fi) - 1ull : ~0ull;          // lanes [0, fi]
-            if (wait & upto) continue;   // a predecessor before it has not published yet
+            if (wait & upto) {   // a predecessor before it has not published yet
+                // bounded: a word that never arrives (a broken dispatch-order assumption) is reported, not waited
+                // for forever (ppe_defrag_info returns PPE_EIO; the batch's admissions are then wrong)
+                if (++spins > (1u << 22)) {
+                    if (lane == 0) atomicAdd(a.ctl + C_LOOK_ERR, 1ull);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
             uint32_t c = lane <= fi ? (uint32_t)(v & kCount) : 0u;
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
@@ -1243,6 +1253,12 @@ int ppe_defrag_info(ppe_defrag_t *d, ppe_defrag_info_t *info) {
         hipMemcpy(d->h_ctl, d->base.ctl, C_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return dfail(d, PPE_EIO, "ppe_defrag_info: device error");
     const unsigned long long *c = d->h_ctl;
+    if (c[C_LOOK_ERR]) {   // reported once: cleared, so only this call fails
+        const unsigned long long zero = 0;
+        (void)hipMemcpy(d->base.ctl + C_LOOK_ERR, &zero, sizeof(zero), hipMemcpyHostToDevice);
+        return dfail(d, PPE_EIO, "ppe_defrag_info: %llu admission look-back timeouts (results of those batches wrong)",
+                     c[C_LOOK_ERR]);
+    }
     memset(info, 0, sizeof(*info));
     info->running = c[C_RUNNING];
     info->new_fcb = c[C_NEW];
