@@ -1,0 +1,10 @@
+# round 4: D1 parse writing every valid fragment's key through to memory before its probe (no store round between a
+# claimer's probe and its CAS)
+set -o pipefail
+O=gpurun_out/${1:-r4al}
+mkdir -p $O
+L=packet-process-engine_amd
+PPE_LIB=$L/libppe_hip_dfks.so timeout -k 10 500 python -u -m pytest -x -v --timeout 240 --timeout-method thread \
+  tests/test_gpu_defrag.py tests/test_gpu_mbuf.py > $O/pytest_defrag.txt 2>&1 || exit 1
+timeout -k 10 300 python -u tools/ab_defrag.py --variant prod=$L/libppe_hip.so --variant ks=$L/libppe_hip_dfks.so \
+  > $O/ab_defrag.txt 2>&1
