@@ -968,10 +968,10 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
         a.dgram_frags[(size_t)j * a.cache_max + tid] = live ? (((uint64_t)e1.w << 32) | e1.z) : ~0ull;
 }
 
-// one wave per batch position w: the stash of fragment w, then datagram slot w (a fixed grid striding over the slots
-// measured slower: 50 vs 40 µs for D1).  The two are independent (the stash writes the store slots of fragments
-// held past this batch; the assembly reads this batch's fragments from the input and earlier batches' from their
-// store slots), so they share one launch.
+// one wave per batch position w: datagram slot w, or (positions past the datagram count) the stashes of a share of
+// the fragments (a fixed grid striding over the slots measured slower: 50 vs 40 µs for D1).  The two are independent
+// (the stash writes the store slots of fragments held past this batch; the assembly reads this batch's fragments
+// from the input and earlier batches' from their store slots), so they share one launch.
 #ifndef DF_ASM_WAVES
 #define DF_ASM_WAVES 0   // > 0: the compiler is held to this many waves per SIMD (A/B builds)
 #endif
@@ -983,8 +983,15 @@ __global__ void __launch_bounds__(kSlotBlock)
 df_assemble_kernel(DfArgs a) {
     const uint32_t w = blockIdx.x * (kSlotBlock / 64) + (threadIdx.x >> 6);
     if (w >= a.n) return;
-    df_stash_one(a, w);
-    df_assemble_slot(a, w, (uint32_t)a.ctl[C_NDGRAM]);
+    const uint32_t nd = (uint32_t)a.ctl[C_NDGRAM];
+    if (w < nd) {
+        df_assemble_slot(a, w, nd);
+        if (nd == a.n) df_stash_one(a, w);   // (every position a datagram: nothing is held, checked anyway)
+    } else {
+        // the stashes go to the waves without a datagram, so no wave copies both: wave w takes fragments
+        // w - nd, w - nd + (n - nd), ...
+        for (uint32_t i = w - nd; i < a.n; i += a.n - nd) df_stash_one(a, i);
+    }
 }
 
 // ---- aging + table rebuild (one workgroup) ----------------------------------------------------------------------------
