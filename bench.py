@@ -403,6 +403,124 @@ def cpu_baseline(pk, rules, image, seconds, what):
             "single_thread_mpps": m / one_s / 1e6}
 
 
+def sharded_cpu(nshards, setup, run_pass, seconds):
+    """Run-to-completion shards on this host's cores (mainloop, main.c:422-425): shard i in its own thread pinned to
+    core i, `run_pass(state, rep)` over and over for `seconds` after one untimed `setup(i)` pass.  ctypes releases
+    the GIL around the oracle's C calls, so the shards run in parallel.  Returns (units per second, passes); a pass
+    returns the units it processed."""
+    import threading
+    cores = host_cores()[:nshards]
+    done = [0] * len(cores)
+    span = [0.0] * len(cores)
+    states = [None] * len(cores)
+    gate = threading.Barrier(len(cores) + 1)
+
+    def worker(i):
+        os.sched_setaffinity(0, {cores[i]})
+        states[i] = setup(i)
+        gate.wait()
+        t0 = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t0 < seconds:
+            done[i] += run_pass(states[i], reps)
+            reps += 1
+        span[i] = time.perf_counter() - t0
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(cores))]
+    for t in th:
+        t.start()
+    gate.wait()
+    for t in th:
+        t.join()
+    return sum(done) / max(span), len(cores)
+
+
+def flow_cpu_baseline(pk, rules, image, flows, seconds):
+    """F1's CPU baseline: the oracle's FlowHandlePacket (tree-walk ACL on misses) over the bench batch after its flows
+    are established, on one core, and on every core with the batch sharded by flow hash, one flow table per core
+    (the reference keeps flow_table[LOCAL_CPU_ID], dataplane/src/flow/flow.c:33,481-490, and the NIC steers a flow
+    to one core, platform/oct-init.c:139-151)."""
+    import pyoracle
+    from ppe import abi
+    n = len(pk["len"])
+    o = pyoracle.Oracle(rules, default_action=abi.ACL_RULE_ACTION_FW, image=image)
+    fh = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=8)["flow_hash"]
+    ncores = len(host_cores())
+
+    def make(shards):
+        def setup(i):
+            idx = np.nonzero(fh % shards == i)[0]
+            h, ln = np.ascontiguousarray(pk["hdr"][idx]), np.ascontiguousarray(pk["len"][idx])
+            ft = pyoracle.OracleFlow(o, capacity=2 * flows // shards + 4096)
+            ft.classify_batch(h, ln, cfg=o.cfg(0, 1, NOW), use_tree=True)  # establish this core's flows
+            return ft, h, ln
+
+        def run_pass(st, rep):
+            ft, h, ln = st
+            ft.classify_batch(h, ln, cfg=o.cfg(0, 1, NOW + 1 + rep), use_tree=True)
+            return len(ln)
+        return setup, run_pass
+
+    one, _ = sharded_cpu(1, *make(1), seconds / 4)
+    allc, used = sharded_cpu(ncores, *make(ncores), seconds)
+    return {"value": allc / 1e6, "unit": "Mpps", "cores": used, "kind": "port",
+            "sample": f"passes of the {n}-packet batch after its flows were established, sharded by flow hash over "
+                      f"{used} pinned threads with one flow table each (oracle FlowHandlePacket, tree-walk ACL on "
+                      f"misses; {seconds:.1f} s); 1 pinned thread, the whole batch in one table: "
+                      f"{one / 1e6:.2f} Mpps",
+            "single_thread_mpps": one / 1e6}
+
+
+def defrag_cpu_baseline(variant, off, lens, fcb_max, seconds):
+    """D1's CPU baseline: the oracle's sequential Defrag (datagram bytes assembled) over fresh copies of the bench
+    batch, on one core, and on every core with the fragments sharded by FCB key (sip, dip, ip_id: every fragment
+    of a datagram on one core), one FCB table per core (dataplane/src/decode/decode-defrag.c keeps its tables per
+    core).  The source-address byte that makes each copy's datagrams fresh is left out of the shard key."""
+    import pyoracle
+    n = len(lens)
+    base = variant(2)
+    l2 = np.where((base[off + 12] == 0x81) & (base[off + 13] == 0x00), 18, 14).astype(np.int64)
+    ip = off.astype(np.int64) + l2
+    b = lambda k: base[ip + k].astype(np.uint32)
+    key = ((b(13) << 16) | (b(14) << 8) | b(15)) * 0x9E3779B1 ^ ((b(16) << 24) | (b(17) << 16) | (b(18) << 8) | b(19)) \
+        ^ ((b(4) << 8) | b(5)) * 0x85EBCA6B
+    key = key.astype(np.uint32)
+    host = [variant(v + 2) for v in range(16)]
+    ncores = len(host_cores())
+
+    def make(shards):
+        def setup(i):
+            idx = np.nonzero(key % shards == i)[0]
+            m = len(idx)
+            o = pyoracle.OracleDefrag(fcb_max=max(1024, fcb_max // shards))
+            so, sl = np.ascontiguousarray(off[idx]), np.ascontiguousarray(lens[idx])
+            ids = idx.astype(np.uint64)
+            oo = dict(status=np.zeros(m, np.uint32), dgram_of=np.zeros(m, np.uint32), dgram_len=np.zeros(m, np.uint32),
+                      dgram_frags=np.zeros((m, 8), np.uint64), dgram_pkt=np.zeros((m, 8168), np.uint8))
+            return o, so, sl, ids, oo
+
+        def run_pass(st, rep):
+            o, so, sl, ids, oo = st
+            a = host[rep % len(host)]
+            o.lib.oracle_defrag_batch(o.h, a.ctypes.data, so.ctypes.data, sl.ctypes.data, ids.ctypes.data, len(sl),
+                                      NOW + rep, oo["status"].ctypes.data, oo["dgram_of"].ctypes.data,
+                                      oo["dgram_pkt"].ctypes.data, oo["dgram_len"].ctypes.data,
+                                      oo["dgram_frags"].ctypes.data)
+            if (rep + 1) % len(host) == 0:
+                o.age(NOW + 10**7 + rep, 20)   # the reference ages once a second; here once per variant cycle
+            return len(sl)
+        return setup, run_pass
+
+    one, _ = sharded_cpu(1, *make(1), seconds / 4)
+    allc, used = sharded_cpu(ncores, *make(ncores), seconds)
+    return {"value": allc / 1e6, "unit": "Mfps", "cores": used, "kind": "port",
+            "sample": f"passes of the {n}-fragment batch (fresh datagrams each pass), sharded by FCB key over {used} "
+                      f"pinned threads with one FCB table each (the oracle's sequential Defrag, datagram bytes "
+                      f"assembled; {seconds:.1f} s); 1 pinned thread, the whole batch in one table: "
+                      f"{one / 1e6:.3f} Mfps",
+            "single_thread_mfps": one / 1e6}
+
+
 def measure_c0(args, dev):
     """C0 (BASELINE configs[0]): the reference's own plumbing case, 10k x 64-B IPv4/UDP packets and 16 rules on ONE
     CPU thread: the oracle restatement on one pinned core (the reported baseline), and beside it the same batch as
@@ -769,8 +887,8 @@ def flow_bytes(stride: int, owner: bool = False) -> float:
 def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     """--config F1: ppe_classify_flow batch after batch (one stream: each batch sees the table the previous ones
     left) over a fixed population of bidirectional flows established during the warmup.  nested: measured after the
-    stateless configs of the default line and returned as its configs.F1 entry (no CPU baseline; at N > 1 every
-    rank owns its flows, as the reference's cores do behind the NIC's flow steering: no exchange)."""
+    stateless configs of the default line and returned as its configs.F1 entry (with a shorter CPU baseline; at N > 1
+    every rank owns its flows, as the reference's cores do behind the NIC's flow steering: no exchange)."""
     import ctypes as C
     from ppe import abi
     name = name or args.config
@@ -896,22 +1014,9 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     batch_achieved = flow_bytes(stride) * n / (my_ms / args.steps / 1e3) / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not nested:
-        import pyoracle
-        pk = bufs[0][4]
-        o = pyoracle.Oracle(rules, default_action=abi.ACL_RULE_ACTION_FW, image=eng.image())
-        ft = pyoracle.OracleFlow(o, capacity=2 * flows)
-        ft.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), use_tree=True)  # establish the flows
-        reps, tc = 0, time.perf_counter()
-        while time.perf_counter() - tc < args.cpu_seconds:
-            ft.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW + 1 + reps), use_tree=True)
-            reps += 1
-        cpu_s = time.perf_counter() - tc
-        ft.close()
-        cpu = {"value": n * reps / cpu_s / 1e6, "unit": "Mpps", "cores": 1, "kind": "port",
-               "sample": f"{reps} passes of one core's flow table (oracle FlowHandlePacket, tree-walk ACL) over the "
-                         f"{n}-packet batch after the flows were established ({n * reps} packets, {cpu_s:.1f} s); the "
-                         f"reference keeps one table per core, so cores scale it by flow-hash sharding"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = flow_cpu_baseline(bufs[0][4], rules, eng.image(), flows,
+                                args.nested_cpu_seconds if nested else args.cpu_seconds)
 
     line = None
     if rank == 0:
@@ -972,7 +1077,8 @@ def nested_line(line):
     """A stateful config's own line, reduced to what a nested configs entry carries."""
     if line is None:
         return None
-    out = {k: line[k] for k in ("metric", "value", "unit", "ms_per_step", "roofline", "parity_sample_ok") if k in line}
+    out = {k: line[k] for k in ("metric", "value", "unit", "ms_per_step", "roofline", "parity_sample_ok",
+                                "cpu_baseline") if k in line}
     out["workload"] = line["config"]["workload"]
     for k in ("flow_table", "new_flows_in_timed_region", "counters", "defrag_info", "held_fragments_per_batch",
               "new_fcb_in_timed_region", "fcb_full_in_timed_region"):
@@ -1103,29 +1209,9 @@ def run_defrag(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     achieved = bytes_call / (call_ms / 1e3) / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not nested:
-        import pyoracle
-        o = pyoracle.OracleDefrag(fcb_max=cfgd["fcb_max"])
-        host = [variant(v + 2) for v in range(min(nvar, 16))]
-        ids = np.arange(n, dtype=np.uint64)
-        oo = dict(status=np.zeros(n, np.uint32), dgram_of=np.zeros(n, np.uint32), dgram_len=np.zeros(n, np.uint32),
-                  dgram_frags=np.zeros((n, 8), np.uint64), dgram_pkt=np.zeros((n, 8168), np.uint8))
-        reps, tc = 0, time.perf_counter()
-        while time.perf_counter() - tc < args.cpu_seconds:
-            a = host[reps % len(host)]
-            o.lib.oracle_defrag_batch(o.h, a.ctypes.data, off.ctypes.data, lens.ctypes.data, ids.ctypes.data, n,
-                                      NOW + reps, oo["status"].ctypes.data, oo["dgram_of"].ctypes.data,
-                                      oo["dgram_pkt"].ctypes.data, oo["dgram_len"].ctypes.data,
-                                      oo["dgram_frags"].ctypes.data)
-            reps += 1
-            if reps % len(host) == 0:
-                o.age(NOW + 10**7 + reps, 20)   # the reference ages once a second; here once per variant cycle
-        cpu_s = time.perf_counter() - tc
-        o.close()
-        cpu = {"value": n * reps / cpu_s / 1e6, "unit": "Mfps", "cores": 1, "kind": "port",
-               "sample": f"{reps} passes of one core's Defrag (the oracle's sequential restatement, datagram bytes "
-                         f"assembled) over the {n}-fragment batch ({n * reps} fragments, {cpu_s:.1f} s); the "
-                         f"reference keeps one FCB table per core"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = defrag_cpu_baseline(variant, off, lens, cfgd["fcb_max"],
+                                  args.nested_cpu_seconds if nested else args.cpu_seconds)
 
     line = None
     if rank == 0:

@@ -10,10 +10,12 @@
  *   reg_fw_alert / DP_Log_Func                            dataplane/src/common/dp_log.c:12-31
  *   int DP_Acl_Lookup(mbuf_t *)                           dataplane/src/flow/flow.c:232
  *
- * The reference decodes one mbuf per call on the calling core.  Here Decode(m) appends the mbuf to the calling
- * thread's own burst (one per thread, as the reference's per-core mainloop) and the burst is classified on the GPU
- * when it reaches the burst size or when that thread calls Decode_Flush(); the
- * verdict is then delivered exactly as the reference does — output_fw_proc(m) / output_drop_proc(m) hooks, with
+ * The reference decodes one mbuf per call on the calling core and has finished with it when Decode returns
+ * (decode.c:13-28).  So does this Decode by default: the burst size is 1, and Decode(m) classifies m on the GPU and
+ * delivers it before it returns.  A caller that wants GPU-sized batches opts in with Decode_Set_Burst(n): Decode(m)
+ * then appends the mbuf to the calling thread's own burst (one per thread, as the reference's per-core mainloop),
+ * classified when it reaches n entries or when that thread calls Decode_Flush() (or exits).  Either way the
+ * verdict is delivered exactly as the reference does — output_fw_proc(m) / output_drop_proc(m) hooks, with
  * DP_Log_Func(m) on the drop reasons the reference logs — and the mbuf's parse fields are filled in.
  * Every classification runs on the GPU; there is no CPU decode path.
  */
@@ -141,8 +143,9 @@ void Decode(mbuf_t *m);
  * reference ends every undelivered packet in output_drop_proc).  Hooks run with no engine lock held, so a hook
  * may call Decode() again (e.g. a punt hook feeding reassembled datagrams back). */
 int  Decode_Flush(void);
-/* Burst size at which Decode() flushes automatically (default 4096); may be changed at any time, it applies to
- * every thread's next Decode(). */
+/* Burst size at which Decode() flushes automatically: 1 (the default) = synchronous, the reference's contract; a
+ * larger n queues up to n mbufs per thread (the caller then calls Decode_Flush() at its batch boundaries).  May be
+ * changed at any time; it applies to every thread's next Decode().  n = 0 is ignored. */
 void Decode_Set_Burst(uint32_t n);
 
 /* Batch form of DP_Acl_Lookup over already-decoded mbufs (ACL_RULE_ACTION_FW / _DROP per mbuf). */

@@ -37,7 +37,7 @@ extern "C" {
 /* 2: ppe_tuning_t grew to 20 B (batches_per_launch) and mbuf_t (ppe_decode.h) took the reference's field layout;
  * 3: ppe_tuple's word 3 carries the TCP window-scale option offset (bits 9-15); 4: ppe_result_t.part8;
  * 5: the tuple carries a fragment's Defrag fields and the option-past-the-window bit; strides 64..256 */
-#define PPE_ABI_VERSION 5
+#define PPE_ABI_VERSION 6
 
 /* error codes (negative return values) */
 #define PPE_OK       0
@@ -172,6 +172,9 @@ typedef struct {
     uint32_t blob_bytes;       /* device image size                                                        */
     uint32_t lds_resident;     /* 1 if the image is staged into LDS by the kernel                          */
     double   build_ms;
+    uint32_t cut_bits;         /* cut-list section (image v7): sip bits | dip bits << 8; 0 with cut_entries
+                                  0 = no cut lists (ABI version 6)                                            */
+    uint32_t cut_entries;      /* entries of the cut lists (rules replicated into the buckets they meet)   */
 } ppe_acl_stats_t;
 
 typedef struct ppe_ctx ppe_ctx_t;
@@ -249,12 +252,13 @@ int  ppe_acl_image(ppe_ctx_t *ctx, uint32_t *words, uint32_t *n_words);
 typedef struct {
     uint32_t block;          /* workgroup size 256, 512 or 1024; 0 = chosen per classifier image   */
     uint32_t blocks_per_cu;  /* workgroups per CU (<= 32); 0 = resident count from the occupancy API */
-    uint32_t pipeline;       /* tile fetch: 0 auto (4 when the image fits in LDS, else 3), 1 first
-                                tile loaded at the loop top, 4 first tile requested before the image
-                                staging, 3 four tiles per wave loaded, decoded and walked together
-                                (one 1024-thread workgroup per CU), 5 one tile per wave walking the
-                                image's 2-level blocks (two 1024-thread workgroups per CU, each
-                                staging the block levels that fit half the LDS); others PPE_EINVAL */
+    uint32_t pipeline;       /* tile fetch / walk: 0 auto (4 when the image's tree fits in LDS, else 5
+                                when it has cut lists, else 3), 1 first tile loaded at the loop top,
+                                4 first tile requested before the image staging, 3 four tiles per
+                                wave loaded, decoded and walked together through the 2-level blocks
+                                (one 1024-thread workgroup per CU), 5 the cut lists (image v7: one
+                                tile per wave, bucket groups in LDS, list entries from L2; an image
+                                without cut lists takes the automatic choice); others PPE_EINVAL   */
     uint32_t lds_image;      /* 1 = stage the image (or its top) in LDS, 0 = read it from global   */
     uint32_t batches_per_launch;  /* ppe_classify_batches: batches one launch takes (<= 4096); 0 = all
                                      of a call's batches in ONE persistent launch (descriptor ring)  */
@@ -263,12 +267,10 @@ int  ppe_set_tuning(ppe_ctx_t *ctx, const ppe_tuning_t *t);
 int  ppe_get_tuning(ppe_ctx_t *ctx, ppe_tuning_t *t);
 
 /* Launch geometry in use (for profiling notes).  variant = image mode (0 global, 1 LDS, 2 split) | fetch << 4
- * (fetch 0 first tile at the loop top, 1 first tile requested before the image staging, 3 four tiles per wave). */
+ * (fetch 0 first tile at the loop top, 1 first tile requested before the image staging, 3 four tiles per wave,
+ * 5 cut lists). */
 int  ppe_launch_info(ppe_ctx_t *ctx, uint32_t *grid, uint32_t *block, uint32_t *lds_bytes, uint32_t *variant);
 
-/* Diagnostics: device buffer for per-wave phase timestamps written by a library built with -DPPE_TRACE (make
- * variant NAME=trace VFLAGS=-DPPE_TRACE=1); the product build ignores it.  Layout: tools/trace_analyze.py. */
-int  ppe_debug_trace(ppe_ctx_t *ctx, void *dev_buf);
 
 /* ---- Stateful flow table (dataplane/src/flow/flow.c) ----
  * One table per context (the reference keeps one per core, flow_table[LOCAL_CPU_ID]; across GPUs, shard packets by

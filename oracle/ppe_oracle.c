@@ -266,6 +266,40 @@ int32_t oracle_acl_blocks(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t d
     return -1;
 }
 
+/* Lookup in the image's cut lists (format v7, ppe_image.h): the bucket of the key's top sip / dip bits, then its
+ * list's entries in priority order, each checked as a compact record (prefix marker bits, port spans, the exit's
+ * protocol bits).  Like the compact leaf, only TCP / UDP keys reach it (the classify path). */
+int32_t oracle_acl_cut(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                       const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action) {
+    const uint32_t *im = g_img;
+    const uint32_t *h = im + im[PPE_IMG_W_OFFCUT];
+    const uint32_t b0 = h[0] & 0xffu, b1 = (h[0] >> 8) & 0xffu;
+    const uint32_t bk = (uint32_t)(((uint64_t)sip >> (32u - b0)) << b1) | (uint32_t)((uint64_t)dip >> (32u - b1));
+    const uint32_t *g = im + h[4] + 4u * (bk >> 4);
+    uint32_t first = g[0];
+    for (uint32_t k = 0; k < (bk & 15u); k++) first += (g[1u + (k >> 3)] >> (4u * (k & 7u))) & 15u;
+    const uint32_t k = bk & 15u, cnt = (g[1u + (k >> 3)] >> (4u * (k & 7u))) & 15u;
+    (void)dmac; (void)smac; (void)ts;
+    for (uint32_t j = 0; j < cnt; j++) {
+        const uint32_t *r = im + h[5] + PPE_CUT_ENT_WORDS * (first + j);
+        const uint32_t x = r[4];
+        const uint32_t ms = (x & PPE_CX_S32) ? ~0u : ~(((r[0] & (0u - r[0])) << 1) - 1u);
+        const uint32_t md = (x & PPE_CX_D32) ? ~0u : ~(((r[1] & (0u - r[1])) << 1) - 1u);
+        const int m = ((sip ^ r[0]) & ms) == 0 && ((dip ^ r[1]) & md) == 0 &&
+                      (uint16_t)(sport - (r[2] & 0xffffu)) <= (r[3] & 0xffffu) &&
+                      (uint16_t)(dport - (r[2] >> 16)) <= (r[3] >> 16) &&
+                      (proto == 6 ? (x & PPE_CX_TCP) : proto == 17 ? (x & PPE_CX_UDP) : 0) != 0;
+        if (m) {
+            const uint32_t id = x & PPE_CX_SLOT;
+            /* the action word a drop-or-forward decision needs: the classify path compares it with DROP only */
+            if (action) *action = (x & PPE_CX_DROP) ? ACL_RULE_ACTION_DROP : oracle_rule_action(id);
+            return (int32_t)id;
+        }
+    }
+    if (action) *action = im[PPE_IMG_W_DEFACT];
+    return -1;
+}
+
 /* ---- flow table: one core's flow_table[LOCAL_CPU_ID] (dataplane/src/flow/flow.c, flow.h) ----
  * FLOW_BUCKET_NUM chained buckets indexed by flow_hashfn & FLOW_BUCKET_MASK (flow.c:76-79, flow.h:87-88), items from
  * a fixed pool of `capacity` (the FPA flow-node pool, mem_pool.h:72), head insertion (FlowInsert, flow.c:69-72). */
@@ -326,7 +360,8 @@ static void flow_miss_drop(omb_t *m, uint32_t st, int c) {
 }
 
 /* ---- FlowHandlePacket, dataplane/src/flow/flow.c:271-310 with FlowGetFlowFromHash :181-245 ---- */
-static __thread int t_use_tree;  /* per shard: 1 = walk the image's nodes, 2 = its blocks, 0 = linear first match */
+static __thread int t_use_tree;  /* per shard: 1 = walk the image's nodes, 2 = its blocks, 3 = its cut lists, 0 = linear
+                                    first match */
 
 static void flow_handle_packet(omb_t *m) {
     oracle_result_t *r = m->r;
@@ -351,7 +386,9 @@ static void flow_handle_packet(omb_t *m) {
         /* PortScan_Detect disabled (portscan_able = 0) */
         uint32_t act;
         r->flags |= PPE_F_ACL;
-        r->acl_hit = t_use_tree == 2 ? oracle_acl_blocks(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac,
+        r->acl_hit = t_use_tree == 3 ? oracle_acl_cut(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac,
+                                                       m->smac, m->ts, &act)
+                   : t_use_tree == 2 ? oracle_acl_blocks(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac,
                                                           m->smac, m->ts, &act)
                    : t_use_tree ? oracle_acl_tree(r->sip, r->dip, r->sport, r->dport, r->proto, m->dmac, m->smac,
                                                   m->ts, &act)

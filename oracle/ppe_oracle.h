@@ -78,6 +78,9 @@ int32_t oracle_acl_tree(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dpo
                         const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action);
 int32_t oracle_acl_blocks(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
                         const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action);
+/* lookup in the image's cut lists (v7; TCP / UDP keys); same contract */
+int32_t oracle_acl_cut(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
+                       const uint8_t *dmac, const uint8_t *smac, uint64_t ts, uint32_t *action);
 
 /* One packet.  pkt holds at least `avail` bytes of the frame; len is the wire length (pkt_totallen).
  * Bytes past `avail` read as 0 (the reach field says whether the verdict depended on them). */

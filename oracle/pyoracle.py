@@ -56,6 +56,9 @@ def load():
         lib.oracle_acl_linear.restype = C.c_int32
         lib.oracle_acl_tree.argtypes = [u32, u32, u32, u32, u32, vp, vp, u64, C.POINTER(u32)]
         lib.oracle_acl_tree.restype = C.c_int32
+        for fn in ("oracle_acl_blocks", "oracle_acl_cut"):
+            getattr(lib, fn).argtypes = [u32, u32, u32, u32, u32, vp, vp, u64, C.POINTER(u32)]
+            getattr(lib, fn).restype = C.c_int32
         lib.oracle_flow_create.argtypes = [u32]
         lib.oracle_flow_create.restype = vp
         lib.oracle_flow_destroy.argtypes = [vp]

@@ -257,6 +257,96 @@ Forest build_forest(const std::vector<Rule> &R, std::vector<Work> roots, uint32_
     return f;
 }
 
+// ---- cut lists (image v7, ppe_image.h) ----
+struct CutLists {
+    uint32_t b0 = 0, b1 = 0, max_len = 0;
+    std::vector<uint8_t> len;        // per bucket
+    std::vector<uint32_t> entries;   // rule slots, bucket after bucket, each bucket's in priority order
+    size_t n_entries = 0;
+};
+
+// The lists of the cut (b0 sip bits, b1 dip bits): per bucket, the rules whose box meets it in ascending index,
+// closed after the first rule that covers the whole bucket for every key that reaches the ACL on the classify path
+// (every sport / dport, protocols 6 and 17).  False when a list would exceed PPE_CUT_MAX_LIST entries or the work
+// (buckets visited) the budget.  store = false: the list lengths only (the width search), no entries.
+bool cut_lists(const std::vector<Rule> &R, uint32_t b0, uint32_t b1, size_t budget, CutLists &out, bool store) {
+    const uint32_t nb = 1u << (b0 + b1);
+    std::vector<uint8_t> len(nb, 0), closed(nb, 0);
+    std::vector<std::vector<uint32_t>> lists(store ? nb : 0u);
+    size_t n_ent = 0;
+    size_t visits = 0;
+    uint32_t max_len = 0;
+    const uint64_t w0 = 1ull << (32 - b0), w1 = 1ull << (32 - b1);  // keys per bucket row / column
+    for (uint32_t s = 0; s < R.size(); ++s) {
+        const Rule &r = R[s];
+        const uint32_t x0 = b0 ? r.lo[PPE_DIM_SIP] >> (32 - b0) : 0u, x1 = b0 ? r.hi[PPE_DIM_SIP] >> (32 - b0) : 0u;
+        const uint32_t y0 = b1 ? r.lo[PPE_DIM_DIP] >> (32 - b1) : 0u, y1 = b1 ? r.hi[PPE_DIM_DIP] >> (32 - b1) : 0u;
+        const bool ports_all = r.lo[PPE_DIM_SPORT] == 0u && r.hi[PPE_DIM_SPORT] == 0xffffu &&
+                               r.lo[PPE_DIM_DPORT] == 0u && r.hi[PPE_DIM_DPORT] == 0xffffu &&
+                               r.lo[PPE_DIM_PROTO] <= 6u && r.hi[PPE_DIM_PROTO] >= 17u;
+        for (uint32_t x = x0; x <= x1; ++x) {
+            // the rule covers bucket row x iff its sip range holds the row's whole key range
+            const bool cx = (uint64_t)r.lo[PPE_DIM_SIP] <= x * w0 && (uint64_t)r.hi[PPE_DIM_SIP] >= x * w0 + w0 - 1u;
+            for (uint32_t y = y0; y <= y1; ++y) {
+                if (++visits > budget) return false;
+                const uint32_t b = (x << b1) | y;
+                if (closed[b]) continue;
+                if (++len[b] > PPE_CUT_MAX_LIST) return false;
+                if (store) lists[b].push_back(s);
+                ++n_ent;
+                max_len = std::max(max_len, (uint32_t)len[b]);
+                const bool cy = (uint64_t)r.lo[PPE_DIM_DIP] <= y * w1 && (uint64_t)r.hi[PPE_DIM_DIP] >= y * w1 + w1 - 1u;
+                if (ports_all && cx && cy) closed[b] = 1;
+            }
+        }
+    }
+    out.b0 = b0;
+    out.b1 = b1;
+    out.max_len = max_len;
+    out.len = std::move(len);
+    out.entries.clear();
+    out.n_entries = n_ent;
+    if (store)
+        for (uint32_t b = 0; b < nb; ++b) out.entries.insert(out.entries.end(), lists[b].begin(), lists[b].end());
+    return true;
+}
+
+// Pick the cut: every split of T = b0 + b1 <= PPE_CUT_MAX_BITS bits between sip and dip, by the expected entries a
+// lookup reads (half for a uniformly random key: entries / buckets; half for a key inside a rule's box, the
+// size-biased list length sum(len^2) / entries), plus a little for the longest list (the wave's trip count) and for
+// every bit (LDS).  PPE_CUT_BITS=T (tests, A/B) fixes the total.  False when no cut qualifies (a list longer than 15
+// entries at every width: then the classify kernel walks the tree).
+bool choose_cut(const std::vector<Rule> &R, CutLists &best) {
+    const char *fb = std::getenv("PPE_CUT_BITS");
+    const int force = fb && *fb ? std::atoi(fb) : -1;
+    const size_t budget = 16u * (R.size() + 1u) + (1u << PPE_CUT_MAX_BITS);
+    double cbest = 1e30;
+    uint32_t bb0 = 0, bb1 = 0;
+    bool found = false;
+    for (uint32_t T = 0; T <= PPE_CUT_MAX_BITS; ++T) {
+        if (force >= 0 && (int)T != force) continue;
+        if (force < 0 && T < 4 && R.size() > 15) continue;  // (too few buckets for any list to fit)
+        for (uint32_t b0 = 0; b0 <= T; ++b0) {
+            CutLists c;
+            if (!cut_lists(R, b0, T - b0, budget, c, false)) continue;
+            const double nb = (double)(1u << T), ne = (double)c.n_entries;
+            double sq = 0;
+            for (uint8_t l : c.len) sq += (double)l * l;
+            const double cost = 0.5 * ne / nb + 0.5 * (ne ? sq / ne : 0.0) + 0.02 * c.max_len + 0.01 * T;
+            if (std::getenv("PPE_ACL_DEBUG"))
+                std::fprintf(stderr, "acl_build: cut sip %u dip %u: entries %zu max %u cost %.3f\n", b0, T - b0,
+                             c.n_entries, c.max_len, cost);
+            if (cost < cbest - 1e-9) {
+                cbest = cost;
+                bb0 = b0;
+                bb1 = T - b0;
+                found = true;
+            }
+        }
+    }
+    return found && cut_lists(R, bb0, bb1, budget, best, true);
+}
+
 }  // namespace
 
 extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
@@ -403,13 +493,13 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         return PPE_BLK_LEAF | slot | (compact ? cx_flags(slot) : 0u);
     };
     if (max_leaf > 1 && lwords.size() >= (1u << 23)) return PPE_ENOMEM;  // leaf exits hold 23-bit list offsets
-    // K-level blocks (ppe_image.h block section): position p of a block holds node pos[p] (p's children are 2p + 1
-    // and 2p + 2); a leaf passes through (threshold ~0, both children itself); the 2^K exits lead to the next
-    // blocks or carry leaf payloads.  Breadth-first from every root.
+    // 2-level blocks (ppe_image.h block section): position p of a block holds node pos[p] (p's children are 2p + 1
+    // and 2p + 2); a leaf passes through (threshold ~0, both children itself); the 4 exits lead to the next blocks
+    // or carry leaf payloads.  Breadth-first from every root.
     std::vector<uint32_t> bwords;
-    uint32_t max_bdepth = 1, KL = 2;
-    auto build_blocks = [&](uint32_t K) {
-        const uint32_t npos = (1u << K) - 1u, bw = K == 2 ? PPE_BLK_WORDS : PPE_BLK3_WORDS;
+    uint32_t max_bdepth = 1;
+    auto build_blocks = [&]() {
+        constexpr uint32_t npos = 3u, bw = PPE_BLK_WORDS;
         std::vector<uint32_t> bnode, bdepth;
         bwords.clear();
         max_bdepth = 1;
@@ -420,7 +510,7 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
             return (uint32_t)bnode.size() - 1u;
         };
         for (uint32_t r = 0; r < best.n_roots; ++r) add_block(r, 1u);
-        uint32_t pos[15];
+        uint32_t pos[npos];
         for (size_t bi = 0; bi < bnode.size(); ++bi) {  // blocks appended while scanning: breadth-first order
             pos[0] = bnode[bi];
             for (uint32_t q = 1; q < npos; ++q) pos[q] = (q & 1u) ? c0(pos[(q - 1u) / 2u]) : c1(pos[(q - 1u) / 2u]);
@@ -445,22 +535,12 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         }
         return (uint32_t)bnode.size();
     };
-    // K = 2 by default.  3-level blocks take one L2 round trip per three levels instead of two (C3: lockstep group
-    // steps with an L2 read 4.6 -> 2.4, tools/block_levels.py), but measured slower on C3 (step 32.4 us per 1M with
-    // 2-level blocks, 33.9 / 36.4 with 3-level blocks at 4 / 3 tiles per wave: gpurun_out/r3c): the
-    // 64-B block in flight per lane and tile costs the registers that would hold more tiles.  PPE_BLOCK_LEVELS=3
-    // selects them (tests, A/B).
-    const char *bl = std::getenv("PPE_BLOCK_LEVELS");
-    const int force_k = bl && *bl ? std::atoi(bl) : 0;
-    uint32_t n_blocks = build_blocks(2);
-    if (force_k == 3) {
-        KL = 3;
-        n_blocks = build_blocks(3);
-    }
+    // (3-level 64-B blocks, an option until round 4, take one L2 round trip per three levels instead of two but
+    // measured slower on C3: the 64-B block in flight per lane and tile costs the registers of more tiles)
+    const uint32_t n_blocks = build_blocks();
     if (n_blocks >= PPE_BLK_LEAF) return PPE_ENOMEM;
-    const uint32_t balign = KL == 2 ? 7u : 15u;  // 32- / 64-B aligned blocks
     const uint32_t off_bsec = (end_resid + 7u) & ~7u;
-    const uint32_t off_blocks = (off_bsec + n_jump + balign) & ~balign;
+    const uint32_t off_blocks = (off_bsec + n_jump + 7u) & ~7u;  // 32-B aligned blocks
     // compact records and the slot → index table follow the blocks, so the block section and the records they lead
     // to are one contiguous range (the multi-tile kernel stages it whole when it fits the CU's LDS)
     bool holes = false;
@@ -468,9 +548,20 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     const uint32_t off_crec = compact ? off_blocks + (uint32_t)bwords.size() : 0u;
     const uint32_t off_idtab = compact && holes ? off_crec + PPE_CREC_WORDS * (n_slots + 1u) : 0u;
     // (the index table has an entry for the sentinel slot too: crec_check reads idtab[slot] for every leaf)
-    const uint32_t total = !compact ? off_blocks + (uint32_t)bwords.size()
-                           : off_idtab ? off_idtab + ((n_slots + 1u + 3u) & ~3u)
-                                       : off_crec + PPE_CREC_WORDS * (n_slots + 1u);
+    const uint32_t end_tree = !compact ? off_blocks + (uint32_t)bwords.size()
+                              : off_idtab ? off_idtab + ((n_slots + 1u + 3u) & ~3u)
+                                          : off_crec + PPE_CREC_WORDS * (n_slots + 1u);
+    // ---- the cut-list section (v7): a classifier of its own for the classify kernel, after the tree ----
+    CutLists cut;
+    const char *cenv = std::getenv("PPE_CUT");
+    const bool want_cut = !any_resid && !(cenv && *cenv == '0');
+    const bool have_cut = want_cut && choose_cut(R, cut) && cut.entries.size() < (1u << 25);  // (< 1 GB of entries)
+    const uint32_t off_cut = have_cut ? (end_tree + 7u) & ~7u : 0u;
+    const uint32_t n_groups = have_cut ? std::max(1u, (1u << (cut.b0 + cut.b1)) / 16u) : 0u;
+    const uint32_t off_grp = off_cut + PPE_CUT_HDR_WORDS;  // 32-B aligned
+    const uint32_t off_ent = off_grp + 4u * n_groups;      // 32-B aligned (n_groups >= 1, 16 B each: see below)
+    const uint32_t off_ent_al = (off_ent + 7u) & ~7u;
+    const uint32_t total = have_cut ? off_ent_al + PPE_CUT_ENT_WORDS * (uint32_t)cut.entries.size() : end_tree;
 
     uint32_t *img = (uint32_t *)std::calloc(total, sizeof(uint32_t));
     if (!img) return PPE_ENOMEM;
@@ -495,7 +586,45 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     img[PPE_IMG_W_MAXBDEPTH] = max_bdepth;
     img[PPE_IMG_W_OFFCREC] = off_crec;
     img[PPE_IMG_W_OFFIDTAB] = off_idtab;
-    img[PPE_IMG_W_BLKLV] = KL;
+    img[PPE_IMG_W_BLKLV] = 2u;
+    img[PPE_IMG_W_OFFCUT] = off_cut;
+    if (have_cut) {
+        uint32_t *h = img + off_cut;
+        h[0] = cut.b0 | (cut.b1 << 8);
+        h[1] = 1u << (cut.b0 + cut.b1);
+        h[2] = (uint32_t)cut.entries.size();
+        h[3] = cut.max_len;
+        h[4] = off_grp;
+        h[5] = off_ent_al;
+        h[6] = n_groups;
+        const uint32_t nb = h[1];
+        uint32_t first = 0;
+        for (uint32_t g = 0; g < n_groups; ++g) {  // {first entry, 8 + 8 four-bit lengths, 0}
+            uint32_t *o = img + off_grp + 4u * g;
+            o[0] = first;
+            for (uint32_t k = 0; k < 16u && 16u * g + k < nb; ++k) {
+                const uint32_t len = cut.len[16u * g + k];
+                o[1u + (k >> 3)] |= len << (4u * (k & 7u));
+                first += len;
+            }
+        }
+        auto pfx = [](uint32_t lo, uint32_t hi) { return lo == hi ? lo : lo | (((hi - lo) >> 1) + 1u); };
+        for (size_t e = 0; e < cut.entries.size(); ++e) {
+            const Rule &r = R[cut.entries[e]];
+            uint32_t *o = img + off_ent_al + PPE_CUT_ENT_WORDS * e;
+            o[0] = pfx(r.lo[PPE_DIM_SIP], r.hi[PPE_DIM_SIP]);
+            o[1] = pfx(r.lo[PPE_DIM_DIP], r.hi[PPE_DIM_DIP]);
+            o[2] = r.lo[PPE_DIM_SPORT] | (r.lo[PPE_DIM_DPORT] << 16);
+            o[3] = (r.hi[PPE_DIM_SPORT] - r.lo[PPE_DIM_SPORT]) | ((r.hi[PPE_DIM_DPORT] - r.lo[PPE_DIM_DPORT]) << 16);
+            uint32_t x = r.id;  // (n <= 2^24: the index fits the exit's 24 bits)
+            if (r.action == ACL_RULE_ACTION_DROP) x |= PPE_CX_DROP;
+            if (r.lo[PPE_DIM_PROTO] <= 6u && 6u <= r.hi[PPE_DIM_PROTO]) x |= PPE_CX_TCP;
+            if (r.lo[PPE_DIM_PROTO] <= 17u && 17u <= r.hi[PPE_DIM_PROTO]) x |= PPE_CX_UDP;
+            if (r.lo[PPE_DIM_SIP] == r.hi[PPE_DIM_SIP]) x |= PPE_CX_S32;
+            if (r.lo[PPE_DIM_DIP] == r.hi[PPE_DIM_DIP]) x |= PPE_CX_D32;
+            o[4] = x;
+        }
+    }
     if (compact) {
         // prefix | marker bit (len 0..31), or the address of a /32
         // (a prefix box spans 2^(32 - len) keys: its marker bit 1 << (31 - len) is half that count)
@@ -584,6 +713,8 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
         st->max_depth = max_depth;
         st->avg_depth = n_leaves ? depth_sum / n_leaves : 0.0;
         st->blob_bytes = total * 4u;
+        st->cut_bits = have_cut ? cut.b0 | (cut.b1 << 8) : 0u;
+        st->cut_entries = have_cut ? (uint32_t)cut.entries.size() : 0u;
         st->build_ms =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }

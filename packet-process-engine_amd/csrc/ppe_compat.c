@@ -7,7 +7,8 @@
  *   DP_Acl_Rule_Release     dataplane/src/platform/oct-init.c:755
  *   DP_Acl_Rule_Commit      the dp_acl_rule_commit protocol, dataplane/src/common/dp_cmd.c:1987-2053
  *   DP_Acl_Lookup           dataplane/src/flow/flow.c:232
- *   Decode                  dataplane/src/decode/decode.c:19-28 (burst-queued; see ppe_decode.h)
+ *   Decode                  dataplane/src/decode/decode.c:19-28 (synchronous by default, burst-queued on request;
+ *                           see ppe_decode.h)
  *   reg_fw_alert/DP_Log_Func dataplane/src/common/dp_log.c:12-31
  *   plugin_modules          dataplane/src/plugin/plugin-mod/plugin.c:8
  * Every packet decision is made by the HIP kernels; nothing here inspects packet bytes to classify them.
@@ -221,7 +222,10 @@ typedef struct {
     uint32_t n, alloc;
 } burst_t;
 
-static volatile uint32_t g_burst_cap = 4096;
+/* 1 (the default): Decode(m) classifies m and delivers it through a hook before it returns, the reference's contract
+ * (decode.c:13-28: the packet is output or dropped inside Decode), so a mainloop linked unchanged (main.c:296-301)
+ * sees every packet completed; a caller that calls Decode_Flush() opts into bursts with Decode_Set_Burst(n). */
+static volatile uint32_t g_burst_cap = 1;
 static pthread_key_t g_burst_key;
 static pthread_once_t g_burst_once = PTHREAD_ONCE_INIT;
 static __thread burst_t *t_burst = NULL;
@@ -335,7 +339,8 @@ static void fill_mbuf(mbuf_t *m, uint32_t v, uint32_t fhash, int32_t hit, const 
     m->payload_len = (uint16_t)(tu[3] >> 16);
     m->payload = l4 + (tcp ? (uint32_t)(l4[12] >> 4) * 4u : 8u);
     const uint32_t ws = PPE_TUPLE_WS(tu[3]);
-    if (tcp && ws) {  /* DecodeTCPOptions' window-scale record (decode-tcp.c:61-70), found by the kernel */
+    if (tcp && ws && !m->tcpvars.ws) {  /* DecodeTCPOptions' window-scale record (decode-tcp.c:61-70), found by the
+                                          * kernel; like the reference, only into an mbuf with none recorded yet */
         uint8_t *o = l4 + ws;
         m->tcpvars.tcp_opts[0].type = o[0];
         m->tcpvars.tcp_opts[0].len = o[1];

@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -106,6 +107,9 @@ struct DfArgs {
     uint32_t shift, sort_blocks;         // radix pass: digit shift, workgroups
     unsigned long long *look;            // admission: per-workgroup look-back words (epoch << 32 | flags | count)
     uint32_t epoch, nlook;               // this call's tag (never 0) and the look-back array's length
+    uint32_t look_spins;                 // admission: polls of an unpublished predecessor before giving up
+    uint32_t look_fail_wg;               // test hook (PPE_DF_LOOK_FAIL): this workgroup's look-back fails at once
+    unsigned long long *err_host;        // pinned, device-mapped: set by a failed look-back (ppe_defrag reports it)
     uint64_t *dropped;                   // age: ids of dropped fragments
     uint32_t max_dropped;
 };
@@ -320,7 +324,12 @@ __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
         if (lane == 0)
             __hip_atomic_store(a.look + blockIdx.x, tag | kAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t excl = 0, spins = 0;
+        bool failed = false;
         for (int end = (int)blockIdx.x; end > 0;) {
+            if (blockIdx.x == a.look_fail_wg) {
+                failed = true;
+                break;
+            }
             const int p = end - 1 - (int)lane;   // lane 0: the nearest predecessor
             const unsigned long long v =
                 p >= 0 ? __hip_atomic_load(a.look + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag | kIncl;
@@ -331,9 +340,9 @@ __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
             const uint64_t upto = fi < 63 ? (2ull << fi) - 1ull : ~0ull;          // lanes [0, fi]
             if (wait & upto) {   // a predecessor before it has not published yet
                 // bounded: a word that never arrives (a broken dispatch-order assumption) is reported, not waited
-                // for forever (ppe_defrag_info returns PPE_EIO; the batch's admissions are then wrong)
-                if (++spins > (1u << 22)) {
-                    if (lane == 0) atomicAdd(a.ctl + C_LOOK_ERR, 1ull);
+                // for forever
+                if (++spins > a.look_spins) {
+                    failed = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -347,19 +356,29 @@ __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
             end -= 64;
         }
         if (lane == 0) {
-            __hip_atomic_store(a.look + blockIdx.x, tag | kIncl | (excl + agg), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            wbase = excl;
+            // a failed look-back publishes no inclusive prefix (its aggregate stands, so the workgroups after it
+            // still sum the right prefix through it) and admits none of its creators (their FCBs are not created:
+            // no two creators can take one record); the failure reaches the caller: the next ppe_defrag call and
+            // ppe_defrag_info return PPE_EIO
+            if (failed) {
+                atomicAdd(a.ctl + C_LOOK_ERR, 1ull);
+                __hip_atomic_store(a.err_host, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                __hip_atomic_store(a.look + blockIdx.x, tag | kIncl | (excl + agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            wbase = failed ? ~0u : excl;
         }
     }
     __syncthreads();
     uint32_t base = wbase;
+    const bool failed = base == ~0u;
     for (uint32_t k = 0; k < w; ++k) base += wc[k];   // the workgroup's earlier waves
     if (!f) return;
     const uint32_t rank = base + (uint32_t)__popcll(b & lanemask_lt());
     const uint32_t s = a.fslot[i];
     // fcb_create (decode-defrag.c:74-81): fetch-and-add, fail when the previous count reached DEFRAG_FCB_MAX
-    if (a.ctl[C_RUNNING] + rank < a.fcb_max) {
+    if (!failed && a.ctl[C_RUNNING] + rank < a.fcb_max) {
         const uint32_t r = a.freestk[a.ctl[C_FREE_TOP] - 1 - rank];
         const uint32_t *fr = a.frec + (size_t)i * kFrecWords;
         uint32_t *k = a.tkey + (size_t)s * 4;
@@ -1073,6 +1092,7 @@ struct ppe_defrag_table {
     void *allocs[24] = {};
     int nalloc = 0;
     unsigned long long *h_ctl = nullptr;   // pinned
+    unsigned long long *h_err = nullptr;   // pinned, device-mapped: a batch's admission look-back failed
     uint32_t epoch = 0;                    // admission look-back tag of the last call
     char err[256] = {0};
 };
@@ -1155,12 +1175,20 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
               dalloc(d, &a.look, blocks(mb, kBlock));
     if (ok && hipHostMalloc((void **)&d->h_ctl, C_WORDS * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
         ok = false;
+    if (ok && (hipHostMalloc((void **)&d->h_err, sizeof(unsigned long long), hipHostMallocMapped) != hipSuccess ||
+               hipHostGetDevicePointer((void **)&a.err_host, d->h_err, 0) != hipSuccess))
+        ok = false;
     if (!ok) {
         ppe_defrag_destroy(d);
         return PPE_ENOMEM;
     }
     a.max_dropped = c.fcb_max * c.cache_max;
     a.nlook = blocks(mb, kBlock);
+    *d->h_err = 0;
+    a.look_spins = 1u << 22;
+    a.look_fail_wg = ~0u;
+    if (const char *e = getenv("PPE_DF_LOOK_FAIL"))  // test hook: this workgroup index fails its look-back
+        a.look_fail_wg = (uint32_t)atoi(e);
     const uint32_t span = std::max(std::max(ns, a.nlook), std::max(c.fcb_max, (uint32_t)C_WORDS));
     hipLaunchKernelGGL(df_init_kernel, dim3(blocks(span, 256)), dim3(256), 0, 0, a);
     if (hipDeviceSynchronize() != hipSuccess) {
@@ -1177,6 +1205,7 @@ int ppe_defrag_destroy(ppe_defrag_t *d) {
     (void)hipDeviceSynchronize();
     for (int k = 0; k < d->nalloc; ++k) (void)hipFree(d->allocs[k]);
     if (d->h_ctl) (void)hipHostFree(d->h_ctl);
+    if (d->h_err) (void)hipHostFree(d->h_err);
     delete d;
     return PPE_OK;
 }
@@ -1192,6 +1221,13 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
         return dfail(d, PPE_EINVAL, "pkt/off/len and status/dgram_hdr/dgram_len are required");
     if (out->hdr_stride != 64 && out->hdr_stride != 128) return dfail(d, PPE_EINVAL, "hdr_stride must be 64 or 128");
     if (hipSetDevice(d->device) != hipSuccess) return PPE_ENODEV;
+    // an earlier batch's admission look-back failed (its creators were not admitted; reported once, then cleared):
+    // read from pinned memory the admit kernel writes, no synchronisation
+    if (__atomic_load_n(d->h_err, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(d->h_err, 0ull, __ATOMIC_RELAXED);
+        return dfail(d, PPE_EIO, "ppe_defrag: an earlier batch's admission look-back timed out: the FCBs of that "
+                                 "batch's workgroup were not created (its fragments' results are wrong)");
+    }
     const hipStream_t s = (hipStream_t)stream;
     DfArgs a = d->base;
     a.pkt = in->pkt;
@@ -1263,6 +1299,7 @@ int ppe_defrag_info(ppe_defrag_t *d, ppe_defrag_info_t *info) {
     if (c[C_LOOK_ERR]) {   // reported once: cleared, so only this call fails
         const unsigned long long zero = 0;
         (void)hipMemcpy(d->base.ctl + C_LOOK_ERR, &zero, sizeof(zero), hipMemcpyHostToDevice);
+        __atomic_store_n(d->h_err, 0ull, __ATOMIC_RELAXED);
         return dfail(d, PPE_EIO, "ppe_defrag_info: %llu admission look-back timeouts (results of those batches wrong)",
                      c[C_LOOK_ERR]);
     }

@@ -30,11 +30,11 @@ constexpr int kHostStreams = 3;
 // ppe_classify_batches: two streams, so a batch's launch ramp-up overlaps the previous batch's tail (C1: 20.6 ->
 // 16.5 us per batch; three streams measured 17.0)
 constexpr int kPipeStreams = 2;
-// tile fetch of the classify kernel (PF_* in ppe_kernels.hip): 0 at the loop top, 1 the first tile's loads issued
-// before the image staging (the default: C1 21.7 us vs 22.2).  Register double-buffering (next tile's window, or
-// only its first 16 B, requested before the current tile is processed) and an LDS-DMA next-tile pipeline were
-// measured slower and are not built.
-constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3, kPfSblk = 5, kPfMulti3 = 6, kPfSblk3 = 7, kPfPc = 8;
+// tile fetch / walk of the classify kernel (PF_* in ppe_kernels.hip): 0 one tile per wave, its window at the loop
+// top; 1 the first tile's loads issued before the image staging (C1 21.7 us vs 22.2); 3 the multi-tile block walk;
+// 5 the cut lists (image v7).  Register double-buffering (next tile's window, or only its first 16 B, requested
+// before the current tile is processed) and an LDS-DMA next-tile pipeline were measured slower.
+constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3, kPfCut = 5;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
 // ppe_classify_batches: batches per launch.  0 = every batch of the call in one persistent launch (descriptor ring in
 // device memory): the launch ramp and tail are paid once per call instead of once per batch
@@ -148,7 +148,6 @@ struct ppe_ctx {
     LookupStage lk;             // ppe_acl_lookup_host
     uint32_t *d_steer = nullptr;  // ppe_steer_partition: per-tile owner counts / offsets
     size_t steer_cap = 0;
-    unsigned long long *trace = nullptr;  // ppe_debug_trace
     char err[256] = {0};
 };
 
@@ -184,7 +183,7 @@ ppe_tuning_t default_tuning() {
     const int bpc = env_int("PPE_BLOCKS_PER_CU", 0);
     t.blocks_per_cu = bpc > 0 && bpc <= (int)kMaxBlocksPerCU ? (uint32_t)bpc : 0u;
     const int pl = env_int("PPE_PIPELINE", 0);
-    t.pipeline = pl == 1 || pl == 3 || pl == 4 || pl == 5 || pl == 6 ? (uint32_t)pl : 0u;
+    t.pipeline = pl == 1 || pl == 3 || pl == 4 || pl == 5 ? (uint32_t)pl : 0u;
     t.lds_image = env_int("PPE_LDS_IMG", 1) != 0 ? 1u : 0u;
     t.batches_per_launch = (uint32_t)std::max(0, std::min(env_int("PPE_BATCHES_PER_LAUNCH", (int)kBatchesPerLaunch),
                                                           PPE_MAX_RING));
@@ -201,6 +200,7 @@ struct StagePlan {
     uint32_t lds_blocks;              // multi-tile walks: blocks [0, lds_blocks) in LDS
     uint32_t bsec_lds, blk_lds;       // LDS byte offsets (from the image base in LDS) of the block section / block 0
     uint32_t crec_lds = ~0u, idtab_lds = ~0u;  // compact records / index table in LDS (byte offsets), ~0u = global
+    uint32_t cut_ent_lds = ~0u;       // cut lists: entries in LDS (byte offset), ~0u = global (the groups: LDS base)
 };
 
 // LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves; a flow-table launch:
@@ -214,11 +214,11 @@ uint32_t image_budget(uint32_t block, int mode, bool flow = false) {
 }
 
 // single: the plan for the single-tile node-walk kernel only (the flow-table classify kernel is built for it: its
-// key slots and node prefix), never the multi-tile or block-walk plans
+// key slots and node prefix), never the multi-tile or cut-list plans
 StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool single = false) {
     const int pf = c->tune.pipeline == 1 ? kPfNone : kPfHoist;
     // the single-tile walk reads the binary nodes only: what it stages "whole" is the image before the block section
-    const uint32_t all_words = (uint32_t)img.size();
+    const uint32_t all_words = img[PPE_IMG_W_OFFCUT] ? img[PPE_IMG_W_OFFCUT] : (uint32_t)img.size();  // tree part
     const uint32_t off_bsec = img[PPE_IMG_W_OFFBSEC], off_blocks = img[PPE_IMG_W_OFFBLOCKS];
     const uint32_t n_blocks = img[PPE_IMG_W_NBLOCKS];
     const uint32_t words = off_bsec, bytes = words * 4u;
@@ -226,8 +226,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
     // the multi-tile walk reads the 2-level blocks: whole image in LDS, else the block jump table and the first
     // block levels (breadth-first), else global
     const uint32_t off_crec = img[PPE_IMG_W_OFFCREC], off_idtab = img[PPE_IMG_W_OFFIDTAB];
-    const bool k3 = img[PPE_IMG_W_BLKLV] == 3u;  // 3-level (64-B) blocks: the PF_MULTI3 / PF_SBLK3 kernels
-    const uint32_t bbytes = k3 ? 64u : 32u;
+    constexpr uint32_t bbytes = 32u;
     auto mt_plan = [&](uint32_t budget) {
         const uint32_t bjt = 4u * (off_blocks - off_bsec);
         if (off_crec && (all_words - off_bsec) * 4u <= budget) {
@@ -256,23 +255,56 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
             p.blk_lds = bjt;
         }
     };
+    // the cut lists (image v7): the bucket groups in LDS (the smallest workgroup whose share at 32 waves per CU holds
+    // them; the entries too when they fit beside them), the entries read from L2 otherwise; one tile per wave at 8
+    // waves per SIMD.  lds_image = 0: both from global memory.
+    const uint32_t off_cut = img[PPE_IMG_W_OFFCUT];
+    auto cut_plan = [&]() {
+        const uint32_t *h = img.data() + off_cut;
+        const uint32_t grp_bytes = 16u * h[6], ent_bytes = 4u * PPE_CUT_ENT_WORDS * h[2];
+        p.pipe = kPfCut;
+        p.mode = 0;
+        p.block = c->tune.block ? c->tune.block : 1024u;
+        if (!c->tune.lds_image) return;
+        auto budget = [&](uint32_t b) {  // (no key slots: the keys stay in registers)
+            const uint32_t per_wg = (160u * 1024u) / std::max(1u, 32u / (b / 64u));
+            const uint32_t fixed = ppe_classify_fixed_lds((int)b, kPfCut, 1) + 1024u;
+            return per_wg > fixed ? per_wg - fixed : 0u;
+        };
+        if (!c->tune.block)
+            for (uint32_t b : {256u, 512u, 1024u})
+                if (grp_bytes <= budget(b)) {
+                    p.block = b;
+                    break;
+                }
+        const uint32_t bud = budget(p.block);
+        if (grp_bytes > bud) return;  // (groups larger than the share: global)
+        p.mode = 1;
+        p.stage_src = h[4];
+        const uint32_t gap = 4u * (h[5] - h[4]);  // groups, then the 32-B aligned entries
+        if (gap + ent_bytes <= bud && env_int("PPE_CUT_ENT_LDS", 1)) {
+            p.stage_words = h[5] - h[4] + PPE_CUT_ENT_WORDS * h[2];
+            p.cut_ent_lds = gap;
+        } else {
+            p.stage_words = 4u * h[6];
+        }
+        p.lds_words = p.stage_words;
+    };
+    if (!single && off_cut && c->tune.pipeline == 5) {
+        cut_plan();
+        return p;
+    }
     if (!c->tune.lds_image) {
         if (!c->tune.block) p.block = 256;
         if (!single && (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && !c->tune.block))) {  // PF_MULTI, global image
-            p.pipe = k3 ? kPfMulti3 : kPfMulti;
-            p.block = 1024u;
-        }
-        if (!single && !k3 && c->tune.pipeline == 6) {  // PF_PC over a global image
-            p.pipe = kPfPc;
+            p.pipe = kPfMulti;
             p.block = 1024u;
         }
         return p;
     }
-    // the whole image in LDS: the smallest workgroup (most copies per CU) whose share holds it.  A single-tile kernel
-    // that walks blocks (ppe_classify_st_blocks) needs the whole image, block section included; a node walk the
-    // part before it.
-    const bool stb = ppe_classify_st_blocks() != 0;
-    const uint32_t lds_bytes = stb ? all_words * 4u : bytes;
+    // the whole image in LDS: the smallest workgroup (most copies per CU) whose share holds it (a node walk reads
+    // the part before the block section)
+    const uint32_t lds_bytes = bytes;
     if (!c->tune.block) {
         for (uint32_t b : {256u, 512u, 1024u}) {
             if (lds_bytes <= image_budget(b, 1, single)) {
@@ -282,53 +314,31 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
         }
     }
     uint32_t budget = image_budget(p.block, 1, single);
-    // PF_MULTI (tuning pipeline 3, and the default) for images that do not fit whole: 1024-thread workgroups, one
-    // per CU, with the CU's whole LDS for the image prefix (C2 / C3 / C4 step 27.2 / 52.1 / 27.3 -> 23.6 / 42.8 /
-    // 22.7 us)
-    // PF_SBLK (tuning pipeline 5): one tile per wave at 8 waves/SIMD, two 1024-thread workgroups per CU, each
-    // staging the block jump table and the block levels that fit half of the CU's LDS
-    if (!single && c->tune.pipeline == 5) {
-        p.pipe = k3 ? kPfSblk3 : kPfSblk;
-        p.block = 1024u;
-        const uint32_t fixed = ppe_classify_fixed_lds(1024, kPfSblk, 2) + 1024u;
-        mt_plan(80u * 1024u > fixed ? 80u * 1024u - fixed : 0u);
+    const bool fits = lds_bytes <= budget;
+    // images that do not fit whole: the cut lists when the image has them (C2 / C3 / C4), else PF_MULTI
+    // (1024-thread workgroups, one per CU, with the CU's whole LDS for the image prefix: C2 / C3 / C4 step 27.2 /
+    // 52.1 / 27.3 -> 23.6 / 42.8 / 22.7 us against the single-tile node walk)
+    if (!single && off_cut && c->tune.pipeline == 0 && !fits && !c->tune.block && env_int("PPE_CUT_PLAN", 1)) {
+        cut_plan();
         return p;
     }
-    // PF_PC (tuning pipeline 6, and the default for split images unless PPE_PC=0): the multi-tile walk with producer
-    // and consumer waves, its LDS tile queue taken from the image budget
-    const bool pc = !single && !k3 &&
-                    (c->tune.pipeline == 6 || (c->tune.pipeline == 0 && !c->tune.block && env_int("PPE_PC", 0) != 0));
-    if (!single && (c->tune.pipeline == 3 || c->tune.pipeline == 6 ||
-                    (c->tune.pipeline == 0 && (lds_bytes > budget || k3) && !c->tune.block))) {
-        p.pipe = k3 ? kPfMulti3 : kPfMulti;
+    if (!single && (c->tune.pipeline == 3 || (c->tune.pipeline == 0 && !fits && !c->tune.block))) {
+        p.pipe = kPfMulti;
         // tuning knobs (A/B only): workgroup size and the LDS bytes each workgroup may take (default: all of it, one
-        // workgroup per CU); less LDS lets more workgroups share a CU (the 3-level kernel is built for 1024 only)
+        // workgroup per CU); less LDS lets more workgroups share a CU
         const int mb = env_int("PPE_MT_BLOCK", 1024);
-        p.block = (!k3 && (mb == 256 || mb == 512)) ? (uint32_t)mb : 1024u;
+        p.block = (mb == 256 || mb == 512) ? (uint32_t)mb : 1024u;
         const uint32_t fixed = ppe_classify_fixed_lds((int)p.block, kPfMulti, 2) + 1024u;  // no key slots
         const uint32_t cap = (uint32_t)std::min(160 * 1024, std::max(8 * 1024, env_int("PPE_MT_LDS", 160 * 1024)));
         budget = cap > fixed ? cap - fixed : 0u;
         mt_plan(budget);
-        if (pc && (p.mode == 2 || c->tune.pipeline == 6)) {  // split images (C3), or forced
-            p = StagePlan{0, kPfPc, 1024u, 0, 0, 0, 0, 0, 0, 0};
-            const uint32_t pfixed = ppe_classify_fixed_lds(1024, kPfPc, 2) + 1024u;
-            mt_plan(cap > pfixed ? cap - pfixed : 0u);
-        }
         return p;
     }
     const uint32_t off_resid = img[PPE_IMG_W_OFFRESID], off_rules = img[PPE_IMG_W_OFFRULES];
     const uint32_t n_nodes = img[PPE_IMG_W_NNODES], off_nodes = img[PPE_IMG_W_OFFNODES];
-    if (lds_bytes <= budget) {
+    if (fits) {
         p.mode = 1;
-        p.lds_words = stb ? all_words : words;
-        if (stb) {
-            p.lds_blocks = n_blocks;
-            p.bsec_lds = 4u * off_bsec;
-            p.blk_lds = 4u * off_blocks;
-            if (off_crec) p.crec_lds = 4u * off_crec;
-            if (off_idtab) p.idtab_lds = 4u * off_idtab;
-        }
-        p.stage_words = p.lds_words;
+        p.lds_words = p.stage_words = words;
         return p;
     }
     budget = image_budget(p.block, 2, single);  // node walks of a partly staged image keep their key slots
@@ -545,6 +555,13 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     a.off_idtab = c->h_img[r][PPE_IMG_W_OFFIDTAB];
     a.crec_lds = plan.crec_lds;
     a.idtab_lds = plan.idtab_lds;
+    if (plan.pipe == kPfCut) {  // (image v7 cut lists: header at PPE_IMG_W_OFFCUT)
+        const uint32_t *h = c->h_img[r].data() + c->h_img[r][PPE_IMG_W_OFFCUT];
+        a.cut = h[0];
+        a.cut_grp = h[4];
+        a.cut_ent = h[5];
+        a.cut_ent_lds = plan.cut_ent_lds;
+    }
     // batch groups: the kernel splits its waves into min(batches, max_groups) groups, group g taking batches g, g + G,
     // ...; when G does not divide the batch count the last round leaves groups idle (20 batches at G = 8: the last
     // 4 run on half the grid; C3 / C4 ring step +12 %, profiles/r3_ab_runs.md r4l).  Take the power-of-two G up to the
@@ -584,7 +601,6 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     a.off_rules = c->h_img[r][PPE_IMG_W_OFFRULES];
     a.off_resid = c->h_img[r][PPE_IMG_W_OFFRESID];
     a.cslots = c->d_cslots + (size_t)slot_set * c->max_grid * PPE_CSLOT_WORDS;
-    a.trace = c->trace;
     if (fl) a.flow = *fl;
     if (grid_out) *grid_out = grid;
 
@@ -959,37 +975,38 @@ int ppe_acl_lookup_host(ppe_ctx_t *c, const ppe_tuples_t *in, int32_t *hit, uint
     if (!in->tuple) return fail(c, PPE_EINVAL, "tuple required");
     HIPCHK(c, use_device(c));
     LookupStage &L = c->lk;
-    const size_t n = in->n;
+    // the staging holds at most kLookupChunk entries (192 KB pinned per context, allocated by the first call); a
+    // larger burst goes through it in chunks of that size
+    constexpr uint32_t kLookupChunk = 4096;
     if (!L.s) HIPCHK(c, hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
-    if (n > L.cap) {  // grown (with headroom) only when a larger burst arrives; the first call allocates
-        const uint32_t cap = (uint32_t)std::max<size_t>({n, (size_t)L.cap * 2u, 1024u});
-        HIPCHK(c, hipStreamSynchronize(L.s));
-        if (L.h) HIPCHK(c, hipHostFree(L.h));
-        L.h = L.d = nullptr;
-        L.cap = 0;
-        HIPCHK(c, hipHostMalloc((void **)&L.h, (size_t)cap * 48u, hipHostMallocMapped));
+    if (!L.h) {
+        HIPCHK(c, hipHostMalloc((void **)&L.h, (size_t)kLookupChunk * 48u, hipHostMallocMapped));
         HIPCHK(c, hipHostGetDevicePointer((void **)&L.d, L.h, 0));
-        L.cap = cap;
+        L.cap = kLookupChunk;
     }
     const size_t cap = L.cap;
     uint8_t *ht = L.h, *hm = L.h + cap * 16, *hts = L.h + cap * 32, *hh = L.h + cap * 40, *ha = L.h + cap * 44;
-    std::memcpy(ht, in->tuple, n * 16);
-    if (in->macs) std::memcpy(hm, in->macs, n * 16);
-    if (in->ts) std::memcpy(hts, in->ts, n * 8);
-    uint8_t *d = L.d;
-    ppe_tuples_t dv = {(const uint32_t *)d, in->macs ? (const uint32_t *)(d + cap * 16) : nullptr,
-                       in->ts ? (const uint64_t *)(d + cap * 32) : nullptr, in->n};
-    int rc = ppe_acl_lookup(c, &dv, (int32_t *)(d + cap * 40), (uint32_t *)(d + cap * 44), now_seconds, L.s);
-    if (rc != PPE_OK) return rc;
-    // spin on this stream alone (a lookup is a few microseconds; a blocking wait would add the wake-up), then block
-    hipError_t q = hipErrorNotReady;
-    const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(2);
-    while ((q = hipStreamQuery(L.s)) == hipErrorNotReady && std::chrono::steady_clock::now() < until)
-        __builtin_ia32_pause();
-    if (q == hipErrorNotReady) q = hipStreamSynchronize(L.s);
-    if (q != hipSuccess) return fail(c, PPE_EIO, "acl lookup kernel failed: %s", hipGetErrorString(q));
-    if (hit) std::memcpy(hit, hh, n * 4);
-    if (action) std::memcpy(action, ha, n * 4);
+    for (uint32_t b = 0; b < in->n; b += (uint32_t)cap) {
+        const size_t n = std::min<size_t>(cap, in->n - b);
+        std::memcpy(ht, in->tuple + 4u * b, n * 16);
+        if (in->macs) std::memcpy(hm, in->macs + 4u * b, n * 16);
+        if (in->ts) std::memcpy(hts, in->ts + b, n * 8);
+        uint8_t *d = L.d;
+        ppe_tuples_t dv = {(const uint32_t *)d, in->macs ? (const uint32_t *)(d + cap * 16) : nullptr,
+                           in->ts ? (const uint64_t *)(d + cap * 32) : nullptr, (uint32_t)n};
+        int rc = ppe_acl_lookup(c, &dv, (int32_t *)(d + cap * 40), (uint32_t *)(d + cap * 44), now_seconds, L.s);
+        if (rc != PPE_OK) return rc;
+        // spin on this stream alone (a lookup is a few microseconds; a blocking wait would add the wake-up), then
+        // block
+        hipError_t q = hipErrorNotReady;
+        const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(2);
+        while ((q = hipStreamQuery(L.s)) == hipErrorNotReady && std::chrono::steady_clock::now() < until)
+            __builtin_ia32_pause();
+        if (q == hipErrorNotReady) q = hipStreamSynchronize(L.s);
+        if (q != hipSuccess) return fail(c, PPE_EIO, "acl lookup kernel failed: %s", hipGetErrorString(q));
+        if (hit) std::memcpy(hit + b, hh, n * 4);
+        if (action) std::memcpy(action + b, ha, n * 4);
+    }
     return PPE_OK;
 }
 
@@ -1084,23 +1101,15 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (!c || !t) return PPE_EINVAL;
     if (t->block != 0 && t->block != 256 && t->block != 512 && t->block != 1024)
         return fail(c, PPE_EINVAL, "block must be 0 (auto), 256, 512 or 1024");
-    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 3 && t->pipeline != 4 && t->pipeline != 5 &&
-        t->pipeline != 6)
-        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto = 4), 1 (first tile at the loop top), 3 (images that do "
-                                   "not fit in LDS: 4 tiles per wave walked together) or 4 (first tile's loads before "
-                                   "the image staging) or 5 (one tile per wave walking the image's blocks, for "
-                                   "split images) or 6 (3 with producer and consumer waves)");
+    if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 3 && t->pipeline != 4 && t->pipeline != 5)
+        return fail(c, PPE_EINVAL, "pipeline must be 0 (auto), 1 (first tile at the loop top), 3 (4 tiles per wave "
+                                   "walking the block section together), 4 (first tile's loads before the image "
+                                   "staging) or 5 (the cut lists of a v7 image)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     if (t->batches_per_launch > PPE_MAX_RING) return fail(c, PPE_EINVAL, "batches_per_launch must be <= 4096");
     c->tune = *t;
     c->tune.pipeline = t->pipeline;
     c->tune.lds_image = t->lds_image ? 1u : 0u;
-    return PPE_OK;
-}
-
-int ppe_debug_trace(ppe_ctx_t *c, void *dev_buf) {
-    if (!c) return PPE_EINVAL;
-    c->trace = (unsigned long long *)dev_buf;
     return PPE_OK;
 }
 

@@ -1,5 +1,5 @@
 /*
- * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v6.
+ * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v7.
  *
  * The image is a HyperSplit-style binary decision tree over the five header dimensions, flattened in BFS order
  * (children of node k are numbered after k, so a walk strictly descends and always terminates), followed by the
@@ -18,9 +18,9 @@
  *           32-B aligned)   word 18  max_bdepth: most blocks on a root-to-leaf path
  *  word 19  off_crec: word offset of the compact records (v6), 0 = the image has none
  *  word 20  off_idtab: word offset of the slot → rule index table, 0 = slot == rule index for every slot
- *  word 21  block levels K: 2 (32-B blocks, the default) or 3 (64-B blocks: images whose block section and compact
- *           records do not fit the CU's LDS, so more of the walk is L2 reads)
- *  words 22..31 reserved
+ *  word 21  block levels: 2 (32-B blocks)
+ *  word 22  off_cut: word offset of the cut-list section (v7), 0 = the image has none
+ *  words 23..31 reserved
  *
  *  jump table (format v4; present iff word 14 != 0): 2^bits words right after the header.  A walk starts at
  *      bucket b = key[dim] >> shift: word b = the byte offset of that bucket's subtree root | its key slot << 24.
@@ -58,17 +58,18 @@
  *  multi-tile walk, which reads the tree from L2 for large rule sets: one 32-B read resolves two levels, so a walk
  *  needs half the dependent memory round trips.
  *      block jump table (present iff word 14 != 0): 2^bits words, bucket → its root block index
- *      blocks (K = 2: 8 words, 32-B aligned; K = 3: 16 words, 64-B aligned; breadth-first by block depth: the
- *      LDS-staged prefix is whole block levels).  A block holds K tree levels: positions p = 0 .. 2^K - 2 in BFS
- *      order (position p's children are 2p + 1 and 2p + 2), then 2^K exits:
- *        w[p]    threshold of position p                         (K = 2: w0..w2; K = 3: w0..w6)
- *        w[2^K - 1]  key slots: position p's at bits 4p..4p+3
- *        w[2^K .. 2^(K+1) - 1]  exits e = the K comparison bits, first level most significant (K = 2: 2 b0 + b1,
- *                K = 3: 4 b0 + 2 b1 + b2; b0: key(pos 0) > w0, b1: key(pos 1 + b0) > w[1 + b0], ...):
- *                PPE_BLK_LEAF | leaf payload (max_leaf <= 1: rule slot / sentinel, or the compact exit below;
- *                else first | count << 23), or the index of the block rooted at that position's child
+ *      blocks (8 words, 32-B aligned; breadth-first by block depth: the LDS-staged prefix is whole block levels).
+ *      A block holds 2 tree levels: positions p = 0 .. 2 in BFS order (position p's children are 2p + 1 and
+ *      2p + 2), then 4 exits:
+ *        w[p]    threshold of position p (w0..w2)
+ *        w[3]    key slots: position p's at bits 4p..4p+3
+ *        w[4..7] exits e = the 2 comparison bits, first level most significant (2 b0 + b1; b0: key(pos 0) > w0,
+ *                b1: key(pos 1 + b0) > w[1 + b0]): PPE_BLK_LEAF | leaf payload (max_leaf <= 1: rule slot /
+ *                sentinel, or the compact exit below; else first | count << 23), or the index of the block rooted
+ *                at that position's child
  *        A leaf at a position is a pass-through: threshold 0xffffffff (no key is greater) and both of its children
- *        positions / exits carry the leaf, so every walk resolves exactly K levels per block.
+ *        positions / exits carry the leaf, so every walk resolves exactly 2 levels per block.  (3-level 64-B blocks
+ *        were an option until round 4: one L2 round trip fewer per three levels, measured slower on C3.)
  *
  *  compact leaves (v6; present iff word 19 != 0: one candidate per leaf (max_leaf <= 1) and no rule with a residual
  *  MAC / time field).  The block walk is the classify kernel's, and only TCP / UDP packets reach the ACL there
@@ -83,12 +84,29 @@
  *      dip: likewise;  sport_lo | dport_lo << 16;  (sport_hi - sport_lo) | (dport_hi - dport_lo) << 16
  *      The address matches iff (key ^ word) has no bit set above the marker bit (every bit for a /32).
  *  idtab (word 20 != 0): n_rules words, the rule index of each slot (when unused entries make slots != indices)
+ *
+ *  cut-list section (v7; present iff word 22 != 0: every rule without residual MAC / time fields).  A second,
+ *  independent classifier for the classify kernel (TCP / UDP keys only): a HyperCuts-style cut of the top b0 bits
+ *  of sip and the top b1 bits of dip into 2^(b0 + b1) buckets, bucket = (sip >> (32 - b0)) << b1 | dip >> (32 - b1)
+ *  (a width 0 contributes nothing), and per bucket the list of the rules whose box meets it, in priority order,
+ *  closed after the first rule that covers the whole bucket (every port, TCP and UDP).  The builder picks b0, b1
+ *  (b0 + b1 <= 16) by the expected list length and rejects the section when a list would exceed 15 entries.  A
+ *  lookup is one read of the bucket's group (LDS) and one round of independent entry reads (L2): no dependent walk.
+ *      header (8 words at off_cut): b0 | b1 << 8, n_buckets, n_entries, max list length, off_grp, off_ent (word
+ *          offsets from the image start), n_groups, 0
+ *      groups (4 words each, 16-B aligned; group g = buckets 16 g .. 16 g + 15): { first entry of bucket 16 g,
+ *          list lengths of buckets 16 g + 0..7 (4 bits each, bucket 16 g + k at bits 4k), of 16 g + 8..15, 0 }
+ *          bucket b's list = entries [first(b), first(b) + len(b)), first(b) = the group's first + the lengths of
+ *          the buckets before b in its group
+ *      entries (8 words each, 32-B aligned, contiguous per bucket in priority order): { sip prefix | marker bit,
+ *          dip prefix | marker bit (as the compact record), sport_lo | dport_lo << 16, the port spans, exit, 0, 0,
+ *          0 }, exit = rule index (bits 0-23) | the compact exit flags PPE_CX_DROP / TCP / UDP / S32 / D32
  */
 #ifndef PPE_IMAGE_H
 #define PPE_IMAGE_H
 
 #define PPE_IMG_MAGIC   0x41455050u /* "PPEA" */
-#define PPE_IMG_VERSION 6u
+#define PPE_IMG_VERSION 7u
 #define PPE_IMG_HDR_WORDS 32u
 
 #define PPE_IMG_W_NNODES   2
@@ -111,9 +129,9 @@
 #define PPE_IMG_W_OFFCREC  19
 #define PPE_IMG_W_OFFIDTAB 20
 #define PPE_IMG_W_BLKLV    21
+#define PPE_IMG_W_OFFCUT   22
 
 #define PPE_BLK_WORDS 8u           /* 2-level block */
-#define PPE_BLK3_WORDS 16u         /* 3-level block */
 #define PPE_BLK_LEAF 0x80000000u  /* exit word: a leaf payload (else a block index) */
 #define PPE_CX_SLOT   0x00ffffffu  /* compact leaf exit fields (v6) */
 #define PPE_CX_DROP   (1u << 24)
@@ -123,6 +141,10 @@
 #define PPE_CX_D32    (1u << 28)
 #define PPE_CX_NOHIT  (1u << 29)
 #define PPE_CREC_WORDS 4u
+#define PPE_CUT_HDR_WORDS 8u
+#define PPE_CUT_ENT_WORDS 8u      /* cut-list entry (32 B) */
+#define PPE_CUT_MAX_LIST 15u      /* longest bucket list (4-bit lengths) */
+#define PPE_CUT_MAX_BITS 16u      /* b0 + b1: 2^16 buckets = 64 KB of groups */
 
 #define PPE_NODE_WORDS 4u
 #define PPE_NODE_LEAF 5u          /* key slot of a leaf: the walk's zero key */

@@ -140,6 +140,10 @@ struct ppe_kargs {
     uint32_t off_bsec, off_blocks, max_bdepth; /* image header words 15, 17, 18                                  */
     uint32_t off_crec, off_idtab; /* image header words 19, 20: compact leaf records / slot → index table (0 = none) */
     uint32_t crec_lds, idtab_lds; /* their LDS byte offsets from the LDS image base, ~0u = read from global memory   */
+    uint32_t cut;             /* cut-list walks (image v7): sip bits | dip bits << 8 of the cut                       */
+    uint32_t cut_grp, cut_ent;  /* word offsets of the bucket groups / the entries in the image                       */
+    uint32_t cut_ent_lds;     /* the entries' LDS byte offset from the LDS image base (the groups are at it), ~0u =
+                                 read from global memory                                                              */
     uint32_t max_groups;      /* most batch groups of waves (concurrently streamed batches)                          */
     uint32_t part_layout;     /* 1: every batch writes verdict + flow hash + ACL hit and one partition list (fw_idx ==
                                  drop_idx), no tile counts, no tuple: the kernel variant with those checks compiled out */
@@ -152,7 +156,6 @@ struct ppe_kargs {
     uint32_t off_leaf, off_rules, off_resid; /* image section offsets (words), from the image header: kernel arguments
                                                 (scalar registers, no load in the loop)                               */
     unsigned long long *cslots; /* [grid][PPE_CSLOT_WORDS] counter slots, one per workgroup */
-    unsigned long long *trace;  /* diagnostic builds (PPE_TRACE) only: per-wave phase timestamps, else unused */
     struct ppe_flowdev flow;    /* flow-table launches (ppe_classify_flow, one batch) */
 };
 
@@ -216,7 +219,6 @@ uint32_t ppe_classify_fixed_lds(int block, int pipe, int mode);
 uint32_t ppe_flow_lds_extra(void);  /* classify LDS of a flow-table launch beyond the stateless kernel's (buckets) */
 uint32_t ppe_flow_waves(void);      /* waves per SIMD of the flow-table classify kernel */
 int ppe_classify_occupancy_flow(uint32_t lds_words, int mode, int block);  /* key slots (node walks only) + counter bins */
-int ppe_classify_st_blocks(void);  /* 1: single-tile walks of a whole-LDS image use the block section */
 int ppe_launch_acl_tuples(const struct ppe_tuple_kargs *a, uint32_t grid, int lds_img, void *stream);
 #ifdef __cplusplus
 }

@@ -34,76 +34,10 @@
 #ifndef PPE_ABLATE
 #define PPE_ABLATE 0
 #endif
-// Diagnostic builds only (make variant NAME=trace VFLAGS=-DPPE_TRACE=1): lane 0 of every wave writes shader-clock
-// timestamps (s_memrealtime, 100 MHz) of its phases to kargs.trace, 32 words per wave (tools/trace_analyze.py):
-//   [0] kernel entry  [1] image staged  [2 + 5i + k] tile iteration i < 4: k 0 loop top, 1 window in registers,
-//   2 decoded + hashed, 3 ACL done, 4 outputs + counters issued   [22] after the loop  [23] counters flushed
-//   [31] tiles processed
-#ifndef PPE_ST_BLOCKS  // 1: the single-tile kernel over a whole-LDS image walks the 2-level blocks, keys in registers
-                      // (C1 A/B: 19.1-19.7 vs 18.6-18.8 us per 1M for the node walk with LDS key slots: 0 kept)
-#define PPE_ST_BLOCKS 0
-#endif
-#ifndef PPE_TRACE
-#define PPE_TRACE 0
-#endif
-#ifndef PPE_TUPLE_SELECT
-#define PPE_TUPLE_SELECT 0
-#endif
-#ifndef PPE_REC_IN_WALK  // experiment: multi-tile walks read compact records inside the walk loop (acl_walk_blocks_mt)
-#define PPE_REC_IN_WALK 0
-#endif
-// PPE_MT_PF: the multi-tile kernel requests the next round's windows while it finishes the current one (software
-// pipeline, one round deep, across batch boundaries).  vmcnt retires loads in issue order, so the request goes where
-// no later global load of the round has to wait for it: before the walk when the whole image is in LDS (the walk and
-// the record check issue no global loads), else after the record checks (overlapping the hash, stores, compaction
-// and counters).  1 = whole-LDS images only, at PPE_MT_LDS tiles per wave (the next round's windows need the
-// registers of two more tiles: C2 / C4 step -4.5 / -3 % at 2 tiles against the round-2 loop at 4, 3 tiles with
-// prefetch -1 %, 4 spills; profiles/r3_ab_runs.md r3h); 2 = every image (split images: C3 +3 %, experiment); 0 = the round-2
-// loop (load, decode, walk, finish) everywhere.
-#ifndef PPE_MT_PF
-#define PPE_MT_PF 1
-#endif
-#ifndef PPE_MT_LDS
-#define PPE_MT_LDS 2
-#endif
-// PPE_WALK_BL: a whole-LDS image's block walk without per-tile branches: every lane reads a block each step (a
-// finished lane its last one again) and the updates are selects, so the wave trades the per-tile exec-mask
-// bookkeeping (scalar instructions) for a few VALU selects (C2 / C4 step -2 / -2.6 %, profiles/r3_ab_runs.md r3j).  The same on
-// split images, and a key select by bit tests instead of the equality chain, measured C3 +6.7 % (profiles/r3_ab_runs.md r3m:
-// SALU 336 -> 159 but VALU 506 -> 702 per tile, profiles/r3_instruction_mix.md r3n), so they are not used.
-#ifndef PPE_WALK_BL
-#define PPE_WALK_BL 1
-#endif
-// PPE_WALK_2PH: a split image's block walk in two phases.  The staged blocks are the breadth-first prefix of the
-// block forest, so a lane that leaves them never returns: phase 1 walks the LDS-resident levels without per-tile
-// branches (a lane outside them, or done, reads block 0 and keeps its state), phase 2 walks the rest from L2 with
-// one exec-masked global read per tile and step (no LDS / global branch pair per step).
-#ifndef PPE_WALK_2PH
-#define PPE_WALK_2PH 1
-#endif
-// PPE_WALK_CMP: the split walk's tail in one virtual tile (acl_walk_blocks_mt phase 2)
-#ifndef PPE_WALK_CMP
-#define PPE_WALK_CMP 1
-#endif
-// PPE_REC_PF: the split multi-tile round requests tile t + 1's compact record before tile t's record check
-#ifndef PPE_REC_PF
-#define PPE_REC_PF 1
-#endif
-// (trace the wave's tile iterations PPE_TRACE_SKIP .. + 3: a skip > 0 samples the steady state of a long launch)
-#ifndef PPE_TRACE_SKIP
-#define PPE_TRACE_SKIP 0u
-#endif
-// minimum resident waves per SIMD the classify kernel is compiled for (VGPR budget 512 / this)
+// minimum resident waves per SIMD the single-tile classify kernel is compiled for (VGPR budget 512 / this)
 #ifndef PPE_WAVES_PER_EU
 #define PPE_WAVES_PER_EU 8
 #endif
-#define TRACE_AT(idx)                                                                      \
-    do {                                                                                   \
-        if (PPE_TRACE) {                                                                   \
-            const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                            \
-            if (lane == 0 && a.trace) a.trace[(size_t)twave * 32u + (idx)] = t_;          \
-        }                                                                                  \
-    } while (0)
 
 namespace {
 
@@ -115,9 +49,9 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // LDS geometry
 #define KEY_SLOTS 6u
 #define KEY_WAVE_BYTES (KEY_SLOTS * 256u)  // 1536
-// KEYS = false: the multi-tile kernel (PF_MULTI) walks with the keys in registers and has no key slots, so its
-// image starts right after the counter bins (24 KB more image per CU at 1024 threads)
-// QB: the producer / consumer kernel's tile queue (PF_PC), between the counter bins and the image
+// KEYS = false: block and cut-list walks keep the keys in registers and have no key slots, so their image starts
+// right after the counter bins (24 KB more image per CU at 1024 threads)
+// QB: the flow-table kernel's owner-update buckets, between the counter bins and the image
 template <int BLOCK, bool KEYS = true, uint32_t QB = 0> struct Lds {
     static constexpr uint32_t KEYB = KEYS ? (BLOCK / 64) * KEY_WAVE_BYTES : 0u;
     static constexpr uint32_t BINS = KEYB;                   // 256 u32 bins, then 32 u32 counters
@@ -137,36 +71,6 @@ __device__ __forceinline__ uint4 lds_u128(uint32_t addr) {
 __device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) {
     *(__attribute__((address_space(3))) uint32_t *)(uintptr_t)addr = v;
 }
-__device__ __forceinline__ void lds_st8(uint32_t addr, uint32_t v) {
-    *(__attribute__((address_space(3))) uint8_t *)(uintptr_t)addr = (uint8_t)v;
-}
-// LDS words shared between the waves of a workgroup (the PF_PC queue): a wave's LDS operations execute in issue
-// order, so a flag stored after `s_waitcnt lgkmcnt(0)` is seen only after the data stored before it, and data read
-// after the flag read returns is the data the flag publishes (volatile: the compiler keeps every access and its order)
-__device__ __forceinline__ uint32_t lds_vld(uint32_t addr) {
-    return *(volatile __attribute__((address_space(3))) uint32_t *)(uintptr_t)addr;
-}
-__device__ __forceinline__ void lds_vst(uint32_t addr, uint32_t v) {
-    *(volatile __attribute__((address_space(3))) uint32_t *)(uintptr_t)addr = v;
-}
-__device__ __forceinline__ uint32_t lds_add(uint32_t addr, uint32_t v) {
-    return __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t *)(uintptr_t)addr, v, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Wait (bounded) until the LDS word at addr equals want; false on timeout (a protocol bug must end the kernel, not hang
-// the GPU).  Every lane reads the same word (a broadcast), so the loop is wave-uniform.
-__device__ __forceinline__ bool lds_wait_eq(uint32_t addr, uint32_t want, uint32_t &polls) {
-#pragma unroll 1
-    for (uint32_t k = 0; k < (1u << 22); ++k) {
-        if (__builtin_amdgcn_readfirstlane(lds_vld(addr)) == want) {
-            asm volatile("" ::: "memory");
-            polls += k;
-            return true;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-    return false;
-}
 // global accesses by 32-bit byte offset from a uniform base (the saddr form: no 64-bit address math per lane)
 // (explicitly global: a select between two output pointers must not degrade to a flat store, whose out-of-order
 // completion makes the compiler wait for vmcnt(0) at the next use of any load)
@@ -184,52 +88,9 @@ template <class T> __device__ __forceinline__ void gst(void *base, uint32_t off,
 // the launch, so they go out with the non-temporal (streaming) policy.  The memory skeleton of this kernel
 // (tools/calib/stream_calib2.hip) runs 3-6 % faster with it; non-temporal LOADS of the windows run 25 % slower
 // (the 4 partial-line loads of a row would each refetch the line), so the loads keep the default policy.
-#ifndef PPE_NT_STORE
-#define PPE_NT_STORE 1
-#endif
-// PPE_SC1_STORE (experiment): 4-B result stores as relaxed agent-scope atomic stores (global_store sc1: write-through,
-// the line leaves the XCD's L2 instead of displacing classifier-image lines)
-#ifndef PPE_SC1_STORE
-#define PPE_SC1_STORE 0
-#endif
 template <class T> __device__ __forceinline__ void gst_nt(void *base, uint32_t off, T v) {
     typedef typename GType<T>::type G;
-    if constexpr (PPE_SC1_STORE && sizeof(T) == 4) {
-        __hip_atomic_store((__attribute__((address_space(1))) uint32_t *)((char *)base + off),
-                           __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (PPE_NT_STORE)
-        __builtin_nontemporal_store(__builtin_bit_cast(G, v), (__attribute__((address_space(1))) G *)((char *)base + off));
-    else
-        gst<T>(base, off, v);
-}
-// PPE_NT_WIN (experiment): the multi-tile kernel's window / length loads with the non-temporal (streaming) policy, so
-// the packet stream is evicted from L2 before the L2-resident half of the classifier image
-#ifndef PPE_NT_WIN
-#define PPE_NT_WIN 0
-#endif
-// PPE_PREFETCH (experiment): single-tile kernel over an LDS image requests tile t + 1's window before processing tile t
-#ifndef PPE_LAST_COND
-#define PPE_LAST_COND 0
-#endif
-#ifndef PPE_PREFETCH
-#define PPE_PREFETCH 0
-#endif
-// PPE_CMP_LDS (default on; C1 step -2 % in one A/B, profiles/r2b_experiments.md): the single-tile kernel's partition-list store is permuted through the wave's key slot 0
-// (free between walks) and leaves in lane order
-#ifndef PPE_CMP_LDS
-#define PPE_CMP_LDS 1
-#endif
-// PPE_CMP_LDS8: the compact (1-B) partition list through the same LDS permutation, stored as 16 dwords; 0: each lane
-// stores its entry byte at its slot (one 64-B byte-store instruction per tile; C1 ring step 16.76 -> 16.68 us, r4h)
-#ifndef PPE_CMP_LDS8
-#define PPE_CMP_LDS8 0
-#endif
-template <class T> __device__ __forceinline__ T gld_win(const void *base, uint32_t off) {
-    typedef typename GType<T>::type G;
-    if constexpr (PPE_NT_WIN != 0)
-        return __builtin_bit_cast(T, __builtin_nontemporal_load((const __attribute__((address_space(1))) G *)((const char *)base + off)));
-    else
-        return gld<T>(base, off);
+    __builtin_nontemporal_store(__builtin_bit_cast(G, v), (__attribute__((address_space(1))) G *)((char *)base + off));
 }
 
 __device__ __forceinline__ uint32_t be16_lo(uint32_t w) { return ((w & 0xffu) << 8) | ((w >> 8) & 0xffu); }
@@ -509,18 +370,8 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[13], uint32_t len32, c
     k.flags = ((l2_ok & is_vl & (vlen >= 4u)) ? PPE_F_VLAN : 0u) | (l4_ok ? PPE_F_L4 : 0u) |
               ((l4_ok & is_tcp) ? PPE_F_TCP : 0u) | ((l4_ok & is_tcp & syn) ? PPE_F_SYN : 0u) |
               ((ip_ok & frag) ? PPE_F_FRAG : 0u);
-#if PPE_TUPLE_SELECT
-    // (diagnostic build, make variant VFLAGS=-DPPE_TUPLE_SELECT=1: the select form one round-2 variant build
-    // miscompiled, kept to re-test it; profiles/r2b_experiments.md)
-    k.sip = ip_ok ? sip : 0u;
-    k.dip = ip_ok ? dip : 0u;
-    k.proto = ip_ok ? proto : 0u;
-    k.sport = l4_ok ? sport : 0u;
-    k.dport = l4_ok ? dport : 0u;
-    k.paylen = l4_ok ? (is_tcp ? l4len - thl : l4len - 8u) : 0u;
-#else
-    // zeroed by masks, not selects: the ROCm 7.2 compiler turned the select form into exec-masked blocks that left
-    // dport zeroed for NO_SYN packets in some builds (tools/variant_diff.py caught it; the product build was right)
+    // zeroed by masks, not selects: ROCm 7.2 miscompiles the select form (dport zeroed for NO_SYN packets;
+    // profiles/r3_select_miscompile.md, tools/repro_select_miscompile.sh)
     const uint32_t ipm = ip_ok ? ~0u : 0u, l4m = l4_ok ? ~0u : 0u;
     k.sip = sip & ipm;
     k.dip = dip & ipm;
@@ -534,7 +385,6 @@ __device__ __forceinline__ Dec decode(const uint32_t (&w)[13], uint32_t len32, c
         k.dport |= ((ipoff & 0x1fffu) << 3) & fm;            // IPV4_GET_IPOFFSET << 3, uint16
         k.paylen |= ((l3len - hlen) & 0xffffu) & fm;         // len - ihl, uint16
     }
-#endif
     return k;
 }
 
@@ -565,6 +415,9 @@ struct AclGeo {
     // compact leaves (image v6): record / index-table word offsets (0 = none), and their LDS byte offsets from the
     // staged image base (~0u = read from global memory)
     uint32_t off_crec, off_idtab, crec_lds, idtab_lds;
+    // cut lists (image v7): sip bits | dip bits << 8, word offsets of the groups / entries, the entries' LDS byte
+    // offset (~0u = global; the groups are at the staged image base when the image mode is IMG_LDS)
+    uint32_t cut, cut_grp, cut_ent, cut_ent_lds;
 };
 
 // One level of the walk, node and key both in flight: the node's child pointer carries the child's key slot, so
@@ -775,6 +628,74 @@ __device__ __forceinline__ void acl_leaf_compact(const uint32_t *__restrict__ gi
     crec_check<IMGB>(gimg, g, x, crec_load<IMGB>(gimg, g, x), sip, dip, sport, dport, tcp, hit, drop);
 }
 
+// Cut-list lookup (image v7, ppe_image.h): the bucket of the key's top sip / dip bits; its group (16 B: LDS when
+// staged) gives the bucket's list, whose entries (32 B each, L2 or LDS) are independent reads, two per round, checked
+// in priority order: one dependent L2 round for lists of up to two entries, where a tree walk through an L2-resident
+// forest takes 5-6 (C3).  The check is the compact record's (crec_check).  Only TCP / UDP keys reach it.
+__device__ __forceinline__ uint32_t nibble_sum(uint32_t x) {  // sum of the eight 4-bit fields of x
+    x = (x & 0x0f0f0f0fu) + ((x >> 4) & 0x0f0f0f0fu);
+    return __builtin_amdgcn_sad_u8(x, 0u, 0u);
+}
+__device__ __forceinline__ bool cut_match(const uint4 r, uint32_t x, uint32_t sip, uint32_t dip, uint32_t ports,
+                                          bool tcp) {
+    const uint32_t ms = (x & PPE_CX_S32) ? ~0u : ~(((r.x & (0u - r.x)) << 1) - 1u);
+    const uint32_t md = (x & PPE_CX_D32) ? ~0u : ~(((r.y & (0u - r.y)) << 1) - 1u);
+    const u16x2 kp = __builtin_bit_cast(u16x2, ports), lo = __builtin_bit_cast(u16x2, r.z),
+                sp = __builtin_bit_cast(u16x2, r.w);
+    const bool pp = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(kp - lo, sp)) == r.w;
+    return (((sip ^ r.x) & ms) == 0u) & (((dip ^ r.y) & md) == 0u) & pp &
+           ((x & (tcp ? PPE_CX_TCP : PPE_CX_UDP)) != 0u);
+}
+template <int MODE, int IMGB>
+__device__ __forceinline__ void acl_cut(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t sip, uint32_t dip,
+                                        uint32_t ports, bool tcp, int32_t &hit, bool &drop) {
+    const uint32_t b0 = g.cut & 0xffu, b1 = (g.cut >> 8) & 0xffu;
+    const uint32_t bk = ((uint32_t)((uint64_t)sip >> (32u - b0)) << b1) | (uint32_t)((uint64_t)dip >> (32u - b1));
+    const uint32_t go = 16u * (bk >> 4), k = bk & 15u;
+    const uint4 gr = MODE == IMG_LDS ? lds_u128(IMGB + go) : gld<uint4>(gimg, 4u * g.cut_grp + go);
+    const uint32_t cw = k < 8u ? gr.y : gr.z, sh = 4u * (k & 7u);
+    const uint32_t cnt = (cw >> sh) & 15u;
+    const uint32_t first = gr.x + nibble_sum(cw & ((1u << sh) - 1u)) + (k >= 8u ? nibble_sum(gr.y) : 0u);
+    const bool ent_lds = MODE == IMG_LDS && g.cut_ent_lds != ~0u;
+    hit = -1;
+    bool found = false;
+    uint32_t xf = 0;
+#pragma unroll 1
+    for (uint32_t j = 0; j < PPE_CUT_MAX_LIST; j += 2u) {
+        const bool a0 = !found && j < cnt, a1 = !found && j + 1u < cnt;
+        if (__builtin_amdgcn_ballot_w64(a0) == 0) break;
+        uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
+        uint32_t x0 = 0u, x1 = 0u;
+        const uint32_t e0 = 32u * (first + j);
+        if (ent_lds) {
+            if (a0) {
+                r0 = lds_u128(IMGB + g.cut_ent_lds + e0);
+                x0 = lds_u32(IMGB + g.cut_ent_lds + e0 + 16u);
+            }
+            if (a1) {
+                r1 = lds_u128(IMGB + g.cut_ent_lds + e0 + 32u);
+                x1 = lds_u32(IMGB + g.cut_ent_lds + e0 + 48u);
+            }
+        } else {
+            const uint32_t o = 4u * g.cut_ent + e0;
+            if (a0) {
+                r0 = gld<uint4>(gimg, o);
+                x0 = gld<uint32_t>(gimg, o + 16u);
+            }
+            if (a1) {
+                r1 = gld<uint4>(gimg, o + 32u);
+                x1 = gld<uint32_t>(gimg, o + 48u);
+            }
+        }
+        const bool m0 = a0 && cut_match(r0, x0, sip, dip, ports, tcp);
+        const bool m1 = a1 && cut_match(r1, x1, sip, dip, ports, tcp);
+        xf = m0 ? x0 : (m1 ? x1 : xf);
+        found = found || m0 || m1;
+    }
+    hit = found ? (int32_t)(xf & PPE_CX_SLOT) : -1;
+    drop = found ? (xf & PPE_CX_DROP) != 0u : g.default_action == ACL_RULE_ACTION_DROP;
+}
+
 // 5-way key select by key slot (multi-tile walks keep the keys in registers)
 // Block walks take the packed key {sip, dip, sport | dport << 16, meta} (meta: proto at bits 16-23; the multi-tile
 // kernel keeps the status and flags in its low bits), 4 registers per tile instead of 5 + the decode's copies.
@@ -783,21 +704,33 @@ __device__ __forceinline__ uint32_t key_sel(uint32_t d, const uint32_t (&k)[4]) 
          : d == 4u ? ((k[3] >> 16) & 0xffu) : 0u;
 }
 
+// One 2-level block step (ppe_image.h block section): position 0 → b0; position 1 + b0 → b1; exit 2 b0 + b1 (a leaf
+// position passes through: threshold ~0)
+__device__ __forceinline__ uint32_t block_step(const uint4 lo, const uint4 hi, const uint32_t (&key)[4]) {
+    const bool b0 = key_sel(lo.w & 15u, key) > lo.x;
+    const uint32_t t1 = b0 ? lo.z : lo.y;
+    const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
+    const bool b1 = key_sel(k1, key) > t1;
+    return b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
+}
+// leaf payload in node form: slot / sentinel, or first | count << 24 for leaf lists (compact images: slot | flags,
+// acl_leaf_compact)
+__device__ __forceinline__ uint32_t block_leaf_payload(const AclGeo &g, uint32_t x) {
+    return g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF) : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
+}
+
 // Multi-tile walk over the image's 2-level blocks (PF_MULTI; ppe_image.h block section): the lanes of MT tiles walk
 // in lockstep, each step one 32-B block read per lane (LDS for the staged block levels, else L2 / HBM) resolving two
 // tree levels, so a deep walk through an L2-resident tree takes half the dependent round trips of a node walk.  Keys
 // come from registers; a lane stops reading at its leaf.  Returns, per tile, a node whose .z is the leaf payload in
 // the node format acl_leaf reads.
-// RECW (experiment, PPE_REC_IN_WALK): on a compact image a lane that reaches its leaf reads its 16-B record in the
-// walk's next step (rec[t]) while the other lanes keep walking, instead of after the walk, tile by tile.
-template <int MODE, int IMGB, int MT, int KL = 2, bool RECW = false>
+template <int MODE, int IMGB, int MT>
 __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ gimg, const AclGeo &g,
                                                    const uint32_t (&key)[MT][4], const bool (&need)[MT],
-                                                   uint4 (&nd)[MT], uint4 *rec = nullptr) {
-    constexpr uint32_t BB = KL == 2 ? 32u : 64u;  // block bytes
-    constexpr int NQ = (int)BB / 16;
+                                                   uint4 (&nd)[MT]) {
+    constexpr uint32_t BB = 32u;  // block bytes
     uint32_t blk[MT];
-    bool done[MT], recp[MT];
+    bool done[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
         blk[t] = 0u;  // single tree: root block 0
@@ -807,59 +740,27 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
             blk[t] = MODE != IMG_GLOBAL ? lds_u32(IMGB + g.bsec_lds + jo) : gld<uint32_t>(gimg, 4u * g.off_bsec + jo);
         }
         done[t] = !need[t];
-        recp[t] = false;
         nd[t] = make_uint4(PPE_LEAF_THR, 0u, 0u, 0u);
     }
-    if constexpr (PPE_WALK_BL && MODE == IMG_LDS && !RECW) {
+    if constexpr (MODE == IMG_LDS) {
+        // whole image in LDS, branchless: every lane reads a block each step (a finished one its last block again)
+        // and the updates are selects, so the wave trades per-tile exec-mask bookkeeping (scalar instructions) for a
+        // few VALU selects (C2 / C4 step -2 / -2.6 %, profiles/r3_ab_runs.md r3j)
 #pragma unroll 1
         for (uint32_t it = 0; it < g.max_bdepth; ++it) {
-            uint4 q[MT][NQ];
+            uint4 lo[MT], hi[MT];
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
-                if constexpr (MODE == IMG_LDS) {  // every lane reads (a finished one its last block again)
-                    const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
-#pragma unroll
-                    for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
-                } else if (!done[t]) {  // (no global traffic for finished lanes)
-                    if (MODE != IMG_GLOBAL && blk[t] < g.lds_blocks) {
-                        const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
-#pragma unroll
-                        for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
-                    } else {
-                        const uint32_t ga = 4u * g.off_blocks + BB * blk[t];
-#pragma unroll
-                        for (int j = 0; j < NQ; ++j) q[t][j] = gld<uint4>(gimg, ga + 16u * j);
-                    }
-                }
+                const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
+                lo[t] = lds_u128(la);
+                hi[t] = lds_u128(la + 16u);
             }
             bool pending = false;
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
-                uint32_t x;
-                if constexpr (KL == 2) {
-                    const uint4 lo = q[t][0], hi = q[t][NQ - 1];
-                    const bool b0 = key_sel(lo.w & 15u, key[t]) > lo.x;
-                    const uint32_t t1 = b0 ? lo.z : lo.y;
-                    const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
-                    const bool b1 = key_sel(k1, key[t]) > t1;
-                    x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
-                } else {
-                    const uint4 a = q[t][0], b = q[t][1], c = q[t][2 % NQ], d = q[t][3 % NQ];
-                    const uint32_t sl = b.w;
-                    const bool b0 = key_sel(sl & 15u, key[t]) > a.x;
-                    const uint32_t t1 = b0 ? a.z : a.y;
-                    const uint32_t k1 = (sl >> (b0 ? 8u : 4u)) & 15u;
-                    const bool b1 = key_sel(k1, key[t]) > t1;
-                    const uint32_t t2 = b0 ? (b1 ? b.z : b.y) : (b1 ? b.x : a.w);
-                    const uint32_t k2 = (sl >> (4u * (3u + 2u * (uint32_t)b0 + (uint32_t)b1))) & 15u;
-                    const bool b2 = key_sel(k2, key[t]) > t2;
-                    const uint4 ex = b0 ? d : c;
-                    x = b1 ? (b2 ? ex.w : ex.z) : (b2 ? ex.y : ex.x);
-                }
+                const uint32_t x = block_step(lo[t], hi[t], key[t]);
                 const bool leaf = (x & PPE_BLK_LEAF) != 0u, act = !done[t];
-                const uint32_t pay = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF)
-                                                      : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
-                nd[t].z = (act & leaf) ? pay : nd[t].z;
+                nd[t].z = (act & leaf) ? block_leaf_payload(g, x) : nd[t].z;
                 blk[t] = (act & !leaf) ? x : blk[t];
                 pending = pending | (act & !leaf);
                 done[t] = done[t] | leaf;
@@ -868,216 +769,129 @@ __device__ __forceinline__ void acl_walk_blocks_mt(const uint32_t *__restrict__ 
         }
         return;
     }
-    if constexpr (PPE_WALK_2PH && MODE == IMG_SPLIT && KL == 2 && !RECW) {
-        // phase 1: the LDS-resident levels, branchless
+    if constexpr (MODE == IMG_SPLIT) {
+        // Two phases: the staged blocks are the breadth-first prefix of the block forest, so a lane that leaves them
+        // never returns.  Phase 1 walks the LDS-resident levels without per-tile branches (a lane outside them, or
+        // done, reads block 0 and keeps its state); phase 2 walks the rest from L2 with one exec-masked global read
+        // per tile and step (no LDS / global branch pair per step).
 #pragma unroll 1
         for (uint32_t it = 0; it < g.max_bdepth; ++it) {
-            uint4 q[MT][NQ];
+            uint4 lo[MT], hi[MT];
             bool inl[MT];
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
                 inl[t] = !done[t] & (blk[t] < g.lds_blocks);
                 const uint32_t la = IMGB + g.blk_lds + BB * (inl[t] ? blk[t] : 0u);
-#pragma unroll
-                for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
+                lo[t] = lds_u128(la);
+                hi[t] = lds_u128(la + 16u);
             }
             bool pending = false;
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
-                const uint4 lo = q[t][0], hi = q[t][NQ - 1];
-                const bool b0 = key_sel(lo.w & 15u, key[t]) > lo.x;
-                const uint32_t t1 = b0 ? lo.z : lo.y;
-                const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
-                const bool b1 = key_sel(k1, key[t]) > t1;
-                const uint32_t x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
+                const uint32_t x = block_step(lo[t], hi[t], key[t]);
                 const bool leaf = (x & PPE_BLK_LEAF) != 0u;
-                const uint32_t pay = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF)
-                                                      : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
-                nd[t].z = (inl[t] & leaf) ? pay : nd[t].z;
+                nd[t].z = (inl[t] & leaf) ? block_leaf_payload(g, x) : nd[t].z;
                 blk[t] = (inl[t] & !leaf) ? x : blk[t];
                 done[t] = done[t] | (inl[t] & leaf);
                 pending = pending | (inl[t] & !leaf & (x < g.lds_blocks));
             }
             if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
         }
-        // phase 2: the levels read from L2
-        uint32_t it = 0;
-#pragma unroll 1
-        for (; it < g.max_bdepth; ++it) {
-            bool pending = false;
-#pragma unroll
-            for (int t = 0; t < MT; ++t) pending = pending | !done[t];
-            if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
-            if constexpr (PPE_WALK_CMP && MT > 1) {  // (the tail: see below)
-                uint32_t tot = 0;
-#pragma unroll
-                for (int t = 0; t < MT; ++t) tot += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(!done[t]));
-                if (tot <= 64u) break;
-            }
-            uint4 q[MT][NQ];
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                if (!done[t]) {
-                    const uint32_t ga = 4u * g.off_blocks + BB * blk[t];
-#pragma unroll
-                    for (int j = 0; j < NQ; ++j) q[t][j] = gld<uint4>(gimg, ga + 16u * j);
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                if (!done[t]) {
-                    const uint4 lo = q[t][0], hi = q[t][NQ - 1];
-                    const bool b0 = key_sel(lo.w & 15u, key[t]) > lo.x;
-                    const uint32_t t1 = b0 ? lo.z : lo.y;
-                    const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
-                    const bool b1 = key_sel(k1, key[t]) > t1;
-                    const uint32_t x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
-                    if (x & PPE_BLK_LEAF) {
-                        done[t] = true;
-                        nd[t].z = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF)
-                                                   : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
-                    } else {
-                        blk[t] = x;
-                    }
-                }
-            }
-        }
-        if constexpr (PPE_WALK_CMP && MT > 1) {
-            // The tail (PPE_WALK_CMP): once the lanes still walking in all MT tiles fit one wave, they move into one
-            // virtual tile (ds_permute of the key and block index: lane l of tile t goes to lane P_t + its rank among
-            // tile t's walking lanes), which walks the remaining levels with one read per step instead of MT, and
-            // hands each lane its leaf back (ds_bpermute).  After the first L2 step about 7 % of C3's lanes walk on.
-            if (it >= g.max_bdepth) return;
-            uint64_t m[MT];
-            uint32_t P[MT + 1];
-            P[0] = 0u;
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                m[t] = __builtin_amdgcn_ballot_w64(!done[t]);
-                P[t + 1] = P[t] + (uint32_t)__popcll(m[t]);
-            }
-            const uint32_t tot = P[MT];
-            if (tot == 0u) return;
-            const uint32_t lane = __lane_id();
-            uint32_t vkey[4], vblk = 0u, vpay = 0u, vt = 0u;
-#pragma unroll
-            for (int t = 1; t < MT; ++t) vt += lane >= P[t] ? 1u : 0u;  // the tile this virtual lane comes from
-#pragma unroll
-            for (int c = 0; c < 4; ++c) vkey[c] = 0u;
-            uint32_t dst[MT];
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[t] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[t], 0u));
-                // a lane that does not walk pushes outside tile t's range [P_t, P_t+1) (its value is not taken there)
-                const uint32_t outside = P[t + 1] < 64u ? P[t + 1] : (P[t] > 0u ? P[t] - 1u : 0u);
-                dst[t] = !done[t] ? P[t] + rank : outside;
-                const uint32_t a4 = dst[t] << 2;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_permute((int)a4, (int)key[t][c]);
-                    vkey[c] = vt == (uint32_t)t ? v : vkey[c];
-                }
-                const uint32_t vb = (uint32_t)__builtin_amdgcn_ds_permute((int)a4, (int)blk[t]);
-                vblk = vt == (uint32_t)t ? vb : vblk;
-            }
-            bool vdone = lane >= tot;
-#pragma unroll 1
-            for (; it < g.max_bdepth; ++it) {
-                if (__builtin_amdgcn_ballot_w64(!vdone) == 0) break;
-                if (!vdone) {
-                    const uint32_t ga = 4u * g.off_blocks + BB * vblk;
-                    uint4 q[NQ];
-#pragma unroll
-                    for (int j = 0; j < NQ; ++j) q[j] = gld<uint4>(gimg, ga + 16u * j);
-                    const uint4 lo = q[0], hi = q[NQ - 1];
-                    const bool b0 = key_sel(lo.w & 15u, vkey) > lo.x;
-                    const uint32_t t1 = b0 ? lo.z : lo.y;
-                    const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
-                    const bool b1 = key_sel(k1, vkey) > t1;
-                    const uint32_t x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
-                    if (x & PPE_BLK_LEAF) {
-                        vdone = true;
-                        vpay = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF) : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
-                    } else {
-                        vblk = x;
-                    }
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {  // each walking lane takes its leaf back from its virtual lane
-                const uint32_t pay = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(dst[t] << 2), (int)vpay);
-                if (!done[t]) nd[t].z = pay;
-            }
-        }
-        return;
     }
+    // the levels read from global memory (L2): one exec-masked read per tile and step
+    uint32_t it = 0;
 #pragma unroll 1
-    for (uint32_t it = 0; it < g.max_bdepth + (RECW ? 1u : 0u); ++it) {
-        uint4 q[MT][NQ];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            if (RECW && recp[t]) q[t][0] = crec_load<IMGB>(gimg, g, nd[t].z);
-            if (!done[t]) {
-                // (a whole-LDS image: every block is staged, no global-load path compiled in)
-                if (MODE == IMG_LDS || (MODE != IMG_GLOBAL && blk[t] < g.lds_blocks)) {
-                    const uint32_t la = IMGB + g.blk_lds + BB * blk[t];
-#pragma unroll
-                    for (int j = 0; j < NQ; ++j) q[t][j] = lds_u128(la + 16u * j);
-                } else {
-                    const uint32_t ga = 4u * g.off_blocks + BB * blk[t];
-#pragma unroll
-                    for (int j = 0; j < NQ; ++j) q[t][j] = gld<uint4>(gimg, ga + 16u * j);
-                }
-            }
-        }
+    for (; it < g.max_bdepth; ++it) {
         bool pending = false;
 #pragma unroll
+        for (int t = 0; t < MT; ++t) pending = pending | !done[t];
+        if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
+        if constexpr (MT > 1) {  // (the tail: see below)
+            uint32_t tot = 0;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) tot += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(!done[t]));
+            if (tot <= 64u) break;
+        }
+        uint4 lo[MT], hi[MT];
+#pragma unroll
         for (int t = 0; t < MT; ++t) {
-            if (RECW && recp[t]) {  // the record requested this step has arrived
-                rec[t] = q[t][0];
-                recp[t] = false;
-            }
             if (!done[t]) {
-                uint32_t x;
-                if constexpr (KL == 2) {
-                    // position 0 → b0; position 1 + b0 → b1; exit 2 b0 + b1 (a leaf position passes through: thr ~0)
-                    const uint4 lo = q[t][0], hi = q[t][NQ - 1];
-                    const bool b0 = key_sel(lo.w & 15u, key[t]) > lo.x;
-                    const uint32_t t1 = b0 ? lo.z : lo.y;
-                    const uint32_t k1 = (lo.w >> (b0 ? 8u : 4u)) & 15u;
-                    const bool b1 = key_sel(k1, key[t]) > t1;
-                    x = b0 ? (b1 ? hi.w : hi.z) : (b1 ? hi.y : hi.x);
-                } else {
-                    // 3 levels: thresholds w0..w6 (a, b.xyz), key slots b.w, exits c, d; position 1 + b0, then
-                    // 3 + 2 b0 + b1; exit 4 b0 + 2 b1 + b2
-                    const uint4 a = q[t][0], b = q[t][1], c = q[t][2 % NQ], d = q[t][3 % NQ];
-                    const uint32_t sl = b.w;
-                    const bool b0 = key_sel(sl & 15u, key[t]) > a.x;
-                    const uint32_t t1 = b0 ? a.z : a.y;
-                    const uint32_t k1 = (sl >> (b0 ? 8u : 4u)) & 15u;
-                    const bool b1 = key_sel(k1, key[t]) > t1;
-                    const uint32_t t2 = b0 ? (b1 ? b.z : b.y) : (b1 ? b.x : a.w);
-                    const uint32_t k2 = (sl >> (4u * (3u + 2u * (uint32_t)b0 + (uint32_t)b1))) & 15u;
-                    const bool b2 = key_sel(k2, key[t]) > t2;
-                    const uint4 ex = b0 ? d : c;
-                    x = b1 ? (b2 ? ex.w : ex.z) : (b2 ? ex.y : ex.x);
-                }
+                const uint32_t ga = 4u * g.off_blocks + BB * blk[t];
+                lo[t] = gld<uint4>(gimg, ga);
+                hi[t] = gld<uint4>(gimg, ga + 16u);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            if (!done[t]) {
+                const uint32_t x = block_step(lo[t], hi[t], key[t]);
                 if (x & PPE_BLK_LEAF) {
                     done[t] = true;
-                    // leaf payload in node form: slot / sentinel, or first | count << 24 for leaf lists
-                    // (compact images: slot | flags, acl_leaf_compact)
-                    nd[t].z = g.max_leaf <= 1u ? (x & ~PPE_BLK_LEAF) : ((x & 0x7fffffu) | (((x >> 23) & 0xffu) << 24));
-                    if (RECW) {
-                        recp[t] = true;
-                        pending = true;
-                    }
+                    nd[t].z = block_leaf_payload(g, x);
                 } else {
                     blk[t] = x;
-                    pending = true;
                 }
             }
         }
-        if (__builtin_amdgcn_ballot_w64(pending) == 0) break;
+    }
+    if constexpr (MT > 1) {
+        // The tail: once the lanes still walking in all MT tiles fit one wave, they move into one virtual tile
+        // (ds_permute of the key and block index: lane l of tile t goes to lane P_t + its rank among tile t's
+        // walking lanes), which walks the remaining levels with one read per step instead of MT, and hands each lane
+        // its leaf back (ds_bpermute).  After the first L2 step about 7 % of C3's lanes walk on.
+        if (it >= g.max_bdepth) return;
+        uint64_t m[MT];
+        uint32_t P[MT + 1];
+        P[0] = 0u;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            m[t] = __builtin_amdgcn_ballot_w64(!done[t]);
+            P[t + 1] = P[t] + (uint32_t)__popcll(m[t]);
+        }
+        const uint32_t tot = P[MT];
+        if (tot == 0u) return;
+        const uint32_t lane = __lane_id();
+        uint32_t vkey[4], vblk = 0u, vpay = 0u, vt = 0u;
+#pragma unroll
+        for (int t = 1; t < MT; ++t) vt += lane >= P[t] ? 1u : 0u;  // the tile this virtual lane comes from
+#pragma unroll
+        for (int c = 0; c < 4; ++c) vkey[c] = 0u;
+        uint32_t dst[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[t] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[t], 0u));
+            // a lane that does not walk pushes outside tile t's range [P_t, P_t+1) (its value is not taken there)
+            const uint32_t outside = P[t + 1] < 64u ? P[t + 1] : (P[t] > 0u ? P[t] - 1u : 0u);
+            dst[t] = !done[t] ? P[t] + rank : outside;
+            const uint32_t a4 = dst[t] << 2;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t v = (uint32_t)__builtin_amdgcn_ds_permute((int)a4, (int)key[t][c]);
+                vkey[c] = vt == (uint32_t)t ? v : vkey[c];
+            }
+            const uint32_t vb = (uint32_t)__builtin_amdgcn_ds_permute((int)a4, (int)blk[t]);
+            vblk = vt == (uint32_t)t ? vb : vblk;
+        }
+        bool vdone = lane >= tot;
+#pragma unroll 1
+        for (; it < g.max_bdepth; ++it) {
+            if (__builtin_amdgcn_ballot_w64(!vdone) == 0) break;
+            if (!vdone) {
+                const uint32_t ga = 4u * g.off_blocks + BB * vblk;
+                const uint32_t x = block_step(gld<uint4>(gimg, ga), gld<uint4>(gimg, ga + 16u), vkey);
+                if (x & PPE_BLK_LEAF) {
+                    vdone = true;
+                    vpay = block_leaf_payload(g, x);
+                } else {
+                    vblk = x;
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {  // each walking lane takes its leaf back from its virtual lane
+            const uint32_t pay = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(dst[t] << 2), (int)vpay);
+            if (!done[t]) nd[t].z = pay;
+        }
     }
 }
 
@@ -1113,9 +927,8 @@ __device__ __forceinline__ uint64_t make_act_table(uint32_t unsup_fw) {
 // Wave-ballot compaction of a 64-packet tile's FW / DROP indices into the tile's 64-slot segment of each list (or
 // the partition layout when fw_idx == drop_idx, or its compact byte form part8), plus the tile count.  Every lane of
 // the wave calls it.
-// scr: a wave-private 256-B LDS scratch (byte address) or ~0u.  With scratch, the partition layout's permuted store
-// goes through LDS (each lane writes its slot, then reads slot `lane`), so the global store is in lane order (part8:
-// 16 lanes store the tile's 64 entries as dwords).
+// scr: a wave-private 256-B LDS scratch (byte address) or ~0u.  With scratch, the 4-B partition layout's permuted
+// store goes through LDS (each lane writes its slot, then reads slot `lane`), so the global store is in lane order.
 __device__ __forceinline__ void compact_tile(uint32_t *fw_idx, uint32_t *drop_idx, uint32_t *tile_cnt, uint32_t n,
                                              uint32_t idx_base, uint32_t tile, uint32_t lane, bool valid, uint32_t act,
                                              uint32_t scr = ~0u, uint8_t *part8 = nullptr) {
@@ -1133,13 +946,9 @@ __device__ __forceinline__ void compact_tile(uint32_t *fw_idx, uint32_t *drop_id
         const uint32_t ndr = (uint32_t)__popcll(bdr), nfw = (uint32_t)__popcll(bfw);
         const uint32_t slot = is_fw ? pfw : (is_drop ? nv - ndr + pdr : nfw + lane - pfw - pdr);
         const uint32_t e = lane | (act << 6);
-        if (PPE_CMP_LDS8 && scr != ~0u && nv == 64u) {  // (LDS ops of one wave complete in order)
-            lds_st8(scr + slot, e);
-            const uint32_t v = lds_u32(scr + 4u * (lane & 15u));
-            if (lane < 16u) gst_nt<uint32_t>(part8, (tile << 6) + 4u * lane, v);
-        } else if (valid) {
-            gst_nt<uint8_t>(part8, (tile << 6) + slot, (uint8_t)e);
-        }
+        // (each lane stores its byte at its slot: one 64-B byte-store instruction per tile; the same permutation
+        // through LDS stored as 16 dwords measured 16.76 against 16.68 us per 1M, r4h)
+        if (valid) gst_nt<uint8_t>(part8, (tile << 6) + slot, (uint8_t)e);
     } else if (fw_idx == drop_idx && fw_idx) {
         // partition layout (one shared list): the tile's segment holds every packet of the tile, FW from the
         // front, DROP at the back, PUNT in between, each in ascending order, the action in bits 31:30 —
@@ -1232,22 +1041,9 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    // every packet of the batch carries the same batch time (PPE_LAST_COND, experiment: store only when it differs)
-    if (!(PPE_ABLATE & 32)) {
-        unsigned long long *lp = f.packed + (size_t)PPE_FLOW_REC_WORDS * s + PPE_FLOW_REC_LAST;
-        if (!PPE_LAST_COND || *lp != now) *lp = now;
-    }
+    // every packet of the batch carries the same batch time (storing only when it differs measured no faster)
+    if (!(PPE_ABLATE & 32)) f.packed[(size_t)PPE_FLOW_REC_WORDS * s + PPE_FLOW_REC_LAST] = now;
     return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
-}
-
-// PPE_UPD_NT (experiment): the owner update's stores (bucket entries, packed counters, last-seen times) with the
-// non-temporal policy, so fewer dirty lines wait in L2 for the write-back at the launch's end
-#ifndef PPE_UPD_NT
-#define PPE_UPD_NT 0
-#endif
-template <class T> __device__ __forceinline__ void upd_st(T *p, T v) {
-    if constexpr (PPE_UPD_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
 }
 
 // PPE_UPD_LDS: the classify workgroup collects its bucket entries in LDS as 4-B entries {wire length (16 bits), dir,
@@ -1274,8 +1070,8 @@ __device__ __forceinline__ uint32_t flow_found(const ppe_flowdev &f, uint32_t *u
             if (upd_small(f))
                 ubuf[o * PPE_UPD_CAP + pos] = wire_len | (d << 16) | ((s & ((1u << f.upd_osh) - 1u)) << 17);
             else
-                upd_st(f.upd + ((size_t)o * f.upd_wgs + blockIdx.x) * PPE_UPD_CAP + pos,
-                       (unsigned long long)s | ((unsigned long long)(wire_len | (d << 31)) << 32));
+                f.upd[((size_t)o * f.upd_wgs + blockIdx.x) * PPE_UPD_CAP + pos] =
+                    (unsigned long long)s | ((unsigned long long)(wire_len | (d << 31)) << 32);
             return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
         }
     }
@@ -1372,64 +1168,26 @@ __device__ __forceinline__ uint32_t flow_find_claim(const ppe_flowdev &f, const 
     return PPE_FLOW_NONE;
 }
 
-// PF: when a tile's window is fetched
-#define PF_NONE 0   // at the top of its own iteration
+// PF: how a wave fetches and walks its tiles
+#define PF_NONE 0   // one tile per wave, its window loaded at the top of its own iteration
 #define PF_HOIST 1  // as PF_NONE, but the first tile's loads are issued before the image staging
-#define PF_SBLK 5   // split images whose block section fits a 1024-thread workgroup's half of the CU's LDS: one tile
-                    // per wave (8 waves/SIMD, two workgroups per CU), the 2-level block walk with the keys in registers
-                    // (staged block levels in LDS, the rest and the rule records from L2)
 #define PF_MULTI 3  // split / global images: each wave loads, decodes and walks PPE_MT tiles together (acl_walk_blocks_mt),
                     // 4 waves/SIMD with 128 VGPRs, one 1024-thread workgroup per CU and its whole LDS for the image
-#define PF_MULTI3 6  // PF_MULTI over an image of 3-level blocks (image word PPE_IMG_W_BLKLV == 3)
-#define PF_SBLK3 7   // PF_SBLK over 3-level blocks
-#define PF_PC 8      // PF_MULTI with its waves in two roles (split images, C3): producer waves stream the header
-                     // windows from HBM, decode and hash them, and hand tiles to consumer waves through an LDS queue;
-                     // consumer waves walk the image (LDS levels, then dependent L2 reads), check the records and
-                     // write the results.  A wave's s_waitcnt vmcnt retires its loads in issue order, so in one wave
-                     // a walk's L2 read would wait behind any HBM window load issued before it: split into roles,
-                     // the window stream never waits for a walk and no walk step waits for the window stream.
+#define PF_CUT 5    // images with cut lists (v7): one tile per wave (8 waves/SIMD), the keys in registers, the bucket
+                    // groups in LDS, the list entries from L2 (acl_cut)
 #ifndef PPE_MT
 #define PPE_MT 4
 #endif
-#ifndef PPE_MT3  // tiles per wave of the PF_MULTI3 kernel (a 64-B block per lane and tile in flight)
-#define PPE_MT3 3
-#endif
-#ifndef PPE_MT3_WAVES
-#define PPE_MT3_WAVES 4
-#endif
+// tiles per wave of the multi-tile kernel over a whole-LDS image (software-pipelined round loop: the next round's
+// windows need the registers of two more tiles; C2 / C4 step -4.5 / -3 % at 2 tiles against the plain loop at 4, 3
+// tiles -1 %, 4 spills; profiles/r3_ab_runs.md r3h)
+#define PPE_MT_LDS 2
 #ifndef PPE_FLOW_WAVES  // waves per SIMD the FLOW classify kernel is compiled for
 #define PPE_FLOW_WAVES 4   // 8 (the stateless kernels' value) measured 3 % slower per F1 batch: profiles/r3_ab_runs.md r4f
 #endif
 #ifndef PPE_MT_WAVES  // waves per SIMD the PF_MULTI kernel is compiled for (VGPR budget 512 / this)
 #define PPE_MT_WAVES 4
 #endif
-// PF_PC geometry: producer waves of the 16 in a 1024-thread workgroup, queue slots (tiles; deadlock freedom needs
-// >= 2 * PPE_MT, see the PF_PC loop), dwords per lane in a slot (key 4, flow hash, payload length, TCP option word)
-#ifndef PPE_PC_PROD
-#define PPE_PC_PROD 4
-#endif
-#ifndef PPE_PC_Q
-#define PPE_PC_Q 12
-#endif
-// diagnostic builds only (make variant NAME=pcstats VFLAGS=-DPPE_PC_STATS=1, tools/pc_stats.py): per role, the polls
-// spent waiting on the queue and the tiles handled, added into kargs.trace[0..7]
-#ifndef PPE_PC_STATS
-#define PPE_PC_STATS 0
-#endif
-// diagnostic builds only (make variant NAME=mttrace VFLAGS="-DPPE_MTTRACE=1 -DPPE_MTTRACE_SKIP=k", tools/trace_mt.py):
-// lane 0 of every wave of the multi-tile round loop writes s_memrealtime stamps of rounds k .. k + 4 to kargs.trace
-// (wave w at [32 w + 1 + 4 r + j]: j 0 round top, 1 decoded (window loads returned), 2 walked, 3 finished)
-#ifndef PPE_MTTRACE
-#define PPE_MTTRACE 0
-#endif
-#ifndef PPE_MTTRACE_SKIP
-#define PPE_MTTRACE_SKIP 8u
-#endif
-#define PC_W 7u
-#define PC_SLOT_BYTES (PC_W * 256u)
-#define PC_QBYTES (PPE_PC_Q * PC_SLOT_BYTES + 8u * PPE_PC_Q + 16u)  // slots, ready[Q] + free[Q], two tickets
-static_assert(PPE_PC_Q >= 2 * PPE_MT, "PF_PC queue: at least two ticket groups of slots");
-static_assert(PC_QBYTES % 16u == 0, "PF_PC queue keeps the image 16-B aligned");
 
 // FLOW: stateful flow-table mode (ppe_classify_flow, one batch): packets whose flow exists are accounted and
 // forwarded here; the rest are recorded (and the would-be creators claim their slots) for the resolve / finalize
@@ -1438,22 +1196,19 @@ static_assert(PC_QBYTES % 16u == 0, "PF_PC queue keeps the image 16-B aligned");
 // list, no tile counts, no tuple: ppe_kargs.part_layout), so the output checks are compile-time and the kernel holds
 // fewer scalars (C1 step -2..4 %, C4 -3.5 %: fewer SGPR spills to VGPR lanes)
 template <int MODE, int PF, int BLOCK, bool FLOW, bool PART = false>
-__global__ __launch_bounds__(BLOCK, ((PF == PF_MULTI || PF == PF_MULTI3 || PF == PF_PC) && !FLOW)
-                                        ? (PF == PF_MULTI3 ? PPE_MT3_WAVES : PPE_MT_WAVES)
-                                        : (FLOW ? PPE_FLOW_WAVES : PPE_WAVES_PER_EU))
+__global__ __launch_bounds__(BLOCK, (PF == PF_MULTI && !FLOW) ? PPE_MT_WAVES
+                                                             : (FLOW ? PPE_FLOW_WAVES : PPE_WAVES_PER_EU))
 void ppe_classify_kernel(ppe_kargs a) {
-    constexpr bool MT_PIPE = PF == PF_MULTI && !FLOW &&
-                             (PPE_MT_PF == 2 || (PPE_MT_PF == 1 && MODE == IMG_LDS));  // the pipelined round loop
-    constexpr bool PC = PF == PF_PC && !FLOW;
-    constexpr int MT = FLOW ? 1
-                     : PF == PF_MULTI ? ((PPE_MT_PF == 1 && MODE == IMG_LDS) ? PPE_MT_LDS : PPE_MT)
-                     : PF == PF_MULTI3 ? PPE_MT3 : PC ? PPE_MT : 1;
-    constexpr int KL = (PF == PF_MULTI3 || PF == PF_SBLK3) ? 3 : 2;  // block levels of the image's block section
+    // the multi-tile kernel over a whole-LDS image runs the software-pipelined round loop: the next round's windows
+    // are requested before the walk (vmcnt retires loads in issue order; the walk and the record check there issue
+    // no global loads, so nothing waits for the prefetch early).  Split images keep the plain round loop: their
+    // walk's L2 reads would wait behind the prefetched windows (C3 +3 %).
+    constexpr bool MT_PIPE = PF == PF_MULTI && !FLOW && MODE == IMG_LDS;
+    constexpr int MT = FLOW ? 1 : PF == PF_MULTI ? (MODE == IMG_LDS ? PPE_MT_LDS : PPE_MT) : 1;
+    constexpr bool CUT = PF == PF_CUT && !FLOW;
+    constexpr bool KEYS = MT == 1 && !CUT;  // node walks: per-wave key slots in LDS
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    // single-tile walks over a whole-LDS image use its 2-level blocks with the keys in registers (no key slots)
-    constexpr bool STB = (PPE_ST_BLOCKS && MT == 1 && MODE == IMG_LDS) || PF == PF_SBLK || PF == PF_SBLK3;
-    using L = Lds<BLOCK, MT == 1 && !STB,
-                  PC ? PC_QBYTES : FLOW ? 4u * PPE_UPD_OWNERS * (1u + (PPE_UPD_LDS ? PPE_UPD_CAP : 0u)) : 0u>;
+    using L = Lds<BLOCK, KEYS, FLOW ? 4u * PPE_UPD_OWNERS * (1u + (PPE_UPD_LDS ? PPE_UPD_CAP : 0u)) : 0u>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
     uint32_t *lcnt = bins + PPE_NBINS;       // [32] per-reason counters of this workgroup
     uint32_t *ucur = smem + L::QUEUE / 4u;   // FLOW: [PPE_UPD_OWNERS] entries in this workgroup's owner buckets
@@ -1462,7 +1217,7 @@ void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t nwaves = gridDim.x * (BLOCK / 64);
-    const uint32_t twave = blockIdx.x * (BLOCK / 64) + wv;  // this wave's index in the grid (trace slot)
+    const uint32_t twave = blockIdx.x * (BLOCK / 64) + wv;  // this wave's index in the grid
     // Batch groups: the grid's waves split into G = min(waves, batches, max_groups) equal groups; group g takes
     // batches g, g + G, ..., and its Wb waves stride over each of them (wave wi of the group: tiles wi, wi + Wb, ...).
     // One batch → every wave on it, as before; a queue of batches → each wave walks G times more tiles of a batch
@@ -1474,8 +1229,6 @@ void ppe_classify_kernel(ppe_kargs a) {
     const uint32_t grp = twave / stride_waves;
     const uint32_t wtile = twave - grp * stride_waves;            // wi
     const bool wave_live = grp < ngroups;
-    uint32_t titer = 0;
-    TRACE_AT(0);
     // the batch being processed (kernel-argument descriptor, or the device descriptor ring: scalar loads either way)
     // (the ring is read through the constant address space: uniform addresses there become scalar loads, so the
     // descriptor lives in SGPRs as the kernel-argument one does)
@@ -1494,45 +1247,30 @@ void ppe_classify_kernel(ppe_kargs a) {
     // the end of the batch re-reads the last packet.  Byte offsets are 32-bit (the engine keeps n * stride < 2^31).
     uint4 q0, q1, q2;
     uint32_t w12 = 0, qlen = 0;
-    auto load_at = [&](const uint8_t *hdr, const uint32_t *lenp, uint32_t n, uint32_t stride, uint32_t t) {
-        const uint32_t pc = min((t << 6) + lane, n - 1u);
-        const uint32_t ro = pc * stride;
-        if constexpr (PPE_NT_WIN == 2) {  // experiment: single-tile kernel too
-            q0 = gld_win<uint4>(hdr, ro);
-            q1 = gld_win<uint4>(hdr, ro + 16u);
-            q2 = gld_win<uint4>(hdr, ro + 32u);
-            w12 = gld_win<uint32_t>(hdr, ro + 48u);
-            qlen = gld_win<uint32_t>(lenp, 4u * pc);
-        } else {
-            q0 = gld<uint4>(hdr, ro);
-            q1 = gld<uint4>(hdr, ro + 16u);
-            q2 = gld<uint4>(hdr, ro + 32u);
-            w12 = gld<uint32_t>(hdr, ro + 48u);
-            qlen = gld<uint32_t>(lenp, 4u * pc);
-        }
+    auto load_tile = [&](uint32_t t) {
+        const uint32_t pc = min((t << 6) + lane, B.n - 1u);
+        const uint32_t ro = pc * B.stride;
+        q0 = gld<uint4>(B.hdr, ro);
+        q1 = gld<uint4>(B.hdr, ro + 16u);
+        q2 = gld<uint4>(B.hdr, ro + 32u);
+        w12 = gld<uint32_t>(B.hdr, ro + 48u);
+        qlen = gld<uint32_t>(B.len, 4u * pc);
     };
-    auto load_tile = [&](uint32_t t) { load_at(B.hdr, B.len, B.n, B.stride, t); };
     // first window in flight during the image staging
-    bool have = (PF == PF_HOIST || PF == PF_SBLK || PF == PF_SBLK3) && wave_live &&
-                wtile < ((B.n + 63u) >> 6);  // (PF_MULTI: at the loop top)
+    bool have = (PF == PF_HOIST || CUT) && wave_live && wtile < ((B.n + 63u) >> 6);  // (PF_MULTI: at the loop top)
     if (have) load_tile(wtile);
 
     for (uint32_t i = tid; i < PPE_NBINS + 32u; i += BLOCK) bins[i] = 0;
     if constexpr (FLOW)
         for (uint32_t i = tid; i < PPE_UPD_OWNERS; i += BLOCK) ucur[i] = 0;
-    if constexpr (PC) {  // the tile queue's flags: ready[s] = none, free[s] = s (slot s takes ticket s first), tickets 0
-        uint32_t *qf = smem + (L::QUEUE + PPE_PC_Q * PC_SLOT_BYTES) / 4u;
-        for (uint32_t i = tid; i < 2u * PPE_PC_Q + 2u; i += BLOCK)
-            qf[i] = i < PPE_PC_Q ? ~0u : (i < 2u * PPE_PC_Q ? i - PPE_PC_Q : 0u);
-    }
     const uint32_t lanebase = wv * KEY_WAVE_BYTES + 4u * lane;  // this lane's key slot 0 (LDS byte address)
-    if (MT == 1 && !STB) lds_st32(lanebase + 256u * PPE_NODE_LEAF, 0u);  // the leaves' zero key
+    if (KEYS) lds_st32(lanebase + 256u * PPE_NODE_LEAF, 0u);  // the leaves' zero key
     if (MODE != IMG_GLOBAL) stage_image<BLOCK>(a.img + a.stage_src, smem + L::IMGB / 4u, a.stage_words, tid);
     __syncthreads();
-    TRACE_AT(1);
     const AclGeo geo = {a.lds_iters, a.max_depth, a.max_leaf, a.root_ks, a.off_leaf, a.off_rules, a.off_resid,
                         a.lds_words, a.default_action, a.jump, a.off_nodes, a.lds_blocks, a.bsec_lds, a.blk_lds,
-                        a.off_bsec, a.off_blocks, a.max_bdepth, a.off_crec, a.off_idtab, a.crec_lds, a.idtab_lds};
+                        a.off_bsec, a.off_blocks, a.max_bdepth, a.off_crec, a.off_idtab, a.crec_lds, a.idtab_lds,
+                        a.cut, a.cut_grp, a.cut_ent, a.cut_ent_lds};
 
     const uint64_t act_table = make_act_table(a.unsup_fw);
     // (this batch's creator counter was zeroed by the previous batch's finalize launch)
@@ -1555,11 +1293,6 @@ void ppe_classify_kernel(ppe_kargs a) {
     auto finish = [&](uint32_t tile, uint32_t p, bool valid, const Dec &k, uint32_t fh, int32_t hit, bool pend) {
         const uint32_t st = k.st;
         const uint32_t act = (uint32_t)(act_table >> (2u * st)) & 3u;
-        if (PPE_TRACE && titer - PPE_TRACE_SKIP < 4u) {
-            asm volatile("" ::"v"(hit), "v"(act));
-            TRACE_AT(5 + 5 * (titer - PPE_TRACE_SKIP));
-        }
-
         const uint32_t po = 4u * p;  // byte offset of this packet's SoA output words
         if (valid) {
             if (PART || B.verdict) gst_nt<uint32_t>(B.verdict, po, st | (act << 8) | (k.flags << 16));
@@ -1604,7 +1337,6 @@ void ppe_classify_kernel(ppe_kargs a) {
             }
             if (pm != 0) {  // the finalize kernel completes this tile (compaction, pending lanes' counters)
                 if (!(PPE_ABLATE & 2) && valid && !pend) atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
-                ++titer;
                 return;
             }
         }
@@ -1613,14 +1345,12 @@ void ppe_classify_kernel(ppe_kargs a) {
             const bool p8 = (B.flags & PPE_BD_PART8) != 0u;  // (the compact list travels in the tile_cnt field)
             compact_tile(p8 ? nullptr : B.fw_idx, p8 ? nullptr : (PART ? B.fw_idx : B.drop_idx),
                          (PART || p8) ? nullptr : B.tile_cnt, B.n, B.idx_base, tile, lane, valid, act,
-                         (PPE_CMP_LDS && MT == 1 && !STB) ? lanebase - 4u * lane + 256u * PPE_DIM_SIP : ~0u,
+                         KEYS ? lanebase - 4u * lane + 256u * PPE_DIM_SIP : ~0u,
                          p8 ? (uint8_t *)B.tile_cnt : nullptr);
         }
 
         // ---- per-reason counters: one LDS add per packet into its (status, flags) bin ----
         if (!(PPE_ABLATE & 2) && valid) atomicAdd(&bins[st | ((k.flags & 7u) << 5)], 1u);
-        if (PPE_TRACE && titer - PPE_TRACE_SKIP < 4u) TRACE_AT(6 + 5 * (titer - PPE_TRACE_SKIP));
-        ++titer;
     };
 
     // one tile: decode, hash, ACL, stores, compaction, counters.  w = the window's first 52 bytes, wlen = wire length
@@ -1633,10 +1363,6 @@ void ppe_classify_kernel(ppe_kargs a) {
         uint32_t fh = 0;
         int32_t hit = -1;
         if (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4)) fh = flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport);
-        if (PPE_TRACE && titer - PPE_TRACE_SKIP < 4u) {
-            asm volatile("" ::"v"(fh), "v"(k.st));  // decoded + hashed before the stamp
-            TRACE_AT(4 + 5 * (titer - PPE_TRACE_SKIP));
-        }
         bool pend = false;  // FLOW: flow not in the table; resolved by the kernels after this one
         if (FLOW && (k.flags & PPE_F_L4)) {  // FlowGetFlowFromHash, flow.c:181-201
             const uint32_t ports = k.sport | (k.dport << 16);
@@ -1654,32 +1380,22 @@ void ppe_classify_kernel(ppe_kargs a) {
             k.st = PPE_ST_ACL_FW;
             k.flags |= PPE_F_ACL;
         }
-        if (!(PPE_ABLATE & 1) && k.st == ST_ACL) {
+        if (!(PPE_ABLATE & 1) && k.st == ST_ACL && CUT) {
+            bool drop;
+            acl_cut<MODE, L::IMGB>(a.img, geo, k.sip, k.dip, k.sport | (k.dport << 16), k.proto == 6u, hit, drop);
+            k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;  // flow.c:232-243
+            k.flags |= PPE_F_ACL;
+        }
+        if (!(PPE_ABLATE & 1) && k.st == ST_ACL && !CUT) {
             uint32_t rule_act;
             const MacFromWindow mac = {B.hdr, p, B.stride};
-            if constexpr (STB) {
-                const uint32_t key[1][4] = {{k.sip, k.dip, k.sport | (k.dport << 16), k.proto << 16}};
-                const bool need[1] = {true};
-                uint4 nd[1];
-                acl_walk_blocks_mt<MODE, L::IMGB, 1, KL>(a.img, geo, key, need, nd);
-                if (geo.off_crec) {
-                    bool drop;
-                    acl_leaf_compact<L::IMGB>(a.img, geo, nd[0].z, k.sip, k.dip, k.sport, k.dport, k.proto == 6u,
-                                              hit, drop);
-                    rule_act = drop ? ACL_RULE_ACTION_DROP : ACL_RULE_ACTION_FW;
-                } else {
-                    acl_leaf<MODE, L::IMGB>(a.img, geo, nd[0], k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts,
-                                            p, a.now, hit, rule_act);
-                }
-            } else {
-                lds_st32(lanebase + 256u * PPE_DIM_SIP, k.sip);
-                lds_st32(lanebase + 256u * PPE_DIM_DIP, k.dip);
-                lds_st32(lanebase + 256u * PPE_DIM_SPORT, k.sport);
-                lds_st32(lanebase + 256u * PPE_DIM_DPORT, k.dport);
-                lds_st32(lanebase + 256u * PPE_DIM_PROTO, k.proto);
-                acl_lookup<MODE, L::IMGB>(a.img, geo, lanebase, k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts,
-                                          p, a.now, hit, rule_act);
-            }
+            lds_st32(lanebase + 256u * PPE_DIM_SIP, k.sip);
+            lds_st32(lanebase + 256u * PPE_DIM_DIP, k.dip);
+            lds_st32(lanebase + 256u * PPE_DIM_SPORT, k.sport);
+            lds_st32(lanebase + 256u * PPE_DIM_DPORT, k.dport);
+            lds_st32(lanebase + 256u * PPE_DIM_PROTO, k.proto);
+            acl_lookup<MODE, L::IMGB>(a.img, geo, lanebase, k.sip, k.dip, k.sport, k.dport, k.proto, mac, B.ts, p,
+                                      a.now, hit, rule_act);
             const bool drop = rule_act == ACL_RULE_ACTION_DROP;  // flow.c:232-243, FlowHandlePacket :309
             k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
             k.flags |= PPE_F_ACL;
@@ -1687,200 +1403,67 @@ void ppe_classify_kernel(ppe_kargs a) {
         finish(tile, p, valid, k, fh, hit, pend);
     };
 
-    if constexpr (PC) {
-        // ---- PF_PC: the workgroup's tiles, batch after batch (workgroup wg takes tiles wg, wg + G, ... of every
-        // batch), are tickets handed out in groups of MT by two LDS counters, one per role.  Ticket u lives in queue
-        // slot u % Q: its producer waits until free[slot] == u (the consumer of u - Q has read the slot), fills it and
-        // sets ready[slot] = u; its consumer waits for that, takes the slot into registers and sets free[slot] = u + Q.
-        // No deadlock: the smallest ticket u not yet filled always proceeds.  Its producer holds the group [u', u' +
-        // MT) with u' <= u and waits only for the consumers of tickets below u' + MT - Q; each of those waits only for
-        // its own group, whose tickets lie below u' + 2 MT - Q <= u' <= u (Q >= 2 MT), all filled.  Every wait is
-        // bounded anyway (lds_wait_eq): a tile lost to a timeout gets verdict 0xffffffff, never a hang.
-        constexpr uint32_t Q = PPE_PC_Q;
-        const uint32_t qbase = L::QUEUE, qf = L::QUEUE + Q * PC_SLOT_BYTES;
-        const uint32_t rdy = qf, fre = qf + 4u * Q, tk_prod = qf + 8u * Q, tk_cons = tk_prod + 4u;
-        const uint32_t G = gridDim.x, wg = blockIdx.x;
-        // this wave's cursor over the batches: tickets [cbase, cbase + ccnt) are batch cb's (a wave's tickets only grow)
-        uint32_t cb = 0, cbase = 0;
-        auto cnt_of = [&](uint32_t n) -> uint32_t {
-            const uint32_t nt = (n + 63u) >> 6;
-            return nt > wg ? (nt - wg + G - 1u) / G : 0u;
-        };
-        uint32_t ccnt = cnt_of(bdesc(0).n);
-        auto locate = [&](uint32_t u, uint32_t &bi, uint32_t &tile) -> bool {
-            while (u >= cbase + ccnt) {
-                if (cb + 1u >= a.nbatch) return false;
-                cbase += ccnt;
-                ++cb;
-                ccnt = cnt_of(bdesc(cb).n);
+    // multi-tile rounds: per tile the packed key (sip, dip, ports, meta = status | flags << 8 | proto << 16) and, for
+    // the tuple output only, payload length and TCP option word; the flow hash is computed after the walk (fewer live
+    // registers while the block reads are in flight)
+    auto mt_decode = [&](uint32_t t0, const uint4 (&r0)[MT], const uint4 (&r1)[MT], const uint4 (&r2)[MT],
+                         const uint32_t (&r3)[MT], const uint32_t (&rl)[MT], uint32_t (&key)[MT][4],
+                         uint32_t (&kpay)[MT], uint32_t (&kopt)[MT], bool (&need)[MT]) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+            const uint32_t p = ((t0 + t) << 6) + lane;
+            if (p < B.n) rx_bytes += rl[t];
+            const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
+                                    r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
+            Dec d = decode<!PART>(w, rl[t], B.hdr, p, B.stride, a.syn_check);
+            if ((PPE_ABLATE & 1) && d.st == ST_ACL) {
+                d.st = PPE_ST_ACL_FW;
+                d.flags |= PPE_F_ACL;
             }
-            bi = cb;
-            tile = wg + (u - cbase) * G;
-            return true;
-        };
-        uint32_t polls = 0, tiles_done = 0;
-        auto take = [&](uint32_t ctr) -> uint32_t {  // the wave's next ticket group
-            uint32_t u = 0;
-            if (lane == 0) u = lds_add(ctr, (uint32_t)MT);
-            return __builtin_amdgcn_readfirstlane(u);
-        };
-        if (wv < PPE_PC_PROD) {
-            // producer: MT tiles' windows in flight at once, then decode + hash each and hand it over
-#pragma unroll 1
-            for (;;) {
-                const uint32_t u0 = take(tk_prod);
-                uint32_t tbi[MT], tti[MT];
-                bool tv[MT];
-#pragma unroll
-                for (int t = 0; t < MT; ++t) tv[t] = locate(u0 + t, tbi[t], tti[t]);
-                if (!tv[0]) break;  // past the last batch (and so is every later ticket)
-                const uint8_t *th[MT];
-                const uint32_t *tl[MT];
-                uint32_t tn[MT], ts[MT];
-                uint4 r0[MT], r1[MT], r2[MT];
-                uint32_t r3[MT], rl[MT];
-#pragma unroll
-                for (int t = 0; t < MT; ++t) {
-                    if (!tv[t]) continue;
-                    const ppe_bdesc D = bdesc(tbi[t]);
-                    th[t] = D.hdr;
-                    tl[t] = D.len;
-                    tn[t] = D.n;
-                    ts[t] = D.stride;
-                    const uint32_t pc = min((tti[t] << 6) + lane, tn[t] - 1u);
-                    const uint32_t ro = pc * ts[t];
-                    r0[t] = gld_win<uint4>(th[t], ro);
-                    r1[t] = gld_win<uint4>(th[t], ro + 16u);
-                    r2[t] = gld_win<uint4>(th[t], ro + 32u);
-                    r3[t] = gld_win<uint32_t>(th[t], ro + 48u);
-                    rl[t] = gld_win<uint32_t>(tl[t], 4u * pc);
-                }
-#pragma unroll
-                for (int t = 0; t < MT; ++t) {
-                    if (!tv[t]) continue;
-                    const uint32_t p = (tti[t] << 6) + lane;
-                    if (p < tn[t]) rx_bytes += rl[t];
-                    const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
-                                            r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
-                    Dec d = decode<!PART>(w, rl[t], th[t], p, ts[t], a.syn_check);
-                    if ((PPE_ABLATE & 1) && d.st == ST_ACL) {
-                        d.st = PPE_ST_ACL_FW;
-                        d.flags |= PPE_F_ACL;
-                    }
-                    const uint32_t fh = (!(PPE_ABLATE & 8) && (d.flags & PPE_F_L4))
-                                            ? flow_hashfn_l4(d.proto == 6u, d.sip, d.dip, d.sport, d.dport) : 0u;
-                    const uint32_t u = u0 + (uint32_t)t, slot = u % Q;
-                    if (!lds_wait_eq(fre + 4u * slot, u, polls)) continue;  // (timeout: the consumer reports it)
-                    ++tiles_done;
-                    const uint32_t sb = qbase + slot * PC_SLOT_BYTES + 4u * lane;
-                    lds_st32(sb, d.sip);
-                    lds_st32(sb + 256u, d.dip);
-                    lds_st32(sb + 512u, d.sport | (d.dport << 16));
-                    lds_st32(sb + 768u, d.st | (d.flags << 8) | (d.proto << 16));
-                    lds_st32(sb + 1024u, fh);
-                    if (!PART) {
-                        lds_st32(sb + 1280u, d.paylen);
-                        lds_st32(sb + 1536u, d.tcpopt);
-                    }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    if (lane == 0) lds_vst(rdy + 4u * slot, u);
-                }
-            }
-        } else {
-            // consumer: MT tiles walked in lockstep (acl_walk_blocks_mt), their records checked, results written
-            uint32_t curB = ~0u;
-#pragma unroll 1
-            for (;;) {
-                const uint32_t u0 = take(tk_cons);
-                uint32_t tbi[MT], tti[MT];
-                bool tv[MT], got[MT];
-#pragma unroll
-                for (int t = 0; t < MT; ++t) tv[t] = locate(u0 + t, tbi[t], tti[t]);
-                if (!tv[0]) break;
-                uint32_t key[MT][4], kfh[MT], kpay[MT], kopt[MT];
-                bool need[MT];
-#pragma unroll
-                for (int t = 0; t < MT; ++t) {
-                    const uint32_t u = u0 + (uint32_t)t, slot = u % Q;
-                    got[t] = tv[t] && lds_wait_eq(rdy + 4u * slot, u, polls);
-                    tiles_done += got[t] ? 1u : 0u;
-                    const uint32_t sb = qbase + (got[t] ? slot : 0u) * PC_SLOT_BYTES + 4u * lane;
-                    key[t][0] = got[t] ? lds_u32(sb) : 0u;
-                    key[t][1] = got[t] ? lds_u32(sb + 256u) : 0u;
-                    key[t][2] = got[t] ? lds_u32(sb + 512u) : 0u;
-                    key[t][3] = got[t] ? lds_u32(sb + 768u) : 0u;
-                    kfh[t] = got[t] ? lds_u32(sb + 1024u) : 0u;
-                    kpay[t] = (!PART && got[t]) ? lds_u32(sb + 1280u) : 0u;
-                    kopt[t] = (!PART && got[t]) ? lds_u32(sb + 1536u) : 0u;
-                    need[t] = got[t] && (key[t][3] & 0xffu) == ST_ACL;
-                }
-                // the slots go back to the producers once their words are in registers
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-                for (int t = 0; t < MT; ++t)
-                    if (got[t] && lane == 0) lds_vst(fre + 4u * ((u0 + (uint32_t)t) % Q), u0 + (uint32_t)t + Q);
-                uint4 nd[MT];
-                acl_walk_blocks_mt<MODE, L::IMGB, MT, KL>(a.img, geo, key, need, nd);
-                constexpr bool RPF = PPE_REC_PF && MODE == IMG_SPLIT;
-                uint4 rnext = make_uint4(0u, 0u, 0u, 0u);
-                if (RPF && geo.off_crec) rnext = crec_load<L::IMGB>(a.img, geo, nd[0].z);
-#pragma unroll
-                for (int t = 0; t < MT; ++t) {
-                    uint4 rcur = rnext;
-                    if (RPF && geo.off_crec && t + 1 < MT) rnext = crec_load<L::IMGB>(a.img, geo, nd[t + 1].z);
-                    if (!tv[t]) continue;
-                    if (tbi[t] != curB) {
-                        B = bdesc(tbi[t]);
-                        curB = tbi[t];
-                    }
-                    const uint32_t tile = tti[t], p = (tile << 6) + lane;
-                    if (!got[t]) {  // (queue timeout: the tile's packets are reported, not classified)
-                        if (p < B.n && B.verdict) B.verdict[p] = 0xffffffffu;
-                        continue;
-                    }
-                    Dec k;
-                    k.sip = key[t][0];
-                    k.dip = key[t][1];
-                    k.sport = key[t][2] & 0xffffu;
-                    k.dport = key[t][2] >> 16;
-                    k.st = key[t][3] & 0xffu;
-                    k.flags = (key[t][3] >> 8) & 0xffu;
-                    k.proto = key[t][3] >> 16;
-                    k.paylen = kpay[t];
-                    k.tcpopt = kopt[t];
-                    int32_t hit = -1;
-                    if (need[t]) {
-                        bool drop;
-                        if (RPF && geo.off_crec) {
-                            crec_check<L::IMGB>(a.img, geo, nd[t].z, rcur, k.sip, k.dip, k.sport, k.dport,
-                                                k.proto == 6u, hit, drop);
-                        } else if (geo.off_crec) {
-                            acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, k.sip, k.dip, k.sport, k.dport,
-                                                      k.proto == 6u, hit, drop);
-                        } else {
-                            uint32_t rule_act;
-                            const MacFromWindow mac = {B.hdr, p, B.stride};
-                            acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], k.sip, k.dip, k.sport, k.dport, k.proto, mac,
-                                                    B.ts, p, a.now, hit, rule_act);
-                            drop = rule_act == ACL_RULE_ACTION_DROP;
-                        }
-                        k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
-                        k.flags |= PPE_F_ACL;
-                    }
-                    finish(tile, p, p < B.n, k, kfh[t], hit, false);
-                }
-            }
+            need[t] = d.st == ST_ACL;
+            key[t][0] = d.sip;
+            key[t][1] = d.dip;
+            key[t][2] = d.sport | (d.dport << 16);
+            key[t][3] = d.st | (d.flags << 8) | (d.proto << 16);
+            kpay[t] = d.paylen;
+            kopt[t] = d.tcpopt;
         }
-        if (PPE_PC_STATS && lane == 0 && a.trace) {
-            const uint32_t r = wv < PPE_PC_PROD ? 0u : 4u;
-            atomicAdd(&a.trace[r + 0], (unsigned long long)polls);
-            atomicAdd(&a.trace[r + 1], (unsigned long long)tiles_done);
-            atomicAdd(&a.trace[r + 2], 1ull);
+    };
+    // a multi-tile round's tile t after the walk: hash, verdict, stores, compaction, counters
+    auto mt_finish = [&](uint32_t tile, const uint32_t (&key)[4], uint32_t kpay, uint32_t kopt, bool need, int32_t hit,
+                         bool drop) {
+        const uint32_t p = (tile << 6) + lane;
+        Dec k;
+        k.sip = key[0];
+        k.dip = key[1];
+        k.sport = key[2] & 0xffffu;
+        k.dport = key[2] >> 16;
+        k.st = key[3] & 0xffu;
+        k.flags = (key[3] >> 8) & 0xffu;
+        k.proto = key[3] >> 16;
+        k.paylen = kpay;
+        k.tcpopt = kopt;
+        const uint32_t fh = (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4))
+                                ? flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport) : 0u;
+        if (need) {
+            k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
+            k.flags |= PPE_F_ACL;
         }
-    } else if constexpr (MT > 1 && MT_PIPE) {
-        // PF_MULTI, pipelined: wave w takes rounds of MT tiles [MT w, MT w + MT), then + MT W, ... of its group's
-        // batches; round r + 1's windows are requested during round r (PPE_MT_PF above)
-        constexpr bool PF_EARLY = MODE == IMG_LDS;  // request before the walk (no global loads in walk / records)
+        finish(tile, p, p < B.n, k, fh, need ? hit : -1, false);
+    };
+    // a leaf's rule check (non-compact images: leaf lists / residual fields, rare)
+    auto mt_leaf = [&](uint32_t tile, const uint32_t (&key)[4], const uint4 &nd, int32_t &hit, bool &drop) {
+        uint32_t rule_act;
+        const uint32_t p = (tile << 6) + lane;
+        const MacFromWindow mac = {B.hdr, p, B.stride};
+        acl_leaf<MODE, L::IMGB>(a.img, geo, nd, key[0], key[1], key[2] & 0xffffu, key[2] >> 16, key[3] >> 16, mac,
+                                B.ts, p, a.now, hit, rule_act);
+        drop = rule_act == ACL_RULE_ACTION_DROP;
+    };
+
+    if constexpr (MT > 1 && MT_PIPE) {
+        // PF_MULTI over a whole-LDS image, pipelined: wave w takes rounds of MT tiles [MT w, MT w + MT), then + MT W,
+        // ... of its group's batches; round r + 1's windows are requested during round r, before its walk
         uint4 r0[MT], r1[MT], r2[MT];
         uint32_t r3[MT], rl[MT];
         auto load_round = [&](const uint8_t *hdr, const uint32_t *lenp, uint32_t n, uint32_t stride, uint32_t t0) {
@@ -1888,11 +1471,11 @@ void ppe_classify_kernel(ppe_kargs a) {
             for (int t = 0; t < MT; ++t) {
                 const uint32_t pc = min(((t0 + t) << 6) + lane, n - 1u);
                 const uint32_t ro = pc * stride;
-                r0[t] = gld_win<uint4>(hdr, ro);
-                r1[t] = gld_win<uint4>(hdr, ro + 16u);
-                r2[t] = gld_win<uint4>(hdr, ro + 32u);
-                r3[t] = gld_win<uint32_t>(hdr, ro + 48u);
-                rl[t] = gld_win<uint32_t>(lenp, 4u * pc);
+                r0[t] = gld<uint4>(hdr, ro);
+                r1[t] = gld<uint4>(hdr, ro + 16u);
+                r2[t] = gld<uint4>(hdr, ro + 32u);
+                r3[t] = gld<uint32_t>(hdr, ro + 48u);
+                rl[t] = gld<uint32_t>(lenp, 4u * pc);
             }
         };
         const uint32_t t_first = wtile * MT, t_step = stride_waves * MT;
@@ -1907,29 +1490,9 @@ void ppe_classify_kernel(ppe_kargs a) {
         if (live) load_round(B.hdr, B.len, B.n, B.stride, t0);
         while (live) {
             const uint32_t ntiles = (B.n + 63u) >> 6;
-            // decode: the packed key (sip, dip, ports, meta = status | flags << 8 | proto << 16) and, for the tuple
-            // output only, payload length and TCP option word
             uint32_t key[MT][4], kpay[MT], kopt[MT];
             bool need[MT];
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                const uint32_t p = ((t0 + t) << 6) + lane;
-                if (p < B.n) rx_bytes += rl[t];
-                const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
-                                        r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
-                Dec d = decode<!PART>(w, rl[t], B.hdr, p, B.stride, a.syn_check);
-                if ((PPE_ABLATE & 1) && d.st == ST_ACL) {
-                    d.st = PPE_ST_ACL_FW;
-                    d.flags |= PPE_F_ACL;
-                }
-                need[t] = d.st == ST_ACL;
-                key[t][0] = d.sip;
-                key[t][1] = d.dip;
-                key[t][2] = d.sport | (d.dport << 16);
-                key[t][3] = d.st | (d.flags << 8) | (d.proto << 16);
-                kpay[t] = d.paylen;
-                kopt[t] = d.tcpopt;
-            }
+            mt_decode(t0, r0, r1, r2, r3, rl, key, kpay, kopt, need);
             // the next round (scalar): this batch's next tiles, else the group's next batch with a tile for this wave
             uint32_t nbi = bi, nt0 = t0 + t_step;
             const uint8_t *nh = B.hdr;
@@ -1952,9 +1515,9 @@ void ppe_classify_kernel(ppe_kargs a) {
                     }
                 }
             }
-            if (PF_EARLY && nlive) load_round(nh, nl, nn, ns, nt0);
+            if (nlive) load_round(nh, nl, nn, ns, nt0);
             uint4 nd[MT];
-            acl_walk_blocks_mt<MODE, L::IMGB, MT, KL>(a.img, geo, key, need, nd);
+            acl_walk_blocks_mt<MODE, L::IMGB, MT>(a.img, geo, key, need, nd);
             int32_t hit[MT];
             bool drop[MT];
 #pragma unroll
@@ -1962,44 +1525,17 @@ void ppe_classify_kernel(ppe_kargs a) {
                 hit[t] = -1;
                 drop[t] = false;
                 if (need[t]) {
-                    const uint32_t sip = key[t][0], dip = key[t][1], sport = key[t][2] & 0xffffu,
-                                   dport = key[t][2] >> 16, proto = key[t][3] >> 16;
-                    if (geo.off_crec) {
-                        acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, sip, dip, sport, dport, proto == 6u, hit[t],
-                                                  drop[t]);
-                    } else {
-                        uint32_t rule_act;
-                        const uint32_t p = ((t0 + t) << 6) + lane;
-                        const MacFromWindow mac = {B.hdr, p, B.stride};
-                        acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], sip, dip, sport, dport, proto, mac, B.ts, p, a.now,
-                                                hit[t], rule_act);
-                        drop[t] = rule_act == ACL_RULE_ACTION_DROP;
-                    }
+                    if (geo.off_crec)
+                        acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, key[t][0], key[t][1], key[t][2] & 0xffffu,
+                                                  key[t][2] >> 16, (key[t][3] >> 16) == 6u, hit[t], drop[t]);
+                    else
+                        mt_leaf(t0 + t, key[t], nd[t], hit[t], drop[t]);
                 }
             }
-            if (!PF_EARLY && nlive) load_round(nh, nl, nn, ns, nt0);
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
-                const uint32_t tile = t0 + t;
-                if (tile >= ntiles) break;  // wave-uniform
-                const uint32_t p = (tile << 6) + lane;
-                Dec k;
-                k.sip = key[t][0];
-                k.dip = key[t][1];
-                k.sport = key[t][2] & 0xffffu;
-                k.dport = key[t][2] >> 16;
-                k.st = key[t][3] & 0xffu;
-                k.flags = (key[t][3] >> 8) & 0xffu;
-                k.proto = key[t][3] >> 16;
-                k.paylen = kpay[t];
-                k.tcpopt = kopt[t];
-                const uint32_t fh = (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4))
-                                        ? flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport) : 0u;
-                if (need[t]) {
-                    k.st = drop[t] ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
-                    k.flags |= PPE_F_ACL;
-                }
-                finish(tile, p, p < B.n, k, fh, hit[t], false);
+                if (t0 + t >= ntiles) break;  // wave-uniform
+                mt_finish(t0 + t, key[t], kpay[t], kopt[t], need[t], hit[t], drop[t]);
             }
             if (nlive && nbi != bi) B = bdesc(nbi);
             bi = nbi;
@@ -2008,71 +1544,31 @@ void ppe_classify_kernel(ppe_kargs a) {
         }
     } else if constexpr (MT > 1) {
         // PF_MULTI: wave w takes tiles [MT w, MT w + MT), then + MT W, ...; all MT windows are requested together
-        uint32_t rnd = 0;
-        auto mt_stamp = [&](uint32_t j) {
-            if (PPE_MTTRACE && lane == 0 && a.trace && rnd - PPE_MTTRACE_SKIP < 5u)
-                a.trace[(size_t)twave * 32u + 1u + 4u * (rnd - PPE_MTTRACE_SKIP) + j] = __builtin_amdgcn_s_memrealtime();
-        };
         for (uint32_t bi = grp; wave_live && bi < a.nbatch; bi += ngroups) {
             if (bi != grp) B = bdesc(bi);
             const uint32_t ntiles = (B.n + 63u) >> 6;
-            for (uint32_t t0 = wtile * MT; t0 < ntiles; t0 += stride_waves * MT, ++rnd) {
-                mt_stamp(0);
+            for (uint32_t t0 = wtile * MT; t0 < ntiles; t0 += stride_waves * MT) {
                 uint4 r0[MT], r1[MT], r2[MT];
                 uint32_t r3[MT], rl[MT];
 #pragma unroll
                 for (int t = 0; t < MT; ++t) {
                     const uint32_t pc = min(((t0 + t) << 6) + lane, B.n - 1u);
                     const uint32_t ro = pc * B.stride;
-                    r0[t] = gld_win<uint4>(B.hdr, ro);
-                    r1[t] = gld_win<uint4>(B.hdr, ro + 16u);
-                    r2[t] = gld_win<uint4>(B.hdr, ro + 32u);
-                    r3[t] = gld_win<uint32_t>(B.hdr, ro + 48u);
-                    rl[t] = gld_win<uint32_t>(B.len, 4u * pc);
+                    r0[t] = gld<uint4>(B.hdr, ro);
+                    r1[t] = gld<uint4>(B.hdr, ro + 16u);
+                    r2[t] = gld<uint4>(B.hdr, ro + 32u);
+                    r3[t] = gld<uint32_t>(B.hdr, ro + 48u);
+                    rl[t] = gld<uint32_t>(B.len, 4u * pc);
                 }
-                // per tile through the walk: the packed key (sip, dip, ports, meta = status | flags << 8 | proto
-                // << 16) and, for the tuple output only, payload length and TCP option word; the flow hash is
-                // computed after the walk (fewer live registers while the block reads are in flight)
                 uint32_t key[MT][4], kpay[MT], kopt[MT];
                 bool need[MT];
-#pragma unroll
-                for (int t = 0; t < MT; ++t) {
-                    const uint32_t p = ((t0 + t) << 6) + lane;
-                    const bool valid = p < B.n;
-                    if (valid) rx_bytes += rl[t];
-                    const uint32_t w[13] = {r0[t].x, r0[t].y, r0[t].z, r0[t].w, r1[t].x, r1[t].y, r1[t].z, r1[t].w,
-                                            r2[t].x, r2[t].y, r2[t].z, r2[t].w, r3[t]};
-                    Dec d = decode<!PART>(w, rl[t], B.hdr, p, B.stride, a.syn_check);
-                    if ((PPE_ABLATE & 1) && d.st == ST_ACL) {
-                        d.st = PPE_ST_ACL_FW;
-                        d.flags |= PPE_F_ACL;
-                    }
-                    need[t] = d.st == ST_ACL;
-                    key[t][0] = d.sip;
-                    key[t][1] = d.dip;
-                    key[t][2] = d.sport | (d.dport << 16);
-                    key[t][3] = d.st | (d.flags << 8) | (d.proto << 16);
-                    kpay[t] = d.paylen;
-                    kopt[t] = d.tcpopt;
-                }
-                if (PPE_MTTRACE) {
-                    asm volatile("" ::"v"(key[0][3]), "v"(key[MT - 1][3]));
-                    mt_stamp(1);
-                }
+                mt_decode(t0, r0, r1, r2, r3, rl, key, kpay, kopt, need);
                 uint4 nd[MT];
-                uint4 rec[MT];
-                if (PPE_REC_IN_WALK && geo.off_crec)
-                    acl_walk_blocks_mt<MODE, L::IMGB, MT, KL, true>(a.img, geo, key, need, nd, rec);
-                else
-                    acl_walk_blocks_mt<MODE, L::IMGB, MT, KL>(a.img, geo, key, need, nd);
-                // PPE_REC_PF (split compact images): tile t + 1's record is requested, by every lane (a lane with no
-                // leaf reads slot 0), before tile t's check, so the L2 round trips of the round's records overlap
-                // the tiles' finish work instead of one after another
-                if (PPE_MTTRACE) {
-                    asm volatile("" ::"v"(nd[0].z), "v"(nd[MT - 1].z));
-                    mt_stamp(2);
-                }
-                constexpr bool RPF = PPE_REC_PF && MODE == IMG_SPLIT && !PPE_REC_IN_WALK;
+                acl_walk_blocks_mt<MODE, L::IMGB, MT>(a.img, geo, key, need, nd);
+                // split compact images: tile t + 1's record is requested, by every lane (a lane with no leaf reads
+                // slot 0), before tile t's check, so the L2 round trips of the round's records overlap the tiles'
+                // finish work instead of one after another (C3 ring step -0.8 %, r4t)
+                constexpr bool RPF = MODE == IMG_SPLIT;
                 uint4 rnext = make_uint4(0u, 0u, 0u, 0u);
                 if (RPF && geo.off_crec) rnext = crec_load<L::IMGB>(a.img, geo, nd[0].z);
 #pragma unroll
@@ -2081,46 +1577,20 @@ void ppe_classify_kernel(ppe_kargs a) {
                     if (tile >= ntiles) break;  // wave-uniform
                     uint4 rcur = rnext;
                     if (RPF && geo.off_crec && t + 1 < MT) rnext = crec_load<L::IMGB>(a.img, geo, nd[t + 1].z);
-                    const uint32_t p = (tile << 6) + lane;
-                    Dec k;
-                    k.sip = key[t][0];
-                    k.dip = key[t][1];
-                    k.sport = key[t][2] & 0xffffu;
-                    k.dport = key[t][2] >> 16;
-                    k.st = key[t][3] & 0xffu;
-                    k.flags = (key[t][3] >> 8) & 0xffu;
-                    k.proto = key[t][3] >> 16;
-                    k.paylen = kpay[t];
-                    k.tcpopt = kopt[t];
-                    const uint32_t fh = (!(PPE_ABLATE & 8) && (k.flags & PPE_F_L4))
-                                            ? flow_hashfn_l4(k.proto == 6u, k.sip, k.dip, k.sport, k.dport) : 0u;
                     int32_t hit = -1;
+                    bool drop = false;
                     if (need[t]) {
-                        bool drop;
-                        if (PPE_REC_IN_WALK && geo.off_crec) {
-                            crec_check<L::IMGB>(a.img, geo, nd[t].z, rec[t], k.sip, k.dip, k.sport, k.dport,
-                                                k.proto == 6u, hit, drop);
-                        } else if (RPF && geo.off_crec) {
-                            crec_check<L::IMGB>(a.img, geo, nd[t].z, rcur, k.sip, k.dip, k.sport, k.dport,
-                                                k.proto == 6u, hit, drop);
-                        } else if (geo.off_crec) {
-                            acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, k.sip, k.dip, k.sport, k.dport,
-                                                      k.proto == 6u, hit, drop);
-                        } else {
-                            uint32_t rule_act;
-                            const MacFromWindow mac = {B.hdr, p, B.stride};
-                            acl_leaf<MODE, L::IMGB>(a.img, geo, nd[t], k.sip, k.dip, k.sport, k.dport, k.proto, mac,
-                                                    B.ts, p, a.now, hit, rule_act);
-                            drop = rule_act == ACL_RULE_ACTION_DROP;
-                        }
-                        k.st = drop ? (uint32_t)PPE_ST_ACL_DROP : (uint32_t)PPE_ST_ACL_FW;
-                        k.flags |= PPE_F_ACL;
+                        const uint32_t sip = key[t][0], dip = key[t][1], sport = key[t][2] & 0xffffu,
+                                       dport = key[t][2] >> 16;
+                        const bool tcp = (key[t][3] >> 16) == 6u;
+                        if (RPF && geo.off_crec)
+                            crec_check<L::IMGB>(a.img, geo, nd[t].z, rcur, sip, dip, sport, dport, tcp, hit, drop);
+                        else if (geo.off_crec)
+                            acl_leaf_compact<L::IMGB>(a.img, geo, nd[t].z, sip, dip, sport, dport, tcp, hit, drop);
+                        else
+                            mt_leaf(tile, key[t], nd[t], hit, drop);
                     }
-                    finish(tile, p, p < B.n, k, fh, hit, false);
-                }
-                if (PPE_MTTRACE) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    mt_stamp(3);
+                    mt_finish(tile, key[t], kpay[t], kopt[t], need[t], hit, drop);
                 }
             }
         }
@@ -2129,31 +1599,13 @@ void ppe_classify_kernel(ppe_kargs a) {
         if (bi != grp) B = bdesc(bi);
         const uint32_t ntiles = (B.n + 63u) >> 6;
         for (uint32_t tile = wtile; tile < ntiles; tile += stride_waves) {
-            if (PPE_TRACE && titer - PPE_TRACE_SKIP < 4u) TRACE_AT(2 + 5 * (titer - PPE_TRACE_SKIP));
             if (!have) load_tile(tile);
             have = false;
-            if constexpr (PPE_PREFETCH && MODE == IMG_LDS && !FLOW) {
-                // experiment: the next tile's window is requested before this tile is processed (one more window of
-                // registers; the LDS-image walk issues no global loads, so nothing waits on the prefetch)
-                const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
-                const uint32_t wl = qlen;
-                const uint32_t nt = tile + stride_waves;
-                if (nt < ntiles) {
-                    load_tile(nt);
-                    have = true;
-                }
-                process(tile, w, wl);
-                continue;
-            }
-            if (PPE_TRACE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (PPE_TRACE && titer - PPE_TRACE_SKIP < 4u) TRACE_AT(3 + 5 * (titer - PPE_TRACE_SKIP));
             const uint32_t w[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, w12};
             process(tile, w, qlen);
         }
     }
 
-    TRACE_AT(22);
-    if (PPE_TRACE && lane == 0 && a.trace) a.trace[(size_t)twave * 32u + 31u] = titer;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) rx_bytes += __shfl_xor(rx_bytes, o, 64);
     if (lane == 0 && rx_bytes)
@@ -2183,8 +1635,6 @@ void ppe_classify_kernel(ppe_kargs a) {
     if (tid < PPE_C__COUNT && lcnt[tid])
         __hip_atomic_fetch_add(&a.cslots[(size_t)blockIdx.x * PPE_CSLOT_WORDS + tid], (unsigned long long)lcnt[tid],
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (PPE_TRACE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    TRACE_AT(23);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -2440,10 +1890,6 @@ __device__ __forceinline__ void flow_finalize_wg(const ppe_flow_kargs &a, uint32
 // batch, never a found flow's), the fold into the wide counters, the last-seen time.  One update per flow and
 // direction instead of one memory-side atomic and one last-seen store per packet.  A slot the full hash cannot take
 // is updated by the atomic path directly.
-// PPE_UPD_AB (diagnostic builds only, wrong outputs): 1 = no apply phase, 2 = no gather phase either
-#ifndef PPE_UPD_AB
-#define PPE_UPD_AB 0
-#endif
 // (owner o's workgroup of the post-classify launch, ppe_flow_post_kernel; usm: its PPE_UPD_HASH * 28 B of LDS)
 template <int BLOCK>
 __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t o, uint32_t *usm) {
@@ -2475,7 +1921,7 @@ __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t
         }
         f.packed[(size_t)PPE_FLOW_REC_WORDS * s + PPE_FLOW_REC_LAST] = a.now;
     };
-    const uint32_t ncol = (PPE_UPD_AB & 2) ? 0u : min(f.upd_grid, f.upd_wgs);
+    const uint32_t ncol = min(f.upd_grid, f.upd_wgs);
     for (uint32_t w = tid; w < ncol; w += BLOCK) {
         const uint32_t n = min(f.ucnt[(size_t)w * f.upd_owners + o], PPE_UPD_CAP);
         // the bucket is one 64-B (4-B entries) or 128-B segment: every entry's load issued before any is used
@@ -2520,7 +1966,6 @@ __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t
         }
     }
     __syncthreads();
-    if (PPE_UPD_AB) return;
     // each touched slot once: both directions' packed words in one 16-B read-modify-write, then the last-seen time
     constexpr uint32_t PER = HC / BLOCK;
     uint32_t ks[PER];
@@ -2552,8 +1997,8 @@ __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t
         }
         // the whole 32-B record: both directions, the last-seen time (one line per flow)
         ulonglong2 *rp = (ulonglong2 *)(f.packed + (size_t)PPE_FLOW_REC_WORDS * s);
-        upd_st(rp, make_ulonglong2(nw[0], nw[1]));
-        upd_st(rp + 1, make_ulonglong2((unsigned long long)a.now, 0ull));
+        rp[0] = make_ulonglong2(nw[0], nw[1]);
+        rp[1] = make_ulonglong2((unsigned long long)a.now, 0ull);
     }
 }
 
@@ -2800,10 +2245,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block, 
     do {                                                             \
         if (pipe == PF_NONE) PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__); \
         if (pipe == PF_MULTI) PPE_DISPATCH_B(FN, M, PF_MULTI, __VA_ARGS__); \
-        if (pipe == PF_SBLK) return FN<M, PF_SBLK, 1024>(__VA_ARGS__);   \
-        if (pipe == PF_MULTI3) return FN<M, PF_MULTI3, 1024>(__VA_ARGS__); \
-        if (pipe == PF_SBLK3) return FN<M, PF_SBLK3, 1024>(__VA_ARGS__);   \
-        if (pipe == PF_PC) return FN<M, PF_PC, 1024>(__VA_ARGS__);         \
+        if (pipe == PF_CUT) PPE_DISPATCH_B(FN, (M == IMG_SPLIT ? IMG_GLOBAL : M), PF_CUT, __VA_ARGS__); \
         PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__);                \
     } while (0)
 #define PPE_DISPATCH(FN, ...)                                        \
@@ -2856,15 +2298,11 @@ extern "C" uint32_t ppe_flow_lds_extra() {
 extern "C" uint32_t ppe_flow_waves() { return PPE_FLOW_WAVES; }
 
 // LDS of a workgroup besides the staged image: the per-wave key slots of node walks and the counter bins.  Block
-// walks (the multi-tile kernel; the single-tile kernel over a whole-LDS image) keep the keys in registers.
+// and cut-list walks keep the keys in registers.
 extern "C" uint32_t ppe_classify_fixed_lds(int block, int pipe, int mode) {
-    const bool blocks = pipe == PF_MULTI || pipe == PF_SBLK || pipe == PF_MULTI3 || pipe == PF_SBLK3 ||
-                        pipe == PF_PC || (PPE_ST_BLOCKS && mode == IMG_LDS);
-    return (blocks ? 0u : (uint32_t)(block / 64) * KEY_WAVE_BYTES) + PPE_LDS_FIXED + (pipe == PF_PC ? PC_QBYTES : 0u);
+    const bool regkeys = pipe == PF_MULTI || pipe == PF_CUT;
+    return (regkeys ? 0u : (uint32_t)(block / 64) * KEY_WAVE_BYTES) + PPE_LDS_FIXED;
 }
-
-// 1: the single-tile kernel walks the block section of a whole-LDS image (the engine stages the whole image)
-extern "C" int ppe_classify_st_blocks(void) { return PPE_ST_BLOCKS; }
 
 extern "C" int ppe_launch_steer(int phase, const ppe_steer_kargs *a, uint32_t grid, void *stream) {
     const hipStream_t s = (hipStream_t)stream;

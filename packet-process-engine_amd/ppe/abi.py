@@ -65,7 +65,8 @@ class Cfg(C.Structure):
 class AclStats(C.Structure):
     _fields_ = [("n_rules", C.c_uint32), ("n_nodes", C.c_uint32), ("n_leaves", C.c_uint32),
                 ("n_leaf_entries", C.c_uint32), ("max_depth", C.c_uint32), ("avg_depth", C.c_double),
-                ("blob_bytes", C.c_uint32), ("lds_resident", C.c_uint32), ("build_ms", C.c_double)]
+                ("blob_bytes", C.c_uint32), ("lds_resident", C.c_uint32), ("build_ms", C.c_double),
+                ("cut_bits", C.c_uint32), ("cut_entries", C.c_uint32)]  # ABI version 6
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -183,7 +184,7 @@ EXPORTS = [
     "ppe_classify_batches", "ppe_classify_host", "ppe_acl_lookup", "ppe_acl_lookup_host", "ppe_dev_alloc", "ppe_dev_free",
     "ppe_host_alloc", "ppe_host_free", "ppe_memcpy_h2d", "ppe_memcpy_d2h", "ppe_memset_d", "ppe_sync",
     "ppe_counters_read", "ppe_counters_clear", "ppe_timing_enable", "ppe_timing_read", "ppe_acl_image",
-    "ppe_launch_info", "ppe_debug_trace", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
+    "ppe_launch_info", "ppe_last_error", "ppe_acl_build_image", "ppe_acl_free_image", "ppe_set_tuning",
     "ppe_get_tuning", "ppe_flow_create", "ppe_flow_destroy", "ppe_classify_flow", "ppe_flow_age", "ppe_flow_info",
     "ppe_flow_clear_stat", "ppe_flow_dump", "ppe_format_pkt_stat", "ppe_format_flow_stat",
     "ppe_format_pkt_stat_ex", "ppe_format_flow_stat_ex",
@@ -204,7 +205,7 @@ EXPORTED_DATA = ["rule_list", "dp_acl_action_default", "gWstDepth", "gAvgDepth",
 _lib = None
 
 
-ABI_VERSION = 5  # include/ppe_hip.h PPE_ABI_VERSION
+ABI_VERSION = 6  # include/ppe_hip.h PPE_ABI_VERSION
 
 
 def load(path: str | os.PathLike | None = None) -> C.CDLL:
@@ -256,7 +257,6 @@ def _open(p: Path, mode, strict: bool = True) -> C.CDLL:
         "ppe_timing_read": ([vp, C.POINTER(C.c_double), C.POINTER(u32), C.c_int], C.c_int),
         "ppe_acl_image": ([vp, vp, C.POINTER(u32)], C.c_int),
         "ppe_launch_info": ([vp, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)], C.c_int),
-        "ppe_debug_trace": ([vp, vp], C.c_int),
         "ppe_last_error": ([vp], C.c_char_p),
         "ppe_set_tuning": ([vp, C.POINTER(Tuning)], C.c_int),
         "ppe_get_tuning": ([vp, C.POINTER(Tuning)], C.c_int),

@@ -209,7 +209,7 @@ class Engine:
         self._check(self.lib.ppe_launch_info(self.ctx, C.byref(g), C.byref(b), C.byref(l), C.byref(v)),
                     "ppe_launch_info")
         return {"grid": g.value, "block": b.value, "lds_bytes": l.value,
-                "image": ("global", "lds", "split")[v.value & 15], "fetch": {0: "none", 1: "hoist", 3: "multi", 5: "sblk", 6: "multi3", 7: "sblk3", 8: "pc"}.get(v.value >> 4, f"v{v.value >> 4}")}
+                "image": ("global", "lds", "split")[v.value & 15], "fetch": {0: "none", 1: "hoist", 3: "multi", 5: "cut"}.get(v.value >> 4, f"v{v.value >> 4}")}
 
     def sync(self):
         self._check(self.lib.ppe_sync(self.ctx), "ppe_sync")

@@ -25,7 +25,7 @@ def header_functions():
 
 def test_library_loads():
     lib = abi.load()
-    assert lib.ppe_abi_version() == abi.ABI_VERSION == 5
+    assert lib.ppe_abi_version() == abi.ABI_VERSION == 6
 
 
 def test_every_declared_function_is_exported():
@@ -63,6 +63,7 @@ def test_struct_layouts():
     assert C.sizeof(abi.Cfg) == 16
     assert C.sizeof(abi.Tuning) == 20  # batches_per_launch (ABI version 2)
     assert C.sizeof(abi.Counters) == 256
+    assert C.sizeof(abi.AclStats) == 56  # cut_bits / cut_entries (ABI version 6)
 
 
 # LP64 offsets of the reference's mbuf_t (dataplane/src/include/mbuf.h:23-87, with cvmx_buf_ptr_t a 64-bit word and

@@ -16,11 +16,14 @@ def compare(rules, used, pk, default_action=1, binth=0, cfg=None):
     cfg = cfg or o.cfg(0, 1, NOW)
     lin = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4)
     tree = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4, use_tree=True)
-    # the image's 2-level block section (what the multi-tile kernel walks) must give the same answers
+    # the image's 2-level block section (what the multi-tile kernel walks) must give the same answers, and so must its
+    # cut lists (image v7: what the cut-list kernel reads) when it has them
     blocks = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4, use_tree=2)
+    cut = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4, use_tree=3) if img[22] else lin
     for k in ("verdict", "acl_hit", "flow_hash", "counters"):
         assert np.array_equal(lin[k], tree[k]), k
         assert np.array_equal(lin[k], blocks[k]), k
+        assert np.array_equal(lin[k], cut[k]), k
     return img, st, lin
 
 
@@ -96,13 +99,14 @@ def test_large_ruleset_builds_bounded():
 
 
 def test_image_layout():
-    """Image format v6 (csrc/ppe_image.h): optional jump table after the 32-word header, 16-B nodes {threshold, left,
+    """Image format v7 (csrc/ppe_image.h): optional jump table after the 32-word header, 16-B nodes {threshold, left,
     right, child key slots}, leaves as walk fixed points, the always-matching sentinel rule at slot n_rules, the
-    2-level block section, and the compact records after it (one candidate per leaf, no residual rules)."""
+    2-level block section, the compact records after it (one candidate per leaf, no residual rules), then the cut
+    lists (32-B aligned header, groups, entries)."""
     for nrules in (64, 256):
         rules = synth.make_rules(nrules)
         img, st = abi.build_image(rules)
-        assert img[0] == 0x41455050 and img[1] == 6
+        assert img[0] == 0x41455050 and img[1] == 7
         assert img[2] == st["n_nodes"] and img[4] == nrules and img[11] == len(img)
         assert img[7] % 8 == 0  # rules 32-B aligned
         off = int(img[5])
@@ -142,7 +146,10 @@ def test_image_layout():
         # every non-leaf exit names a later block, every block but the roots is named exactly once
         ob, nb, oblk = int(img[15]), int(img[16]), int(img[17])
         oc, oi = int(img[19]), int(img[20])
-        assert oc == oblk + 8 * nb and oi == 0 and oc + 4 * (nrules + 1) == len(img)  # compact, no holes
+        oct_ = int(img[22])
+        assert oc == oblk + 8 * nb and oi == 0 and oct_ == (oc + 4 * (nrules + 1) + 7) // 8 * 8  # compact, no holes
+        h = cut_header(img)
+        assert h["grp"] == oct_ + 8 and h["ent"] % 8 == 0 and h["ent"] + 8 * h["entries"] == len(img)
         assert ob >= int(img[8]) and ob % 8 == 0 and oblk % 8 == 0
         if jw:
             assert np.array_equal(img[ob:ob + (1 << bits)].astype(np.int64), (roots - 4 * off) // 16)
@@ -154,7 +161,7 @@ def test_image_layout():
         slot = leaf_ex & 0xFFFFFF
         assert (slot <= nrules).all()
         assert (((leaf_ex >> 29) & 1) == (slot == nrules)).all()  # NOHIT exactly on the sentinel
-        crec = img[oc:].reshape(nrules + 1, 4)
+        crec = img[oc:oc + 4 * (nrules + 1)].reshape(nrules + 1, 4)
         assert np.array_equal(crec[nrules], [0x80000000, 0x80000000, 0, 0xFFFFFFFF])
 
 
@@ -230,18 +237,15 @@ def test_compact_leaves_edge_cases(monkeypatch, compact):
         assert len(np.unique(pr[hit])) >= 4 and (r["sip_mask"][hit] == 32).any() and (r["sip_mask"][hit] == 0).any()
 
 
-@pytest.mark.parametrize("levels", ["2", "3"])
 @pytest.mark.parametrize("nrules,resid,binth", [(256, 0.0, 1), (2048, 0.0, 1), (300, 0.3, 1), (1024, 0.0, 4)])
-def test_block_levels_equal_linear(monkeypatch, levels, nrules, resid, binth):
-    """2- and 3-level blocks (image word 21; 64-B blocks of 7 thresholds, their key slots and 8 exits) walk to the
-    same leaves as the node tree: compact leaves, leaf lists (binth 4) and residual rules, jump root on."""
-    monkeypatch.setenv("PPE_BLOCK_LEVELS", levels)
+def test_blocks_equal_linear(nrules, resid, binth):
+    """The 2-level blocks (image word 21) walk to the same leaves as the node tree: compact leaves, leaf lists
+    (binth 4) and residual rules, jump root on."""
     rules = synth.make_rules(nrules, seed=nrules + 7, resid_frac=resid, any_ip_frac=0.1)
     pk = synth.make_packets(6000, rules, seed=12, kind="imix", stride=128, malformed_frac=0.02, with_ts=True)
     img, st, lin = compare(rules, None, pk, binth=binth)
-    assert int(img[21]) == int(levels)
-    bw = 8 if levels == "2" else 16
-    assert int(img[17]) % bw == 0 and (lin["acl_hit"] >= 0).sum() > 500
+    assert int(img[21]) == 2
+    assert int(img[17]) % 8 == 0 and (lin["acl_hit"] >= 0).sum() > 500
 
 
 def test_default_block_levels_and_lds_fit():
@@ -249,4 +253,78 @@ def test_default_block_levels_and_lds_fit():
     records (4,096 rules) fits a 1024-thread workgroup's LDS whole."""
     img2, _ = abi.build_image(synth.make_rules(4096))
     assert int(img2[21]) == 2
-    assert (len(img2) - int(img2[15])) * 4 <= 158 * 1024
+    assert (int(img2[22]) - int(img2[15])) * 4 <= 158 * 1024  # the block section and records end where the cut starts
+
+
+def cut_header(img):
+    h = int(img[22])
+    return dict(b0=int(img[h]) & 0xFF, b1=(int(img[h]) >> 8) & 0xFF, buckets=int(img[h + 1]), entries=int(img[h + 2]),
+                max_len=int(img[h + 3]), grp=int(img[h + 4]), ent=int(img[h + 5]), groups=int(img[h + 6]))
+
+
+@pytest.mark.parametrize("bits", ["0", "1", "4", "8", "11", "16"])
+def test_cut_lists_equal_linear(monkeypatch, bits):
+    """The cut lists (image v7) at every width, forced by PPE_CUT_BITS, against the linear definition: prefix lengths
+    0 / 1 / 7 / 8 / 31 / 32 (rules replicated into the buckets they meet, lists closed after a rule that covers the
+    whole bucket), any-port rules, protocol ranges with and without 6 / 17, actions other than 0 / 1, unused
+    entries, default FW and DROP.  The image's group table encodes each bucket's list exactly."""
+    monkeypatch.setenv("PPE_CUT_BITS", bits)
+    rng = np.random.default_rng(1234 + int(bits))
+    n = {0: 12, 1: 20, 4: 80}.get(int(bits), 700)  # (every list within 15 entries)
+    r = synth.make_rules(n, seed=90 + int(bits))
+    r["sip_mask"] = rng.choice([0, 1, 7, 8, 16, 31, 32], n, p=[0.02, 0.03, 0.1, 0.25, 0.3, 0.15, 0.15])
+    r["dip_mask"] = rng.choice([0, 1, 8, 24, 32], n, p=[0.02, 0.03, 0.35, 0.3, 0.3])
+    anyport = rng.random(n) < 0.3
+    for f in ("sport", "dport"):
+        r[f + "_start"][anyport] = 0
+        r[f + "_end"][anyport] = 65535
+    pr = rng.integers(0, 4, n)
+    r["protocol_start"] = np.choose(pr, [6, 17, 0, 7])
+    r["protocol_end"] = np.choose(pr, [6, 17, 255, 16])
+    r["action"] = rng.choice([0, 1, 2], n)
+    used = (rng.random(n) < 0.9).astype(np.uint8)
+    for da in (0, 1):
+        pk = synth.make_packets(6000, r, seed=91 + da, kind="imix", stride=128, malformed_frac=0.02, hit_frac=0.9)
+        img, st, lin = compare(r, used, pk, default_action=da)
+        assert int(img[22]) != 0, "cut lists expected"
+        h = cut_header(img)
+        assert h["b0"] + h["b1"] == int(bits) and st["cut_bits"] == h["b0"] | h["b1"] << 8
+        assert h["buckets"] == 1 << int(bits) and h["groups"] == max(1, h["buckets"] // 16)
+        # the groups' lengths add up to the entries, each at most 15, and the first-entry words are their prefix sums
+        g = np.asarray(img[h["grp"]:h["grp"] + 4 * h["groups"]], np.uint32).reshape(-1, 4)
+        lens = np.array([(g[b >> 4, 1 + ((b & 15) >> 3)] >> (4 * (b & 7))) & 15 for b in range(h["buckets"])])
+        assert lens.sum() == h["entries"] == st["cut_entries"] and lens.max() == h["max_len"] <= 15
+        assert np.array_equal(g[:, 0], np.concatenate([[0], np.cumsum(lens)])[: h["groups"] * 16 : 16])
+        assert (lin["acl_hit"] >= 0).sum() > 1000
+
+
+def test_cut_lists_rejected_or_absent():
+    """No cut lists for rule sets with MAC / time fields (the classify kernel's cut check has none), and none when
+    every width leaves a bucket with more than 15 candidates (then the kernel walks the tree)."""
+    img, st = abi.build_image(synth.make_rules(300, seed=3, resid_frac=0.3))
+    assert int(img[22]) == 0 and st["cut_entries"] == 0
+    r = synth.make_rules(40, seed=5)
+    r["sip_mask"] = 0
+    r["dip_mask"] = 0  # 40 overlapping wildcard-address rules: every bucket holds all 40
+    r["sport_start"] = np.arange(40) * 100
+    r["sport_end"] = np.arange(40) * 100 + 50
+    img, st = abi.build_image(r)
+    assert int(img[22]) == 0
+    pk = synth.make_packets(3000, r, seed=6, stride=128, hit_frac=0.9)
+    compare(r, None, pk)
+
+
+def test_cut_lists_of_the_bench_rule_sets():
+    """C3's 65,536 rules (every prefix /8 or longer): a 16-bit cut of 8 sip and 8 dip bits, no replication, at most
+    15 entries per bucket; C4's 4,096 rules: 16 bits too.  Both walks equal the linear definition."""
+    for nrules, seed in ((65536, 0x5EED), (4096, 0x5EED)):
+        rules = synth.make_rules(nrules)
+        img, st = abi.build_image(rules)
+        h = cut_header(img)
+        assert (h["b0"], h["b1"]) == (8, 8) and h["entries"] <= nrules and h["max_len"] <= 15, h
+        pk = synth.make_packets(20000, rules, seed=seed + 1, stride=64)
+        o = pyoracle.Oracle(rules, None, default_action=1, image=img)
+        lin = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=8)
+        cut = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=8, use_tree=3)
+        for k in ("verdict", "acl_hit", "counters"):
+            assert np.array_equal(lin[k], cut[k]), k

@@ -98,6 +98,71 @@ def test_rule_store_commit_decode_hooks():
     unhook(lib)
 
 
+def mainloop_no_flush(lib, n=300, seed=95):
+    """A reference-shaped mainloop (dataplane/src/main.c:296-301): Decode(mb) per received packet and nothing else, no
+    Decode_Flush.  Every mbuf must reach exactly one output hook before its Decode returns (decode.c:13-28), with
+    the oracle's verdict."""
+    lib.ppe_set_output_hooks.argtypes = [HOOK, HOOK, HOOK]
+    assert lib.DP_Acl_Rule_Init() == 0
+    lib.ppe_rule_list_free()
+    assert lib.ppe_rule_list_init() == 0
+    rules = synth.make_rules(64, seed=seed)
+    for i in range(len(rules)):
+        rid = C.c_uint32()
+        assert lib.Rule_add(rules[i:i + 1].ctypes.data, C.byref(rid)) == 0
+    assert lib.DP_Acl_Rule_Commit() == 0
+    pk = synth.make_packets(n, rules, seed=seed + 1, kind="imix", stride=128, malformed_frac=0.1)
+    bufs = [C.create_string_buffer(bytes(pk["hdr"][i][: min(int(pk["len"][i]) & 0xFFFF, 128)]), 144) for i in range(n)]
+    mbufs = (Mbuf * n)()
+    for i in range(n):
+        mbufs[i].pkt_ptr = C.cast(bufs[i], C.c_void_p)
+        mbufs[i].pkt_totallen = int(pk["len"][i])
+    base = C.addressof(mbufs)
+    seen = []
+    hooks = [HOOK(lambda m, a=a: seen.append(((C.addressof(m.contents) - base) // C.sizeof(Mbuf), a)))
+             for a in (0, 1, 2)]
+    lib.ppe_set_output_hooks(*hooks)
+    try:
+        for i in range(n):
+            lib.Decode(C.byref(mbufs[i]))
+            assert len(seen) == i + 1 and seen[-1][0] == i, f"mbuf {i} not delivered when Decode returned"
+    finally:
+        lib.ppe_set_output_hooks(HOOK(), HOOK(), HOOK())
+    o = pyoracle.Oracle(rules, default_action=1)
+    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, 0))
+    assert [a for _, a in seen] == ((ref["verdict"] >> 8) & 0xFF).tolist()
+    assert np.array_equal(np.array([mbufs[i].ppe_verdict for i in range(n)], np.uint32), ref["verdict"])
+    lib.ppe_rule_list_free()
+    lib.DP_Acl_Rule_Release()
+
+
+def test_mainloop_without_flush_burst_one():
+    """Decode_Set_Burst(1) (the default) in this process, after earlier tests used bursts."""
+    lib = abi.load()
+    lib.Decode_Set_Burst(1)
+    mainloop_no_flush(lib)
+
+
+def test_mainloop_without_flush_default():
+    """A fresh process that never calls Decode_Set_Burst: the library's default delivers every mbuf before Decode
+    returns (a PPE mainloop linked unchanged sees the reference's completion contract)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    code = ("import sys; sys.path[:0] = [%r, %r, %r]\n"
+            "import torch\n"
+            "from ppe import abi\n"
+            "import test_gpu_compat as t\n"
+            "t.mainloop_no_flush(abi.load())\n"
+            "print('mainloop ok')\n") % (str(root / "packet-process-engine_amd"), str(root / "oracle"),
+                                          str(root / "tests"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ))
+    assert r.returncode == 0 and "mainloop ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
 def unhook(lib):
     """The library keeps the hook pointers: clear them before this test's ctypes thunks are freed."""
     lib.ppe_set_output_hooks(HOOK(), HOOK(), HOOK())

@@ -262,3 +262,30 @@ def test_show_text_after_reassembly(eng):
         assert f"new fcb is: {oi.new_fcb}\n" in texts[0][1]
     finally:
         p.close()
+
+
+def test_failed_admission_lookback_is_reported(eng, monkeypatch):
+    """A workgroup whose admission look-back fails (forced by the PPE_DF_LOOK_FAIL test hook) admits none of its
+    creators and sets a pinned error word: the NEXT ppe_defrag call fails with PPE_EIO (once), ppe_defrag_info
+    too, and the table keeps working afterwards (the failure must not stay silent)."""
+    from ppe.engine import PPEError
+    monkeypatch.setenv("PPE_DF_LOOK_FAIL", "3")
+    g = Defrag(eng, fcb_max=1 << 16)
+    monkeypatch.delenv("PPE_DF_LOOK_FAIL")
+    try:
+        a, off, lens = synth.make_fragment_stream(4000, seed=4242)
+        n = min(len(lens), 8192)   # >= 4 admission workgroups of 256 fragments
+        off, lens = off[:n].copy(), lens[:n].copy()
+        out = g.alloc_out(n, 128)
+        ta = torch.from_numpy(a).to(DEV)
+        to = torch.from_numpy(off.view(np.int64)).to(DEV)
+        tl = torch.from_numpy(lens.view(np.int32)).to(DEV)
+        g.run_torch(ta, to, tl, out, NOW)   # (asynchronous: the failure is on the device)
+        torch.cuda.synchronize()
+        with pytest.raises(PPEError, match="look-back"):
+            g.run_torch(ta, to, tl, out, NOW + 1)
+        with pytest.raises(PPEError):
+            g.info()   # the device counter of failed look-backs (then cleared)
+        g.info()
+    finally:
+        g.close()

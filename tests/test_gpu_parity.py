@@ -295,44 +295,62 @@ def test_c3_64k_rules_vs_oracle(eng):
     # the compiler too, not only the walk: 16,384 packets against the linear first-match definition
     lin = o.classify_batch(pk["hdr"][:16384], pk["len"][:16384], cfg=o.cfg(0, 1, NOW), nthreads=16)
     assert_same({k: v[:16384] for k, v in res.items()}, lin)
-    # the single-tile block walk (pipeline 5): fewer block levels in LDS, the rest from L2; the multi-tile walk with
-    # and without producer / consumer waves (pipelines 6 and 3), at several ticket-queue positions (ragged sizes)
+    # the default walk is the cut lists (image v7: 8 sip x 8 dip bits, groups in LDS, entries from L2); the multi-tile
+    # block walk (pipeline 3: the top block levels in LDS, the rest from L2) and both from global memory too, at
+    # ragged sizes (partial rounds of the multi-tile walk, a partial last tile)
+    assert eng.launch_info()["fetch"] == "cut" and eng.launch_info()["image"] == "lds"
     old = eng.tuning()
     try:
-        for pl, fetch in ((5, "sblk"), (6, "pc"), (3, "multi")):
-            eng.tuning(pipeline=pl)
-            assert eng.launch_info()["fetch"] == fetch and eng.launch_info()["image"] == "split"
+        for tune, fetch, image in ((dict(pipeline=3), "multi", "split"), (dict(pipeline=5, lds_image=0), "cut", "global"),
+                                   (dict(pipeline=3, lds_image=0), "multi", "global")):
+            eng.tuning(**tune)
+            assert eng.launch_info()["fetch"] == fetch and eng.launch_info()["image"] == image, tune
             assert_same(gpu_classify(eng, pk["hdr"], pk["len"]), ref)
-        eng.tuning(pipeline=6)
-        for m in (1, 63, 64, 65, 4097, 99_999):
-            r = gpu_classify(eng, pk["hdr"][:m], pk["len"][:m])
-            assert_same(r, {k: v[:m] for k, v in ref.items()})
-            check_compaction(r, m)
+        for pl in (3, 5):
+            eng.tuning(pipeline=pl, lds_image=1)
+            for m in (1, 63, 64, 65, 4097, 99_999):
+                r = gpu_classify(eng, pk["hdr"][:m], pk["len"][:m])
+                assert_same(r, {k: v[:m] for k, v in ref.items()})
+                check_compaction(r, m)
     finally:
         eng.tuning(**old)
 
 
-@pytest.mark.parametrize("nrules", [256, 4096])
-@pytest.mark.parametrize("pipeline", [0, 5])
-def test_three_level_blocks_forced(eng, monkeypatch, nrules, pipeline):
-    """3-level (64-B) blocks forced on rule sets that would get 2-level ones (PPE_BLOCK_LEVELS=3): the PF_MULTI3
-    kernel (default pipeline) and PF_SBLK3 (pipeline 5), IMIX with malformed packets, against the linear oracle."""
-    monkeypatch.setenv("PPE_BLOCK_LEVELS", "3")
-    rules = synth.make_rules(nrules, seed=500 + nrules)
-    pk = synth.make_packets(65_536, rules, seed=501, kind="imix", stride=128, malformed_frac=0.05)
-    st = eng.commit(rules, default_action=1)
+@pytest.mark.parametrize("bits", ["0", "4", "11", "16"])
+def test_cut_lists_forced_widths(eng, monkeypatch, bits):
+    """The cut-list kernel (pipeline 5) at forced cut widths (PPE_CUT_BITS) over rules with short and wildcard
+    prefixes (replicated into every bucket they meet), any-port rules and protocol ranges with and without 6 / 17,
+    IMIX with VLAN tags, TCP and malformed packets, groups and entries in LDS or global: against the linear oracle."""
+    monkeypatch.setenv("PPE_CUT_BITS", bits)
+    rng = np.random.default_rng(600 + int(bits))
+    n = {0: 12, 4: 80}.get(int(bits), 1500)
+    r = synth.make_rules(n, seed=601)
+    r["sip_mask"] = rng.choice([0, 1, 7, 8, 16, 31, 32], n, p=[0.01, 0.02, 0.1, 0.25, 0.32, 0.15, 0.15])
+    r["dip_mask"] = rng.choice([0, 1, 8, 24, 32], n, p=[0.01, 0.02, 0.37, 0.3, 0.3])
+    anyport = rng.random(n) < 0.3
+    for f in ("sport", "dport"):
+        r[f + "_start"][anyport] = 0
+        r[f + "_end"][anyport] = 65535
+    pr = rng.integers(0, 4, n)
+    r["protocol_start"] = np.choose(pr, [6, 17, 0, 7])
+    r["protocol_end"] = np.choose(pr, [6, 17, 255, 16])
+    pk = synth.make_packets(65_536, r, seed=602, kind="imix", stride=128, malformed_frac=0.05, hit_frac=0.9)
     old = eng.tuning()
     try:
-        eng.tuning(pipeline=pipeline)
-        assert eng.launch_info()["fetch"] == ("multi3" if pipeline == 0 else "sblk3")
-        res = gpu_classify(eng, pk["hdr"], pk["len"])
+        for da in (0, 1):
+            st = eng.commit(r, default_action=da)
+            assert (st["cut_bits"] & 0xFF) + (st["cut_bits"] >> 8) == int(bits) and st["cut_entries"] > 0
+            o = pyoracle.Oracle(r, default_action=da)
+            ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16)
+            for tune in (dict(pipeline=5, lds_image=1), dict(pipeline=5, lds_image=0)):
+                eng.tuning(**tune)
+                assert eng.launch_info()["fetch"] == "cut"
+                res = gpu_classify(eng, pk["hdr"], pk["len"])
+                assert_same(res, ref)
+                check_compaction(res, len(pk["len"]))
+            assert (ref["acl_hit"] >= 0).sum() > 20_000
     finally:
         eng.tuning(**old)
-    o = pyoracle.Oracle(rules, default_action=1)
-    ref = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16)
-    assert_same(res, ref)
-    check_compaction(res, len(pk["len"]))
-    assert st["n_rules"] == nrules
 
 
 def test_residual_rules_with_timestamps(eng):
@@ -410,7 +428,8 @@ def test_argument_errors(eng):
     assert (ob == 0x5A).all()
     t = abi.Tuning(block=300)
     assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
-    for pl in (2, 7, 8):  # the register / LDS-DMA prefetch variants are not built; 6 is PF_PC
+    for pl in (2, 6, 7, 8):  # the register / LDS-DMA prefetch variants are not built; round 4's
+        # single-tile block walk, 3-level blocks and producer / consumer waves are gone (5 is the cut lists now)
         t = abi.Tuning(pipeline=pl)
         assert lib.ppe_set_tuning(eng.ctx, C.byref(t)) == -22
 
@@ -419,7 +438,7 @@ TUNINGS = [dict(lds_image=0), dict(block=512), dict(block=1024), dict(block=256)
            dict(pipeline=4), dict(pipeline=1, block=256), dict(pipeline=1, block=512), dict(pipeline=1, lds_image=0),
            dict(pipeline=4, lds_image=0), dict(pipeline=4, block=1024), dict(blocks_per_cu=16), dict(blocks_per_cu=1),
            dict(pipeline=3), dict(pipeline=3, lds_image=0), dict(pipeline=5), dict(pipeline=5, block=1024),
-           dict(pipeline=6), dict(pipeline=6, lds_image=0)]
+           dict(pipeline=5, lds_image=0), dict(pipeline=5, block=256)]
 
 
 @pytest.mark.parametrize("tune", TUNINGS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
