@@ -3,7 +3,7 @@
 # VARIANT = name=libpath[:key=val,...] as tools/ab_bench.py takes it (E_NAME=value sets an environment variable for
 # that variant).  Each config runs through tools/gpu_ab.sh; the "kernel med" lines collect in gpurun_out/TAG/summary.txt.
 # Round-3 runs recorded in profiles/r3_ab_runs.md used it as, e.g. (L=packet-process-engine_amd, O=api=batches,bpl=0,outs=part):
-#   r3c  C3 "k3=$L/libppe_hip.so:$O k2=$L/libppe_hip.so:E_PPE_BLOCK_LEVELS=2,$O"     (3- vs 2-level blocks)
+#   r5   C3 "cut=$L/libppe_hip.so:$O multi=$L/libppe_hip.so:pipeline=3,$O"           (cut lists vs block walk)
 #   r3g  "C4 C3" "full=$L/libppe_hip.so none=$L/libppe_hip_abl15.so ..."             (ablation builds)
 #   r3h / r3j / r3k / r3p  "C4 C3 C2" "new=$L/libppe_hip.so:$O old=$L/libppe_hip_bl.so:$O" -- --steps 20 --rounds 4 --check
 set -o pipefail
