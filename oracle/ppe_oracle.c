@@ -274,26 +274,46 @@ int32_t oracle_acl_cut(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dpor
     const uint32_t *im = g_img;
     const uint32_t *h = im + im[PPE_IMG_W_OFFCUT];
     const uint32_t b0 = h[0] & 0xffu, b1 = (h[0] >> 8) & 0xffu;
-    const uint32_t bk = (uint32_t)(((uint64_t)sip >> (32u - b0)) << b1) | (uint32_t)((uint64_t)dip >> (32u - b1));
-    const uint32_t *g = im + h[4] + 4u * (bk >> 4);
-    uint32_t first = g[0];
-    for (uint32_t k = 0; k < (bk & 15u); k++) first += (g[1u + (k >> 3)] >> (4u * (k & 7u))) & 15u;
-    const uint32_t k = bk & 15u, cnt = (g[1u + (k >> 3)] >> (4u * (k & 7u))) & 15u;
+    const uint32_t bk = ((sip >> (32u - b0)) << b1) | (dip >> (32u - b1));
+    /* the bucket's list: the group's base + the bit-sliced lengths of the buckets before it in its group */
+    const uint32_t *sl = im + h[4] + 4u * (bk >> 5);
+    uint32_t first = im[h[8] + (bk >> 5)], cnt = 0;
+    for (uint32_t k = 0; k <= (bk & 31u); k++) {
+        uint32_t len = 0;
+        for (uint32_t b = 0; b < 4u; b++) len |= ((sl[b] >> k) & 1u) << b;
+        if (k < (bk & 31u)) first += len;
+        else cnt = len;
+    }
+    const uint32_t ks = sip << b0, kd = dip << b1;
+    const uint32_t ksb = (sip >> (31u - b0)) & 1u, kdb = (dip >> (31u - b1)) & 1u;
+    const uint8_t *fp = (const uint8_t *)(im + h[9]);
     (void)dmac; (void)smac; (void)ts;
     for (uint32_t j = 0; j < cnt; j++) {
-        const uint32_t *r = im + h[5] + PPE_CUT_ENT_WORDS * (first + j);
-        const uint32_t x = r[4];
-        const uint32_t ms = (x & PPE_CX_S32) ? ~0u : ~(((r[0] & (0u - r[0])) << 1) - 1u);
-        const uint32_t md = (x & PPE_CX_D32) ? ~0u : ~(((r[1] & (0u - r[1])) << 1) - 1u);
-        const int m = ((sip ^ r[0]) & ms) == 0 && ((dip ^ r[1]) & md) == 0 &&
+        const uint32_t e = first + j;
+        const uint32_t *r = im + h[5] + PPE_CUT_ENT_WORDS * e;
+        /* the prefixes relative to the bucket: the bits above the marker (lowest set bit without the flag bit 0) */
+        const uint32_t sm = r[0] & ~1u, dm = r[1] & ~1u;
+        const uint32_t ms = ~(((sm & (0u - sm)) << 1) - 1u), md = ~(((dm & (0u - dm)) << 1) - 1u);
+        const int m = ((ks ^ sm) & ms) == 0 && ((kd ^ dm) & md) == 0 &&
                       (uint16_t)(sport - (r[2] & 0xffffu)) <= (r[3] & 0xffffu) &&
                       (uint16_t)(dport - (r[2] >> 16)) <= (r[3] >> 16) &&
-                      (proto == 6 ? (x & PPE_CX_TCP) : proto == 17 ? (x & PPE_CX_UDP) : 0) != 0;
+                      (proto == 6 ? (r[0] & 1u) : proto == 17 ? (r[1] & 1u) : 0) != 0;
+        /* the kernel skips an entry whose fingerprint rejects the key: such an entry must never match */
+        const uint32_t f = (fp[e >> 1] >> (4u * (e & 1u))) & 15u;
+        const int rejected = ((f & 2u) && (f & 1u) != ksb) || ((f & 8u) && ((f >> 2) & 1u) != kdb);
+        if (rejected && m) return -2;  /* a fingerprint that would drop a match: an image error, reported as hit -2 */
         if (m) {
-            const uint32_t id = x & PPE_CX_SLOT;
+            uint32_t id;
+            if (h[0] & PPE_CUT_IDS16) {
+                id = ((const uint16_t *)(im + h[7]))[e];
+                id = (id & 0x7fffu) | ((id & 0x8000u) << 16);
+            } else {
+                id = im[h[7] + e];
+            }
+            const uint32_t rid = id & 0x7fffffffu;
             /* the action word a drop-or-forward decision needs: the classify path compares it with DROP only */
-            if (action) *action = (x & PPE_CX_DROP) ? ACL_RULE_ACTION_DROP : oracle_rule_action(id);
-            return (int32_t)id;
+            if (action) *action = (id >> 31) ? ACL_RULE_ACTION_DROP : oracle_rule_action(rid);
+            return (int32_t)rid;
         }
     }
     if (action) *action = im[PPE_IMG_W_DEFACT];

@@ -311,11 +311,12 @@ bool cut_lists(const std::vector<Rule> &R, uint32_t b0, uint32_t b1, size_t budg
     return true;
 }
 
-// Pick the cut: every split of T = b0 + b1 <= PPE_CUT_MAX_BITS bits between sip and dip, by the expected entries a
-// lookup reads (half for a uniformly random key: entries / buckets; half for a key inside a rule's box, the
+// Pick the cut: every split of T = b0 + b1 <= PPE_CUT_MAX_BITS bits between sip and dip (each >= 2), by the expected
+// entries a lookup reads (half for a uniformly random key: entries / buckets; half for a key inside a rule's box, the
 // size-biased list length sum(len^2) / entries), plus a little for the longest list (the wave's trip count) and for
-// every bit (LDS).  PPE_CUT_BITS=T (tests, A/B) fixes the total.  False when no cut qualifies (a list longer than 15
-// entries at every width: then the classify kernel walks the tree).
+// every bit (LDS), a quarter of that when the whole cut fits half a CU's LDS (no L2 reads at all).
+// PPE_CUT_BITS=T (tests, A/B) fixes the total.  False when no cut qualifies (a list longer than 15 entries at every
+// width: then the classify kernel walks the tree).
 bool choose_cut(const std::vector<Rule> &R, CutLists &best) {
     const char *fb = std::getenv("PPE_CUT_BITS");
     const int force = fb && *fb ? std::atoi(fb) : -1;
@@ -323,16 +324,20 @@ bool choose_cut(const std::vector<Rule> &R, CutLists &best) {
     double cbest = 1e30;
     uint32_t bb0 = 0, bb1 = 0;
     bool found = false;
-    for (uint32_t T = 0; T <= PPE_CUT_MAX_BITS; ++T) {
+    for (uint32_t T = 4; T <= PPE_CUT_MAX_BITS; ++T) {
         if (force >= 0 && (int)T != force) continue;
-        if (force < 0 && T < 4 && R.size() > 15) continue;  // (too few buckets for any list to fit)
-        for (uint32_t b0 = 0; b0 <= T; ++b0) {
+        for (uint32_t b0 = 2; b0 + 2 <= T; ++b0) {  // (b0, b1 >= 2: each relative prefix has a free low bit)
             CutLists c;
             if (!cut_lists(R, b0, T - b0, budget, c, false)) continue;
             const double nb = (double)(1u << T), ne = (double)c.n_entries;
             double sq = 0;
             for (uint8_t l : c.len) sq += (double)l * l;
-            const double cost = 0.5 * ne / nb + 0.5 * (ne ? sq / ne : 0.0) + 0.02 * c.max_len + 0.01 * T;
+            // groups (20 B per 32 buckets), 4-bit fingerprints, 16-B entries and 2-B ids in half a CU's LDS (two
+            // 1024-thread workgroups, the counter bins and the staging's 1-KB rounding beside them): the whole lookup
+            // runs from LDS, no L2 round
+            const bool lds = 0.625 * nb + 18.5 * ne + 3.0 * 1024 <= 80.0 * 1024 && R.size() <= 0x8000u;
+            const double cost = (0.5 * ne / nb + 0.5 * (ne ? sq / ne : 0.0) + 0.02 * c.max_len + 0.01 * T) *
+                                (lds ? 0.25 : 1.0);
             if (std::getenv("PPE_ACL_DEBUG"))
                 std::fprintf(stderr, "acl_build: cut sip %u dip %u: entries %zu max %u cost %.3f\n", b0, T - b0,
                              c.n_entries, c.max_len, cost);
@@ -556,12 +561,19 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     const char *cenv = std::getenv("PPE_CUT");
     const bool want_cut = !any_resid && !(cenv && *cenv == '0');
     const bool have_cut = want_cut && choose_cut(R, cut) && cut.entries.size() < (1u << 25);  // (< 1 GB of entries)
+    // layout (ppe_image.h): header, bucket-length slices, group bases, fingerprints (what a lookup reads from LDS
+    // when only they are staged), then the entries and ids
     const uint32_t off_cut = have_cut ? (end_tree + 7u) & ~7u : 0u;
-    const uint32_t n_groups = have_cut ? std::max(1u, (1u << (cut.b0 + cut.b1)) / 16u) : 0u;
-    const uint32_t off_grp = off_cut + PPE_CUT_HDR_WORDS;  // 32-B aligned
-    const uint32_t off_ent = off_grp + 4u * n_groups;      // 32-B aligned (n_groups >= 1, 16 B each: see below)
-    const uint32_t off_ent_al = (off_ent + 7u) & ~7u;
-    const uint32_t total = have_cut ? off_ent_al + PPE_CUT_ENT_WORDS * (uint32_t)cut.entries.size() : end_tree;
+    const uint32_t n_groups = have_cut ? std::max(1u, (1u << (cut.b0 + cut.b1)) / 32u) : 0u;
+    const uint32_t n_ent = have_cut ? (uint32_t)cut.entries.size() : 0u;
+    const uint32_t off_slc = off_cut + PPE_CUT_HDR_WORDS;                // 16 B per group, 16-B aligned
+    const uint32_t off_gbase = off_slc + 4u * n_groups;                  // 4 B per group
+    const uint32_t off_fp = off_gbase + n_groups;                        // 4 bits per entry (+ 2 pad words)
+    const uint32_t off_ent = (off_fp + (n_ent + 7u) / 8u + 2u + 3u) & ~3u;  // 16 B per entry, 16-B aligned
+    const bool ids16 = R.size() <= 0x8000u;  // rule ids (and the DROP bit) in 16-bit words
+    const uint32_t off_id = off_ent + PPE_CUT_ENT_WORDS * n_ent;
+    const uint32_t id_words = ids16 ? (n_ent + 1u) / 2u : n_ent;
+    const uint32_t total = have_cut ? off_id + id_words : end_tree;
 
     uint32_t *img = (uint32_t *)std::calloc(total, sizeof(uint32_t));
     if (!img) return PPE_ENOMEM;
@@ -590,39 +602,55 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     img[PPE_IMG_W_OFFCUT] = off_cut;
     if (have_cut) {
         uint32_t *h = img + off_cut;
-        h[0] = cut.b0 | (cut.b1 << 8);
+        h[0] = cut.b0 | (cut.b1 << 8) | (ids16 ? PPE_CUT_IDS16 : 0u);
         h[1] = 1u << (cut.b0 + cut.b1);
-        h[2] = (uint32_t)cut.entries.size();
+        h[2] = n_ent;
         h[3] = cut.max_len;
-        h[4] = off_grp;
-        h[5] = off_ent_al;
+        h[4] = off_slc;
+        h[5] = off_ent;
         h[6] = n_groups;
+        h[7] = off_id;
+        h[8] = off_gbase;
+        h[9] = off_fp;
         const uint32_t nb = h[1];
         uint32_t first = 0;
-        for (uint32_t g = 0; g < n_groups; ++g) {  // {first entry, 8 + 8 four-bit lengths, 0}
-            uint32_t *o = img + off_grp + 4u * g;
-            o[0] = first;
-            for (uint32_t k = 0; k < 16u && 16u * g + k < nb; ++k) {
-                const uint32_t len = cut.len[16u * g + k];
-                o[1u + (k >> 3)] |= len << (4u * (k & 7u));
+        for (uint32_t g = 0; g < n_groups; ++g) {  // the group's first entry, its 32 lengths bit-sliced
+            img[off_gbase + g] = first;
+            uint32_t *sl = img + off_slc + 4u * g;
+            for (uint32_t k = 0; k < 32u && 32u * g + k < nb; ++k) {
+                const uint32_t len = cut.len[32u * g + k];
+                for (uint32_t b = 0; b < 4u; ++b) sl[b] |= ((len >> b) & 1u) << k;
                 first += len;
             }
         }
-        auto pfx = [](uint32_t lo, uint32_t hi) { return lo == hi ? lo : lo | (((hi - lo) >> 1) + 1u); };
-        for (size_t e = 0; e < cut.entries.size(); ++e) {
+        // an address prefix relative to its bucket (ppe_image.h): the bits below the cut's b top bits shifted to the
+        // top, their end marked by the next bit; a prefix no longer than b matches the whole bucket (marker bit 31)
+        auto plen = [](uint32_t lo, uint32_t hi) { return 32u - (uint32_t)__builtin_popcount(hi - lo); };
+        auto rel = [&](uint32_t lo, uint32_t hi, uint32_t b) -> uint32_t {
+            const uint32_t len = plen(lo, hi);  // (hi - lo = 2^(32 - len) - 1)
+            if (len <= b) return 0x80000000u;
+            return (lo << b) | (1u << (31u - (len - b)));
+        };
+        uint16_t *id16 = (uint16_t *)(img + off_id);
+        uint8_t *fp = (uint8_t *)(img + off_fp);
+        for (uint32_t e = 0; e < n_ent; ++e) {
             const Rule &r = R[cut.entries[e]];
-            uint32_t *o = img + off_ent_al + PPE_CUT_ENT_WORDS * e;
-            o[0] = pfx(r.lo[PPE_DIM_SIP], r.hi[PPE_DIM_SIP]);
-            o[1] = pfx(r.lo[PPE_DIM_DIP], r.hi[PPE_DIM_DIP]);
+            uint32_t *o = img + off_ent + PPE_CUT_ENT_WORDS * e;
+            const bool tcp = r.lo[PPE_DIM_PROTO] <= 6u && 6u <= r.hi[PPE_DIM_PROTO];
+            const bool udp = r.lo[PPE_DIM_PROTO] <= 17u && 17u <= r.hi[PPE_DIM_PROTO];
+            o[0] = rel(r.lo[PPE_DIM_SIP], r.hi[PPE_DIM_SIP], cut.b0) | (tcp ? 1u : 0u);
+            o[1] = rel(r.lo[PPE_DIM_DIP], r.hi[PPE_DIM_DIP], cut.b1) | (udp ? 1u : 0u);
             o[2] = r.lo[PPE_DIM_SPORT] | (r.lo[PPE_DIM_DPORT] << 16);
             o[3] = (r.hi[PPE_DIM_SPORT] - r.lo[PPE_DIM_SPORT]) | ((r.hi[PPE_DIM_DPORT] - r.lo[PPE_DIM_DPORT]) << 16);
-            uint32_t x = r.id;  // (n <= 2^24: the index fits the exit's 24 bits)
-            if (r.action == ACL_RULE_ACTION_DROP) x |= PPE_CX_DROP;
-            if (r.lo[PPE_DIM_PROTO] <= 6u && 6u <= r.hi[PPE_DIM_PROTO]) x |= PPE_CX_TCP;
-            if (r.lo[PPE_DIM_PROTO] <= 17u && 17u <= r.hi[PPE_DIM_PROTO]) x |= PPE_CX_UDP;
-            if (r.lo[PPE_DIM_SIP] == r.hi[PPE_DIM_SIP]) x |= PPE_CX_S32;
-            if (r.lo[PPE_DIM_DIP] == r.hi[PPE_DIM_DIP]) x |= PPE_CX_D32;
-            o[4] = x;
+            const bool drop = r.action == ACL_RULE_ACTION_DROP;
+            if (ids16) id16[e] = (uint16_t)(r.id | (drop ? 0x8000u : 0u));
+            else img[off_id + e] = r.id | (drop ? 0x80000000u : 0u);
+            // fingerprint: the first sip / dip bit below the cut, each with its "the prefix fixes it" flag
+            const bool sv = plen(r.lo[PPE_DIM_SIP], r.hi[PPE_DIM_SIP]) > cut.b0;
+            const bool dv = plen(r.lo[PPE_DIM_DIP], r.hi[PPE_DIM_DIP]) > cut.b1;
+            const uint32_t f = (sv ? ((r.lo[PPE_DIM_SIP] >> (31u - cut.b0)) & 1u) | 2u : 0u) |
+                               (dv ? (((r.lo[PPE_DIM_DIP] >> (31u - cut.b1)) & 1u) << 2) | 8u : 0u);
+            fp[e >> 1] |= (uint8_t)(f << (4u * (e & 1u)));
         }
     }
     if (compact) {

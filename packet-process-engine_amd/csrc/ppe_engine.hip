@@ -200,7 +200,8 @@ struct StagePlan {
     uint32_t lds_blocks;              // multi-tile walks: blocks [0, lds_blocks) in LDS
     uint32_t bsec_lds, blk_lds;       // LDS byte offsets (from the image base in LDS) of the block section / block 0
     uint32_t crec_lds = ~0u, idtab_lds = ~0u;  // compact records / index table in LDS (byte offsets), ~0u = global
-    uint32_t cut_ent_lds = ~0u;       // cut lists: entries in LDS (byte offset), ~0u = global (the groups: LDS base)
+    uint32_t cut_gbase_lds = 0, cut_fp_lds = 0;    // cut lists: LDS byte offsets of the group bases / fingerprints
+    uint32_t cut_ent_lds = ~0u, cut_id_lds = ~0u;  // cut lists: entries / ids in LDS (byte offsets), ~0u = global
 };
 
 // LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves; a flow-table launch:
@@ -261,7 +262,8 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
     const uint32_t off_cut = img[PPE_IMG_W_OFFCUT];
     auto cut_plan = [&]() {
         const uint32_t *h = img.data() + off_cut;
-        const uint32_t grp_bytes = 16u * h[6], ent_bytes = 4u * PPE_CUT_ENT_WORDS * h[2];
+        const uint32_t grp_bytes = 4u * (h[5] - h[4]);  // slices, bases and fingerprints (the L2-entry plan's LDS)
+        const uint32_t all_words = (h[0] & PPE_CUT_IDS16 ? (h[2] + 1u) / 2u : h[2]) + h[7] - h[4];  // ... to the ids
         p.pipe = kPfCut;
         p.mode = 0;
         p.block = c->tune.block ? c->tune.block : 1024u;
@@ -273,20 +275,23 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
         };
         if (!c->tune.block)
             for (uint32_t b : {256u, 512u, 1024u})
-                if (grp_bytes <= budget(b)) {
+                if (4u * all_words <= budget(b) || (b == 1024u && grp_bytes <= budget(b))) {
                     p.block = b;
                     break;
                 }
         const uint32_t bud = budget(p.block);
         if (grp_bytes > bud) return;  // (groups larger than the share: global)
-        p.mode = 1;
         p.stage_src = h[4];
-        const uint32_t gap = 4u * (h[5] - h[4]);  // groups, then the 32-B aligned entries
-        if (gap + ent_bytes <= bud && env_int("PPE_CUT_ENT_LDS", 1)) {
-            p.stage_words = h[5] - h[4] + PPE_CUT_ENT_WORDS * h[2];
-            p.cut_ent_lds = gap;
-        } else {
-            p.stage_words = 4u * h[6];
+        p.cut_gbase_lds = 4u * (h[8] - h[4]);
+        p.cut_fp_lds = 4u * (h[9] - h[4]);
+        if (4u * all_words <= bud && env_int("PPE_CUT_ENT_LDS", 1)) {  // everything in LDS (IMG_LDS)
+            p.mode = 1;
+            p.stage_words = all_words;
+            p.cut_ent_lds = 4u * (h[5] - h[4]);
+            p.cut_id_lds = 4u * (h[7] - h[4]);
+        } else {  // slices, bases and fingerprints in LDS, entries and ids from L2 (IMG_SPLIT)
+            p.mode = 2;
+            p.stage_words = h[5] - h[4];
         }
         p.lds_words = p.stage_words;
     };
@@ -558,9 +563,15 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     if (plan.pipe == kPfCut) {  // (image v7 cut lists: header at PPE_IMG_W_OFFCUT)
         const uint32_t *h = c->h_img[r].data() + c->h_img[r][PPE_IMG_W_OFFCUT];
         a.cut = h[0];
-        a.cut_grp = h[4];
+        a.cut_slc = h[4];
         a.cut_ent = h[5];
+        a.cut_id = h[7];
+        a.cut_gbase = h[8];
+        a.cut_fp = h[9];
+        a.cut_gbase_lds = plan.cut_gbase_lds;
+        a.cut_fp_lds = plan.cut_fp_lds;
         a.cut_ent_lds = plan.cut_ent_lds;
+        a.cut_id_lds = plan.cut_id_lds;
     }
     // batch groups: the kernel splits its waves into min(batches, max_groups) groups, group g taking batches g, g + G,
     // ...; when G does not divide the batch count the last round leaves groups idle (20 batches at G = 8: the last

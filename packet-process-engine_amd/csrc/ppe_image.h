@@ -88,20 +88,31 @@
  *  cut-list section (v7; present iff word 22 != 0: every rule without residual MAC / time fields).  A second,
  *  independent classifier for the classify kernel (TCP / UDP keys only): a HyperCuts-style cut of the top b0 bits
  *  of sip and the top b1 bits of dip into 2^(b0 + b1) buckets, bucket = (sip >> (32 - b0)) << b1 | dip >> (32 - b1)
- *  (a width 0 contributes nothing), and per bucket the list of the rules whose box meets it, in priority order,
- *  closed after the first rule that covers the whole bucket (every port, TCP and UDP).  The builder picks b0, b1
- *  (b0 + b1 <= 16) by the expected list length and rejects the section when a list would exceed 15 entries.  A
- *  lookup is one read of the bucket's group (LDS) and one round of independent entry reads (L2): no dependent walk.
- *      header (8 words at off_cut): b0 | b1 << 8, n_buckets, n_entries, max list length, off_grp, off_ent (word
- *          offsets from the image start), n_groups, 0
- *      groups (4 words each, 16-B aligned; group g = buckets 16 g .. 16 g + 15): { first entry of bucket 16 g,
- *          list lengths of buckets 16 g + 0..7 (4 bits each, bucket 16 g + k at bits 4k), of 16 g + 8..15, 0 }
- *          bucket b's list = entries [first(b), first(b) + len(b)), first(b) = the group's first + the lengths of
- *          the buckets before b in its group
- *      entries (8 words each, 32-B aligned, contiguous per bucket in priority order): { sip prefix | marker bit,
- *          dip prefix | marker bit (as the compact record), sport_lo | dport_lo << 16, the port spans, exit, 0, 0,
- *          0 }, exit = rule index (bits 0-23) | the compact exit flags PPE_CX_DROP / TCP / UDP / S32 / D32
- */
+ *  (b0, b1 >= 2), and per bucket the list of the rules whose box meets it, in priority order, closed after the first
+ *  rule that covers the whole bucket (every port, TCP and UDP).  The builder picks b0, b1 (b0 + b1 <= 16) by the
+ *  expected list length (strongly preferring a cut whose groups, entries and ids fit half a CU's LDS) and rejects the
+ *  section when a list would exceed 15 entries.  A lookup is one read of the bucket's group and one round of
+ *  independent 16-B entry reads (LDS, or L2 for large sets): no dependent walk; a match reads its rule id.
+ *      header (16 words at off_cut): b0 | b1 << 8 | PPE_CUT_IDS16, n_buckets, n_entries, max list length,
+ *          off_slc, off_ent, n_groups, off_id, off_gbase, off_fp (word offsets from the image start), 0...
+ *      groups of 32 buckets (group g = buckets 32 g .. 32 g + 31): slices (4 words, 16-B aligned, at off_slc + 4 g):
+ *          bit k of word i = bit i of bucket 32 g + k's list length (0..15); base (1 word, at off_gbase + g): the
+ *          group's first entry.  Bucket b's list = entries [first(b), first(b) + len(b)), first(b) = base +
+ *          sum over i of 2^i popcount(slice i & (2^(b mod 32) - 1)).
+ *      fingerprints (4 bits per entry, entry e at bits 4 (e mod 8) of word off_fp + e / 8; two spare words after):
+ *          bit 0 = the rule's sip bit 31 - b0 (the first below the cut), bit 1 = its prefix fixes that bit, bits 2 / 3
+ *          likewise for dip bit 31 - b1.  A lookup skips an entry whose fixed bits differ from the key's (it cannot
+ *          match), so most entries that would not match are never read.
+  *      entries (4 words each, 16-B aligned, contiguous per bucket in priority order):
+ *          sip relative to the bucket | TCP: the prefix's bits below the top b0, shifted up by b0, then a marker bit
+ *              (so the bits above the lowest set bit of the word without bit 0 must equal the key's sip << b0); a
+ *              /32 puts the marker at bit b0 - 1 (>= 1); a prefix of at most b0 bits matches the whole bucket:
+ *              0x80000000.  Bit 0: the rule's protocol range contains 6.
+ *          dip relative to the bucket | UDP (bit 0: contains 17), likewise with b1
+ *          sport_lo | dport_lo << 16;  (sport_hi - sport_lo) | (dport_hi - dport_lo) << 16
+ *      ids (one per entry, read on a match): rule index | DROP (action == ACL_RULE_ACTION_DROP) in the top bit,
+ *          16-bit words when PPE_CUT_IDS16 (every index < 2^15), else 32-bit words
+  */
 #ifndef PPE_IMAGE_H
 #define PPE_IMAGE_H
 
@@ -141,8 +152,9 @@
 #define PPE_CX_D32    (1u << 28)
 #define PPE_CX_NOHIT  (1u << 29)
 #define PPE_CREC_WORDS 4u
-#define PPE_CUT_HDR_WORDS 8u
-#define PPE_CUT_ENT_WORDS 8u      /* cut-list entry (32 B) */
+#define PPE_CUT_HDR_WORDS 16u
+#define PPE_CUT_ENT_WORDS 4u      /* cut-list entry (16 B) */
+#define PPE_CUT_IDS16 0x10000u    /* cut header word 0: 16-bit rule ids */
 #define PPE_CUT_MAX_LIST 15u      /* longest bucket list (4-bit lengths) */
 #define PPE_CUT_MAX_BITS 16u      /* b0 + b1: 2^16 buckets = 64 KB of groups */
 

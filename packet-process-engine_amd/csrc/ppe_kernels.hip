@@ -415,9 +415,10 @@ struct AclGeo {
     // compact leaves (image v6): record / index-table word offsets (0 = none), and their LDS byte offsets from the
     // staged image base (~0u = read from global memory)
     uint32_t off_crec, off_idtab, crec_lds, idtab_lds;
-    // cut lists (image v7): sip bits | dip bits << 8, word offsets of the groups / entries, the entries' LDS byte
-    // offset (~0u = global; the groups are at the staged image base when the image mode is IMG_LDS)
-    uint32_t cut, cut_grp, cut_ent, cut_ent_lds;
+    // cut lists (image v7): header word 0 (sip bits | dip bits << 8 | PPE_CUT_IDS16), word offsets of the length
+    // slices / group bases / fingerprints / entries / ids, and the LDS byte offsets of the bases, fingerprints,
+    // entries and ids from the staged image base (the slices are at it; entries and ids only when the mode is IMG_LDS)
+    uint32_t cut, cut_slc, cut_gbase, cut_fp, cut_ent, cut_id, cut_gbase_lds, cut_fp_lds, cut_ent_lds, cut_id_lds;
 };
 
 // One level of the walk, node and key both in flight: the node's child pointer carries the child's key slot, so
@@ -628,72 +629,82 @@ __device__ __forceinline__ void acl_leaf_compact(const uint32_t *__restrict__ gi
     crec_check<IMGB>(gimg, g, x, crec_load<IMGB>(gimg, g, x), sip, dip, sport, dport, tcp, hit, drop);
 }
 
-// Cut-list lookup (image v7, ppe_image.h): the bucket of the key's top sip / dip bits; its group (16 B: LDS when
-// staged) gives the bucket's list, whose entries (32 B each, L2 or LDS) are independent reads, two per round, checked
-// in priority order: one dependent L2 round for lists of up to two entries, where a tree walk through an L2-resident
-// forest takes 5-6 (C3).  The check is the compact record's (crec_check).  Only TCP / UDP keys reach it.
-__device__ __forceinline__ uint32_t nibble_sum(uint32_t x) {  // sum of the eight 4-bit fields of x
-    x = (x & 0x0f0f0f0fu) + ((x >> 4) & 0x0f0f0f0fu);
-    return __builtin_amdgcn_sad_u8(x, 0u, 0u);
-}
-__device__ __forceinline__ bool cut_match(const uint4 r, uint32_t x, uint32_t sip, uint32_t dip, uint32_t ports,
-                                          bool tcp) {
-    const uint32_t ms = (x & PPE_CX_S32) ? ~0u : ~(((r.x & (0u - r.x)) << 1) - 1u);
-    const uint32_t md = (x & PPE_CX_D32) ? ~0u : ~(((r.y & (0u - r.y)) << 1) - 1u);
+// Cut-list lookup (image v7, ppe_image.h): the bucket of the key's top sip / dip bits; its group's length slices
+// and base (LDS when staged) give the bucket's list; the entries' 4-bit fingerprints (LDS) drop the entries whose
+// fixed sip / dip bit below the cut differs from the key's; the rest are independent 16-B reads (LDS, or L2 for large
+// sets), two per round, checked in priority order; a match reads its rule id.  Only TCP / UDP keys reach it (the
+// classify path).
+// one entry against the key's bucket-relative addresses (ks = sip << b0, kd = dip << b1): each prefix matches iff the
+// bits above its marker (the lowest set bit without the flag bit 0) equal the key's; ports by packed 16-bit spans
+__device__ __forceinline__ bool cut_match(const uint4 r, uint32_t ks, uint32_t kd, uint32_t ports, bool tcp) {
+    const uint32_t sm = r.x & ~1u, dm = r.y & ~1u;
+    const uint32_t ms = ~(((sm & (0u - sm)) << 1) - 1u), md = ~(((dm & (0u - dm)) << 1) - 1u);
     const u16x2 kp = __builtin_bit_cast(u16x2, ports), lo = __builtin_bit_cast(u16x2, r.z),
                 sp = __builtin_bit_cast(u16x2, r.w);
     const bool pp = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(kp - lo, sp)) == r.w;
-    return (((sip ^ r.x) & ms) == 0u) & (((dip ^ r.y) & md) == 0u) & pp &
-           ((x & (tcp ? PPE_CX_TCP : PPE_CX_UDP)) != 0u);
+    return (((ks ^ sm) & ms) == 0u) & (((kd ^ dm) & md) == 0u) & pp & (((tcp ? r.x : r.y) & 1u) != 0u);
 }
+// MODE: IMG_GLOBAL everything from global memory; IMG_SPLIT slices, bases and fingerprints in LDS, entries and ids
+// from global (L2); IMG_LDS all of it in LDS
 template <int MODE, int IMGB>
 __device__ __forceinline__ void acl_cut(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t sip, uint32_t dip,
                                         uint32_t ports, bool tcp, int32_t &hit, bool &drop) {
-    const uint32_t b0 = g.cut & 0xffu, b1 = (g.cut >> 8) & 0xffu;
-    const uint32_t bk = ((uint32_t)((uint64_t)sip >> (32u - b0)) << b1) | (uint32_t)((uint64_t)dip >> (32u - b1));
-    const uint32_t go = 16u * (bk >> 4), k = bk & 15u;
-    const uint4 gr = MODE == IMG_LDS ? lds_u128(IMGB + go) : gld<uint4>(gimg, 4u * g.cut_grp + go);
-    const uint32_t cw = k < 8u ? gr.y : gr.z, sh = 4u * (k & 7u);
-    const uint32_t cnt = (cw >> sh) & 15u;
-    const uint32_t first = gr.x + nibble_sum(cw & ((1u << sh) - 1u)) + (k >= 8u ? nibble_sum(gr.y) : 0u);
-    const bool ent_lds = MODE == IMG_LDS && g.cut_ent_lds != ~0u;
-    hit = -1;
+    constexpr bool L = MODE != IMG_GLOBAL;
+    const uint32_t b0 = g.cut & 0xffu, b1 = (g.cut >> 8) & 0xffu;  // (2..14 each)
+    const uint32_t bk = ((sip >> (32u - b0)) << b1) | (dip >> (32u - b1));
+    const uint32_t gi = bk >> 5, k = bk & 31u;
+    const uint4 sl = L ? lds_u128(IMGB + 16u * gi) : gld<uint4>(gimg, 4u * g.cut_slc + 16u * gi);
+    const uint32_t base = L ? lds_u32(IMGB + g.cut_gbase_lds + 4u * gi) : gld<uint32_t>(gimg, 4u * g.cut_gbase + 4u * gi);
+    const uint32_t m = (1u << k) - 1u;
+    const uint32_t cnt = ((sl.x >> k) & 1u) | (((sl.y >> k) & 1u) << 1) | (((sl.z >> k) & 1u) << 2) |
+                         (((sl.w >> k) & 1u) << 3);
+    const uint32_t first = base + __popc(sl.x & m) + 2u * __popc(sl.y & m) + 4u * __popc(sl.z & m) +
+                           8u * __popc(sl.w & m);
+    // the list's fingerprints (a window of at least 9 from the aligned dword pair: a longer list's tail is unfiltered)
+    const uint32_t fo = 4u * (first >> 3);
+    const uint32_t f0 = L ? lds_u32(IMGB + g.cut_fp_lds + fo) : gld<uint32_t>(gimg, 4u * g.cut_fp + fo);
+    const uint32_t f1 = L ? lds_u32(IMGB + g.cut_fp_lds + fo + 4u) : gld<uint32_t>(gimg, 4u * g.cut_fp + fo + 4u);
+    const uint64_t F = (((uint64_t)f1 << 32) | f0) >> (4u * (first & 7u));
+    const uint64_t kn = (uint64_t)(((sip >> (31u - b0)) & 1u) | (((dip >> (31u - b1)) & 1u) << 2)) * 0x1111111111111111ull;
+    const uint64_t M = (F ^ kn) & (F >> 1) & 0x5555555555555555ull;  // a fixed bit that differs
+    const uint64_t fail = (M | (M >> 2)) & 0x1111111111111111ull;
+    uint64_t P = ((1ull << (4u * cnt)) - 1u) & 0x1111111111111111ull & ~fail;  // candidate j at bit 4 j
+    const uint32_t ks = sip << b0, kd = dip << b1;
     bool found = false;
-    uint32_t xf = 0;
+    uint32_t ef = 0;  // the matching entry
 #pragma unroll 1
-    for (uint32_t j = 0; j < PPE_CUT_MAX_LIST; j += 2u) {
-        const bool a0 = !found && j < cnt, a1 = !found && j + 1u < cnt;
+    for (uint32_t round = 0; round < 8u; ++round) {
+        const bool a0 = !found && P != 0u;
         if (__builtin_amdgcn_ballot_w64(a0) == 0) break;
+        const uint32_t j0 = a0 ? (uint32_t)__builtin_ctzll(P) >> 2 : 0u;
+        P = a0 ? P & (P - 1u) : P;
+        const bool a1 = a0 && P != 0u;
+        const uint32_t j1 = a1 ? (uint32_t)__builtin_ctzll(P) >> 2 : 0u;
+        P = a1 ? P & (P - 1u) : P;
         uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
-        uint32_t x0 = 0u, x1 = 0u;
-        const uint32_t e0 = 32u * (first + j);
-        if (ent_lds) {
-            if (a0) {
-                r0 = lds_u128(IMGB + g.cut_ent_lds + e0);
-                x0 = lds_u32(IMGB + g.cut_ent_lds + e0 + 16u);
-            }
-            if (a1) {
-                r1 = lds_u128(IMGB + g.cut_ent_lds + e0 + 32u);
-                x1 = lds_u32(IMGB + g.cut_ent_lds + e0 + 48u);
-            }
-        } else {
-            const uint32_t o = 4u * g.cut_ent + e0;
-            if (a0) {
-                r0 = gld<uint4>(gimg, o);
-                x0 = gld<uint32_t>(gimg, o + 16u);
-            }
-            if (a1) {
-                r1 = gld<uint4>(gimg, o + 32u);
-                x1 = gld<uint32_t>(gimg, o + 48u);
-            }
-        }
-        const bool m0 = a0 && cut_match(r0, x0, sip, dip, ports, tcp);
-        const bool m1 = a1 && cut_match(r1, x1, sip, dip, ports, tcp);
-        xf = m0 ? x0 : (m1 ? x1 : xf);
+        const uint32_t e0 = first + j0, e1 = first + j1;
+        if (a0) r0 = MODE == IMG_LDS ? lds_u128(IMGB + g.cut_ent_lds + 16u * e0) : gld<uint4>(gimg, 4u * g.cut_ent + 16u * e0);
+        if (a1) r1 = MODE == IMG_LDS ? lds_u128(IMGB + g.cut_ent_lds + 16u * e1) : gld<uint4>(gimg, 4u * g.cut_ent + 16u * e1);
+        const bool m0 = a0 && cut_match(r0, ks, kd, ports, tcp);  // (in priority order: the first match wins)
+        const bool m1 = a1 && !m0 && cut_match(r1, ks, kd, ports, tcp);
+        ef = m0 ? e0 : (m1 ? e1 : ef);
         found = found || m0 || m1;
     }
-    hit = found ? (int32_t)(xf & PPE_CX_SLOT) : -1;
-    drop = found ? (xf & PPE_CX_DROP) != 0u : g.default_action == ACL_RULE_ACTION_DROP;
+    hit = -1;
+    drop = g.default_action == ACL_RULE_ACTION_DROP;
+    if (found) {  // the rule index and its DROP bit
+        uint32_t id;
+        if (g.cut & PPE_CUT_IDS16) {
+            const uint32_t o = 2u * ef, w = MODE == IMG_LDS ? lds_u32(IMGB + g.cut_id_lds + (o & ~3u))
+                                                              : gld<uint32_t>(gimg, 4u * g.cut_id + (o & ~3u));
+            id = (w >> (8u * (o & 2u))) & 0xffffu;
+            id = (id & 0x7fffu) | ((id & 0x8000u) << 16);
+        } else {
+            id = MODE == IMG_LDS ? lds_u32(IMGB + g.cut_id_lds + 4u * ef) : gld<uint32_t>(gimg, 4u * g.cut_id + 4u * ef);
+        }
+        hit = (int32_t)(id & 0x7fffffffu);
+        drop = (id >> 31) != 0u;
+    }
 }
 
 // 5-way key select by key slot (multi-tile walks keep the keys in registers)
@@ -1174,7 +1185,7 @@ __device__ __forceinline__ uint32_t flow_find_claim(const ppe_flowdev &f, const 
 #define PF_MULTI 3  // split / global images: each wave loads, decodes and walks PPE_MT tiles together (acl_walk_blocks_mt),
                     // 4 waves/SIMD with 128 VGPRs, one 1024-thread workgroup per CU and its whole LDS for the image
 #define PF_CUT 5    // images with cut lists (v7): one tile per wave (8 waves/SIMD), the keys in registers, the bucket
-                    // groups in LDS, the list entries from L2 (acl_cut)
+                    // groups in LDS, the list entries and ids in LDS (IMG_LDS) or from L2 (IMG_SPLIT) (acl_cut)
 #ifndef PPE_MT
 #define PPE_MT 4
 #endif
@@ -1270,7 +1281,8 @@ void ppe_classify_kernel(ppe_kargs a) {
     const AclGeo geo = {a.lds_iters, a.max_depth, a.max_leaf, a.root_ks, a.off_leaf, a.off_rules, a.off_resid,
                         a.lds_words, a.default_action, a.jump, a.off_nodes, a.lds_blocks, a.bsec_lds, a.blk_lds,
                         a.off_bsec, a.off_blocks, a.max_bdepth, a.off_crec, a.off_idtab, a.crec_lds, a.idtab_lds,
-                        a.cut, a.cut_grp, a.cut_ent, a.cut_ent_lds};
+                        a.cut, a.cut_slc, a.cut_gbase, a.cut_fp, a.cut_ent, a.cut_id, a.cut_gbase_lds,
+                        a.cut_fp_lds, a.cut_ent_lds, a.cut_id_lds};
 
     const uint64_t act_table = make_act_table(a.unsup_fw);
     // (this batch's creator counter was zeroed by the previous batch's finalize launch)
@@ -2245,7 +2257,7 @@ static size_t classify_shmem(uint32_t lds_words, int mode, int pipe, int block, 
     do {                                                             \
         if (pipe == PF_NONE) PPE_DISPATCH_B(FN, M, PF_NONE, __VA_ARGS__); \
         if (pipe == PF_MULTI) PPE_DISPATCH_B(FN, M, PF_MULTI, __VA_ARGS__); \
-        if (pipe == PF_CUT) PPE_DISPATCH_B(FN, (M == IMG_SPLIT ? IMG_GLOBAL : M), PF_CUT, __VA_ARGS__); \
+        if (pipe == PF_CUT) PPE_DISPATCH_B(FN, M, PF_CUT, __VA_ARGS__); \
         PPE_DISPATCH_B(FN, M, PF_HOIST, __VA_ARGS__);                \
     } while (0)
 #define PPE_DISPATCH(FN, ...)                                        \

@@ -149,7 +149,9 @@ def test_image_layout():
         oct_ = int(img[22])
         assert oc == oblk + 8 * nb and oi == 0 and oct_ == (oc + 4 * (nrules + 1) + 7) // 8 * 8  # compact, no holes
         h = cut_header(img)
-        assert h["grp"] == oct_ + 8 and h["ent"] % 8 == 0 and h["ent"] + 8 * h["entries"] == len(img)
+        assert h["slc"] == oct_ + 16 and h["gbase"] == h["slc"] + 4 * h["groups"] and h["fp"] == h["gbase"] + h["groups"]
+        assert h["ent"] % 4 == 0 and h["ent"] >= h["fp"] + (h["entries"] + 7) // 8 + 2
+        assert h["ids"] == h["ent"] + 4 * h["entries"] and h["ids16"] and h["ids"] + (h["entries"] + 1) // 2 == len(img)
         assert ob >= int(img[8]) and ob % 8 == 0 and oblk % 8 == 0
         if jw:
             assert np.array_equal(img[ob:ob + (1 << bits)].astype(np.int64), (roots - 4 * off) // 16)
@@ -258,11 +260,20 @@ def test_default_block_levels_and_lds_fit():
 
 def cut_header(img):
     h = int(img[22])
-    return dict(b0=int(img[h]) & 0xFF, b1=(int(img[h]) >> 8) & 0xFF, buckets=int(img[h + 1]), entries=int(img[h + 2]),
-                max_len=int(img[h + 3]), grp=int(img[h + 4]), ent=int(img[h + 5]), groups=int(img[h + 6]))
+    return dict(b0=int(img[h]) & 0xFF, b1=(int(img[h]) >> 8) & 0xFF, ids16=bool(int(img[h]) & 0x10000),
+                buckets=int(img[h + 1]), entries=int(img[h + 2]), max_len=int(img[h + 3]), slc=int(img[h + 4]),
+                ent=int(img[h + 5]), groups=int(img[h + 6]), ids=int(img[h + 7]), gbase=int(img[h + 8]),
+                fp=int(img[h + 9]))
 
 
-@pytest.mark.parametrize("bits", ["0", "1", "4", "8", "11", "16"])
+def cut_lengths(img, h):
+    """Each bucket's list length from the bit-sliced groups."""
+    sl = np.asarray(img[h["slc"]:h["slc"] + 4 * h["groups"]], np.uint32).reshape(-1, 4)
+    b = np.arange(h["buckets"])
+    return sum(((sl[b >> 5, i] >> (b & 31)) & 1).astype(np.int64) << i for i in range(4))
+
+
+@pytest.mark.parametrize("bits", ["4", "5", "8", "11", "16"])
 def test_cut_lists_equal_linear(monkeypatch, bits):
     """The cut lists (image v7) at every width, forced by PPE_CUT_BITS, against the linear definition: prefix lengths
     0 / 1 / 7 / 8 / 31 / 32 (rules replicated into the buckets they meet, lists closed after a rule that covers the
@@ -270,7 +281,7 @@ def test_cut_lists_equal_linear(monkeypatch, bits):
     entries, default FW and DROP.  The image's group table encodes each bucket's list exactly."""
     monkeypatch.setenv("PPE_CUT_BITS", bits)
     rng = np.random.default_rng(1234 + int(bits))
-    n = {0: 12, 1: 20, 4: 80}.get(int(bits), 700)  # (every list within 15 entries)
+    n = {4: 80, 5: 120}.get(int(bits), 700)  # (every list within 15 entries)
     r = synth.make_rules(n, seed=90 + int(bits))
     r["sip_mask"] = rng.choice([0, 1, 7, 8, 16, 31, 32], n, p=[0.02, 0.03, 0.1, 0.25, 0.3, 0.15, 0.15])
     r["dip_mask"] = rng.choice([0, 1, 8, 24, 32], n, p=[0.02, 0.03, 0.35, 0.3, 0.3])
@@ -288,21 +299,27 @@ def test_cut_lists_equal_linear(monkeypatch, bits):
         img, st, lin = compare(r, used, pk, default_action=da)
         assert int(img[22]) != 0, "cut lists expected"
         h = cut_header(img)
-        assert h["b0"] + h["b1"] == int(bits) and st["cut_bits"] == h["b0"] | h["b1"] << 8
-        assert h["buckets"] == 1 << int(bits) and h["groups"] == max(1, h["buckets"] // 16)
-        # the groups' lengths add up to the entries, each at most 15, and the first-entry words are their prefix sums
-        g = np.asarray(img[h["grp"]:h["grp"] + 4 * h["groups"]], np.uint32).reshape(-1, 4)
-        lens = np.array([(g[b >> 4, 1 + ((b & 15) >> 3)] >> (4 * (b & 7))) & 15 for b in range(h["buckets"])])
+        assert h["b0"] + h["b1"] == int(bits) and h["b0"] >= 2 and h["b1"] >= 2
+        assert st["cut_bits"] == h["b0"] | h["b1"] << 8
+        assert h["buckets"] == 1 << int(bits) and h["groups"] == max(1, h["buckets"] // 32)
+        # the groups' lengths add up to the entries, each at most 15, and the group bases are their prefix sums
+        lens = cut_lengths(img, h)
         assert lens.sum() == h["entries"] == st["cut_entries"] and lens.max() == h["max_len"] <= 15
-        assert np.array_equal(g[:, 0], np.concatenate([[0], np.cumsum(lens)])[: h["groups"] * 16 : 16])
+        gb = np.asarray(img[h["gbase"]:h["gbase"] + h["groups"]], np.int64)
+        assert np.array_equal(gb, np.concatenate([[0], np.cumsum(lens)])[: h["groups"] * 32 : 32])
         assert (lin["acl_hit"] >= 0).sum() > 1000
 
 
-def test_cut_lists_rejected_or_absent():
-    """No cut lists for rule sets with MAC / time fields (the classify kernel's cut check has none), and none when
-    every width leaves a bucket with more than 15 candidates (then the kernel walks the tree)."""
+def test_cut_lists_rejected_or_absent(monkeypatch):
+    """No cut lists for rule sets with MAC / time fields (the classify kernel's cut check has none), none when
+    every width leaves a bucket with more than 15 candidates (then the kernel walks the tree), and none below 4 bits
+    (each of b0, b1 >= 2 keeps a flag bit free in its relative prefix)."""
     img, st = abi.build_image(synth.make_rules(300, seed=3, resid_frac=0.3))
     assert int(img[22]) == 0 and st["cut_entries"] == 0
+    monkeypatch.setenv("PPE_CUT_BITS", "3")
+    img, st = abi.build_image(synth.make_rules(8, seed=3))
+    assert int(img[22]) == 0
+    monkeypatch.delenv("PPE_CUT_BITS")
     r = synth.make_rules(40, seed=5)
     r["sip_mask"] = 0
     r["dip_mask"] = 0  # 40 overlapping wildcard-address rules: every bucket holds all 40
@@ -316,12 +333,17 @@ def test_cut_lists_rejected_or_absent():
 
 def test_cut_lists_of_the_bench_rule_sets():
     """C3's 65,536 rules (every prefix /8 or longer): a 16-bit cut of 8 sip and 8 dip bits, no replication, at most
-    15 entries per bucket; C4's 4,096 rules: 16 bits too.  Both walks equal the linear definition."""
-    for nrules, seed in ((65536, 0x5EED), (4096, 0x5EED)):
+    15 entries per bucket, 32-bit ids; C4's 4,096 rules: a 12-bit cut, whose groups, 16-B entries and 16-bit ids fit
+    half a CU's LDS.  Both walks equal the linear definition."""
+    for nrules, seed, bits in ((65536, 0x5EED, 16), (4096, 0x5EED, 12)):
         rules = synth.make_rules(nrules)
         img, st = abi.build_image(rules)
         h = cut_header(img)
-        assert (h["b0"], h["b1"]) == (8, 8) and h["entries"] <= nrules and h["max_len"] <= 15, h
+        assert h["b0"] + h["b1"] == bits and h["entries"] <= nrules and h["max_len"] <= 15, h
+        assert nrules == 4096 or (h["b0"], h["b1"]) == (8, 8)
+        assert h["ids16"] == (nrules <= 32768)
+        if nrules == 4096:
+            assert (len(img) - h["slc"]) * 4 + 3 * 1024 <= 80 * 1024  # groups .. ids in half the LDS
         pk = synth.make_packets(20000, rules, seed=seed + 1, stride=64)
         o = pyoracle.Oracle(rules, None, default_action=1, image=img)
         lin = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=8)
