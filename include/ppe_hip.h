@@ -172,7 +172,7 @@ typedef struct {
     uint32_t blob_bytes;       /* device image size                                                        */
     uint32_t lds_resident;     /* 1 if the image is staged into LDS by the kernel                          */
     double   build_ms;
-    uint32_t cut_bits;         /* cut-list section (image v7): sip bits | dip bits << 8; 0 with cut_entries
+    uint32_t cut_bits;         /* cut-list section (image v8): sip bits | dip bits << 8; 0 with cut_entries
                                   0 = no cut lists (ABI version 6)                                            */
     uint32_t cut_entries;      /* entries of the cut lists (rules replicated into the buckets they meet)   */
 } ppe_acl_stats_t;

@@ -266,7 +266,7 @@ int32_t oracle_acl_blocks(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t d
     return -1;
 }
 
-/* Lookup in the image's cut lists (format v7, ppe_image.h): the bucket of the key's top sip / dip bits, then its
+/* Lookup in the image's cut lists (format v8, ppe_image.h): the bucket of the key's top sip / dip bits, then its
  * list's entries in priority order, each checked as a compact record (prefix marker bits, port spans, the exit's
  * protocol bits).  Like the compact leaf, only TCP / UDP keys reach it (the classify path). */
 int32_t oracle_acl_cut(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dport, uint32_t proto,
@@ -290,9 +290,11 @@ int32_t oracle_acl_cut(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dpor
     (void)dmac; (void)smac; (void)ts;
     for (uint32_t j = 0; j < cnt; j++) {
         const uint32_t e = first + j;
-        const uint32_t *r = im + h[5] + PPE_CUT_ENT_WORDS * e;
-        /* the prefixes relative to the bucket: the bits above the marker (lowest set bit without the flag bit 0) */
-        const uint32_t sm = r[0] & ~1u, dm = r[1] & ~1u;
+        const uint32_t *line = im + h[5] + PPE_CUT_LINE_WORDS * (e / h[7]);  /* 128-B line of h[7] entries + ids */
+        const uint32_t *r = line + PPE_CUT_ENT_WORDS * (e % h[7]);
+        /* the prefixes relative to the bucket: the bits above the marker (lowest set bit above the flag bits: TCP and
+         * DROP at bits 0-1 of the sip word, UDP at bit 0 of the dip word) */
+        const uint32_t sm = r[0] & ~3u, dm = r[1] & ~1u;
         const uint32_t ms = ~(((sm & (0u - sm)) << 1) - 1u), md = ~(((dm & (0u - dm)) << 1) - 1u);
         const int m = ((ks ^ sm) & ms) == 0 && ((kd ^ dm) & md) == 0 &&
                       (uint16_t)(sport - (r[2] & 0xffffu)) <= (r[3] & 0xffffu) &&
@@ -303,16 +305,14 @@ int32_t oracle_acl_cut(uint32_t sip, uint32_t dip, uint32_t sport, uint32_t dpor
         const int rejected = ((f & 2u) && (f & 1u) != ksb) || ((f & 8u) && ((f >> 2) & 1u) != kdb);
         if (rejected && m) return -2;  /* a fingerprint that would drop a match: an image error, reported as hit -2 */
         if (m) {
-            uint32_t id;
-            if (h[0] & PPE_CUT_IDS16) {
-                id = ((const uint16_t *)(im + h[7]))[e];
-                id = (id & 0x7fffu) | ((id & 0x8000u) << 16);
-            } else {
-                id = im[h[7] + e];
-            }
-            const uint32_t rid = id & 0x7fffffffu;
-            /* the action word a drop-or-forward decision needs: the classify path compares it with DROP only */
-            if (action) *action = (id >> 31) ? ACL_RULE_ACTION_DROP : oracle_rule_action(rid);
+            /* the ids after the line's entries (PPE_CUT_LINES), else in the array at h[12] */
+            const uint32_t *ids = (h[0] & PPE_CUT_LINES) ? line + PPE_CUT_ENT_WORDS * h[7] : im + h[12];
+            const uint32_t k = (h[0] & PPE_CUT_LINES) ? e % h[7] : e;
+            const uint32_t rid = (h[0] & PPE_CUT_IDS16) ? ((const uint16_t *)ids)[k] : ids[k];
+            /* the entry's DROP flag must agree with the rule's action (the classify path compares it with DROP only) */
+            const uint32_t act = oracle_rule_action(rid);
+            if (((r[0] >> 1) & 1u) != (act == ACL_RULE_ACTION_DROP)) return -3;
+            if (action) *action = act;
             return (int32_t)rid;
         }
     }

@@ -317,16 +317,17 @@ bool cut_lists(const std::vector<Rule> &R, uint32_t b0, uint32_t b1, size_t budg
 // every bit (LDS), a quarter of that when the whole cut fits half a CU's LDS (no L2 reads at all).
 // PPE_CUT_BITS=T (tests, A/B) fixes the total.  False when no cut qualifies (a list longer than 15 entries at every
 // width: then the classify kernel walks the tree).
-bool choose_cut(const std::vector<Rule> &R, CutLists &best) {
+bool choose_cut(const std::vector<Rule> &R, bool ids16, CutLists &best, bool &lds_fit) {
     const char *fb = std::getenv("PPE_CUT_BITS");
     const int force = fb && *fb ? std::atoi(fb) : -1;
     const size_t budget = 16u * (R.size() + 1u) + (1u << PPE_CUT_MAX_BITS);
     double cbest = 1e30;
     uint32_t bb0 = 0, bb1 = 0;
     bool found = false;
-    for (uint32_t T = 4; T <= PPE_CUT_MAX_BITS; ++T) {
+    lds_fit = false;
+    for (uint32_t T = 5; T <= PPE_CUT_MAX_BITS; ++T) {
         if (force >= 0 && (int)T != force) continue;
-        for (uint32_t b0 = 2; b0 + 2 <= T; ++b0) {  // (b0, b1 >= 2: each relative prefix has a free low bit)
+        for (uint32_t b0 = 3; b0 + 2 <= T; ++b0) {  // (b0 >= 3, b1 >= 2: the flag bits below the relative prefixes)
             CutLists c;
             if (!cut_lists(R, b0, T - b0, budget, c, false)) continue;
             const double nb = (double)(1u << T), ne = (double)c.n_entries;
@@ -335,7 +336,7 @@ bool choose_cut(const std::vector<Rule> &R, CutLists &best) {
             // groups (20 B per 32 buckets), 4-bit fingerprints, 16-B entries and 2-B ids in half a CU's LDS (two
             // 1024-thread workgroups, the counter bins and the staging's 1-KB rounding beside them): the whole lookup
             // runs from LDS, no L2 round
-            const bool lds = 0.625 * nb + 18.5 * ne + 3.0 * 1024 <= 80.0 * 1024 && R.size() <= 0x8000u;
+            const bool lds = 0.625 * nb + 18.5 * ne + 3.0 * 1024 <= 80.0 * 1024 && ids16;
             const double cost = (0.5 * ne / nb + 0.5 * (ne ? sq / ne : 0.0) + 0.02 * c.max_len + 0.01 * T) *
                                 (lds ? 0.25 : 1.0);
             if (std::getenv("PPE_ACL_DEBUG"))
@@ -346,6 +347,7 @@ bool choose_cut(const std::vector<Rule> &R, CutLists &best) {
                 bb0 = b0;
                 bb1 = T - b0;
                 found = true;
+                lds_fit = lds;
             }
         }
     }
@@ -560,7 +562,14 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     CutLists cut;
     const char *cenv = std::getenv("PPE_CUT");
     const bool want_cut = !any_resid && !(cenv && *cenv == '0');
-    const bool have_cut = want_cut && choose_cut(R, cut) && cut.entries.size() < (1u << 25);  // (< 1 GB of entries)
+    // rule ids in 16-bit words when every index fits (R is in index order: its last id is the largest)
+    const bool ids16 = R.empty() || R.back().id < 0x10000u;
+    bool lds_fit = false;
+    const bool have_cut = want_cut && choose_cut(R, ids16, cut, lds_fit) && cut.entries.size() < (1u << 25);  // (< 1 GB)
+    // entry lines with in-line ids for cuts read from L2 (the id read after a match hits L1); dense entries and a
+    // separate id array for those that fit LDS (where the id read costs nothing and lines would waste room)
+    const char *lenv = std::getenv("PPE_CUT_LINES");
+    const bool lines = lenv && *lenv ? *lenv == '1' : !lds_fit;
     // layout (ppe_image.h): header, bucket-length slices, group bases, fingerprints (what a lookup reads from LDS
     // when only they are staged), then the entries and ids
     const uint32_t off_cut = have_cut ? (end_tree + 7u) & ~7u : 0u;
@@ -569,11 +578,14 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     const uint32_t off_slc = off_cut + PPE_CUT_HDR_WORDS;                // 16 B per group, 16-B aligned
     const uint32_t off_gbase = off_slc + 4u * n_groups;                  // 4 B per group
     const uint32_t off_fp = off_gbase + n_groups;                        // 4 bits per entry (+ 2 pad words)
-    const uint32_t off_ent = (off_fp + (n_ent + 7u) / 8u + 2u + 3u) & ~3u;  // 16 B per entry, 16-B aligned
-    const bool ids16 = R.size() <= 0x8000u;  // rule ids (and the DROP bit) in 16-bit words
-    const uint32_t off_id = off_ent + PPE_CUT_ENT_WORDS * n_ent;
-    const uint32_t id_words = ids16 ? (n_ent + 1u) / 2u : n_ent;
-    const uint32_t total = have_cut ? off_id + id_words : end_tree;
+    // 128-B entry lines: epl 16-B entries, then (lines) their ids: 7 + 7 x 16 bit, or 6 + 6 x 32 bit; dense: 8
+    // entries, the ids after the last line
+    const uint32_t epl = !lines ? 8u : ids16 ? 7u : 6u;
+    const uint32_t off_ent = (off_fp + (n_ent + 7u) / 8u + 2u + 31u) & ~31u;  // 128-B aligned
+    const uint32_t n_lines = (n_ent + epl - 1u) / epl;
+    const uint32_t off_id = lines ? 0u : off_ent + PPE_CUT_LINE_WORDS * n_lines;
+    const uint32_t id_words = lines ? 0u : ids16 ? (n_ent + 1u) / 2u : n_ent;
+    const uint32_t total = have_cut ? off_ent + PPE_CUT_LINE_WORDS * n_lines + id_words : end_tree;
 
     uint32_t *img = (uint32_t *)std::calloc(total, sizeof(uint32_t));
     if (!img) return PPE_ENOMEM;
@@ -602,16 +614,19 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     img[PPE_IMG_W_OFFCUT] = off_cut;
     if (have_cut) {
         uint32_t *h = img + off_cut;
-        h[0] = cut.b0 | (cut.b1 << 8) | (ids16 ? PPE_CUT_IDS16 : 0u);
+        h[0] = cut.b0 | (cut.b1 << 8) | (ids16 ? PPE_CUT_IDS16 : 0u) | (lines ? PPE_CUT_LINES : 0u);
         h[1] = 1u << (cut.b0 + cut.b1);
         h[2] = n_ent;
         h[3] = cut.max_len;
         h[4] = off_slc;
         h[5] = off_ent;
         h[6] = n_groups;
-        h[7] = off_id;
+        h[7] = epl;
         h[8] = off_gbase;
         h[9] = off_fp;
+        h[10] = epl == 8u ? 0x20000000u : epl == 7u ? 0x24924925u : 0x2AAAAAABu;  // e / epl = umulhi(e, h[10]), e < 2^25
+        h[11] = n_lines;
+        h[12] = off_id;
         const uint32_t nb = h[1];
         uint32_t first = 0;
         for (uint32_t g = 0; g < n_groups; ++g) {  // the group's first entry, its 32 lengths bit-sliced
@@ -631,20 +646,22 @@ extern "C" int ppe_acl_build_image(const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
             if (len <= b) return 0x80000000u;
             return (lo << b) | (1u << (31u - (len - b)));
         };
-        uint16_t *id16 = (uint16_t *)(img + off_id);
         uint8_t *fp = (uint8_t *)(img + off_fp);
         for (uint32_t e = 0; e < n_ent; ++e) {
             const Rule &r = R[cut.entries[e]];
-            uint32_t *o = img + off_ent + PPE_CUT_ENT_WORDS * e;
+            uint32_t *line = img + off_ent + PPE_CUT_LINE_WORDS * (e / epl);
+            uint32_t *o = line + PPE_CUT_ENT_WORDS * (e % epl);
             const bool tcp = r.lo[PPE_DIM_PROTO] <= 6u && 6u <= r.hi[PPE_DIM_PROTO];
             const bool udp = r.lo[PPE_DIM_PROTO] <= 17u && 17u <= r.hi[PPE_DIM_PROTO];
-            o[0] = rel(r.lo[PPE_DIM_SIP], r.hi[PPE_DIM_SIP], cut.b0) | (tcp ? 1u : 0u);
+            const bool drop = r.action == ACL_RULE_ACTION_DROP;
+            o[0] = rel(r.lo[PPE_DIM_SIP], r.hi[PPE_DIM_SIP], cut.b0) | (drop ? 2u : 0u) | (tcp ? 1u : 0u);
             o[1] = rel(r.lo[PPE_DIM_DIP], r.hi[PPE_DIM_DIP], cut.b1) | (udp ? 1u : 0u);
             o[2] = r.lo[PPE_DIM_SPORT] | (r.lo[PPE_DIM_DPORT] << 16);
             o[3] = (r.hi[PPE_DIM_SPORT] - r.lo[PPE_DIM_SPORT]) | ((r.hi[PPE_DIM_DPORT] - r.lo[PPE_DIM_DPORT]) << 16);
-            const bool drop = r.action == ACL_RULE_ACTION_DROP;
-            if (ids16) id16[e] = (uint16_t)(r.id | (drop ? 0x8000u : 0u));
-            else img[off_id + e] = r.id | (drop ? 0x80000000u : 0u);
+            uint32_t *ids = lines ? line + PPE_CUT_ENT_WORDS * epl : img + off_id;
+            const uint32_t k = lines ? e % epl : e;
+            if (ids16) ((uint16_t *)ids)[k] = (uint16_t)r.id;
+            else ids[k] = r.id;
             // fingerprint: the first sip / dip bit below the cut, each with its "the prefix fixes it" flag
             const bool sv = plen(r.lo[PPE_DIM_SIP], r.hi[PPE_DIM_SIP]) > cut.b0;
             const bool dv = plen(r.lo[PPE_DIM_DIP], r.hi[PPE_DIM_DIP]) > cut.b1;

@@ -32,7 +32,7 @@ constexpr int kHostStreams = 3;
 constexpr int kPipeStreams = 2;
 // tile fetch / walk of the classify kernel (PF_* in ppe_kernels.hip): 0 one tile per wave, its window at the loop
 // top; 1 the first tile's loads issued before the image staging (C1 21.7 us vs 22.2); 3 the multi-tile block walk;
-// 5 the cut lists (image v7).  Register double-buffering (next tile's window, or only its first 16 B, requested
+// 5 the cut lists (image v8).  Register double-buffering (next tile's window, or only its first 16 B, requested
 // before the current tile is processed) and an LDS-DMA next-tile pipeline were measured slower.
 constexpr int kPfNone = 0, kPfHoist = 1, kPfMulti = 3, kPfCut = 5;
 constexpr uint32_t kMaxBlocksPerCU = 32;  // > resident: the grid then runs in rounds (non-persistent)
@@ -201,7 +201,7 @@ struct StagePlan {
     uint32_t bsec_lds, blk_lds;       // LDS byte offsets (from the image base in LDS) of the block section / block 0
     uint32_t crec_lds = ~0u, idtab_lds = ~0u;  // compact records / index table in LDS (byte offsets), ~0u = global
     uint32_t cut_gbase_lds = 0, cut_fp_lds = 0;    // cut lists: LDS byte offsets of the group bases / fingerprints
-    uint32_t cut_ent_lds = ~0u, cut_id_lds = ~0u;  // cut lists: entries / ids in LDS (byte offsets), ~0u = global
+    uint32_t cut_ent_lds = ~0u;                    // cut lists: entry lines in LDS (byte offset), ~0u = global
 };
 
 // LDS left for the image per workgroup when the CU holds 2048 / block workgroups (32 waves; a flow-table launch:
@@ -256,14 +256,15 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
             p.blk_lds = bjt;
         }
     };
-    // the cut lists (image v7): the bucket groups in LDS (the smallest workgroup whose share at 32 waves per CU holds
+    // the cut lists (image v8): the bucket groups in LDS (the smallest workgroup whose share at 32 waves per CU holds
     // them; the entries too when they fit beside them), the entries read from L2 otherwise; one tile per wave at 8
     // waves per SIMD.  lds_image = 0: both from global memory.
     const uint32_t off_cut = img[PPE_IMG_W_OFFCUT];
     auto cut_plan = [&]() {
         const uint32_t *h = img.data() + off_cut;
         const uint32_t grp_bytes = 4u * (h[5] - h[4]);  // slices, bases and fingerprints (the L2-entry plan's LDS)
-        const uint32_t all_words = (h[0] & PPE_CUT_IDS16 ? (h[2] + 1u) / 2u : h[2]) + h[7] - h[4];  // ... to the ids
+        const uint32_t all_words = h[5] - h[4] + 32u * h[11] +  // ... to the end of the entry lines (and the ids)
+                                   (h[0] & PPE_CUT_LINES ? 0u : h[0] & PPE_CUT_IDS16 ? (h[2] + 1u) / 2u : h[2]);
         p.pipe = kPfCut;
         p.mode = 0;
         p.block = c->tune.block ? c->tune.block : 1024u;
@@ -288,8 +289,7 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
             p.mode = 1;
             p.stage_words = all_words;
             p.cut_ent_lds = 4u * (h[5] - h[4]);
-            p.cut_id_lds = 4u * (h[7] - h[4]);
-        } else {  // slices, bases and fingerprints in LDS, entries and ids from L2 (IMG_SPLIT)
+        } else {  // slices, bases and fingerprints in LDS, the entry lines from L2 (IMG_SPLIT)
             p.mode = 2;
             p.stage_words = h[5] - h[4];
         }
@@ -560,18 +560,19 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     a.off_idtab = c->h_img[r][PPE_IMG_W_OFFIDTAB];
     a.crec_lds = plan.crec_lds;
     a.idtab_lds = plan.idtab_lds;
-    if (plan.pipe == kPfCut) {  // (image v7 cut lists: header at PPE_IMG_W_OFFCUT)
+    if (plan.pipe == kPfCut) {  // (image v8 cut lists: header at PPE_IMG_W_OFFCUT)
         const uint32_t *h = c->h_img[r].data() + c->h_img[r][PPE_IMG_W_OFFCUT];
         a.cut = h[0];
         a.cut_slc = h[4];
         a.cut_ent = h[5];
-        a.cut_id = h[7];
+        a.cut_epl = h[7];
+        a.cut_div = h[10];
+        a.cut_idrel = (h[0] & PPE_CUT_LINES) ? 0u : 4u * (h[12] - h[5]);
         a.cut_gbase = h[8];
         a.cut_fp = h[9];
         a.cut_gbase_lds = plan.cut_gbase_lds;
         a.cut_fp_lds = plan.cut_fp_lds;
         a.cut_ent_lds = plan.cut_ent_lds;
-        a.cut_id_lds = plan.cut_id_lds;
     }
     // batch groups: the kernel splits its waves into min(batches, max_groups) groups, group g taking batches g, g + G,
     // ...; when G does not divide the batch count the last round leaves groups idle (20 batches at G = 8: the last
@@ -1115,7 +1116,7 @@ int ppe_set_tuning(ppe_ctx_t *c, const ppe_tuning_t *t) {
     if (t->pipeline != 0 && t->pipeline != 1 && t->pipeline != 3 && t->pipeline != 4 && t->pipeline != 5)
         return fail(c, PPE_EINVAL, "pipeline must be 0 (auto), 1 (first tile at the loop top), 3 (4 tiles per wave "
                                    "walking the block section together), 4 (first tile's loads before the image "
-                                   "staging) or 5 (the cut lists of a v7 image)");
+                                   "staging) or 5 (the cut lists of a v8 image)");
     if (t->blocks_per_cu > kMaxBlocksPerCU) return fail(c, PPE_EINVAL, "blocks_per_cu must be <= 32");
     if (t->batches_per_launch > PPE_MAX_RING) return fail(c, PPE_EINVAL, "batches_per_launch must be <= 4096");
     c->tune = *t;

@@ -1,5 +1,5 @@
 /*
- * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v7.
+ * ppe_image.h — layout of the device classifier image (one flat array of u32 words), format v8.
  *
  * The image is a HyperSplit-style binary decision tree over the five header dimensions, flattened in BFS order
  * (children of node k are numbered after k, so a walk strictly descends and always terminates), followed by the
@@ -19,7 +19,7 @@
  *  word 19  off_crec: word offset of the compact records (v6), 0 = the image has none
  *  word 20  off_idtab: word offset of the slot → rule index table, 0 = slot == rule index for every slot
  *  word 21  block levels: 2 (32-B blocks)
- *  word 22  off_cut: word offset of the cut-list section (v7), 0 = the image has none
+ *  word 22  off_cut: word offset of the cut-list section (v8), 0 = the image has none
  *  words 23..31 reserved
  *
  *  jump table (format v4; present iff word 14 != 0): 2^bits words right after the header.  A walk starts at
@@ -85,16 +85,17 @@
  *      The address matches iff (key ^ word) has no bit set above the marker bit (every bit for a /32).
  *  idtab (word 20 != 0): n_rules words, the rule index of each slot (when unused entries make slots != indices)
  *
- *  cut-list section (v7; present iff word 22 != 0: every rule without residual MAC / time fields).  A second,
+ *  cut-list section (v8; present iff word 22 != 0: every rule without residual MAC / time fields).  A second,
  *  independent classifier for the classify kernel (TCP / UDP keys only): a HyperCuts-style cut of the top b0 bits
  *  of sip and the top b1 bits of dip into 2^(b0 + b1) buckets, bucket = (sip >> (32 - b0)) << b1 | dip >> (32 - b1)
- *  (b0, b1 >= 2), and per bucket the list of the rules whose box meets it, in priority order, closed after the first
+ *  (b0 >= 3, b1 >= 2), and per bucket the list of the rules whose box meets it, in priority order, closed after the first
  *  rule that covers the whole bucket (every port, TCP and UDP).  The builder picks b0, b1 (b0 + b1 <= 16) by the
  *  expected list length (strongly preferring a cut whose groups, entries and ids fit half a CU's LDS) and rejects the
  *  section when a list would exceed 15 entries.  A lookup is one read of the bucket's group and one round of
  *  independent 16-B entry reads (LDS, or L2 for large sets): no dependent walk; a match reads its rule id.
  *      header (16 words at off_cut): b0 | b1 << 8 | PPE_CUT_IDS16, n_buckets, n_entries, max list length,
- *          off_slc, off_ent, n_groups, off_id, off_gbase, off_fp (word offsets from the image start), 0...
+ *          off_slc, off_ent, n_groups, epl (entries per line), off_gbase, off_fp (word offsets from the image start),
+ *          div (e / epl = umulhi(e, div) for e < 2^25), n_lines, off_id (0 with PPE_CUT_LINES), 0...
  *      groups of 32 buckets (group g = buckets 32 g .. 32 g + 31): slices (4 words, 16-B aligned, at off_slc + 4 g):
  *          bit k of word i = bit i of bucket 32 g + k's list length (0..15); base (1 word, at off_gbase + g): the
  *          group's first entry.  Bucket b's list = entries [first(b), first(b) + len(b)), first(b) = base +
@@ -103,21 +104,24 @@
  *          bit 0 = the rule's sip bit 31 - b0 (the first below the cut), bit 1 = its prefix fixes that bit, bits 2 / 3
  *          likewise for dip bit 31 - b1.  A lookup skips an entry whose fixed bits differ from the key's (it cannot
  *          match), so most entries that would not match are never read.
-  *      entries (4 words each, 16-B aligned, contiguous per bucket in priority order):
- *          sip relative to the bucket | TCP: the prefix's bits below the top b0, shifted up by b0, then a marker bit
- *              (so the bits above the lowest set bit of the word without bit 0 must equal the key's sip << b0); a
- *              /32 puts the marker at bit b0 - 1 (>= 1); a prefix of at most b0 bits matches the whole bucket:
- *              0x80000000.  Bit 0: the rule's protocol range contains 6.
- *          dip relative to the bucket | UDP (bit 0: contains 17), likewise with b1
+  *      entry lines (128 B each, 128-B aligned, at off_ent): epl entries (16 B each, entry e in line e / epl at slot
+ *          e mod epl; contiguous per bucket in priority order).  PPE_CUT_LINES (cuts read from L2): then the line's
+ *          rule ids (a matching entry's id shares its line: read right after it, from L1), epl = 7 with 16-bit ids,
+ *          6 with 32-bit ids.  Otherwise (cuts that fit LDS) epl = 8 and the ids follow the last line, one per entry
+ *          (at off_id).  16-bit ids when PPE_CUT_IDS16 (every index < 2^16), else 32-bit.  An entry:
+ *          sip relative to the bucket | DROP | TCP: the prefix's bits below the top b0, shifted up by b0, then a
+ *              marker bit (so the bits above the lowest set bit of the word without bits 0-1 must equal the key's
+ *              sip << b0); a /32 puts the marker at bit b0 - 1 (>= 2); a prefix of at most b0 bits matches the whole
+ *              bucket: 0x80000000.  Bit 0: the rule's protocol range contains 6; bit 1: its action is
+ *              ACL_RULE_ACTION_DROP (the verdict needs no id read).
+ *          dip relative to the bucket | UDP (bit 0: contains 17), likewise with b1 (marker at bit >= 1)
  *          sport_lo | dport_lo << 16;  (sport_hi - sport_lo) | (dport_hi - dport_lo) << 16
- *      ids (one per entry, read on a match): rule index | DROP (action == ACL_RULE_ACTION_DROP) in the top bit,
- *          16-bit words when PPE_CUT_IDS16 (every index < 2^15), else 32-bit words
   */
 #ifndef PPE_IMAGE_H
 #define PPE_IMAGE_H
 
 #define PPE_IMG_MAGIC   0x41455050u /* "PPEA" */
-#define PPE_IMG_VERSION 7u
+#define PPE_IMG_VERSION 8u
 #define PPE_IMG_HDR_WORDS 32u
 
 #define PPE_IMG_W_NNODES   2
@@ -154,7 +158,9 @@
 #define PPE_CREC_WORDS 4u
 #define PPE_CUT_HDR_WORDS 16u
 #define PPE_CUT_ENT_WORDS 4u      /* cut-list entry (16 B) */
+#define PPE_CUT_LINE_WORDS 32u    /* cut-list entry line (128 B) */
 #define PPE_CUT_IDS16 0x10000u    /* cut header word 0: 16-bit rule ids */
+#define PPE_CUT_LINES 0x20000u    /* cut header word 0: rule ids inside the entry lines */
 #define PPE_CUT_MAX_LIST 15u      /* longest bucket list (4-bit lengths) */
 #define PPE_CUT_MAX_BITS 16u      /* b0 + b1: 2^16 buckets = 64 KB of groups */
 

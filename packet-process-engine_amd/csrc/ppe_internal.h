@@ -140,11 +140,13 @@ struct ppe_kargs {
     uint32_t off_bsec, off_blocks, max_bdepth; /* image header words 15, 17, 18                                  */
     uint32_t off_crec, off_idtab; /* image header words 19, 20: compact leaf records / slot → index table (0 = none) */
     uint32_t crec_lds, idtab_lds; /* their LDS byte offsets from the LDS image base, ~0u = read from global memory   */
-    uint32_t cut;             /* cut-list walks (image v7): cut header word 0 (sip bits | dip bits << 8 | ids16)     */
-    uint32_t cut_slc, cut_gbase, cut_fp, cut_ent, cut_id;  /* word offsets of the length slices / group bases /
-                                                              fingerprints / entries / ids in the image              */
-    uint32_t cut_gbase_lds, cut_fp_lds, cut_ent_lds, cut_id_lds;  /* their LDS byte offsets from the LDS image base
-                                                              (the slices are at it; entries and ids: IMG_LDS only)  */
+    uint32_t cut;             /* cut-list walks (image v8): cut header word 0 (sip bits | dip bits << 8 | ids16)     */
+    uint32_t cut_slc, cut_gbase, cut_fp, cut_ent;  /* word offsets of the length slices / group bases / fingerprints /
+                                                      entry lines in the image                                       */
+    uint32_t cut_epl, cut_div;  /* entries per 128-B line, and the divisor magic (e / epl = umulhi(e, cut_div))      */
+    uint32_t cut_idrel;         /* without PPE_CUT_LINES: the id array's byte offset from the entry lines             */
+    uint32_t cut_gbase_lds, cut_fp_lds, cut_ent_lds;  /* their LDS byte offsets from the LDS image base (the slices
+                                                         are at it; the entry lines: IMG_LDS only)                   */
     uint32_t max_groups;      /* most batch groups of waves (concurrently streamed batches)                          */
     uint32_t part_layout;     /* 1: every batch writes verdict + flow hash + ACL hit and one partition list (fw_idx ==
                                  drop_idx), no tile counts, no tuple: the kernel variant with those checks compiled out */

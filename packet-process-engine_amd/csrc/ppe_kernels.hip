@@ -415,10 +415,12 @@ struct AclGeo {
     // compact leaves (image v6): record / index-table word offsets (0 = none), and their LDS byte offsets from the
     // staged image base (~0u = read from global memory)
     uint32_t off_crec, off_idtab, crec_lds, idtab_lds;
-    // cut lists (image v7): header word 0 (sip bits | dip bits << 8 | PPE_CUT_IDS16), word offsets of the length
-    // slices / group bases / fingerprints / entries / ids, and the LDS byte offsets of the bases, fingerprints,
-    // entries and ids from the staged image base (the slices are at it; entries and ids only when the mode is IMG_LDS)
-    uint32_t cut, cut_slc, cut_gbase, cut_fp, cut_ent, cut_id, cut_gbase_lds, cut_fp_lds, cut_ent_lds, cut_id_lds;
+    // cut lists (image v8): header word 0 (sip bits | dip bits << 8 | PPE_CUT_IDS16), word offsets of the length
+    // slices / group bases / fingerprints / entry lines, entries per line and its divisor magic, and the LDS byte
+    // offsets of the bases, fingerprints and entry lines from the staged image base (the slices are at it; the entry
+    // lines only when the mode is IMG_LDS)
+    uint32_t cut, cut_slc, cut_gbase, cut_fp, cut_ent, cut_epl, cut_div, cut_idrel, cut_gbase_lds, cut_fp_lds,
+        cut_ent_lds;
 };
 
 // One level of the walk, node and key both in flight: the node's child pointer carries the child's key slot, so
@@ -629,15 +631,17 @@ __device__ __forceinline__ void acl_leaf_compact(const uint32_t *__restrict__ gi
     crec_check<IMGB>(gimg, g, x, crec_load<IMGB>(gimg, g, x), sip, dip, sport, dport, tcp, hit, drop);
 }
 
-// Cut-list lookup (image v7, ppe_image.h): the bucket of the key's top sip / dip bits; its group's length slices
+// Cut-list lookup (image v8, ppe_image.h): the bucket of the key's top sip / dip bits; its group's length slices
 // and base (LDS when staged) give the bucket's list; the entries' 4-bit fingerprints (LDS) drop the entries whose
 // fixed sip / dip bit below the cut differs from the key's; the rest are independent 16-B reads (LDS, or L2 for large
-// sets), two per round, checked in priority order; a match reads its rule id.  Only TCP / UDP keys reach it (the
-// classify path).
+// sets), two per round, checked in priority order.  The matching entry carries the verdict (its DROP flag); its rule
+// id, for the hit output, sits in the same 128-B line (an L1 hit after the entry's read).  Only TCP / UDP keys reach
+// it (the classify path).
 // one entry against the key's bucket-relative addresses (ks = sip << b0, kd = dip << b1): each prefix matches iff the
-// bits above its marker (the lowest set bit without the flag bit 0) equal the key's; ports by packed 16-bit spans
+// bits above its marker (the lowest set bit above the flag bits: 0-1 in the sip word, 0 in the dip word) equal the
+// key's; ports by packed 16-bit spans
 __device__ __forceinline__ bool cut_match(const uint4 r, uint32_t ks, uint32_t kd, uint32_t ports, bool tcp) {
-    const uint32_t sm = r.x & ~1u, dm = r.y & ~1u;
+    const uint32_t sm = r.x & ~3u, dm = r.y & ~1u;
     const uint32_t ms = ~(((sm & (0u - sm)) << 1) - 1u), md = ~(((dm & (0u - dm)) << 1) - 1u);
     const u16x2 kp = __builtin_bit_cast(u16x2, ports), lo = __builtin_bit_cast(u16x2, r.z),
                 sp = __builtin_bit_cast(u16x2, r.w);
@@ -646,6 +650,17 @@ __device__ __forceinline__ bool cut_match(const uint4 r, uint32_t ks, uint32_t k
 }
 // MODE: IMG_GLOBAL everything from global memory; IMG_SPLIT slices, bases and fingerprints in LDS, entries and ids
 // from global (L2); IMG_LDS all of it in LDS
+#ifndef PPE_CUT_SPEC
+#define PPE_CUT_SPEC 1
+#endif
+// candidate entries read per round: from L2, 4 (about 1 wave in 3 has a lane with a third candidate after the
+// fingerprints, which would cost it a second round trip at 2: C3 ring step -1.5 %, r5p); from LDS, 2 (4: +1 %)
+#ifndef PPE_CUT_W_L2
+#define PPE_CUT_W_L2 4
+#endif
+#ifndef PPE_CUT_W_LDS
+#define PPE_CUT_W_LDS 2
+#endif
 template <int MODE, int IMGB>
 __device__ __forceinline__ void acl_cut(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t sip, uint32_t dip,
                                         uint32_t ports, bool tcp, int32_t &hit, bool &drop) {
@@ -670,40 +685,64 @@ __device__ __forceinline__ void acl_cut(const uint32_t *__restrict__ gimg, const
     const uint64_t fail = (M | (M >> 2)) & 0x1111111111111111ull;
     uint64_t P = ((1ull << (4u * cnt)) - 1u) & 0x1111111111111111ull & ~fail;  // candidate j at bit 4 j
     const uint32_t ks = sip << b0, kd = dip << b1;
-    bool found = false;
-    uint32_t ef = 0;  // the matching entry
+    // entry e: line e / epl (e / epl = umulhi(e, div)), slot e mod epl; byte offset from the entry section
+    const uint32_t epl = g.cut_epl;
+    auto ebyte = [&](uint32_t e) {
+        const uint32_t ln = __umulhi(e, g.cut_div);
+        return 128u * ln + 16u * (e - ln * epl);
+    };
+    bool found = false, edrop = false;  // a match; its DROP flag
+    uint32_t eb = 0;                    // its byte offset
+    const bool i16 = (g.cut & PPE_CUT_IDS16) != 0u;
+    const uint32_t iw = i16 ? 2u : 4u;
+    // the id's byte offset (after the line's epl entries by slot, or in the id array by entry: dense eb = 16 e)
+    auto ibyte = [&](uint32_t b) {
+        return (g.cut & PPE_CUT_LINES) ? (b & ~127u) + 16u * epl + iw * ((b & 127u) >> 4) : g.cut_idrel + iw * (b >> 4);
+    };
+    // entry lines from L2: each candidate's id word is requested right behind its entry, from the same line (the
+    // second request joins the first's miss: no L2 request of its own, and no dependent id round after a match)
+    const bool spec = PPE_CUT_SPEC && MODE != IMG_LDS && (g.cut & PPE_CUT_LINES) != 0u;
+    constexpr int W = MODE == IMG_LDS ? PPE_CUT_W_LDS : PPE_CUT_W_L2;
+    uint32_t idw = 0;  // (spec) the match's id word
 #pragma unroll 1
     for (uint32_t round = 0; round < 8u; ++round) {
-        const bool a0 = !found && P != 0u;
-        if (__builtin_amdgcn_ballot_w64(a0) == 0) break;
-        const uint32_t j0 = a0 ? (uint32_t)__builtin_ctzll(P) >> 2 : 0u;
-        P = a0 ? P & (P - 1u) : P;
-        const bool a1 = a0 && P != 0u;
-        const uint32_t j1 = a1 ? (uint32_t)__builtin_ctzll(P) >> 2 : 0u;
-        P = a1 ? P & (P - 1u) : P;
-        uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0;
-        const uint32_t e0 = first + j0, e1 = first + j1;
-        if (a0) r0 = MODE == IMG_LDS ? lds_u128(IMGB + g.cut_ent_lds + 16u * e0) : gld<uint4>(gimg, 4u * g.cut_ent + 16u * e0);
-        if (a1) r1 = MODE == IMG_LDS ? lds_u128(IMGB + g.cut_ent_lds + 16u * e1) : gld<uint4>(gimg, 4u * g.cut_ent + 16u * e1);
-        const bool m0 = a0 && cut_match(r0, ks, kd, ports, tcp);  // (in priority order: the first match wins)
-        const bool m1 = a1 && !m0 && cut_match(r1, ks, kd, ports, tcp);
-        ef = m0 ? e0 : (m1 ? e1 : ef);
-        found = found || m0 || m1;
-    }
-    hit = -1;
-    drop = g.default_action == ACL_RULE_ACTION_DROP;
-    if (found) {  // the rule index and its DROP bit
-        uint32_t id;
-        if (g.cut & PPE_CUT_IDS16) {
-            const uint32_t o = 2u * ef, w = MODE == IMG_LDS ? lds_u32(IMGB + g.cut_id_lds + (o & ~3u))
-                                                              : gld<uint32_t>(gimg, 4u * g.cut_id + (o & ~3u));
-            id = (w >> (8u * (o & 2u))) & 0xffffu;
-            id = (id & 0x7fffu) | ((id & 0x8000u) << 16);
-        } else {
-            id = MODE == IMG_LDS ? lds_u32(IMGB + g.cut_id_lds + 4u * ef) : gld<uint32_t>(gimg, 4u * g.cut_id + 4u * ef);
+        bool a[W];
+        a[0] = !found && P != 0u;
+        if (__builtin_amdgcn_ballot_w64(a[0]) == 0) break;
+        uint32_t be[W], iv[W];
+        uint4 r[W];
+#pragma unroll
+        for (int c = 0; c < W; ++c) {  // the next W candidates, in priority order
+            if (c) a[c] = a[c - 1] && P != 0u;
+            const uint32_t j = a[c] ? (uint32_t)__builtin_ctzll(P) >> 2 : 0u;
+            P = a[c] ? P & (P - 1u) : P;
+            be[c] = ebyte(first + j);
         }
-        hit = (int32_t)(id & 0x7fffffffu);
-        drop = (id >> 31) != 0u;
+#pragma unroll
+        for (int c = 0; c < W; ++c) {
+            r[c] = make_uint4(0u, 0u, 0u, 0u);
+            iv[c] = 0u;
+            if (a[c]) {
+                r[c] = MODE == IMG_LDS ? lds_u128(IMGB + g.cut_ent_lds + be[c]) : gld<uint4>(gimg, 4u * g.cut_ent + be[c]);
+                if (spec) iv[c] = gld<uint32_t>(gimg, 4u * g.cut_ent + (ibyte(be[c]) & ~3u));
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < W; ++c) {  // the first match wins
+            const bool m = a[c] && !found && cut_match(r[c], ks, kd, ports, tcp);
+            eb = m ? be[c] : eb;
+            idw = m ? iv[c] : idw;
+            edrop = m ? (r[c].x & 2u) != 0u : edrop;
+            found = found || m;
+        }
+    }
+    drop = found ? edrop : g.default_action == ACL_RULE_ACTION_DROP;
+    hit = -1;
+    if (found) {  // the rule index
+        const uint32_t ib = ibyte(eb);
+        if (!spec)
+            idw = MODE == IMG_LDS ? lds_u32(IMGB + g.cut_ent_lds + (ib & ~3u)) : gld<uint32_t>(gimg, 4u * g.cut_ent + (ib & ~3u));
+        hit = (int32_t)(i16 ? (idw >> (8u * (ib & 2u))) & 0xffffu : idw);
     }
 }
 
@@ -1281,8 +1320,8 @@ void ppe_classify_kernel(ppe_kargs a) {
     const AclGeo geo = {a.lds_iters, a.max_depth, a.max_leaf, a.root_ks, a.off_leaf, a.off_rules, a.off_resid,
                         a.lds_words, a.default_action, a.jump, a.off_nodes, a.lds_blocks, a.bsec_lds, a.blk_lds,
                         a.off_bsec, a.off_blocks, a.max_bdepth, a.off_crec, a.off_idtab, a.crec_lds, a.idtab_lds,
-                        a.cut, a.cut_slc, a.cut_gbase, a.cut_fp, a.cut_ent, a.cut_id, a.cut_gbase_lds,
-                        a.cut_fp_lds, a.cut_ent_lds, a.cut_id_lds};
+                        a.cut, a.cut_slc, a.cut_gbase, a.cut_fp, a.cut_ent, a.cut_epl, a.cut_div, a.cut_idrel,
+                        a.cut_gbase_lds, a.cut_fp_lds, a.cut_ent_lds};
 
     const uint64_t act_table = make_act_table(a.unsup_fw);
     // (this batch's creator counter was zeroed by the previous batch's finalize launch)

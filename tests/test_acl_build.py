@@ -17,7 +17,7 @@ def compare(rules, used, pk, default_action=1, binth=0, cfg=None):
     lin = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4)
     tree = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4, use_tree=True)
     # the image's 2-level block section (what the multi-tile kernel walks) must give the same answers, and so must its
-    # cut lists (image v7: what the cut-list kernel reads) when it has them
+    # cut lists (image v8: what the cut-list kernel reads) when it has them
     blocks = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4, use_tree=2)
     cut = o.classify_batch(pk["hdr"], pk["len"], ts=pk.get("ts"), cfg=cfg, nthreads=4, use_tree=3) if img[22] else lin
     for k in ("verdict", "acl_hit", "flow_hash", "counters"):
@@ -99,14 +99,14 @@ def test_large_ruleset_builds_bounded():
 
 
 def test_image_layout():
-    """Image format v7 (csrc/ppe_image.h): optional jump table after the 32-word header, 16-B nodes {threshold, left,
+    """Image format v8 (csrc/ppe_image.h): optional jump table after the 32-word header, 16-B nodes {threshold, left,
     right, child key slots}, leaves as walk fixed points, the always-matching sentinel rule at slot n_rules, the
     2-level block section, the compact records after it (one candidate per leaf, no residual rules), then the cut
     lists (32-B aligned header, groups, entries)."""
     for nrules in (64, 256):
         rules = synth.make_rules(nrules)
         img, st = abi.build_image(rules)
-        assert img[0] == 0x41455050 and img[1] == 7
+        assert img[0] == 0x41455050 and img[1] == 8
         assert img[2] == st["n_nodes"] and img[4] == nrules and img[11] == len(img)
         assert img[7] % 8 == 0  # rules 32-B aligned
         off = int(img[5])
@@ -150,8 +150,10 @@ def test_image_layout():
         assert oc == oblk + 8 * nb and oi == 0 and oct_ == (oc + 4 * (nrules + 1) + 7) // 8 * 8  # compact, no holes
         h = cut_header(img)
         assert h["slc"] == oct_ + 16 and h["gbase"] == h["slc"] + 4 * h["groups"] and h["fp"] == h["gbase"] + h["groups"]
-        assert h["ent"] % 4 == 0 and h["ent"] >= h["fp"] + (h["entries"] + 7) // 8 + 2
-        assert h["ids"] == h["ent"] + 4 * h["entries"] and h["ids16"] and h["ids"] + (h["entries"] + 1) // 2 == len(img)
+        assert h["ent"] % 32 == 0 and h["fp"] + (h["entries"] + 7) // 8 + 2 <= h["ent"] < h["fp"] + (h["entries"] + 7) // 8 + 34
+        # (a cut that fits LDS: dense lines of 8 entries, the 16-bit ids after them)
+        assert h["ids16"] and not h["lines_ids"] and h["epl"] == 8 and h["div"] == 1 << 29
+        assert h["off_id"] == h["ent"] + 32 * h["lines"] and h["off_id"] + (h["entries"] + 1) // 2 == len(img)
         assert ob >= int(img[8]) and ob % 8 == 0 and oblk % 8 == 0
         if jw:
             assert np.array_equal(img[ob:ob + (1 << bits)].astype(np.int64), (roots - 4 * off) // 16)
@@ -261,9 +263,24 @@ def test_default_block_levels_and_lds_fit():
 def cut_header(img):
     h = int(img[22])
     return dict(b0=int(img[h]) & 0xFF, b1=(int(img[h]) >> 8) & 0xFF, ids16=bool(int(img[h]) & 0x10000),
+                lines_ids=bool(int(img[h]) & 0x20000), off_id=int(img[h + 12]),
                 buckets=int(img[h + 1]), entries=int(img[h + 2]), max_len=int(img[h + 3]), slc=int(img[h + 4]),
-                ent=int(img[h + 5]), groups=int(img[h + 6]), ids=int(img[h + 7]), gbase=int(img[h + 8]),
-                fp=int(img[h + 9]))
+                ent=int(img[h + 5]), groups=int(img[h + 6]), epl=int(img[h + 7]), gbase=int(img[h + 8]),
+                fp=int(img[h + 9]), div=int(img[h + 10]), lines=int(img[h + 11]))
+
+
+def cut_entries(img, h):
+    """The entries (n x 4 words) and rule ids of the image's 128-B entry lines (ids in-line, or the id array)."""
+    lines = np.asarray(img[h["ent"]:h["ent"] + 32 * h["lines"]], np.uint32).reshape(-1, 32)
+    epl = h["epl"]
+    ent = lines[:, : 4 * epl].reshape(-1, 4)[: h["entries"]]
+    if h["lines_ids"]:
+        tail = lines[:, 4 * epl:]
+        ids = (tail.view(np.uint16)[:, :epl] if h["ids16"] else tail[:, :epl]).reshape(-1)
+    else:
+        arr = np.asarray(img[h["off_id"]:], np.uint32)
+        ids = arr.view(np.uint16) if h["ids16"] else arr
+    return ent, ids[: h["entries"]].astype(np.int64)
 
 
 def cut_lengths(img, h):
@@ -273,15 +290,18 @@ def cut_lengths(img, h):
     return sum(((sl[b >> 5, i] >> (b & 31)) & 1).astype(np.int64) << i for i in range(4))
 
 
-@pytest.mark.parametrize("bits", ["4", "5", "8", "11", "16"])
-def test_cut_lists_equal_linear(monkeypatch, bits):
-    """The cut lists (image v7) at every width, forced by PPE_CUT_BITS, against the linear definition: prefix lengths
+@pytest.mark.parametrize("lines", ["0", "1"])
+@pytest.mark.parametrize("bits", ["5", "6", "8", "11", "16"])
+def test_cut_lists_equal_linear(monkeypatch, bits, lines):
+    """The cut lists (image v8) at every width, forced by PPE_CUT_BITS, against the linear definition: prefix lengths
     0 / 1 / 7 / 8 / 31 / 32 (rules replicated into the buckets they meet, lists closed after a rule that covers the
     whole bucket), any-port rules, protocol ranges with and without 6 / 17, actions other than 0 / 1, unused
-    entries, default FW and DROP.  The image's group table encodes each bucket's list exactly."""
+    entries, default FW and DROP, with the ids in the entry lines and in their own array (PPE_CUT_LINES).  The image's
+    group table encodes each bucket's list exactly."""
     monkeypatch.setenv("PPE_CUT_BITS", bits)
+    monkeypatch.setenv("PPE_CUT_LINES", lines)
     rng = np.random.default_rng(1234 + int(bits))
-    n = {4: 80, 5: 120}.get(int(bits), 700)  # (every list within 15 entries)
+    n = {5: 80, 6: 120}.get(int(bits), 700)  # (every list within 15 entries)
     r = synth.make_rules(n, seed=90 + int(bits))
     r["sip_mask"] = rng.choice([0, 1, 7, 8, 16, 31, 32], n, p=[0.02, 0.03, 0.1, 0.25, 0.3, 0.15, 0.15])
     r["dip_mask"] = rng.choice([0, 1, 8, 24, 32], n, p=[0.02, 0.03, 0.35, 0.3, 0.3])
@@ -299,7 +319,7 @@ def test_cut_lists_equal_linear(monkeypatch, bits):
         img, st, lin = compare(r, used, pk, default_action=da)
         assert int(img[22]) != 0, "cut lists expected"
         h = cut_header(img)
-        assert h["b0"] + h["b1"] == int(bits) and h["b0"] >= 2 and h["b1"] >= 2
+        assert h["b0"] + h["b1"] == int(bits) and h["b0"] >= 3 and h["b1"] >= 2
         assert st["cut_bits"] == h["b0"] | h["b1"] << 8
         assert h["buckets"] == 1 << int(bits) and h["groups"] == max(1, h["buckets"] // 32)
         # the groups' lengths add up to the entries, each at most 15, and the group bases are their prefix sums
@@ -308,15 +328,38 @@ def test_cut_lists_equal_linear(monkeypatch, bits):
         gb = np.asarray(img[h["gbase"]:h["gbase"] + h["groups"]], np.int64)
         assert np.array_equal(gb, np.concatenate([[0], np.cumsum(lens)])[: h["groups"] * 32 : 32])
         assert (lin["acl_hit"] >= 0).sum() > 1000
+        # each entry's DROP flag (sip word bit 1) is its rule's action; 16-bit ids (every index < 2^16)
+        ent, ids = cut_entries(img, h)
+        assert h["lines_ids"] == (lines == "1")
+        epl = 7 if h["lines_ids"] else 8
+        assert h["ids16"] and h["epl"] == epl and h["lines"] == -(-h["entries"] // epl) and h["ent"] % 32 == 0
+        assert np.array_equal((ent[:, 0] >> 1) & 1, (np.asarray(r["action"])[ids] == 1).astype(np.uint32))
+
+
+def test_cut_lists_rule_indices_above_32767():
+    """40,000 rules, half of them unused: 20,000 in the image but indices up to 39,999, which the 16-bit id words
+    hold whole (the DROP flag lives in the entry); the cut walk equals the linear definition."""
+    n = 40_000
+    rng = np.random.default_rng(77)
+    r = synth.make_rules(n, seed=78)
+    r["action"] = rng.choice([0, 1, 2], n)
+    used = (rng.random(n) < 0.5).astype(np.uint8)
+    pk = synth.make_packets(20000, r, seed=79, stride=64, hit_frac=0.8)
+    img, st, lin = compare(r, used, pk, default_action=1)
+    h = cut_header(img)
+    assert h["ids16"] and h["entries"] > 0
+    _, ids = cut_entries(img, h)
+    assert ids.max() >= 32768 and used[ids].all()
+    assert (lin["acl_hit"] >= 32768).sum() > 1000
 
 
 def test_cut_lists_rejected_or_absent(monkeypatch):
     """No cut lists for rule sets with MAC / time fields (the classify kernel's cut check has none), none when
-    every width leaves a bucket with more than 15 candidates (then the kernel walks the tree), and none below 4 bits
-    (each of b0, b1 >= 2 keeps a flag bit free in its relative prefix)."""
+    every width leaves a bucket with more than 15 candidates (then the kernel walks the tree), and none below 5 bits
+    (b0 >= 3 and b1 >= 2 keep the flag bits free below the relative prefixes)."""
     img, st = abi.build_image(synth.make_rules(300, seed=3, resid_frac=0.3))
     assert int(img[22]) == 0 and st["cut_entries"] == 0
-    monkeypatch.setenv("PPE_CUT_BITS", "3")
+    monkeypatch.setenv("PPE_CUT_BITS", "4")
     img, st = abi.build_image(synth.make_rules(8, seed=3))
     assert int(img[22]) == 0
     monkeypatch.delenv("PPE_CUT_BITS")
@@ -333,7 +376,7 @@ def test_cut_lists_rejected_or_absent(monkeypatch):
 
 def test_cut_lists_of_the_bench_rule_sets():
     """C3's 65,536 rules (every prefix /8 or longer): a 16-bit cut of 8 sip and 8 dip bits, no replication, at most
-    15 entries per bucket, 32-bit ids; C4's 4,096 rules: a 12-bit cut, whose groups, 16-B entries and 16-bit ids fit
+    15 entries per bucket, 16-bit ids; C4's 4,096 rules: a 12-bit cut, whose groups, 16-B entries and 16-bit ids fit
     half a CU's LDS.  Both walks equal the linear definition."""
     for nrules, seed, bits in ((65536, 0x5EED, 16), (4096, 0x5EED, 12)):
         rules = synth.make_rules(nrules)
@@ -341,7 +384,9 @@ def test_cut_lists_of_the_bench_rule_sets():
         h = cut_header(img)
         assert h["b0"] + h["b1"] == bits and h["entries"] <= nrules and h["max_len"] <= 15, h
         assert nrules == 4096 or (h["b0"], h["b1"]) == (8, 8)
-        assert h["ids16"] == (nrules <= 32768)
+        assert h["ids16"]
+        # C3 reads its entries from L2: ids in the lines; C4's cut fits LDS: dense entries and the id array
+        assert h["lines_ids"] == (nrules == 65536)
         if nrules == 4096:
             assert (len(img) - h["slc"]) * 4 + 3 * 1024 <= 80 * 1024  # groups .. ids in half the LDS
         pk = synth.make_packets(20000, rules, seed=seed + 1, stride=64)

@@ -316,14 +316,16 @@ def test_c3_64k_rules_vs_oracle(eng):
         eng.tuning(**old)
 
 
-@pytest.mark.parametrize("bits", ["4", "5", "11", "16"])
+@pytest.mark.parametrize("bits", ["5", "6", "11", "16"])
 def test_cut_lists_forced_widths(eng, monkeypatch, bits):
     """The cut-list kernel (pipeline 5) at forced cut widths (PPE_CUT_BITS) over rules with short and wildcard
     prefixes (replicated into every bucket they meet), any-port rules and protocol ranges with and without 6 / 17,
-    IMIX with VLAN tags, TCP and malformed packets, groups and entries in LDS or global: against the linear oracle."""
+    IMIX with VLAN tags, TCP and malformed packets, groups and entries in LDS or global, rule ids in the entry lines
+    (5 / 16 bits) or in their own array (6 / 11): against the linear oracle."""
     monkeypatch.setenv("PPE_CUT_BITS", bits)
+    monkeypatch.setenv("PPE_CUT_LINES", "1" if bits in ("5", "16") else "0")
     rng = np.random.default_rng(600 + int(bits))
-    n = {4: 80, 5: 120}.get(int(bits), 1500)
+    n = {5: 80, 6: 120}.get(int(bits), 1500)
     r = synth.make_rules(n, seed=601)
     r["sip_mask"] = rng.choice([0, 1, 7, 8, 16, 31, 32], n, p=[0.01, 0.02, 0.1, 0.25, 0.32, 0.15, 0.15])
     r["dip_mask"] = rng.choice([0, 1, 8, 24, 32], n, p=[0.01, 0.02, 0.37, 0.3, 0.3])
