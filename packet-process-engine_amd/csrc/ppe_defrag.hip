@@ -13,11 +13,12 @@
  *              records while running + rank < fcb_max (fcb_create's fetch-and-add cap); the others fail, and with
  *              them every later fragment of their key in this batch, because the running count cannot fall inside
  *              a batch;
- *   group      stable LSD radix sort of the fragments by FCB, keyed by the FCB's first fragment index in the batch
- *              (8-bit digits, wave multisplit ranks, each scatter workgroup scanning the digit histogram itself; 2
- *              passes for 65,536 fragments), so each FCB's fragments are contiguous and in arrival order;
- *   process    one lane per FCB runs the reference state machine over its fragments in order (chain ≤ cache_max
- *              entries, kept as a nibble list of store slots);
+ *   group      one launch: each fragment's group key is its FCB's first fragment index in the batch; every other
+ *              fragment of the FCB takes one of the group's 15 slots by an atomic ticket (past them, an overflow
+ *              list).  (Until round 4: a stable 2-pass LSD radix sort of the fragments by that key, 4 launches.)
+ *   process    one lane per FCB (the group's first fragment) sorts its group's slots into arrival order in registers
+ *              and runs the reference state machine over the fragments in that order (chain ≤ cache_max entries,
+ *              kept as a nibble list of store slots);
  *   place      completing fragments in index order get datagram indices (ballot counts, summed per workgroup)
  *              and write their datagram's assembly plan;
  *   stash      one wave per held fragment copies its frame into the FCB's store slot (PACKET_HW2SW, mbuf.c:117-156);
@@ -51,7 +52,6 @@ constexpr uint32_t kBlock = 256;        // workgroup size of the per-fragment ke
 #endif
 constexpr uint32_t kSlotBlock = 64 * DF_SLOT_WAVES;   // workgroup size of the wave-per-item kernels (stash, assemble)
 constexpr uint32_t kScanT = 1024;       // one-workgroup scans
-constexpr uint32_t kSortBlock = 1024;   // radix sort: elements (= threads) per workgroup (64k-word histogram)
 
 // FCB record header word 0
 constexpr uint32_t kRecLive = 1u << 0;
@@ -64,9 +64,9 @@ constexpr uint32_t kRecWords = 8;
 
 // control words (u64)
 enum { C_RUNNING = 0, C_NEW, C_DEL, C_FREE_TOP, C_DGRAMS, C_TEARDROP, C_TIMEOUT_DROP, C_NDGRAM, C_ST0 = 8,
-       C_CREATORS = C_ST0 + PPE_DF__COUNT + 2, C_AGE_DROPPED, C_AGE_FREED, C_SCRATCH, C_LOOK_ERR,
-       C_WORDS = 24 };
-static_assert(C_LOOK_ERR < C_WORDS, "control words");
+       C_CREATORS = C_ST0 + PPE_DF__COUNT + 2, C_AGE_DROPPED, C_AGE_FREED, C_SCRATCH, C_LOOK_ERR, C_GOVF,
+       C_WORDS = 26 };
+static_assert(C_GOVF < C_WORDS, "control words");
 
 // parsed fragment record words (frec): sip, dip, id | proto << 16 | mf << 24, off | flen << 16, totlen,
 // l2 | ihl4 << 8, hash, valid
@@ -103,8 +103,10 @@ struct DfArgs {
     // batch scratch
     uint32_t *frec, *fslot, *inserted, *dgrec, *tcnt;
     uint32_t *plan;                      // assembly plan: min(max_batch, fcb_max) × cache_max entries of 8 words
-    uint32_t *skey[2], *sval[2], *hist;
-    uint32_t shift, sort_blocks;         // radix pass: digit shift, workgroups
+    // grouping (df_group_kernel): each fragment's group key; per group key, its members besides the key fragment
+    // (count, kGroupSlots slots in claim order), past that the overflow list of (key, index) pairs; the per-tile
+    // counts of completing fragments (process → place)
+    uint32_t *gkey, *gcnt, *gslot, *govf, *dcnt;
     unsigned long long *look;            // admission: per-workgroup look-back words (epoch << 32 | flags | count)
     uint32_t epoch, nlook;               // this call's tag (never 0) and the look-back array's length
     uint32_t look_spins;                 // admission: polls of an unpublished predecessor before giving up
@@ -112,6 +114,7 @@ struct DfArgs {
     unsigned long long *err_host;        // pinned, device-mapped: set by a failed look-back (ppe_defrag reports it)
     uint64_t *dropped;                   // age: ids of dropped fragments
     uint32_t max_dropped;
+    uint32_t max_batch;
 };
 
 __device__ __forceinline__ uint32_t ld_be16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
@@ -400,122 +403,60 @@ __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
     }
 }
 
-// ---- stable LSD radix sort of (record, index) by record -------------------------------------------------------------
-__device__ __forceinline__ uint32_t df_sort_key(const DfArgs &a, uint32_t i) {
+// ---- grouping: each FCB's fragments of this batch, under the key of its first one ------------------------------------
+__device__ __forceinline__ uint32_t df_group_key(const DfArgs &a, uint32_t i) {
     const uint32_t s = a.fslot[i];
     // fragments without a record (not a fragment, or its FCB could not be created) form singleton groups keyed by
     // their own index, which no FCB group uses (a group's key is the index of one of its own fragments)
     if (s >= kNone - 1 || a.tstate[s] != kLive) return i;
-    return a.creator[s];   // the FCB's first fragment in this batch: keys < n, so ceil(log2 n) / 8 radix passes
+    return a.creator[s];   // the FCB's first fragment in this batch
 }
+constexpr uint32_t kGroupSlots = 15;      // members besides the key fragment held in a group's slots
+constexpr uint32_t kGroupStride = 16;     // words per group in gslot (64 B)
 
-// in: skey[0]/sval[0] → out: skey[1]/sval[1]; hist layout digit-major: hist[d * sort_blocks + block]
-// INIT (first histogram pass): the keys are computed here and written to skey[0] / sval[0] (no separate init launch)
-template <bool SCATTER, bool INIT>
-__global__ void __launch_bounds__(kSortBlock) df_sort_pass_kernel(DfArgs a) {
-    __shared__ uint32_t cnt[kSortBlock / 64][256];
-    const uint32_t w = threadIdx.x >> 6;
-    for (uint32_t k = threadIdx.x; k < (kSortBlock / 64) * 256; k += kSortBlock) (&cnt[0][0])[k] = 0;
-    __syncthreads();
-    const uint32_t j = blockIdx.x * kSortBlock + threadIdx.x;
-    const bool v = j < a.n;
-    // the first scatter pass runs after every reader of the admission counts: it clears the tile counts for the
-    // process kernel, which counts each tile's completing fragments into them (no second count launch)
-    if (SCATTER && a.shift == 0u && v && __lane_id() == 0) a.tcnt[j >> 6] = 0u;
-    uint32_t key = 0u;
-    if (INIT && v) {
-        key = df_sort_key(a, j);
-        a.skey[0][j] = key;
-        a.sval[0][j] = j;
-        // the process kernel's view of the fragment, in its parsed record's last two words (the hash and the valid
-        // flag are dead after the claim): word 6 = its FCB record (kNone: none), word 7 = its table slot (kNone: not
-        // a fragment).  The group head then reaches its FCB header in one load instead of three dependent ones.
-        const uint32_t s = a.fslot[j];
-        const bool rec = s < kNone - 1 && a.tstate[s] == kLive;
-        uint2 w67;
-        w67.x = rec ? a.tkey[(size_t)s * 4 + 3] : kNone;
-        w67.y = s < kNone - 1 ? s : kNone;
-        *(uint2 *)(a.frec + (size_t)j * kFrecWords + 6) = w67;
-    } else if (v) {
-        key = a.skey[0][j];
+// One lane per fragment: its group key; a member (key != its index) takes a slot of its group by an atomic ticket
+// (claim order, sorted back into batch order by the group's head in df_process_kernel), or past kGroupSlots an
+// overflow entry.  Also: the parsed record's words 6-7 for the process kernel, the completion tile counts cleared,
+// and (workgroup 0) the running count and free-stack top moved past this batch's admissions.
+__global__ void __launch_bounds__(kBlock) df_group_kernel(DfArgs a) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (blockIdx.x == 0) {
+        // after the admission kernel: the creators of this batch (the tile counts it ranked) move the running count
+        // and the free-stack top (fcb_create's fetch-and-add, decode-defrag.c:74-81)
+        uint32_t creators = 0;
+        wg_tile_prefix<kBlock>(a.tcnt, 0u, (a.n + 63) / 64, &creators);
+        if (threadIdx.x == 0) {
+            const unsigned long long run = a.ctl[C_RUNNING];
+            const unsigned long long room = run < a.fcb_max ? a.fcb_max - run : 0ull;
+            const unsigned long long adm = creators < room ? creators : room;
+            a.ctl[C_CREATORS] = creators;
+            a.ctl[C_RUNNING] = run + adm;
+            a.ctl[C_FREE_TOP] -= adm;
+            a.ctl[C_NEW] += adm;
+        }
     }
-    const uint32_t d = (key >> a.shift) & 0xffu;
-    // wave multisplit: lanes with the same digit
-    uint64_t peers = __builtin_amdgcn_ballot_w64(v);
-    for (int b = 0; b < 8; ++b) {
-        const bool bit = (d >> b) & 1u;
-        const uint64_t m = __builtin_amdgcn_ballot_w64(bit);
-        peers &= bit ? m : ~m;
+    if (j >= a.n) return;
+    if (__lane_id() == 0) a.dcnt[j >> 6] = 0u;
+    const uint32_t key = df_group_key(a, j);
+    a.gkey[j] = key;
+    // the process kernel's view of the fragment, in its parsed record's last two words (the hash and the valid flag
+    // are dead after the claim): word 6 = its FCB record (kNone: none), word 7 = its table slot (kNone: not a
+    // fragment).  The group head then reaches its FCB header in one load instead of three dependent ones.
+    const uint32_t s = a.fslot[j];
+    const bool rec = s < kNone - 1 && a.tstate[s] == kLive;
+    uint2 w67;
+    w67.x = rec ? a.tkey[(size_t)s * 4 + 3] : kNone;
+    w67.y = s < kNone - 1 ? s : kNone;
+    *(uint2 *)(a.frec + (size_t)j * kFrecWords + 6) = w67;
+    if (key != j) {
+        const uint32_t pos = atomicAdd(a.gcnt + key, 1u);
+        if (pos < kGroupSlots) {
+            a.gslot[(size_t)key * kGroupStride + pos] = j;
+        } else {
+            const uint32_t o = (uint32_t)atomicAdd(a.ctl + C_GOVF, 1ull);
+            *(uint2 *)(a.govf + 2ull * o) = make_uint2(key, j);
+        }
     }
-    const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-    if (v && rank == 0) cnt[w][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    if (!SCATTER) {
-        for (uint32_t dd = threadIdx.x; dd < 256; dd += kSortBlock) {
-            uint32_t t = 0;
-            for (uint32_t k = 0; k < kSortBlock / 64; ++k) t += cnt[k][dd];
-            a.hist[dd * a.sort_blocks + blockIdx.x] = t;
-        }
-        if (INIT && blockIdx.x == 0) {
-            // after the admission kernel: the creators of this batch (the tile counts it ranked) move the running
-            // count and the free-stack top (fcb_create's fetch-and-add, decode-defrag.c:74-81)
-            uint32_t creators = 0;
-            wg_tile_prefix<kSortBlock>(a.tcnt, 0u, (a.n + 63) / 64, &creators);
-            if (threadIdx.x == 0) {
-                const unsigned long long run = a.ctl[C_RUNNING];
-                const unsigned long long room = run < a.fcb_max ? a.fcb_max - run : 0ull;
-                const unsigned long long adm = creators < room ? creators : room;
-                a.ctl[C_CREATORS] = creators;
-                a.ctl[C_RUNNING] = run + adm;
-                a.ctl[C_FREE_TOP] -= adm;
-                a.ctl[C_NEW] += adm;
-            }
-        }
-        return;
-    }
-    // the digit bases of this workgroup from the histogram (every workgroup scans it itself; no scan launch):
-    // digit d starts after every smaller digit of all workgroups and digit d of the earlier workgroups.  Four
-    // threads per digit read its row of sort_blocks words.
-    __shared__ uint32_t dsum[256], dbase[256], wtot[4];
-    {
-        const uint32_t dd = threadIdx.x >> 2, qq = threadIdx.x & 3u;
-        const uint32_t chunk = (a.sort_blocks + 3u) / 4u, b0 = qq * chunk;
-        const uint32_t b1 = b0 + chunk < a.sort_blocks ? b0 + chunk : a.sort_blocks;
-        uint32_t col = 0, part = 0;
-        for (uint32_t bb = b0; bb < b1; ++bb) {
-            const uint32_t h = a.hist[dd * a.sort_blocks + bb];
-            col += h;
-            part += bb < blockIdx.x ? h : 0u;
-        }
-        col += __shfl_xor(col, 1, 64);
-        col += __shfl_xor(col, 2, 64);
-        part += __shfl_xor(part, 1, 64);
-        part += __shfl_xor(part, 2, 64);
-        if (qq == 0) dsum[dd] = col;
-        __syncthreads();
-        if (threadIdx.x < 256) {   // exclusive scan of the 256 digit totals (4 waves)
-            const uint32_t c = dsum[threadIdx.x];
-            uint32_t x = c;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o, 64);
-                if ((int)__lane_id() >= o) x += y;
-            }
-            dbase[threadIdx.x] = x - c;   // within the wave; the earlier waves' totals are added below
-            if (__lane_id() == 63) wtot[threadIdx.x >> 6] = x;
-        }
-        __syncthreads();
-        if (qq == 0) {
-            uint32_t carry = 0;
-            for (uint32_t k = 0; k < (dd >> 6); ++k) carry += wtot[k];
-            dbase[dd] += carry + part;
-        }
-        __syncthreads();
-    }
-    if (!v) return;
-    uint32_t pos = dbase[d] + rank;
-    for (uint32_t k = 0; k < w; ++k) pos += cnt[k][d];
-    a.skey[1][pos] = key;
-    a.sval[1][pos] = a.sval[0][j];
 }
 
 // ---- the reference state machine, one lane per FCB --------------------------------------------------------------------
@@ -525,10 +466,10 @@ __device__ __forceinline__ uint32_t chain_at(uint64_t order, uint32_t pos) { ret
 // LDS round trips instead of global ones.  Private per lane ([slot][lane]: no bank conflicts), no barrier.
 // cidx: batch index + 1 of the fragment each chain slot received in this batch (0: an earlier batch).  When the FCB
 // completes, these go to descriptor word 3 and the fragments are not stashed: the assembly reads them from the input.
-// The lane's loads come in three dependent rounds, not one per chain step: (1) the sorted keys and indices of the
-// next kWin positions (contiguous) and the neighbour's key; (2) the head's parsed record, which carries its FCB record
-// and table slot (df_sort_pass_kernel INIT), and the window's parsed records and ids; (3) the FCB header (and, for an
-// FCB from an earlier batch, its chain descriptors).  A segment longer than the window refills one position per step.
+// The head lane's loads come in three dependent rounds, not one per chain step: (1) its group's member count and
+// slots (one 64-B row; a bitonic network puts them in batch order); (2) the head's parsed record, which carries its
+// FCB record and table slot (df_group_kernel), and the members' parsed records; (3) the FCB header (and, for an FCB
+// from an earlier batch, its chain descriptors).  A group with more members than slots steps them one by one.
 #ifndef DF_PROC_WIN
 #define DF_PROC_WIN 16
 #endif
@@ -536,25 +477,32 @@ constexpr uint32_t kWin = DF_PROC_WIN;
 __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint32_t (*cdesc)[kBlock],
                                                uint32_t (*cidx)[kBlock], uint32_t *st, uint32_t &teardrop) {
     const uint32_t tl = threadIdx.x;
-    const uint32_t *key = a.skey[0];
-    const uint32_t *val = a.sval[0];
-    const uint32_t g = key[j];
-    const uint32_t kprev = j > 0 ? key[j - 1] : ~g;
-    uint32_t kq[kWin], iq[kWin];
-#pragma unroll
-    for (uint32_t u = 1; u < kWin; ++u) {
-        const bool in = j + u < a.n;
-        kq[u] = in ? key[j + u] : ~g;
-        iq[u] = in ? val[j + u] : 0u;
-    }
-    if (kprev == g) return;   // not the head of its FCB's segment
-    // a group's key is the batch index of its first fragment (df_sort_key), which the stable sort puts first
+    if (a.gkey[j] != j) return;   // not the head of its group: the group's key is its first fragment's index
+    const uint32_t g = j;
+    const uint32_t cnt = a.gcnt[g];    // members besides the head (in slots, past kGroupSlots in the overflow list)
+    uint32_t iq[kWin];
     iq[0] = g;
-    uint32_t m = 1;           // valid window entries [0, m): keys equal g are contiguous
 #pragma unroll
-    for (uint32_t u = 1; u < kWin; ++u) m += kq[u] == g ? 1u : 0u;
-    bool more = m == kWin;    // the segment may continue past the window
-    uint32_t qn = j + kWin;   // the next sorted position to read into the window
+    for (uint32_t u = 1; u < kWin; ++u) iq[u] = u <= cnt ? a.gslot[(size_t)g * kGroupStride + u - 1] : kNone;
+    if (cnt) a.gcnt[g] = 0;            // (for the next call)
+    const bool more = cnt > kGroupSlots;   // (rare) the members are stepped one by one, by index, below
+    // the slots hold the members in ticket order: a bitonic network puts the window in batch order (the head, the
+    // group's smallest index, stays first; the unused entries, kNone, last)
+    static_assert(kWin == kGroupSlots + 1 && (kWin & (kWin - 1)) == 0, "window = head + slots, a power of two");
+#pragma unroll
+    for (uint32_t k = 2; k <= kWin; k <<= 1)
+#pragma unroll
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1)
+#pragma unroll
+            for (uint32_t i = 0; i < kWin; ++i) {
+                const uint32_t l = i ^ jj;
+                if (l > i) {
+                    const uint32_t x = iq[i], y = iq[l], lo = min(x, y), hi = max(x, y);
+                    iq[i] = (i & k) == 0 ? lo : hi;
+                    iq[l] = (i & k) == 0 ? hi : lo;
+                }
+            }
+    const uint32_t m = more ? 1u : 1u + cnt;   // window entries stepped from registers
     // the window's parsed-record words 2-5 (id | proto | mf, offset | frag_len, frame length, l2 | ihl*4): the state
     // machine reads nothing else of a fragment (its id goes to the FCB's id list in the stash / place kernels)
     uint4 fw[kWin];
@@ -689,16 +637,31 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
         a.status[i] = out | (tear ? PPE_DF_TEARDROP : 0u);
         a.inserted[i] = ins;
         a.dgrec[i] = done;
-        // the place kernel's per-tile count of completing fragments (zeroed by the first scatter pass)
-        if (done != kNone) atomicAdd(a.tcnt + (i >> 6), 1u);
+        // the place kernel's per-tile count of completing fragments (zeroed by the group kernel)
+        if (done != kNone) atomicAdd(a.dcnt + (i >> 6), 1u);
         atomicAdd(st + out, 1u);
     };
 #pragma unroll
     for (uint32_t u = 0; u < kWin; ++u)
         if (u < m) step(iq[u], fw[u]);
-    for (uint32_t q = qn; more && q < a.n && key[q] == g; ++q) {
-        const uint32_t x = val[q];
-        step(x, *(const uint4 *)(a.frec + (size_t)x * kFrecWords + 2));
+    if (more) {
+        // more members than slots: the slots hold an arbitrary kGroupSlots of them, the overflow list the rest;
+        // each next member is the smallest index above the last one stepped
+        const uint32_t no = (uint32_t)a.ctl[C_GOVF];
+        uint32_t last = g;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            uint32_t x = kNone;
+            for (uint32_t u = 0; u < kGroupSlots; ++u) {
+                const uint32_t y = a.gslot[(size_t)g * kGroupStride + u];
+                if (y > last && y < x) x = y;
+            }
+            for (uint32_t e = 0; e < no; ++e) {
+                const uint2 q = *(const uint2 *)(a.govf + 2ull * e);
+                if (q.x == g && q.y > last && q.y < x) x = q.y;
+            }
+            step(x, *(const uint4 *)(a.frec + (size_t)x * kFrecWords + 2));
+            last = x;
+        }
     }
     *(uint4 *)h = make_uint4(flags | (last_in << 8) | (cache_num << 16) | (nlist << 24), (uint32_t)total,
                              (uint32_t)meat, h03.w);
@@ -764,9 +727,10 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t t0 = blockIdx.x * (kBlock / 64), w = threadIdx.x >> 6;
     uint32_t nd = 0;
-    uint32_t base = wg_tile_prefix<kBlock>(a.tcnt, t0, (a.n + 63) / 64, &nd);
-    for (uint32_t k = 0; k < w; ++k) base += a.tcnt[t0 + k];   // the workgroup's earlier waves
+    uint32_t base = wg_tile_prefix<kBlock>(a.dcnt, t0, (a.n + 63) / 64, &nd);
+    for (uint32_t k = 0; k < w; ++k) base += a.dcnt[t0 + k];   // the workgroup's earlier waves
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // the datagram count (read by the assembly kernel, next)
+        a.ctl[C_GOVF] = 0;   // (the process kernel, the overflow list's only reader, has completed)
         a.ctl[C_NDGRAM] = nd;
         a.ctl[C_DGRAMS] += nd;
         if (a.n_dgram) *a.n_dgram = nd;
@@ -1080,6 +1044,7 @@ __global__ void df_init_kernel(DfArgs a) {
     }
     if (t < C_WORDS) a.ctl[t] = t == C_FREE_TOP ? a.fcb_max : 0ull;
     if (t < a.nlook) a.look[t] = 0ull;
+    if (t < a.max_batch) a.gcnt[t] = 0u;   // (then each group's head clears its count after use)
 }
 
 }  // namespace
@@ -1159,7 +1124,6 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
     a.reasm_buf = c.reasm_buf_bytes;
     a.sstride = d->sstride;
     const uint32_t mb = c.max_batch;
-    const uint32_t sb = blocks(mb, kSortBlock);
     // the store carries 64 spare bytes: df_assemble_kernel reads whole aligned dwords past a frame's last byte
     bool ok = dalloc(d, &a.tstate, ns) && dalloc(d, &a.tkey, (size_t)ns * 4) && dalloc(d, &a.creator, ns) &&
               dalloc(d, &a.rhdr, (size_t)c.fcb_max * kRecWords) &&
@@ -1169,8 +1133,9 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
               dalloc(d, &a.ctl, C_WORDS) && dalloc(d, &a.frec, (size_t)mb * kFrecWords) && dalloc(d, &a.fslot, mb) &&
               dalloc(d, &a.inserted, mb) && dalloc(d, &a.dgrec, mb) &&
               dalloc(d, &a.plan, (size_t)std::min(mb, c.fcb_max) * c.cache_max * 8) &&
-              dalloc(d, &a.tcnt, blocks(mb, 64)) && dalloc(d, &a.skey[0], mb) && dalloc(d, &a.sval[0], mb) &&
-              dalloc(d, &a.skey[1], mb) && dalloc(d, &a.sval[1], mb) && dalloc(d, &a.hist, (size_t)256 * sb) &&
+              dalloc(d, &a.tcnt, blocks(mb, 64)) && dalloc(d, &a.dcnt, blocks(mb, 64)) && dalloc(d, &a.gkey, mb) &&
+              dalloc(d, &a.gcnt, mb) && dalloc(d, &a.gslot, (size_t)mb * kGroupStride) &&
+              dalloc(d, &a.govf, 2ull * mb) &&
               dalloc(d, &a.dropped, (size_t)c.fcb_max * c.cache_max) &&
               dalloc(d, &a.look, blocks(mb, kBlock));
     if (ok && hipHostMalloc((void **)&d->h_ctl, C_WORDS * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
@@ -1183,13 +1148,14 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
         return PPE_ENOMEM;
     }
     a.max_dropped = c.fcb_max * c.cache_max;
+    a.max_batch = mb;
     a.nlook = blocks(mb, kBlock);
     *d->h_err = 0;
     a.look_spins = 1u << 22;
     a.look_fail_wg = ~0u;
     if (const char *e = getenv("PPE_DF_LOOK_FAIL"))  // test hook: this workgroup index fails its look-back
         a.look_fail_wg = (uint32_t)atoi(e);
-    const uint32_t span = std::max(std::max(ns, a.nlook), std::max(c.fcb_max, (uint32_t)C_WORDS));
+    const uint32_t span = std::max(std::max(std::max(ns, a.nlook), std::max(c.fcb_max, (uint32_t)C_WORDS)), mb);
     hipLaunchKernelGGL(df_init_kernel, dim3(blocks(span, 256)), dim3(256), 0, 0, a);
     if (hipDeviceSynchronize() != hipSuccess) {
         ppe_defrag_destroy(d);
@@ -1245,23 +1211,11 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
     a.n_dgram = out->n_dgram;
     a.hdr_stride = out->hdr_stride;
     const uint32_t g = blocks(a.n, kBlock);
-    a.sort_blocks = blocks(a.n, kSortBlock);
     hipLaunchKernelGGL(df_parse_kernel, dim3(g), dim3(kBlock), 0, s, a);
     if (++d->epoch == 0) d->epoch = 1;   // (0 is the cleared array's tag)
     a.epoch = d->epoch;
     hipLaunchKernelGGL(df_admit_kernel, dim3(g), dim3(kBlock), 0, s, a);
-    uint32_t passes = 1;   // sort keys are batch indices < n
-    while (passes < 4 && (uint64_t)a.n > (1ull << (8 * passes))) ++passes;
-    for (uint32_t p = 0; p < passes; ++p) {
-        a.shift = 8 * p;
-        if (p == 0)
-            hipLaunchKernelGGL((df_sort_pass_kernel<false, true>), dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
-        else
-            hipLaunchKernelGGL((df_sort_pass_kernel<false, false>), dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
-        hipLaunchKernelGGL((df_sort_pass_kernel<true, false>), dim3(a.sort_blocks), dim3(kSortBlock), 0, s, a);
-        std::swap(a.skey[0], a.skey[1]);
-        std::swap(a.sval[0], a.sval[1]);
-    }
+    hipLaunchKernelGGL(df_group_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_process_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_place_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_assemble_kernel, dim3(blocks(a.n, kSlotBlock / 64)), dim3(kSlotBlock), 0, s, a);

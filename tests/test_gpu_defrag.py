@@ -229,6 +229,29 @@ def test_small_cases_and_errors(eng):
         p.close()
 
 
+def test_groups_past_the_slots(eng):
+    """FCBs with more fragments in one batch than the grouping's 15 slots per group (the rest go to the overflow
+    list and the group's head steps them in index order): datagrams cut into 12 / 15 / 16 / 17 / 40 eight-byte
+    fragments plus duplicates, shuffled together in one batch, with cache_max 8 (CACHE_FULL past it: the statuses
+    depend on the order) and 16."""
+    rng = np.random.default_rng(77)
+    S, D = 0x0A000001, 0x0A0000FE
+    frames = []
+    for k, nf in enumerate([12, 15, 16, 17, 40]):
+        l4 = udp(1000 + k, 53, rng.integers(0, 256, 8 * nf - 8, dtype=np.uint8).tobytes())
+        frs = [ip_frag(17, S + k, D, 100 + k, 8 * f, f < nf - 1, l4[8 * f:8 * f + 8]) for f in range(nf)]
+        frames += frs + [frs[f] for f in rng.choice(nf, 4)]
+    frames = [frames[i] for i in rng.permutation(len(frames))]
+    a, o, l = arena(frames)
+    for cm in (8, 16):
+        p = DfPair(eng, cache_max=cm)
+        try:
+            p.batch(a, o, l, NOW)
+            p.check_stats()
+        finally:
+            p.close()
+
+
 def test_show_text_after_reassembly(eng):
     """`show packet statistic` / `show flow statistic` after defrag batches: the ip_frag_stat
     lines, new / del fcb and (monitor on) teardrop formatted from the GPU table's ppe_defrag_info equal the text
