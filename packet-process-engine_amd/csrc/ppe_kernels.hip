@@ -1985,10 +1985,8 @@ __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t
 #pragma unroll
         for (uint32_t q = 0; q < PPE_UPD_CAP / 2; ++q)
             v[q] = (sm ? q < PPE_UPD_CAP / 4u : 2u * q < n) ? e[q] : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-        for (uint32_t i = 0; i < PPE_UPD_CAP; ++i) {
-            if (i >= n) continue;  // (not break: the loop must unroll, v[] stays in registers)
-            uint32_t s, d, len;
+        // the bucket's entries: slot, direction, wire length (an entry past n: slot ~0, skipped)
+        auto entry = [&](uint32_t i, uint32_t &s, uint32_t &d, uint32_t &len) {
             if (sm) {
                 const uint4 q = v[i >> 2];
                 const uint32_t x = (i & 3u) == 0u ? q.x : (i & 3u) == 1u ? q.y : (i & 3u) == 2u ? q.z : q.w;
@@ -2001,19 +1999,37 @@ __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t
                 d = hi >> 31;
                 len = hi & 0x7fffffffu;
             }
+            if (i >= n) s = ~0u;
+        };
+        // every entry's claim at its home position issued before any result is used (one LDS round trip for the
+        // bucket instead of one per entry: the per-entry probe loop was half the update's time, r5w / r5x); the
+        // rare entry whose home holds another slot probes on, one by one.  (Two entries of one slot in one bucket:
+        // the lane's CASes execute in order, the second finds the first's key.)
+        uint32_t got[PPE_UPD_CAP];
+#pragma unroll
+        for (uint32_t i = 0; i < PPE_UPD_CAP; ++i) {
+            uint32_t s, d, len;
+            entry(i, s, d, len);
+            got[i] = s != ~0u ? atomicCAS(&hkey[((s * 0x9E3779B1u) >> (32 - HB)) & f.upd_hmask], 0u, s + 1u) : 0u;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < PPE_UPD_CAP; ++i) {
+            uint32_t s, d, len;
+            entry(i, s, d, len);
+            if (s == ~0u) continue;  // (not break: the loop must unroll, v[] stays in registers)
             uint32_t h = ((s * 0x9E3779B1u) >> (32 - HB)) & f.upd_hmask;
-            bool done = false;
-            for (uint32_t t = 0; t <= f.upd_hmask && !done; ++t) {
+            bool done = got[i] == 0u || got[i] == s + 1u;
+            for (uint32_t t = 1; t <= f.upd_hmask && !done; ++t) {
+                h = (h + 1u) & f.upd_hmask;
                 const uint32_t prev = atomicCAS(&hkey[h], 0u, s + 1u);
-                if (prev == 0u || prev == s + 1u) {
-                    atomicAdd(&hpk[d * HC + h], 1u);
-                    atomicAdd(&hby[d * HC + h], (unsigned long long)len);
-                    done = true;
-                } else {
-                    h = (h + 1u) & f.upd_hmask;
-                }
+                done = prev == 0u || prev == s + 1u;
             }
-            if (!done) direct(s, d, len);
+            if (done) {
+                atomicAdd(&hpk[d * HC + h], 1u);
+                atomicAdd(&hby[d * HC + h], (unsigned long long)len);
+            } else {
+                direct(s, d, len);
+            }
         }
     }
     __syncthreads();
