@@ -59,7 +59,9 @@ enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_N
  * atomic per packet; each owner's workgroup then sums its buckets in LDS and updates each touched slot once. */
 #define PPE_UPD_OWNERS 256u
 #define PPE_UPD_CAP 16u        /* entries per (owner, classify workgroup) bucket; a full bucket: the direct atomic */
-#define PPE_UPD_HASH 2048u     /* LDS hash entries of an owner workgroup (slots it accumulates; more: direct atomics) */
+#ifndef PPE_UPD_HASH
+#define PPE_UPD_HASH 4096u     /* LDS hash entries of an owner workgroup (slots it accumulates; more: direct atomics) */
+#endif
 #define PPE_FLOW_POST_BLOCK 512 /* workgroup size of the post-classify launch (finalize + update) */
 struct ppe_flowdev {
     uint32_t *keys;               /* nslots × {sip, dip, sport | dport << 16, state, last-seen (u64), 0, 0}: the key in

@@ -1941,22 +1941,24 @@ __device__ __forceinline__ void flow_finalize_wg(const ppe_flow_kargs &a, uint32
 // batch, never a found flow's), the fold into the wide counters, the last-seen time.  One update per flow and
 // direction instead of one memory-side atomic and one last-seen store per packet.  A slot the full hash cannot take
 // is updated by the atomic path directly.
-// (owner o's workgroup of the post-classify launch, ppe_flow_post_kernel; usm: its PPE_UPD_HASH * 28 B of LDS)
+// (owner o's workgroup of the post-classify launch, ppe_flow_post_kernel; usm: its PPE_UPD_HASH * 20 B of LDS)
 template <int BLOCK>
 __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t o, uint32_t *usm) {
     constexpr uint32_t HC = PPE_UPD_HASH, HB = __builtin_ctz(PPE_UPD_HASH);  // HC = 2^HB
     static_assert(HC == (1u << HB) && HC % BLOCK == 0, "hash geometry");
-    // per entry: slot + 1 (0 = empty), then per direction the packets (u32) and the bytes (u64, no field limit)
-    uint32_t *hkey = usm;                                             // [HC]
-    uint32_t *hpk = usm + HC;                                         // [2][HC]
-    unsigned long long *hby = (unsigned long long *)(usm + 3u * HC);  // [2][HC]
+    // per entry: slot + 1 (0 = empty), then per direction the batch's packets and bytes in the packed counters'
+    // format (packets << PPE_PK_SHIFT | bytes): one non-returning LDS add per bucket entry, 20 B per entry.  The
+    // fields cannot carry: fewer than 2^24 packets in the batch (else every entry takes the direct path) and wire
+    // lengths below 2^16 (longer ones: direct).
+    uint32_t *hkey = usm;                                       // [HC]
+    unsigned long long *hv = (unsigned long long *)(usm + HC);  // [2][HC]
     const ppe_flowdev &f = a.f;
     const uint32_t tid = threadIdx.x;
     const unsigned long long bmask = (1ull << PPE_PK_SHIFT) - 1u;
+    const bool packed_ok = a.n < (1u << (64u - PPE_PK_SHIFT));
     for (uint32_t i = tid; i < HC; i += BLOCK) {
         hkey[i] = 0u;
-        hpk[i] = hpk[HC + i] = 0u;
-        hby[i] = hby[HC + i] = 0ull;
+        hv[i] = hv[HC + i] = 0ull;
     }
     __syncthreads();
     // a slot's update the direct way (the hash is full): flow_account's atomic and fold, the last-seen store
@@ -2024,12 +2026,10 @@ __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t
                 const uint32_t prev = atomicCAS(&hkey[h], 0u, s + 1u);
                 done = prev == 0u || prev == s + 1u;
             }
-            if (done) {
-                atomicAdd(&hpk[d * HC + h], 1u);
-                atomicAdd(&hby[d * HC + h], (unsigned long long)len);
-            } else {
+            if (done && packed_ok && len < 0x10000u)
+                atomicAdd(&hv[d * HC + h], (1ull << PPE_PK_SHIFT) | (unsigned long long)len);
+            else
                 direct(s, d, len);
-            }
         }
     }
     __syncthreads();
@@ -2050,9 +2050,9 @@ __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t
         unsigned long long nw[2] = {old[j].x, old[j].y};
 #pragma unroll
         for (uint32_t d = 0; d < 2u; ++d) {
-            const uint32_t np = hpk[d * HC + h];
-            if (!np) continue;
-            const unsigned long long p = (nw[d] >> PPE_PK_SHIFT) + np, b = (nw[d] & bmask) + hby[d * HC + h];
+            const unsigned long long v = hv[d * HC + h];
+            if (!v) continue;
+            const unsigned long long p = (nw[d] >> PPE_PK_SHIFT) + (v >> PPE_PK_SHIFT), b = (nw[d] & bmask) + (v & bmask);
             if (p >= f.fold_pkts || b >= f.fold_bytes) {  // the fold: into the wide counters, the packed word to 0
                 unsigned long long *wd = f.stats + 4ull * s + 2u * d;
                 wd[0] += p;
@@ -2336,7 +2336,7 @@ extern "C" int ppe_launch_flow(int kind, const ppe_flow_kargs *a, uint32_t grid,
     switch (kind) {
         case PPE_FLOW_K_POST:
             hipLaunchKernelGGL(ppe_flow_post_kernel<PPE_FLOW_POST_BLOCK>, g, dim3(PPE_FLOW_POST_BLOCK),
-                               a->f.upd_wgs ? PPE_UPD_HASH * 28u : 0u, s, *a);
+                               a->f.upd_wgs ? PPE_UPD_HASH * 20u : 0u, s, *a);
             break;
         case PPE_FLOW_K_AGE: hipLaunchKernelGGL(ppe_flow_age_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
         case PPE_FLOW_K_REHASH: hipLaunchKernelGGL(ppe_flow_rehash_kernel<PPE_FLOW_BLOCK>, g, b, 0, s, *a); break;
