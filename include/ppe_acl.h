@@ -29,6 +29,8 @@
 #include <stdio.h>
 #include <pthread.h>
 
+#include "ppe_rwlock.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -104,6 +106,14 @@ typedef struct {
     TreeSet  *TreeSet;
     TreeNode *TreeNode;
 } unit_tree_t;
+
+/* The pair dp_cmd.c switches between (get_back_acltree / set_running_acltree, dp_cmd.c:1963-1985), owned here as the
+ * absent ACL engine owned them: DP_Acl_Load_Rule(rl, &back->TreeSet, &back->TreeNode) builds and uploads the back
+ * classifier without publishing it; g_acltree_running := &back (under acltree_running_rwlock) makes it the one the
+ * next classify step and DP_Acl_Lookup use.  DP_Acl_Rule_Commit runs the whole protocol on this pair. */
+extern unit_tree_t g_acltree_1, g_acltree_2;
+extern unsigned long g_acltree_running;
+extern rwlock_t acltree_running_rwlock;
 
 /* ---- rule store (include/rule.h:25-31, rule/rule.c) ---- */
 int  ppe_rule_list_init(void);          /* zeroed list, def_act DROP, build_status COMMIT (srv_rule.c:82-86) */

@@ -37,7 +37,7 @@ extern "C" {
 /* 2: ppe_tuning_t grew to 20 B (batches_per_launch) and mbuf_t (ppe_decode.h) took the reference's field layout;
  * 3: ppe_tuple's word 3 carries the TCP window-scale option offset (bits 9-15); 4: ppe_result_t.part8;
  * 5: the tuple carries a fragment's Defrag fields and the option-past-the-window bit; strides 64..256 */
-#define PPE_ABI_VERSION 6
+#define PPE_ABI_VERSION 7
 
 /* error codes (negative return values) */
 #define PPE_OK       0
@@ -190,6 +190,15 @@ int  ppe_ctx_device(ppe_ctx_t *ctx);
  * n may exceed RULE_ENTRY_MAX (extended rule API, up to 1<<24).  default_action: ACL_RULE_ACTION_FW/DROP. */
 int  ppe_rules_commit(ppe_ctx_t *ctx, const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
                       uint32_t default_action, ppe_acl_stats_t *stats);
+/* The two steps of ppe_rules_commit, as the reference's commit protocol takes them (dp_cmd.c:2019-2030: build the
+ * back tree, then set_running_acltree): ppe_rules_stage builds the classifier and uploads it into the back image
+ * slot without publishing it (launches keep reading the running image; the upload waits only for launches that read
+ * the slot it overwrites) and returns a token (> 0); ppe_rules_publish(token) makes that image the running one for
+ * later launches.  A later stage replaces an unpublished one: publishing the earlier token then fails (PPE_EINVAL),
+ * as does publishing a token twice.  ABI version 7. */
+int  ppe_rules_stage(ppe_ctx_t *ctx, const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                     uint32_t default_action, ppe_acl_stats_t *stats, uint64_t *token);
+int  ppe_rules_publish(ppe_ctx_t *ctx, uint64_t token);
 
 /* Classify one device-resident batch, enqueued on `stream` (a hipStream_t; NULL = the legacy default stream). */
 int  ppe_classify(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,

@@ -2,7 +2,8 @@
  * ppe_compat.c — the reference's decoder / ACL / plugin / log entry points as thin shims over the GPU engine.
  *
  *   DP_Acl_Rule_Init        main.c:177
- *   DP_Acl_Load_Rule        dataplane/src/common/dp_cmd.c:2019
+ *   DP_Acl_Load_Rule        dataplane/src/common/dp_cmd.c:2019 (builds the back classifier; published when
+ *                           g_acltree_running names its unit_tree_t, set_running_acltree, dp_cmd.c:1980-1985)
  *   DP_Acl_Rule_Clean       dataplane/src/common/dp_cmd.c:2030
  *   DP_Acl_Rule_Release     dataplane/src/platform/oct-init.c:755
  *   DP_Acl_Rule_Commit      the dp_acl_rule_commit protocol, dataplane/src/common/dp_cmd.c:1987-2053
@@ -28,6 +29,7 @@ PluginModule plugin_modules[PLUGIN_SIZE];
 
 struct ppe_tree_set {
     uint32_t generation;
+    uint64_t token;  /* ppe_rules_stage's: published when this set's unit becomes the running one */
     ppe_acl_stats_t stats;
 };
 struct ppe_tree_node {
@@ -36,6 +38,11 @@ struct ppe_tree_node {
 
 static ppe_ctx_t *g_ctx = NULL;
 static uint32_t g_generation = 0;
+
+unit_tree_t g_acltree_1, g_acltree_2;
+unsigned long g_acltree_running = 0;
+rwlock_t acltree_running_rwlock = PPE_RWLOCK_INITIALIZER;
+static uint64_t g_published = 0;  /* the token of the classifier the engine runs (under g_ctx_lock) */
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
 /* The engine context is thread-compatible, not thread-safe (include/ppe_hip.h): every call that uses g_ctx — a
  * Decode flush's classify, a rule commit, an ACL lookup, the release — holds g_ctx_lock, always the innermost lock
@@ -81,6 +88,18 @@ static void publish_stats(const ppe_acl_stats_t *st) {
     gNumLeafNode = (int)st->n_leaves;
 }
 
+/* The classifier the running unit names (g_acltree_running, set by dp_cmd.c's set_running_acltree) becomes the
+ * engine's running image at the next classify step or lookup: its token is read under the rwlock's read side (the
+ * unit's handles stay valid while it is running: dp_cmd.c cleans only the back unit), then published once.
+ * Caller holds g_ctx_lock. */
+static void sync_running_locked(void) {
+    read_lock(&acltree_running_rwlock);
+    const unit_tree_t *u = (const unit_tree_t *)g_acltree_running;
+    const uint64_t token = (u && u->TreeSet) ? u->TreeSet->token : 0;
+    read_unlock(&acltree_running_rwlock);
+    if (g_ctx && token && token != g_published && ppe_rules_publish(g_ctx, token) == PPE_OK) g_published = token;
+}
+
 uint32_t DP_Acl_Load_Rule(rule_list_t *rl, TreeSet **tset, TreeNode **tnode) {
     if (!rl) return SEC_NO;
     RCP_BLOCK_ACL_RULE_TUPLE *t = (RCP_BLOCK_ACL_RULE_TUPLE *)malloc(sizeof(*t) * RULE_ENTRY_MAX);
@@ -95,8 +114,10 @@ uint32_t DP_Acl_Load_Rule(rule_list_t *rl, TreeSet **tset, TreeNode **tnode) {
         used[i] = (uint8_t)rl->rule_entry[i].entry_status;
     }
     ppe_acl_stats_t st;
+    uint64_t token = 0;
     pthread_mutex_lock(&g_ctx_lock);
-    const int rc = g_ctx ? ppe_rules_commit(g_ctx, t, used, RULE_ENTRY_MAX, dp_acl_action_default, &st) : PPE_ENODEV;
+    const int rc = g_ctx ? ppe_rules_stage(g_ctx, t, used, RULE_ENTRY_MAX, dp_acl_action_default, &st, &token)
+                         : PPE_ENODEV;
     pthread_mutex_unlock(&g_ctx_lock);
     free(t);
     free(used);
@@ -107,6 +128,7 @@ uint32_t DP_Acl_Load_Rule(rule_list_t *rl, TreeSet **tset, TreeNode **tnode) {
         struct ppe_tree_set *s = (struct ppe_tree_set *)calloc(1, sizeof *s);
         if (s) {
             s->generation = g_generation;
+            s->token = token;
             s->stats = st;
         }
         *tset = s;
@@ -135,7 +157,13 @@ void DP_Acl_Rule_Release(void) {
     pthread_mutex_lock(&g_ctx_lock);  /* no flush, commit or lookup is using the context being destroyed */
     if (g_ctx) ppe_ctx_destroy(g_ctx);
     g_ctx = NULL;
+    g_published = 0;  /* (a new context numbers its tokens from 1 again) */
     pthread_mutex_unlock(&g_ctx_lock);
+    write_lock(&acltree_running_rwlock);
+    g_acltree_running = 0;
+    write_unlock(&acltree_running_rwlock);
+    DP_Acl_Rule_Clean(&g_acltree_1.TreeSet, &g_acltree_1.TreeNode);
+    DP_Acl_Rule_Clean(&g_acltree_2.TreeSet, &g_acltree_2.TreeNode);
     pthread_mutex_unlock(&g_lock);
 }
 
@@ -144,10 +172,20 @@ int DP_Acl_Rule_Commit(void) {
     int rc = SEC_OK;
     pthread_mutex_lock(&rule_list->rulelist_mutex);
     if (rule_list->build_status != RULE_BUILD_COMMIT) {
-        TreeSet *ts = NULL;
-        TreeNode *tn = NULL;
-        if (DP_Acl_Load_Rule(rule_list, &ts, &tn) != SEC_OK) rc = SEC_NO;  /* "commit failed" */
-        DP_Acl_Rule_Clean(&ts, &tn);
+        /* dp_cmd.c:2017-2031: build the back tree, make it the running one, clean the new back one */
+        unit_tree_t *back = g_acltree_running == (unsigned long)(void *)&g_acltree_1 ? &g_acltree_2 : &g_acltree_1;
+        if (DP_Acl_Load_Rule(rule_list, &back->TreeSet, &back->TreeNode) != SEC_OK) {
+            rc = SEC_NO;  /* "commit failed" */
+        } else {
+            write_lock(&acltree_running_rwlock);
+            g_acltree_running = (unsigned long)(void *)back;
+            write_unlock(&acltree_running_rwlock);
+            pthread_mutex_lock(&g_ctx_lock);
+            sync_running_locked();  /* (published now, not at the next batch: the commit's caller expects it) */
+            pthread_mutex_unlock(&g_ctx_lock);
+            unit_tree_t *old = back == &g_acltree_1 ? &g_acltree_2 : &g_acltree_1;
+            DP_Acl_Rule_Clean(&old->TreeSet, &old->TreeNode);
+        }
         rule_list->build_status = RULE_BUILD_COMMIT;  /* set either way, dp_cmd.c:2048 */
     }
     pthread_mutex_unlock(&rule_list->rulelist_mutex);
@@ -187,6 +225,7 @@ int DP_Acl_Lookup_Burst(mbuf_t **m, uint32_t n, int *actions) {
         }
         ppe_tuples_t in = {tw, mw, ts, n};
         pthread_mutex_lock(&g_ctx_lock);
+        sync_running_locked();
         rc = g_ctx ? ppe_acl_lookup_host(g_ctx, &in, hit, act, 0) : PPE_EINVAL;
         pthread_mutex_unlock(&g_ctx_lock);
         if (rc == PPE_OK)
@@ -378,6 +417,7 @@ static int classify_mbufs(mbuf_t **mb, uint32_t n) {
         r.tuple = tuple;
         ppe_cfg_t cfg = {unsupport_proto_action ? 1u : 0u, syn_check ? 1u : 0u, 0};
         pthread_mutex_lock(&g_ctx_lock);
+        sync_running_locked();
         rc = g_ctx ? ppe_classify_host(g_ctx, &b, &r, &cfg, 0) : PPE_ENODEV;
         pthread_mutex_unlock(&g_ctx_lock);
         if (rc == PPE_OK)

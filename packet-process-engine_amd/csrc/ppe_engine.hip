@@ -114,6 +114,8 @@ struct ppe_ctx {
                                                                        // their last launch with it
     hipStream_t aux = nullptr;                 // image uploads
     int running = 0;
+    int staged = -1;              // ppe_rules_stage: the slot holding an unpublished image (-1: none)
+    uint64_t stage_token = 0, tokens = 0;
     // counters
     unsigned long long *d_cslots = nullptr;
     uint32_t max_grid = 0;
@@ -759,8 +761,8 @@ int ppe_ctx_destroy(ppe_ctx_t *c) {
 
 int ppe_ctx_device(ppe_ctx_t *c) { return c ? c->device : PPE_EINVAL; }
 
-int ppe_rules_commit(ppe_ctx_t *c, const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
-                     uint32_t default_action, ppe_acl_stats_t *stats) {
+int ppe_rules_stage(ppe_ctx_t *c, const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                    uint32_t default_action, ppe_acl_stats_t *stats, uint64_t *token) {
     if (!c) return PPE_EINVAL;
     if (default_action > 0xffffu) return fail(c, PPE_EINVAL, "default action out of range");
     HIPCHK(c, hipSetDevice(c->device));
@@ -770,13 +772,33 @@ int ppe_rules_commit(ppe_ctx_t *c, const RCP_BLOCK_ACL_RULE_TUPLE *rules, const 
     const uint32_t binth = bt ? (uint32_t)atoi(bt) : 0u;
     int rc = ppe_acl_build_image(rules, used, n, default_action, binth, &words, &n_words, &st);
     if (rc != PPE_OK) return fail(c, rc, "classifier build failed (%d)", rc);
+    // the back slot (the context's creation commits an image, so the running slot is never empty after it)
     const int back = c->h_img[c->running].empty() ? c->running : 1 - c->running;
+    c->staged = -1;  // (an unpublished image there is replaced: its token no longer publishes)
     rc = upload_image(c, back, words, n_words, &st);
     ppe_acl_free_image(words);
     if (rc != PPE_OK) return rc;
-    c->running = back;  // publish: later launches read the new image (set_running_acltree, dp_cmd.c:1980-1985)
+    c->staged = back;
+    c->stage_token = ++c->tokens;
+    if (token) *token = c->stage_token;
     if (stats) *stats = c->stats[back];
     return PPE_OK;
+}
+
+int ppe_rules_publish(ppe_ctx_t *c, uint64_t token) {
+    if (!c) return PPE_EINVAL;
+    if (token == 0 || c->staged < 0 || token != c->stage_token)
+        return fail(c, PPE_EINVAL, "no staged classifier with token %llu", (unsigned long long)token);
+    c->running = c->staged;  // later launches read the new image (set_running_acltree, dp_cmd.c:1980-1985)
+    c->staged = -1;
+    return PPE_OK;
+}
+
+int ppe_rules_commit(ppe_ctx_t *c, const RCP_BLOCK_ACL_RULE_TUPLE *rules, const uint8_t *used, uint32_t n,
+                     uint32_t default_action, ppe_acl_stats_t *stats) {
+    uint64_t token = 0;
+    const int rc = ppe_rules_stage(c, rules, used, n, default_action, stats, &token);
+    return rc != PPE_OK ? rc : ppe_rules_publish(c, token);
 }
 
 int ppe_classify(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,

@@ -180,7 +180,7 @@ TUPLE_OPT_PAST = 1 << 15  # include/ppe_hip.h PPE_TUPLE_OPT_PAST (tuple word 3)
 # every symbol include/*.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     # ppe_hip.h
-    "ppe_abi_version", "ppe_ctx_create", "ppe_ctx_destroy", "ppe_ctx_device", "ppe_rules_commit", "ppe_classify",
+    "ppe_abi_version", "ppe_ctx_create", "ppe_ctx_destroy", "ppe_ctx_device", "ppe_rules_commit", "ppe_rules_stage", "ppe_rules_publish", "ppe_classify",
     "ppe_classify_batches", "ppe_classify_host", "ppe_acl_lookup", "ppe_acl_lookup_host", "ppe_dev_alloc", "ppe_dev_free",
     "ppe_host_alloc", "ppe_host_free", "ppe_memcpy_h2d", "ppe_memcpy_d2h", "ppe_memset_d", "ppe_sync",
     "ppe_counters_read", "ppe_counters_clear", "ppe_timing_enable", "ppe_timing_read", "ppe_acl_image",
@@ -200,12 +200,13 @@ EXPORTS = [
     "reg_fw_alert", "DP_Log_Func", "ppe_compat_ctx",
 ]
 EXPORTED_DATA = ["rule_list", "dp_acl_action_default", "gWstDepth", "gAvgDepth", "gChildCount", "gNumTreeNode",
-                 "gNumLeafNode", "unsupport_proto_action", "syn_check", "plugin_modules"]
+                 "gNumLeafNode", "unsupport_proto_action", "syn_check", "plugin_modules", "g_acltree_1", "g_acltree_2",
+                 "g_acltree_running", "acltree_running_rwlock"]
 
 _lib = None
 
 
-ABI_VERSION = 6  # include/ppe_hip.h PPE_ABI_VERSION
+ABI_VERSION = 7  # include/ppe_hip.h PPE_ABI_VERSION
 
 
 def load(path: str | os.PathLike | None = None) -> C.CDLL:
@@ -238,6 +239,8 @@ def _open(p: Path, mode, strict: bool = True) -> C.CDLL:
         "ppe_ctx_destroy": ([vp], C.c_int),
         "ppe_ctx_device": ([vp], C.c_int),
         "ppe_rules_commit": ([vp, vp, vp, u32, u32, C.POINTER(AclStats)], C.c_int),
+        "ppe_rules_stage": ([vp, vp, vp, u32, u32, C.POINTER(AclStats), C.POINTER(C.c_uint64)], C.c_int),
+        "ppe_rules_publish": ([vp, C.c_uint64], C.c_int),
         "ppe_classify": ([vp, C.POINTER(Batch), C.POINTER(Result), C.POINTER(Cfg), vp], C.c_int),
         "ppe_classify_host": ([vp, C.POINTER(Batch), C.POINTER(Result), C.POINTER(Cfg), u32], C.c_int),
         "ppe_classify_batches": ([vp, C.POINTER(Batch), C.POINTER(Result), u32, C.POINTER(Cfg), vp], C.c_int),

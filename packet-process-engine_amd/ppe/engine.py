@@ -51,6 +51,24 @@ class Engine:
         self._check(rc, "ppe_rules_commit")
         return st.as_dict()
 
+    def stage(self, rules: np.ndarray, used: np.ndarray | None = None,
+              default_action: int = abi.ACL_RULE_ACTION_DROP) -> tuple[int, dict]:
+        """ppe_rules_stage: build and upload the back classifier without publishing it; returns (token, stats)."""
+        rules = np.ascontiguousarray(rules, dtype=abi.RULE_DTYPE)
+        if used is not None:
+            used = np.ascontiguousarray(used, dtype=np.uint8)
+        st = abi.AclStats()
+        tok = C.c_uint64(0)
+        rc = self.lib.ppe_rules_stage(self.ctx, rules.ctypes.data if len(rules) else None,
+                                      used.ctypes.data if used is not None else None, len(rules),
+                                      int(default_action), C.byref(st), C.byref(tok))
+        self._check(rc, "ppe_rules_stage")
+        return tok.value, st.as_dict()
+
+    def publish(self, token: int) -> None:
+        """ppe_rules_publish: the staged classifier of `token` runs for later launches."""
+        self._check(self.lib.ppe_rules_publish(self.ctx, int(token)), "ppe_rules_publish")
+
     def image(self) -> np.ndarray:
         n = C.c_uint32(0)
         self._check(self.lib.ppe_acl_image(self.ctx, None, C.byref(n)), "ppe_acl_image")

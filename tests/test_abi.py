@@ -25,7 +25,7 @@ def header_functions():
 
 def test_library_loads():
     lib = abi.load()
-    assert lib.ppe_abi_version() == abi.ABI_VERSION == 6
+    assert lib.ppe_abi_version() == abi.ABI_VERSION == 7
 
 
 def test_every_declared_function_is_exported():
@@ -101,3 +101,37 @@ def test_mbuf_layout_matches_reference(tmp_path):
     for k in names:
         assert ct[k] == got[k], k
     assert C.sizeof(abi.Mbuf) == got["sizeof"]
+
+
+def test_running_tree_switch_links(tmp_path):
+    """dp_cmd.c's get_back_acltree / set_running_acltree (dp_cmd.c:1963-1985), written against include/ppe_acl.h and
+    its rwlock stand-in, compile and link against the library and switch the exported running pointer (no GPU
+    call: the engine context is never created)."""
+    import subprocess
+    src = tmp_path / "sw.c"
+    src.write_text(
+        '#include "ppe_acl.h"\n'
+        "static unit_tree_t *back_tree(void) {\n"
+        "    return g_acltree_running == (unsigned long)(void *)&g_acltree_1 ? &g_acltree_2 : &g_acltree_1;\n"
+        "}\n"
+        "static void set_running(unit_tree_t *t) {\n"
+        "    write_lock(&acltree_running_rwlock);\n"
+        "    g_acltree_running = (unsigned long)(void *)t;\n"
+        "    write_unlock(&acltree_running_rwlock);\n"
+        "}\n"
+        "int main(void) {\n"
+        "    unit_tree_t *a = back_tree();\n"
+        "    set_running(a);\n"
+        "    unit_tree_t *b = back_tree();\n"
+        "    read_lock(&acltree_running_rwlock);\n"
+        "    const int ok = a == &g_acltree_1 && b == &g_acltree_2 && read_trylock(&acltree_running_rwlock) &&\n"
+        "                   !write_trylock(&acltree_running_rwlock);\n"
+        "    read_unlock(&acltree_running_rwlock);\n"
+        "    read_unlock(&acltree_running_rwlock);\n"
+        "    return ok && write_trylock(&acltree_running_rwlock) ? 0 : 1;\n"
+        "}\n")
+    exe = tmp_path / "sw"
+    lib = ROOT / "packet-process-engine_amd"
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{ROOT / 'include'}", str(src), f"-L{lib}", "-lppe_hip",
+                    f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True)
+    assert subprocess.run([str(exe)]).returncode == 0

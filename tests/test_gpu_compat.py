@@ -284,3 +284,78 @@ def test_contexts_on_concurrent_threads():
         assert np.array_equal(res[k]["verdict"].view(np.uint32)[ok], ref["verdict"][ok])
         assert np.array_equal(res[k]["acl_hit"][ok], ref["acl_hit"][ok])
         assert np.array_equal(res[k]["flow_hash"].view(np.uint32)[ok], ref["flow_hash"][ok])
+
+
+class UnitTree(C.Structure):
+    _fields_ = [("TreeSet", C.c_void_p), ("TreeNode", C.c_void_p)]
+
+
+def test_load_rule_then_set_running_tree():
+    """dp_cmd.c's own two steps (dp_acl_rule_commit, dp_cmd.c:2017-2031): DP_Acl_Load_Rule into the back unit_tree_t
+    builds and uploads the classifier without publishing it — Decode and DP_Acl_Lookup keep classifying with the
+    running rules — and only when g_acltree_running names that unit (set_running_acltree) does the next classify step
+    use the new rules.  Then DP_Acl_Rule_Clean of the old unit, as dp_cmd.c does."""
+    lib = abi.load()
+    lib.ppe_set_output_hooks.argtypes = [HOOK, HOOK, HOOK]
+    lib.DP_Acl_Load_Rule.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.DP_Acl_Rule_Clean.argtypes = [C.c_void_p, C.c_void_p]
+    lib.DP_Acl_Lookup.argtypes = [C.POINTER(Mbuf)]
+    assert lib.DP_Acl_Rule_Init() == 0
+    lib.ppe_rule_list_free()
+    assert lib.ppe_rule_list_init() == 0
+    lib.Decode_Set_Burst(1)
+    ra = synth.make_rules(64, seed=97)
+    for i in range(len(ra)):
+        assert lib.Rule_add(ra[i:i + 1].ctypes.data, C.byref(C.c_uint32())) == 0
+    assert lib.DP_Acl_Rule_Commit() == 0   # rules A run
+    # rules B: one wildcard FW rule, added after A's removal (A drops most packets: its actions and the DROP default)
+    rb = synth.make_rules(1, seed=98)
+    rb["sip_mask"] = rb["dip_mask"] = 0
+    rb["sport_start"] = rb["dport_start"] = 0
+    rb["sport_end"] = rb["dport_end"] = 65535
+    rb["protocol_start"], rb["protocol_end"] = 0, 255
+    rb["action"] = 0
+    assert lib.Rule_del_all() == 0
+    assert lib.Rule_add(rb.ctypes.data, C.byref(C.c_uint32())) == 0
+
+    pk = synth.make_packets(400, ra, seed=99, kind="udp64", stride=128, hit_frac=0.8)
+    n = len(pk["len"])
+    bufs = [C.create_string_buffer(bytes(pk["hdr"][i][: min(int(pk["len"][i]) & 0xFFFF, 128)]), 144) for i in range(n)]
+    mbufs = (Mbuf * n)()
+    for i in range(n):
+        mbufs[i].pkt_ptr = C.cast(bufs[i], C.c_void_p)
+        mbufs[i].pkt_totallen = int(pk["len"][i])
+
+    def decode_all():  # (verdict, ACL hit) of every mbuf
+        for i in range(n):
+            lib.Decode(C.byref(mbufs[i]))
+        return np.array([(mbufs[i].ppe_verdict, mbufs[i].ppe_acl_hit) for i in range(n)], np.int64)
+
+    def ref(o):
+        r = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, 0))
+        return np.stack([r["verdict"].astype(np.int64), r["acl_hit"].astype(np.int64)], 1)
+
+    ref_a, ref_b = ref(pyoracle.Oracle(ra, default_action=1)), ref(pyoracle.Oracle(rb, default_action=1))
+    assert not np.array_equal(ref_a, ref_b)
+    g1, g2 = UnitTree.in_dll(lib, "g_acltree_1"), UnitTree.in_dll(lib, "g_acltree_2")
+    running = C.c_ulong.in_dll(lib, "g_acltree_running")
+    assert running.value in (C.addressof(g1), C.addressof(g2))   # DP_Acl_Rule_Commit set it
+    back, old = (g2, g1) if running.value == C.addressof(g1) else (g1, g2)
+    rl = C.c_void_p.in_dll(lib, "rule_list").value
+    try:
+        assert lib.DP_Acl_Load_Rule(rl, C.addressof(back) + UnitTree.TreeSet.offset,
+                                    C.addressof(back) + UnitTree.TreeNode.offset) == 0
+        assert back.TreeSet and back.TreeNode
+        assert np.array_equal(decode_all(), ref_a)               # built, not running: rules A still classify
+        l4 = np.nonzero((ref_a[:, 0] >> 16) & 0x10)[0][:20]
+        for i in l4:   # DP_Acl_Lookup too
+            assert lib.DP_Acl_Lookup(C.byref(mbufs[i])) == (1 if ref_a[i, 0] & 0xFF == ST["ACL_DROP"] else 0)
+            assert mbufs[i].ppe_acl_hit == ref_a[i, 1]
+        running.value = C.addressof(back)                       # set_running_acltree (one thread here: no lock)
+        assert np.array_equal(decode_all(), ref_b)               # the next classify step runs rules B
+        lib.DP_Acl_Rule_Clean(C.addressof(old) + UnitTree.TreeSet.offset, C.addressof(old) + UnitTree.TreeNode.offset)
+        assert not old.TreeSet
+        assert np.array_equal(decode_all(), ref_b)
+    finally:
+        lib.ppe_rule_list_free()
+        lib.DP_Acl_Rule_Release()

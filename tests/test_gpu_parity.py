@@ -200,6 +200,30 @@ def test_flow_hash_matches_reference_tluhash(eng, ref_hash):
     assert np.array_equal(res["flow_hash"], want[sel])
 
 
+def test_stage_then_publish(eng):
+    """ppe_rules_stage builds and uploads the back classifier without publishing it (launches keep the running one);
+    ppe_rules_publish(token) switches; a token replaced by a later stage, or published already, is refused."""
+    from ppe.engine import PPEError
+    ra, rb = synth.make_rules(300, seed=41), synth.make_rules(4096, seed=42)
+    pk = synth.make_packets(20_000, rb, seed=43, stride=128, hit_frac=0.8)
+    refs = {}
+    for name, r in (("a", ra), ("b", rb)):
+        o = pyoracle.Oracle(r, default_action=1)
+        refs[name] = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=16)
+    eng.commit(ra, default_action=1)
+    t1, _ = eng.stage(rb, default_action=1)
+    assert_same(gpu_classify(eng, pk["hdr"], pk["len"]), refs["a"])   # staged, not running
+    t2, st = eng.stage(rb, default_action=1)                            # replaces the unpublished t1
+    assert t2 > t1 and st["n_rules"] == 4096
+    with pytest.raises(PPEError):
+        eng.publish(t1)
+    eng.publish(t2)
+    assert_same(gpu_classify(eng, pk["hdr"], pk["len"]), refs["b"])
+    with pytest.raises(PPEError):
+        eng.publish(t2)
+    assert_same(gpu_classify(eng, pk["hdr"], pk["len"]), refs["b"])
+
+
 # ---------------------------------------------------------------- seeded random batches per benchmark config
 @pytest.mark.parametrize("cfgname,n", [("C0", 10_000), ("C1", 200_000), ("C2", 200_000)])
 def test_config_batches_vs_oracle(eng, cfgname, n):
