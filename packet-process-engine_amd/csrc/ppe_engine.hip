@@ -65,7 +65,7 @@ struct LookupStage {
 // Device flow table (ppe_classify_flow) and what the host knows about it without synchronising.
 struct FlowArrays {
     uint32_t *keys = nullptr, *creator = nullptr;
-    unsigned long long *stats = nullptr;
+    unsigned long long *stats = nullptr, *recs = nullptr;
 };
 struct FlowTable {
     uint32_t capacity = 0, max_batch = 0, nslots = 0;
@@ -1180,13 +1180,15 @@ static void flow_free_arrays(FlowArrays &a) {
     (void)hipFree(a.keys);
     (void)hipFree(a.creator);
     (void)hipFree(a.stats);
+    (void)hipFree(a.recs);
     a = FlowArrays();
 }
 
 // allocate (if needed) and clear one slot-array set: every slot EMPTY with zero counters, no creator
 static int flow_clear_arrays(ppe_ctx *c, FlowArrays &a, uint32_t nslots, hipStream_t s) {
-    if (!a.keys) {  // (the packed counters and last-seen times live in the slot records: `packed` views them)
+    if (!a.keys) {
         if (hipMalloc(&a.keys, (size_t)nslots * 4u * PPE_FLOW_SLOT_WORDS) != hipSuccess ||
+            hipMalloc(&a.recs, (size_t)nslots * 8u * PPE_FLOW_REC_WORDS) != hipSuccess ||
             hipMalloc(&a.creator, (size_t)nslots * 4u) != hipSuccess ||
             hipMalloc(&a.stats, (size_t)nslots * 32u) != hipSuccess) {
             flow_free_arrays(a);
@@ -1194,6 +1196,7 @@ static int flow_clear_arrays(ppe_ctx *c, FlowArrays &a, uint32_t nslots, hipStre
         }
     }
     HIPCHK(c, hipMemsetAsync(a.keys, 0, (size_t)nslots * 4u * PPE_FLOW_SLOT_WORDS, s));
+    HIPCHK(c, hipMemsetAsync(a.recs, 0, (size_t)nslots * 8u * PPE_FLOW_REC_WORDS, s));
     HIPCHK(c, hipMemsetAsync(a.creator, 0xff, (size_t)nslots * 4u, s));
     HIPCHK(c, hipMemsetAsync(a.stats, 0, (size_t)nslots * 32u, s));
     return PPE_OK;
@@ -1205,7 +1208,7 @@ static ppe_flowdev flow_dev(const FlowTable &t, int which) {
     const FlowArrays &a = t.arr[which];
     d.keys = a.keys;
     d.stats = a.stats;
-    d.packed = (unsigned long long *)(a.keys + 4);
+    d.packed = a.recs;
     d.miss_tiles = t.miss_tiles;
     d.parity = (uint32_t)(t.batches & 1u);
     d.fold_pkts = t.fold_pkts;
@@ -1511,10 +1514,12 @@ int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_
     constexpr uint32_t W = PPE_FLOW_SLOT_WORDS;
     std::vector<uint32_t> keys((size_t)t.nslots * W);
     HIPCHK(c, hipMemcpy(keys.data(), a.keys, keys.size() * 4u, hipMemcpyDeviceToHost));
-    std::vector<unsigned long long> stats;
+    std::vector<unsigned long long> stats, recs;
     if (entries && max) {
         stats.resize((size_t)t.nslots * 4u);
         HIPCHK(c, hipMemcpy(stats.data(), a.stats, stats.size() * 8u, hipMemcpyDeviceToHost));
+        recs.resize((size_t)t.nslots * PPE_FLOW_REC_WORDS);
+        HIPCHK(c, hipMemcpy(recs.data(), a.recs, recs.size() * 8u, hipMemcpyDeviceToHost));
     }
     uint32_t k = 0;
     for (uint32_t s = 0; s < t.nslots; ++s) {
@@ -1529,8 +1534,7 @@ int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_
             e.dport = (uint16_t)(kw[2] >> 16);
             e.protocol = (uint8_t)(st >> 8);
             e.slot = s;
-            unsigned long long pr[3];  // the record's packed counters and last-seen time (words 4-9)
-            std::memcpy(pr, kw + 4, sizeof pr);
+            const unsigned long long *pr = &recs[(size_t)PPE_FLOW_REC_WORDS * s];  // packed counters, last-seen
             const unsigned long long bmask = (1ull << PPE_PK_SHIFT) - 1u, p0 = pr[0], p1 = pr[1];
             e.pktcnts2d = stats[4u * s] + (p0 >> PPE_PK_SHIFT);
             e.bytecnts2d = stats[4u * s + 1u] + (p0 & bmask);

@@ -24,15 +24,15 @@ struct ppe_bdesc {
 #define PPE_BD_PART8 1u
 
 /* Device flow table (ppe_classify_flow; ppe_kernels.hip "flow table").  Open addressing over groups of
- * PPE_FLOW_GROUP slots (one 64-B line segment of slot records), linear probing from group flow_hash & gmask; a key lies
- * before the first EMPTY slot of its probe sequence (slots never return to EMPTY: deletions leave TOMBs, reclaimed by
- * a rehash).  A slot record is 64 B: {sip, dip, sport | dport << 16, state}, then the packed counters of both
- * directions and the last-seen time (`packed` points at them: u64 words 0-2 of each record's second 16 B), so a
- * probe group of 2 slots is one 128-B line and the owner-computed update (flow_update_wg) rewrites the line
- * the probe read. */
-#define PPE_FLOW_GROUP 2u       /* slots per probe group */
-#define PPE_FLOW_SLOT_WORDS 16u /* u32 words per slot record */
-#define PPE_FLOW_REC_WORDS 8u   /* u64 stride of the counter records {s2d, d2s, last-seen, 0} (= the slot record) */
+ * PPE_FLOW_GROUP slots, linear probing from group flow_hash & gmask; a key lies before the first EMPTY slot of its
+ * probe sequence (slots never return to EMPTY: deletions leave TOMBs, reclaimed by a rehash).  The probe array holds
+ * only the keys, 16 B per slot {sip, dip, sport | dport << 16, state}, so a probe group of 4 slots is one 64-B
+ * segment: one HBM request per probe (round 5; until then a 64-B slot record with the counters inside, a 128-B line
+ * per probe group of 2).  The counters live in a record array of their own, 32 B per slot: the packed counters of
+ * both directions and the last-seen time (`packed`). */
+#define PPE_FLOW_GROUP 4u       /* slots per probe group */
+#define PPE_FLOW_SLOT_WORDS 4u  /* u32 words per slot key */
+#define PPE_FLOW_REC_WORDS 4u   /* u64 stride of the counter records {s2d, d2s, last-seen, 0} */
 #define PPE_FLOW_REC_LAST 2u    /* the counter record's last-seen time */
 #define PPE_FS_EMPTY 0u
 #define PPE_FS_TOMB 1u
@@ -64,10 +64,10 @@ enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_N
 #endif
 #define PPE_FLOW_POST_BLOCK 512 /* workgroup size of the post-classify launch (finalize + update) */
 struct ppe_flowdev {
-    uint32_t *keys;               /* nslots × {sip, dip, sport | dport << 16, state, last-seen (u64), 0, 0}: the key in
-                                     the creating packet's orientation                                                 */
-    unsigned long long *packed;   /* keys + 4 words, stride PPE_FLOW_REC_WORDS: {s2d, d2s, last-seen, 0}, packets << 40
-                                     | bytes per direction (FlowUpdate) and the last-seen time, inside the slot record */
+    uint32_t *keys;               /* nslots × {sip, dip, sport | dport << 16, state}: the key in the creating packet's
+                                     orientation (the probe array)                                                     */
+    unsigned long long *packed;   /* nslots × {s2d, d2s, last-seen, 0} (stride PPE_FLOW_REC_WORDS): packets << 40 |
+                                     bytes per direction (FlowUpdate) and the last-seen time                          */
     unsigned long long *stats;    /* nslots × {pkts s2d, bytes s2d, pkts d2s, bytes d2s}: folded from `packed` before a
                                      field can overflow; a flow's counters = stats + the packed fields               */
     uint32_t *creator;            /* nslots: lowest index of the packets claiming the slot in this batch (| REVOKED)   */

@@ -635,7 +635,7 @@ __device__ __forceinline__ void acl_leaf_compact(const uint32_t *__restrict__ gi
 // and base (LDS when staged) give the bucket's list; the entries' 4-bit fingerprints (LDS) drop the entries whose
 // fixed sip / dip bit below the cut differs from the key's; the rest are independent 16-B reads (LDS, or L2 for large
 // sets), two per round, checked in priority order.  The matching entry carries the verdict (its DROP flag); its rule
-// id, for the hit output, sits in the same 128-B line (an L1 hit after the entry's read).  Only TCP / UDP keys reach
+// id, for the hit output, sits in the same 128-B line (requested right behind the entry, it joins the entry's miss).  Only TCP / UDP keys reach
 // it (the classify path).
 // one entry against the key's bucket-relative addresses (ks = sip << b0, kd = dip << b1): each prefix matches iff the
 // bits above its marker (the lowest set bit above the flag bits: 0-1 in the sip word, 0 in the dip word) equal the
@@ -1040,7 +1040,7 @@ __device__ __forceinline__ bool key_match(uint32_t ax, uint32_t ay, uint32_t az,
 }
 
 // FlowFind (flow.c:96-115) over the table as it stood at the start of the batch: the slot of the live flow of
-// this 5-tuple, or -1.  One 64-B group (PPE_FLOW_GROUP 32-B slot records, their key halves read) per probe step;
+// this 5-tuple, or -1.  One 64-B group (PPE_FLOW_GROUP 16-B keys of the probe array) per probe step;
 // stops at the first EMPTY slot.
 __device__ __forceinline__ int32_t flow_find(const ppe_flowdev &f, uint32_t fh, uint32_t sip, uint32_t dip,
                                              uint32_t ports, uint32_t proto, uint32_t &fsip, uint32_t &fports) {
@@ -1068,7 +1068,7 @@ __device__ __forceinline__ int32_t flow_find(const ppe_flowdev &f, uint32_t fh, 
 }
 
 // FlowGetPacketDirection (flow.c:248-269) + FlowUpdate (flow.c:163-178) + FLOW_UPDATE_TIMESTAMP: the packet's
-// direction flag; per-direction packet / byte counters by one memory-side atomic, last-seen time into the slot record
+// direction flag; per-direction packet / byte counters by one memory-side atomic, last-seen time into the counter record
 // (whose line the probe has just read).
 __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t s, uint32_t fsip, uint32_t fports,
                                                  uint32_t sip, uint32_t ports, uint32_t wire_len, uint64_t now) {
@@ -2062,7 +2062,7 @@ __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t
                 nw[d] = (p << PPE_PK_SHIFT) | b;
             }
         }
-        // the whole 32-B record: both directions, the last-seen time (one line per flow)
+        // the whole 32-B counter record: both directions, the last-seen time
         ulonglong2 *rp = (ulonglong2 *)(f.packed + (size_t)PPE_FLOW_REC_WORDS * s);
         rp[0] = make_ulonglong2(nw[0], nw[1]);
         rp[1] = make_ulonglong2((unsigned long long)a.now, 0ull);
