@@ -412,6 +412,7 @@ typedef struct {
     uint32_t *dgram_len;       /* n: its pkt_totallen (a ppe_batch_t.len); 0 for j >= the datagram count        */
     uint8_t  *dgram_pkt;       /* optional n × reasm_buf_bytes: the whole reassembled frames                    */
     uint64_t *dgram_frags;     /* optional n × cache_max: ids of datagram j's fragments in chain order, ~0 pad   */
+                               /* (dgram_hdr / dgram_pkt / dgram_frags rows j >= the datagram count: not written) */
     uint32_t *n_dgram;         /* optional device word: datagrams written                                      */
     uint32_t  hdr_stride;      /* 64 or 128                                                                    */
     uint32_t  pad;
@@ -432,8 +433,9 @@ typedef struct ppe_defrag_table ppe_defrag_t;
 int  ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t **out);
 int  ppe_defrag_destroy(ppe_defrag_t *d);                              /* FragModule_Release */
 /* Defrag for a device-resident batch of fragments, stream-ordered on `stream` (batches in call order).
- * Every output is written for all n entries (dgram_* entries past the datagram count: length 0), so a
- * ppe_classify of {dgram_hdr, dgram_len, n, hdr_stride} can follow on the same stream without a host sync. */
+ * status, dgram_of and dgram_len are written for all n entries (dgram_len 0 past the datagram count: a runt frame
+ * whose verdict does not depend on its window bytes), so a ppe_classify of {dgram_hdr, dgram_len, n, hdr_stride}
+ * can follow on the same stream without a host sync. */
 int  ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out_t *out, void *stream);
 /* Frag_defrag_timeout: free FCBs that completed, or with now > last && now - last > timeout_seconds; the ids of
  * the fragments they still held go to dropped[0..max) (host; may be NULL), *n_dropped = their count, *n_freed =

@@ -735,27 +735,9 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
         a.ctl[C_DGRAMS] += nd;
         if (a.n_dgram) *a.n_dgram = nd;
     }
-    {
-        // the slots of this workgroup's range past the datagram count: zero window, length 0, ~0 id row (the ABI's
-        // "every output written"), as whole-workgroup coalesced stores instead of one assembly wave per slot
-        const uint32_t s0 = max(nd, blockIdx.x * kBlock), s1 = min(a.n, (blockIdx.x + 1) * kBlock);
-        if (s0 < s1) {
-            if (a.dgram_hdr) {
-                const size_t lo = (size_t)s0 * a.hdr_stride, hi = (size_t)s1 * a.hdr_stride;
-                if (((uintptr_t)a.dgram_hdr & 15u) == 0 && (a.hdr_stride & 15u) == 0) {
-                    for (size_t o = lo + 16u * threadIdx.x; o < hi; o += 16u * kBlock)
-                        *(uint4 *)(a.dgram_hdr + o) = make_uint4(0u, 0u, 0u, 0u);
-                } else {
-                    for (size_t o = lo + threadIdx.x; o < hi; o += kBlock) a.dgram_hdr[o] = 0;
-                }
-            }
-            if (a.dgram_len)
-                for (uint32_t t = s0 + threadIdx.x; t < s1; t += kBlock) a.dgram_len[t] = 0;
-            if (a.dgram_frags)
-                for (size_t e = (size_t)s0 * a.cache_max + threadIdx.x; e < (size_t)s1 * a.cache_max; e += kBlock)
-                    a.dgram_frags[e] = ~0ull;
-        }
-    }
+    // the slots of this workgroup's range past the datagram count: length 0 (a classify over all n slots sees runt
+    // frames there, whatever their window bytes; the window and id rows past the count are not written)
+    if (a.dgram_len && i < a.n && i >= nd) a.dgram_len[i] = 0;
     const uint32_t r = i < a.n ? a.dgrec[i] : kNone;
     const bool f = r != kNone;
     const uint64_t b = __builtin_amdgcn_ballot_w64(f);
