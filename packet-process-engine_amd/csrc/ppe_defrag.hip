@@ -688,8 +688,15 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
                   (unsigned long long)wg[threadIdx.x]);
 }
 
+// DF_AB (diagnostic builds only, wrong outputs): 2 = no window bytes, 4 = no header checksum, 8 = datagram bytes not
+// copied, 16 = held frames not stashed
+#ifndef DF_AB
+#define DF_AB 0
+#endif
+
 // ---- stash: copy held frames into their FCB's store slot (PACKET_HW2SW; run in the assembly launch) ------------------
 __device__ __forceinline__ void df_stash_one(const DfArgs &a, uint32_t i) {
+    if (DF_AB & 16) return;
     const uint32_t ins = a.inserted[i];
     if (ins == kNone) return;
     const uint32_t r = ins >> 8, k = ins & 0xffu;
@@ -789,18 +796,13 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
 }
 
 // ---- assemble: one wave per datagram slot ----------------------------------------------------------------------
-// DF_AB (diagnostic builds only, wrong outputs): 2 = no window bytes, 4 = no header checksum, 8 = datagram bytes not
-// copied
-#ifndef DF_AB
-#define DF_AB 0
-#endif
 #ifndef DF_COPY_U
 #define DF_COPY_U 8
 #endif
 __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, uint32_t nd) {
     const uint32_t tid = __lane_id();
     uint8_t *win = (a.dgram_hdr && !(DF_AB & 2)) ? a.dgram_hdr + (size_t)j * a.hdr_stride : nullptr;
-    if (j >= nd) return;   // an empty slot: the place kernel wrote its window, length and id row
+    if (j >= nd) return;   // an empty slot: the place kernel wrote its length
     // lane p holds chain entry p of the plan (df_place_kernel): descriptor words 0 (offset | frag_len << 16), 1 (frame
     // length), 2 (l2 | ihl*4 << 8 | proto << 16), the frame's base (the input frame when the fragment arrived in
     // this batch, else its store slot) and its id: one read for the whole chain, used below by lane broadcasts
