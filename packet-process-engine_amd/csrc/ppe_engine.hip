@@ -92,6 +92,7 @@ struct FlowTable {
     // thing the stream runs, and its snapshot follows within microseconds (blocking-sync: the host sleeps on it)
     hipEvent_t pre_launch = nullptr;
     bool use_event = true;
+    uint32_t fin_cap = 0;  // finalize workgroups at most (0: one per CU; PPE_FLOW_FIN_WGS, default half the CUs)
     // ring over the last kSnapRing batches: packets submitted before batch b (of batches that may revoke: _rev)
     static constexpr uint32_t kSnapRing = 4096;
     std::vector<uint64_t> cum_n, cum_rev;
@@ -1329,6 +1330,9 @@ int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
     t->capacity = capacity;
     t->max_batch = max_batch;
     t->use_event = env_int("PPE_FLOW_EVENT", 0) != 0;
+    // finalize on half the CUs: the update workgroups (one per CU by their LDS) start on the other half at once
+    // (F1 batch 67.1 -> 66.3 µs against one per CU, 69.3 / 71.9 at 64 / 32: profiles/r5_ab_runs.md r5aq)
+    t->fin_cap = (uint32_t)std::max(0, env_int("PPE_FLOW_FIN_WGS", (int)std::max(1u, c->n_cu / 2u)));
     // test hook: lower fold thresholds so the fold path runs on small inputs (values <= the defaults only)
     const int fp = env_int("PPE_FLOW_FOLD_PKTS", 0), fb = env_int("PPE_FLOW_FOLD_BYTES", 0);
     if (fp > 0 && (unsigned long long)fp < t->fold_pkts) t->fold_pkts = (unsigned long long)fp;
@@ -1435,7 +1439,8 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     // (disjoint from the slots finalize touches).  When the host's bound says the pool may overflow, finalize checks
     // the exact counts and, on an overflow, marks the creators and has its workgroup 0 revoke those past the pool's
     // room first.
-    const uint32_t fg = std::min(flow_grid(c, (in->n + 63u) / 64u, PPE_FLOW_POST_BLOCK / 64u), c->n_cu);
+    const uint32_t fg = std::min(std::min(flow_grid(c, (in->n + 63u) / 64u, PPE_FLOW_POST_BLOCK / 64u), c->n_cu),
+                                 t.fin_cap ? t.fin_cap : c->n_cu);
     const bool may_overflow = t.live_ub + in->n > t.capacity;
     k.revoke = may_overflow ? 1u : 0u;
     k.fin_wgs = fg;
