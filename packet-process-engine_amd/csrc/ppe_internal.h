@@ -57,7 +57,9 @@ enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_N
 /* Owner-computed FlowUpdate (flow_update_wg, ppe_flow_post_kernel): a found packet's counter update goes to a bucket of its slot's
  * owner (one of at most PPE_UPD_OWNERS slot ranges) in its classify workgroup's column, instead of a memory-side
  * atomic per packet; each owner's workgroup then sums its buckets in LDS and updates each touched slot once. */
+#ifndef PPE_UPD_OWNERS
 #define PPE_UPD_OWNERS 256u
+#endif
 #define PPE_UPD_CAP 16u        /* entries per (owner, classify workgroup) bucket; a full bucket: the direct atomic */
 #ifndef PPE_UPD_HASH
 #define PPE_UPD_HASH 4096u     /* LDS hash entries of an owner workgroup (slots it accumulates; more: direct atomics) */
