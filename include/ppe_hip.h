@@ -318,7 +318,10 @@ typedef struct {
 /* FlowInit (flow.c:471-516): create / replace the context's table.  capacity 0 = 100000, max_batch 0 = 1<<20. */
 int  ppe_flow_create(ppe_ctx_t *ctx, uint32_t capacity, uint32_t max_batch);
 int  ppe_flow_destroy(ppe_ctx_t *ctx);                                /* FlowRelease (flow.c:519-530) */
-/* FlowHandlePacket for a device-resident batch (same buffers as ppe_classify), stream-ordered on `stream`. */
+/* FlowHandlePacket for a device-resident batch (same buffers as ppe_classify), stream-ordered on `stream`.
+ * A batch is two launches (classify, then finalize + counter update).  If the second one cannot be launched, the call
+ * returns PPE_EIO and the table is unusable from then on: every later ppe_classify_flow / ppe_flow_age / _info /
+ * _clear_stat / _dump returns PPE_EIO at once, until ppe_flow_destroy (or a new ppe_flow_create). */
 int  ppe_classify_flow(ppe_ctx_t *ctx, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
                        void *stream);
 /* FlowAgeTimeoutCB: delete flows with now > last_seen && now - last_seen > timeout_seconds; *deleted = count

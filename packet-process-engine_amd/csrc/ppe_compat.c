@@ -116,6 +116,9 @@ uint32_t DP_Acl_Load_Rule(rule_list_t *rl, TreeSet **tset, TreeNode **tnode) {
     ppe_acl_stats_t st;
     uint64_t token = 0;
     pthread_mutex_lock(&g_ctx_lock);
+    /* A switch of g_acltree_running that no classify step has synced yet reaches the engine first: the engine has
+     * two slots, and the stage below reuses the back one, which may hold exactly that unpublished classifier. */
+    sync_running_locked();
     const int rc = g_ctx ? ppe_rules_stage(g_ctx, t, used, RULE_ENTRY_MAX, dp_acl_action_default, &st, &token)
                          : PPE_ENODEV;
     pthread_mutex_unlock(&g_ctx_lock);

@@ -64,9 +64,12 @@ constexpr uint32_t kRecWords = 8;
 
 // control words (u64)
 enum { C_RUNNING = 0, C_NEW, C_DEL, C_FREE_TOP, C_DGRAMS, C_TEARDROP, C_TIMEOUT_DROP, C_NDGRAM, C_ST0 = 8,
-       C_CREATORS = C_ST0 + PPE_DF__COUNT + 2, C_AGE_DROPPED, C_AGE_FREED, C_SCRATCH, C_LOOK_ERR, C_GOVF,
-       C_WORDS = 26 };
-static_assert(C_GOVF < C_WORDS, "control words");
+       C_CREATORS = C_ST0 + PPE_DF__COUNT + 2, C_AGE_DROPPED, C_AGE_FREED, C_SCRATCH, C_LOOK_ERR,
+       C_FAILN, C_FAIL0, C_WORDS = C_FAIL0 + 4 + 3 };
+// C_FAILN / C_FAIL0..: this call's admission workgroups whose look-back failed (count, then the first kMaxFail ids):
+// the group kernel returns the free-stack records their creators' ranks skipped
+constexpr uint32_t kMaxFail = 4;
+static_assert(C_FAIL0 + kMaxFail <= C_WORDS, "control words");
 
 // parsed fragment record words (frec): sip, dip, id | proto << 16 | mf << 24, off | flen << 16, totlen,
 // l2 | ihl4 << 8, hash, valid
@@ -104,9 +107,9 @@ struct DfArgs {
     uint32_t *frec, *fslot, *inserted, *dgrec, *tcnt;
     uint32_t *plan;                      // assembly plan: min(max_batch, fcb_max) × cache_max entries of 8 words
     // grouping (df_group_kernel): each fragment's group key; per group key, its members besides the key fragment
-    // (count, kGroupSlots slots in claim order), past that the overflow list of (key, index) pairs; the per-tile
+    // (count, kGroupSlots slots in claim order; a group with more members is enumerated from gkey); the per-tile
     // counts of completing fragments (process → place)
-    uint32_t *gkey, *gcnt, *gslot, *govf, *dcnt;
+    uint32_t *gkey, *gcnt, *gslot, *dcnt;
     unsigned long long *look;            // admission: per-workgroup look-back words (epoch << 32 | flags | count)
     uint32_t epoch, nlook;               // this call's tag (never 0) and the look-back array's length
     uint32_t look_spins;                 // admission: polls of an unpublished predecessor before giving up
@@ -365,6 +368,8 @@ __global__ void __launch_bounds__(kBlock) df_admit_kernel(DfArgs a) {
             // ppe_defrag_info return PPE_EIO
             if (failed) {
                 atomicAdd(a.ctl + C_LOOK_ERR, 1ull);
+                const unsigned long long q = atomicAdd(a.ctl + C_FAILN, 1ull);
+                if (q < kMaxFail) a.ctl[C_FAIL0 + q] = blockIdx.x;
                 __hip_atomic_store(a.err_host, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             } else {
                 __hip_atomic_store(a.look + blockIdx.x, tag | kIncl | (excl + agg), __ATOMIC_RELAXED,
@@ -415,24 +420,45 @@ constexpr uint32_t kGroupSlots = 15;      // members besides the key fragment he
 constexpr uint32_t kGroupStride = 16;     // words per group in gslot (64 B)
 
 // One lane per fragment: its group key; a member (key != its index) takes a slot of its group by an atomic ticket
-// (claim order, sorted back into batch order by the group's head in df_process_kernel), or past kGroupSlots an
-// overflow entry.  Also: the parsed record's words 6-7 for the process kernel, the completion tile counts cleared,
+// (claim order, sorted back into batch order by the group's head in df_process_kernel) while slots remain; past
+// kGroupSlots it is only counted (the head then finds every member from gkey).  Also: the parsed record's words 6-7 for the process kernel, the completion tile counts cleared,
 // and (workgroup 0) the running count and free-stack top moved past this batch's admissions.
 __global__ void __launch_bounds__(kBlock) df_group_kernel(DfArgs a) {
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     if (blockIdx.x == 0) {
         // after the admission kernel: the creators of this batch (the tile counts it ranked) move the running count
         // and the free-stack top (fcb_create's fetch-and-add, decode-defrag.c:74-81)
+        const uint32_t tiles = (a.n + 63) / 64;
         uint32_t creators = 0;
-        wg_tile_prefix<kBlock>(a.tcnt, 0u, (a.n + 63) / 64, &creators);
+        wg_tile_prefix<kBlock>(a.tcnt, 0u, tiles, &creators);
+        const unsigned long long run = a.ctl[C_RUNNING], top = a.ctl[C_FREE_TOP];
+        const unsigned long long room = run < a.fcb_max ? a.fcb_max - run : 0ull;
+        const uint32_t adm = (uint32_t)(creators < room ? creators : room);
+        // A workgroup whose look-back failed created none of its creators' FCBs, but its count stands in every later
+        // rank: the records at its ranks (below adm) were skipped.  They go back onto the stack, under the new top, so
+        // the running count and the free stack stay exact.  (Rare: no failure, nothing to do.)
+        const uint32_t nfail = (uint32_t)(a.ctl[C_FAILN] < kMaxFail ? a.ctl[C_FAILN] : kMaxFail);
+        uint32_t skipped = 0, held[kMaxFail], hn[kMaxFail], ho[kMaxFail];
+        for (uint32_t f = 0; f < nfail; ++f) {
+            const uint32_t t0 = min((uint32_t)a.ctl[C_FAIL0 + f] * (kBlock / 64), tiles);
+            __syncthreads();   // (wg_tile_prefix's partial sums are reused)
+            const uint32_t lo = min(wg_tile_prefix<kBlock>(a.tcnt, t0, tiles, nullptr), adm);
+            __syncthreads();
+            const uint32_t hi = min(wg_tile_prefix<kBlock>(a.tcnt, min(t0 + kBlock / 64, tiles), tiles, nullptr), adm);
+            hn[f] = hi - lo;
+            ho[f] = skipped;
+            skipped += hi - lo;
+            if (threadIdx.x < hi - lo) held[f] = a.freestk[top - 1 - (lo + threadIdx.x)];
+        }
+        __syncthreads();   // every skipped record read before any is written
+        for (uint32_t f = 0; f < nfail; ++f)
+            if (threadIdx.x < hn[f]) a.freestk[top - adm + ho[f] + threadIdx.x] = held[f];
         if (threadIdx.x == 0) {
-            const unsigned long long run = a.ctl[C_RUNNING];
-            const unsigned long long room = run < a.fcb_max ? a.fcb_max - run : 0ull;
-            const unsigned long long adm = creators < room ? creators : room;
             a.ctl[C_CREATORS] = creators;
-            a.ctl[C_RUNNING] = run + adm;
-            a.ctl[C_FREE_TOP] -= adm;
-            a.ctl[C_NEW] += adm;
+            a.ctl[C_RUNNING] = run + adm - skipped;
+            a.ctl[C_FREE_TOP] = top - adm + skipped;
+            a.ctl[C_NEW] += adm - skipped;
+            a.ctl[C_FAILN] = 0;
         }
     }
     if (j >= a.n) return;
@@ -450,12 +476,7 @@ __global__ void __launch_bounds__(kBlock) df_group_kernel(DfArgs a) {
     *(uint2 *)(a.frec + (size_t)j * kFrecWords + 6) = w67;
     if (key != j) {
         const uint32_t pos = atomicAdd(a.gcnt + key, 1u);
-        if (pos < kGroupSlots) {
-            a.gslot[(size_t)key * kGroupStride + pos] = j;
-        } else {
-            const uint32_t o = (uint32_t)atomicAdd(a.ctl + C_GOVF, 1ull);
-            *(uint2 *)(a.govf + 2ull * o) = make_uint2(key, j);
-        }
+        if (pos < kGroupSlots) a.gslot[(size_t)key * kGroupStride + pos] = j;
     }
 }
 
@@ -645,22 +666,33 @@ __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint
     for (uint32_t u = 0; u < kWin; ++u)
         if (u < m) step(iq[u], fw[u]);
     if (more) {
-        // more members than slots: the slots hold an arbitrary kGroupSlots of them, the overflow list the rest;
-        // each next member is the smallest index above the last one stepped
-        const uint32_t no = (uint32_t)a.ctl[C_GOVF];
-        uint32_t last = g;
-        for (uint32_t k = 0; k < cnt; ++k) {
-            uint32_t x = kNone;
-            for (uint32_t u = 0; u < kGroupSlots; ++u) {
-                const uint32_t y = a.gslot[(size_t)g * kGroupStride + u];
-                if (y > last && y < x) x = y;
+        // more members than slots (rare): the members are the indices above the head whose group key is the head's,
+        // found in batch order by one pass over gkey from g + 1 that stops at the last member.  Cost: the span from
+        // the head to its last member in 16-index rounds (independent key loads, then the matches' records loaded
+        // together), plus one step per member: linear in the batch, whatever the number of members or of groups
+        // past their slots (a scan of a shared overflow list per member was O(cnt x overflow)).
+        constexpr uint32_t R = 16;
+        uint32_t left = cnt;
+        for (uint32_t base = g + 1; left && base < a.n; base += R) {
+            uint32_t mask = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < R; ++u) {
+                const uint32_t x = base + u;
+                mask |= (x < a.n && a.gkey[x] == g) ? 1u << u : 0u;
             }
-            for (uint32_t e = 0; e < no; ++e) {
-                const uint2 q = *(const uint2 *)(a.govf + 2ull * e);
-                if (q.x == g && q.y > last && q.y < x) x = q.y;
+            uint4 fr[R];
+#pragma unroll
+            for (uint32_t u = 0; u < R; ++u)
+                if ((mask >> u) & 1u) fr[u] = *(const uint4 *)(a.frec + (size_t)(base + u) * kFrecWords + 2);
+            while (mask) {
+                const uint32_t u = (uint32_t)__builtin_ctz(mask);
+                mask &= mask - 1u;
+                uint4 w = fr[0];
+#pragma unroll
+                for (uint32_t v = 1; v < R; ++v) w = v == u ? fr[v] : w;   // (a select chain: no indexed registers)
+                step(base + u, w);
+                --left;
             }
-            step(x, *(const uint4 *)(a.frec + (size_t)x * kFrecWords + 2));
-            last = x;
         }
     }
     *(uint4 *)h = make_uint4(flags | (last_in << 8) | (cache_num << 16) | (nlist << 24), (uint32_t)total,
@@ -737,7 +769,6 @@ __global__ void __launch_bounds__(kBlock) df_place_kernel(DfArgs a) {
     uint32_t base = wg_tile_prefix<kBlock>(a.dcnt, t0, (a.n + 63) / 64, &nd);
     for (uint32_t k = 0; k < w; ++k) base += a.dcnt[t0 + k];   // the workgroup's earlier waves
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // the datagram count (read by the assembly kernel, next)
-        a.ctl[C_GOVF] = 0;   // (the process kernel, the overflow list's only reader, has completed)
         a.ctl[C_NDGRAM] = nd;
         a.ctl[C_DGRAMS] += nd;
         if (a.n_dgram) *a.n_dgram = nd;
@@ -1119,7 +1150,6 @@ int ppe_defrag_create(ppe_ctx_t *ctx, const ppe_defrag_cfg_t *cfg, ppe_defrag_t 
               dalloc(d, &a.plan, (size_t)std::min(mb, c.fcb_max) * c.cache_max * 8) &&
               dalloc(d, &a.tcnt, blocks(mb, 64)) && dalloc(d, &a.dcnt, blocks(mb, 64)) && dalloc(d, &a.gkey, mb) &&
               dalloc(d, &a.gcnt, mb) && dalloc(d, &a.gslot, (size_t)mb * kGroupStride) &&
-              dalloc(d, &a.govf, 2ull * mb) &&
               dalloc(d, &a.dropped, (size_t)c.fcb_max * c.cache_max) &&
               dalloc(d, &a.look, blocks(mb, kBlock));
     if (ok && hipHostMalloc((void **)&d->h_ctl, C_WORDS * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)

@@ -97,6 +97,10 @@ struct FlowTable {
     static constexpr uint32_t kSnapRing = 4096;
     std::vector<uint64_t> cum_n, cum_rev;
     uint64_t tot_n = 0, tot_rev = 0;
+    // set when a batch's post-classify launch failed after its classify launch ran: that batch's claims were never
+    // finalized (miss-tile counter, snapshot, creators), so every later call on the table fails until
+    // ppe_flow_destroy / ppe_flow_create
+    bool broken = false;
 };
 
 }  // namespace
@@ -1294,6 +1298,25 @@ static int flow_maybe_rehash(ppe_ctx *c) {
     return PPE_OK;
 }
 
+// Test hook (tests/test_gpu_flow.py only, not in the public headers): the next `k` post-classify launches of
+// ppe_classify_flow fail as a launch error would, after the batch's classify launch has run.
+static uint32_t g_fail_post = 0;
+extern "C" void ppe_flow_debug_fail_post(uint32_t k) { __atomic_store_n(&g_fail_post, k, __ATOMIC_RELAXED); }
+static bool take_fail_post() {
+    uint32_t k = __atomic_load_n(&g_fail_post, __ATOMIC_RELAXED);
+    while (k)
+        if (__atomic_compare_exchange_n(&g_fail_post, &k, k - 1, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) return true;
+    return false;
+}
+
+// the table exists and no batch was left half-done by a failed post-classify launch
+static int flow_usable(ppe_ctx *c) {
+    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    if (c->flow->broken)
+        return fail(c, PPE_EIO, "flow table unusable: a batch's post-classify launch failed (ppe_flow_destroy it)");
+    return PPE_OK;
+}
+
 int ppe_flow_destroy(ppe_ctx_t *c) {
     if (!c) return PPE_EINVAL;
     if (!c->flow) return PPE_OK;
@@ -1384,7 +1407,7 @@ int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
 int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *out, const ppe_cfg_t *cfg,
                       void *stream) {
     if (!c || !out) return PPE_EINVAL;
-    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    if (const int u = flow_usable(c)) return u;
     if (!out->verdict) return fail(c, PPE_EINVAL, "ppe_classify_flow needs the verdict output");
     int rc = check_batch(c, in, cfg);
     if (rc != PPE_OK || in->n == 0) return rc;
@@ -1445,8 +1468,12 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
     k.revoke = may_overflow ? 1u : 0u;
     k.fin_wgs = fg;
     {
-        const int e = ppe_launch_flow(PPE_FLOW_K_POST, &k, fg + (t.upd_wgs ? t.upd_owners : 0u), (void *)s);
-        if (e != 0) return fail(c, PPE_EIO, "flow post-classify launch failed: %s", hipGetErrorString((hipError_t)e));
+        const int e = take_fail_post() ? (int)hipErrorLaunchFailure
+                                       : ppe_launch_flow(PPE_FLOW_K_POST, &k, fg + (t.upd_wgs ? t.upd_owners : 0u), (void *)s);
+        if (e != 0) {
+            t.broken = true;  // the classify launch above claimed slots that nothing will finalize
+            return fail(c, PPE_EIO, "flow post-classify launch failed: %s", hipGetErrorString((hipError_t)e));
+        }
     }
     t.cum_n[t.batches % FlowTable::kSnapRing] = t.tot_n;
     t.cum_rev[t.batches % FlowTable::kSnapRing] = t.tot_rev;
@@ -1460,7 +1487,7 @@ int ppe_classify_flow(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
 
 int ppe_flow_age(ppe_ctx_t *c, uint64_t now_seconds, uint64_t timeout_seconds, uint64_t *deleted) {
     if (!c) return PPE_EINVAL;
-    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    if (const int u = flow_usable(c)) return u;
     HIPCHK(c, use_device(c));
     FlowTable &t = *c->flow;
     unsigned long long before[PPE_FCTL_WORDS], after[PPE_FCTL_WORDS];
@@ -1482,7 +1509,7 @@ int ppe_flow_age(ppe_ctx_t *c, uint64_t now_seconds, uint64_t timeout_seconds, u
 
 int ppe_flow_info(ppe_ctx_t *c, ppe_flow_info_t *info) {
     if (!c || !info) return PPE_EINVAL;
-    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    if (const int u = flow_usable(c)) return u;
     HIPCHK(c, use_device(c));
     unsigned long long ctl[PPE_FCTL_WORDS];
     const int rc = flow_sync_counts(c, ctl);
@@ -1502,7 +1529,7 @@ int ppe_flow_info(ppe_ctx_t *c, ppe_flow_info_t *info) {
 
 int ppe_flow_clear_stat(ppe_ctx_t *c) {
     if (!c) return PPE_EINVAL;
-    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    if (const int u = flow_usable(c)) return u;
     HIPCHK(c, use_device(c));
     HIPCHK(c, hipDeviceSynchronize());
     HIPCHK(c, hipMemset(c->flow->ctl + PPE_FCTL_NEW_FLOW, 0, 16u));  // new_flow, del_flow
@@ -1511,7 +1538,7 @@ int ppe_flow_clear_stat(ppe_ctx_t *c) {
 
 int ppe_flow_dump(ppe_ctx_t *c, ppe_flow_entry_t *entries, uint32_t max, uint32_t *n) {
     if (!c || !n) return PPE_EINVAL;
-    if (!c->flow) return fail(c, PPE_EINVAL, "no flow table (ppe_flow_create)");
+    if (const int u = flow_usable(c)) return u;
     HIPCHK(c, use_device(c));
     HIPCHK(c, hipDeviceSynchronize());
     const FlowTable &t = *c->flow;

@@ -112,23 +112,31 @@ int Rule_del_all(void) {
 
 /* ---- '@' rule line parser: field readers follow rule/rule.c:27-173 ---- */
 
+/* The reference reads every number with %d into an unsigned int (rule/rule.c:34,52,85,100): glibc converts with
+ * strtol (saturating at LONG_MAX / LONG_MIN) and stores the low 32 bits.  %d into an int and a cast give the same bits
+ * for every input, %u does not (it converts with strtoul: "9223372036854775808" is 0 there, 0xffffffff here).
+ * Pinned against the reference's own rule.c by tests/test_rules.py (tests/golden/ref_rule_v1.npz). */
 static int read_ip(FILE *fp, uint32_t *ip_out, uint32_t *mask_out) {
-    unsigned int o[4], mask;
+    int o[4], mask;
     char slash;
-    if (fscanf(fp, "%u.%u.%u.%u", &o[0], &o[1], &o[2], &o[3]) != 4) return -1;
+    if (fscanf(fp, "%d.%d.%d.%d", &o[0], &o[1], &o[2], &o[3]) != 4) return -1;
     if (fscanf(fp, "%c", &slash) != 1 || slash != '/') return -1;
-    if (fscanf(fp, "%u", &mask) != 1) return -1;
+    if (fscanf(fp, "%d", &mask) != 1) return -1;
     /* octets are shifted and OR'ed without range checks (rule/rule.c:58-61) */
     const uint32_t ip = ((uint32_t)o[0] << 24) | ((uint32_t)o[1] << 16) | ((uint32_t)o[2] << 8) | (uint32_t)o[3];
-    if (ip == 0 && mask != 0) return -1;  /* rule/rule.c:63-68 */
-    if (ip != 0 && mask > 32) return -1;  /* rule/rule.c:69-73 */
+    if (ip == 0 && mask != 0) return -1;            /* rule/rule.c:63-68 */
+    if (ip != 0 && (uint32_t)mask > 32u) return -1; /* rule/rule.c:69-73 (an unsigned compare there) */
     *ip_out = ip;
-    *mask_out = mask;
+    *mask_out = (uint32_t)mask;
     return 0;
 }
 
 static int read_range(FILE *fp, unsigned int *from, unsigned int *to) {
-    return fscanf(fp, "%u : %u", from, to) == 2 ? 0 : -1;
+    int a, b;
+    if (fscanf(fp, "%d : %d", &a, &b) != 2) return -1;
+    *from = (unsigned int)a;
+    *to = (unsigned int)b;
+    return 0;
 }
 
 static int read_mac(FILE *fp, uint8_t *mac) {

@@ -359,3 +359,74 @@ def test_load_rule_then_set_running_tree():
     finally:
         lib.ppe_rule_list_free()
         lib.DP_Acl_Rule_Release()
+
+
+def test_load_after_unsynced_running_switch():
+    """set_running_acltree(B) followed by DP_Acl_Load_Rule into the other unit with no classify step in
+    between.  The engine has two slots; the second load must not overwrite B's unpublished classifier: the next
+    classify runs rules B, and rules C only once g_acltree_running names C's unit."""
+    lib = abi.load()
+    lib.ppe_set_output_hooks.argtypes = [HOOK, HOOK, HOOK]
+    lib.DP_Acl_Load_Rule.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.DP_Acl_Rule_Clean.argtypes = [C.c_void_p, C.c_void_p]
+    assert lib.DP_Acl_Rule_Init() == 0
+    lib.ppe_rule_list_free()
+    assert lib.ppe_rule_list_init() == 0
+    lib.Decode_Set_Burst(1)
+    ra = synth.make_rules(64, seed=97)
+    rb = synth.make_rules(1, seed=98)
+    rb["sip_mask"] = rb["dip_mask"] = 0
+    rb["sport_start"] = rb["dport_start"] = 0
+    rb["sport_end"] = rb["dport_end"] = 65535
+    rb["protocol_start"], rb["protocol_end"] = 0, 255
+    rc = rb.copy()
+    rb["action"] = 0   # B: forward everything
+    rc["action"] = 1   # C: drop everything
+
+    def load(rules):
+        assert lib.Rule_del_all() == 0
+        for i in range(len(rules)):
+            assert lib.Rule_add(rules[i:i + 1].ctypes.data, C.byref(C.c_uint32())) == 0
+
+    pk = synth.make_packets(300, ra, seed=101, kind="udp64", stride=128, hit_frac=0.8)
+    n = len(pk["len"])
+    bufs = [C.create_string_buffer(bytes(pk["hdr"][i][: min(int(pk["len"][i]) & 0xFFFF, 128)]), 144) for i in range(n)]
+    mbufs = (Mbuf * n)()
+    for i in range(n):
+        mbufs[i].pkt_ptr = C.cast(bufs[i], C.c_void_p)
+        mbufs[i].pkt_totallen = int(pk["len"][i])
+
+    def decode_all():
+        for i in range(n):
+            lib.Decode(C.byref(mbufs[i]))
+        return np.array([(mbufs[i].ppe_verdict, mbufs[i].ppe_acl_hit) for i in range(n)], np.int64)
+
+    def ref(rules):
+        o = pyoracle.Oracle(rules, default_action=1)
+        r = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, 0))
+        return np.stack([r["verdict"].astype(np.int64), r["acl_hit"].astype(np.int64)], 1)
+
+    ref_b, ref_c = ref(rb), ref(rc)
+    assert not np.array_equal(ref_b, ref_c)
+    g1, g2 = UnitTree.in_dll(lib, "g_acltree_1"), UnitTree.in_dll(lib, "g_acltree_2")
+    running = C.c_ulong.in_dll(lib, "g_acltree_running")
+    rl = C.c_void_p.in_dll(lib, "rule_list").value
+    ts = lambda u: C.addressof(u) + UnitTree.TreeSet.offset   # noqa: E731
+    tn = lambda u: C.addressof(u) + UnitTree.TreeNode.offset  # noqa: E731
+    try:
+        load(ra)
+        assert lib.DP_Acl_Rule_Commit() == 0                      # rules A run
+        x = g1 if running.value == C.addressof(g1) else g2
+        y = g2 if x is g1 else g1
+        load(rb)
+        assert lib.DP_Acl_Load_Rule(rl, ts(y), tn(y)) == 0        # B staged into unit y
+        running.value = C.addressof(y)                          # set_running_acltree(y): nothing classified yet
+        load(rc)
+        lib.DP_Acl_Rule_Clean(ts(x), tn(x))
+        assert lib.DP_Acl_Load_Rule(rl, ts(x), tn(x)) == 0        # C staged into unit x
+        assert np.array_equal(decode_all(), ref_b)               # B runs, not A and not C
+        running.value = C.addressof(x)
+        assert np.array_equal(decode_all(), ref_c)
+    finally:
+        lib.ppe_rule_list_free()
+        lib.DP_Acl_Rule_Release()

@@ -252,6 +252,43 @@ def test_groups_past_the_slots(eng):
             p.close()
 
 
+def test_one_key_flood_is_linear(eng):
+    """one batch of 40,000 fragments of which 24,000 share one FCB key (duplicates of one datagram's
+    fragments, as an attacker would send them), interleaved with 400 other datagrams that each pass their group's 15
+    slots too.  Parity with the oracle, and the batch must finish in well under a second: the group heads enumerate
+    their members in one pass over the batch, not one scan of a shared overflow list per member (which took
+    ~10^9 serial loads here)."""
+    import time
+    rng = np.random.default_rng(78)
+    S, D = 0x0B000001, 0x0B0000FE
+    l4 = udp(4000, 53, rng.integers(0, 256, 8 * 5, dtype=np.uint8).tobytes())
+    flood = [ip_frag(17, S, D, 7, 8 * f, f < 5, l4[8 * f:8 * f + 8]) for f in range(6)]
+    frames = [flood[f] for f in rng.integers(0, 6, 24000)]
+    for k in range(400):
+        l4k = udp(5000 + k, 53, rng.integers(0, 256, 8 * 3, dtype=np.uint8).tobytes())
+        frs = [ip_frag(17, S + 1 + k, D, 9, 8 * f, f < 3, l4k[8 * f:8 * f + 8]) for f in range(4)]
+        frames += [frs[f] for f in rng.integers(0, 4, 40)]
+    frames = [frames[i] for i in rng.permutation(len(frames))]
+    a, o, l = arena(frames)
+    p = DfPair(eng, max_batch=1 << 16)
+    try:
+        p.batch(a, o[:64], l[:64], NOW)   # (warm-up: module load, first-touch)
+        t0 = time.perf_counter()
+        p.g.run_torch(*(torch.from_numpy(x).to(DEV) for x in (a, o[64:].view(np.int64), l[64:].view(np.int32))),
+                      p.g.alloc_out(len(l) - 64, 128), NOW + 1)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert dt < 1.0, f"defrag batch with a 24k-member group took {dt:.2f} s"
+    finally:
+        p.close()
+    p = DfPair(eng, max_batch=1 << 16)
+    try:
+        p.batch(a, o, l, NOW)
+        p.check_stats()
+    finally:
+        p.close()
+
+
 def test_show_text_after_reassembly(eng):
     """`show packet statistic` / `show flow statistic` after defrag batches: the ip_frag_stat
     lines, new / del fcb and (monitor on) teardrop formatted from the GPU table's ppe_defrag_info equal the text
@@ -290,25 +327,39 @@ def test_show_text_after_reassembly(eng):
 def test_failed_admission_lookback_is_reported(eng, monkeypatch):
     """A workgroup whose admission look-back fails (forced by the PPE_DF_LOOK_FAIL test hook) admits none of its
     creators and sets a pinned error word: the NEXT ppe_defrag call fails with PPE_EIO (once), ppe_defrag_info
-    too, and the table keeps working afterwards (the failure must not stay silent)."""
+    too, and the table keeps working afterwards (the failure must not stay silent).  The records its
+    creators' ranks skipped go back onto the free stack: after aging everything out the running count is
+    0 with new_fcb == del_fcb, and a batch with more new datagrams than fcb_max then matches a fresh oracle exactly
+    (FCB_FULL at the same fragments: no record lost, none used twice)."""
     from ppe.engine import PPEError
+    fcb_max = 1 << 12
     monkeypatch.setenv("PPE_DF_LOOK_FAIL", "3")
-    g = Defrag(eng, fcb_max=1 << 16)
+    p = DfPair(eng, fcb_max=fcb_max)
     monkeypatch.delenv("PPE_DF_LOOK_FAIL")
+    g = p.g
     try:
         a, off, lens = synth.make_fragment_stream(4000, seed=4242)
         n = min(len(lens), 8192)   # >= 4 admission workgroups of 256 fragments
-        off, lens = off[:n].copy(), lens[:n].copy()
+        off1, lens1 = off[:n].copy(), lens[:n].copy()
         out = g.alloc_out(n, 128)
         ta = torch.from_numpy(a).to(DEV)
-        to = torch.from_numpy(off.view(np.int64)).to(DEV)
-        tl = torch.from_numpy(lens.view(np.int32)).to(DEV)
+        to = torch.from_numpy(off1.view(np.int64)).to(DEV)
+        tl = torch.from_numpy(lens1.view(np.int32)).to(DEV)
         g.run_torch(ta, to, tl, out, NOW)   # (asynchronous: the failure is on the device)
         torch.cuda.synchronize()
         with pytest.raises(PPEError, match="look-back"):
             g.run_torch(ta, to, tl, out, NOW + 1)
         with pytest.raises(PPEError):
             g.info()   # the device counter of failed look-backs (then cleared)
-        g.info()
+        info = g.info()
+        assert 0 < info["running"] <= fcb_max and info["new_fcb"] - info["del_fcb"] == info["running"]
+        g.age(NOW + 10**6, 20)
+        info = g.info()
+        assert info["running"] == 0 and info["new_fcb"] == info["del_fcb"]
+        # the whole free stack is back: a fresh oracle sees the same FCB_FULL boundary
+        a2, off2, lens2 = synth.make_fragment_stream(9000, seed=4343)
+        n2 = min(len(lens2), 20000)
+        got, ref = p.batch(a2, off2[:n2], lens2[:n2], NOW + 2 * 10**6)
+        assert ((ref["status"] & 0xFF) == abi.DF["FCB_FULL"]).any()
     finally:
-        g.close()
+        p.close()

@@ -224,6 +224,47 @@ def test_flow_known_answers(eng):
         p.close()
 
 
+def test_failed_post_launch_fails_fast(eng):
+    """when a batch's post-classify launch fails (forced by the test hook, after the classify launch
+    ran), that call and every later call on the table return PPE_EIO immediately instead of running against an
+    un-finalized batch; ppe_flow_destroy + ppe_flow_create give a working table again."""
+    import ctypes as C
+    import time
+    lib = eng.lib
+    lib.ppe_flow_debug_fail_post.argtypes = [C.c_uint32]
+    rules = synth.make_rules(64, seed=25)
+    p = Pair(eng, rules, capacity=10000, max_batch=1 << 13, default_action=0)
+    pk = [synth.make_flow_packets(8000, rules, n_flows=800, seed=600 + b, template_seed=600) for b in range(3)]
+    try:
+        p.batch(pk[0]["hdr"], pk[0]["len"], NOW)
+        lib.ppe_flow_debug_fail_post(1)
+        with pytest.raises(RuntimeError, match="-5"):
+            gpu_flow(eng, pk[1]["hdr"], pk[1]["len"], NOW + 1)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            with pytest.raises(RuntimeError, match="-5"):
+                gpu_flow(eng, pk[2]["hdr"], pk[2]["len"], NOW + 2)
+        assert time.perf_counter() - t0 < 10.0
+        info = abi.FlowInfo()
+        assert lib.ppe_flow_info(eng.ctx, C.byref(info)) == -5
+        assert lib.ppe_flow_age(eng.ctx, NOW + 3, 10, None) == -5
+        assert lib.ppe_flow_clear_stat(eng.ctx) == -5
+        n = C.c_uint32()
+        assert lib.ppe_flow_dump(eng.ctx, None, 0, C.byref(n)) == -5
+        assert b"unusable" in lib.ppe_last_error(eng.ctx)
+    finally:
+        lib.ppe_flow_debug_fail_post(0)
+        p.close()
+    # a fresh table works and matches the oracle again
+    p = Pair(eng, rules, capacity=10000, max_batch=1 << 13, default_action=0)
+    try:
+        for b in range(2):
+            p.batch(pk[b]["hdr"], pk[b]["len"], NOW + b)
+            p.same_table()
+    finally:
+        p.close()
+
+
 def test_flow_argument_errors(eng):
     import ctypes as C
     lib = eng.lib
