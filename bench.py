@@ -20,10 +20,11 @@ packets / the slowest rank's time (barrier + synchronize around the timed region
 verdict gather a consumer would add is timed apart (`gather`).
 
 `roofline`: the config's launch timed with its dispatch start/end timestamps (hipExtLaunchKernelGGL events on the
-launch stream); achieved = SURVEY.md 8(d)'s 80 algorithmic bytes per 64-B packet (68 read + 12 written; the kernel
-also writes a 1-B compacted-list entry (the compact partition list, ppe_result_t.part8), reported as
-`written_bytes_per_pkt`) x packets in the launch / its
-duration.  `traffic` = HBM bytes of the launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE profile of the
+launch stream) inside the same timed region as `value`; achieved = SURVEY.md 8(d)'s algorithmic bytes per 64-B
+packet (68 read + the verdict, flow hash and ACL hit written: 8 B in the default packed result layout, 12 B as three
+4-B words with `--layout soa`; the kernel also writes a 1-B compacted-list entry (the compact partition list,
+ppe_result_t.part8), counted in `written_bytes_per_pkt`) x packets in the launch / its duration; `read_frac` is the
+68 read bytes alone against the peak (north_star's read-bandwidth target).  `traffic` = HBM bytes of the launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE profile of the
 same launch shape (per packet, scaled), when one exists.  `cpu_baseline` = the oracle's C restatement (tree-walk
 ACL) timed on this host's cores as pinned run-to-completion pthreads (rank 0, N = 1).
 
@@ -103,6 +104,10 @@ def parse(argv=None):
     ap.add_argument("--packets", "--n", dest="n", type=int, default=0,
                     help="packets per GPU per step (default: the config's; strong: 8M / ranks)")
     ap.add_argument("--stride", type=int, default=64)
+    ap.add_argument("--layout", default="packed", choices=("packed", "soa"),
+                    help="result layout of the stateless configs: packed = one 8-B word per packet (flow hash, status, "
+                         "action, flags, ACL hit + 1: ppe_result_t.packed) + the 1-B compact partition list (9 B "
+                         "written); soa = the 4-B verdict, flow hash and ACL hit words + the 1-B list (13 B)")
     ap.add_argument("--nbufs", type=int, default=0, help="distinct resident batches (default: >= 8, > 600 MB and >= "
                                                           "the batches of one launch)")
     ap.add_argument("--batches-per-launch", type=int, default=0,
@@ -180,10 +185,10 @@ class Resident:
     """`nbufs` distinct device batches of one config (2 generated batches, cloned / tiled on the device: every
     buffer is its own HBM allocation) with their output buffers and pre-built C argument blocks."""
 
-    def __init__(self, name, n, stride, nbufs, rules, rank, dev):
+    def __init__(self, name, n, stride, nbufs, rules, rank, dev, layout="packed"):
         from ppe import abi
         cfgd = synth.CONFIGS[name]
-        self.n, self.stride, self.nbufs = n, stride, nbufs
+        self.n, self.stride, self.nbufs, self.layout = n, stride, nbufs, layout
         gen_n = min(n, 1 << 20)
         self.host = []
         for g in range(2):
@@ -198,16 +203,33 @@ class Resident:
             if reps > 1:
                 hdr = hdr.repeat(reps, 1)[:n].contiguous()
                 lens = lens.repeat(reps)[:n].contiguous()
-            out = {k: torch.empty(n, dtype=torch.int32, device=dev) for k in ("verdict", "flow_hash", "acl_hit")}
+            if layout == "packed":  # one 8-B word per packet: include/ppe_hip.h PPE_PACKED_*
+                out = {"packed": torch.empty(n, dtype=torch.int64, device=dev)}
+            else:
+                out = {k: torch.empty(n, dtype=torch.int32, device=dev) for k in ("verdict", "flow_hash", "acl_hit")}
             out["part8"] = torch.empty(n, dtype=torch.uint8, device=dev)
             bb = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, stride)
             # the compacted FW / PUNT / DROP lists in the compact partition layout (one byte per packet: its offset
             # in the tile and its action, include/ppe_hip.h ppe_result_t.part8)
-            rr = abi.Result(out["verdict"].data_ptr(), out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(),
-                            None, None, None, None, out["part8"].data_ptr())
+            ptr = lambda k: out[k].data_ptr() if k in out else None  # noqa: E731
+            rr = abi.Result(ptr("verdict"), ptr("flow_hash"), ptr("acl_hit"), None, None, None, None,
+                            out["part8"].data_ptr(), ptr("packed"))
             self.bufs.append((hdr, lens, out, bb, rr))
         lens0 = self.host[0]["len"].astype(np.int64)
         self.read_bytes_per_pkt = float(np.minimum(lens0 & 0xFFFF, 64).mean() + 4.0) if stride == 64 else None
+        # algorithmic result bytes (the verdict, flow hash and ACL hit: 12 B as three words, 8 B
+        # packed) and the bytes the launch really writes per packet (+ the 1-B compact list entry)
+        self.result_bytes = 8.0 if layout == "packed" else 12.0
+        self.written_bytes = self.result_bytes + 1.0
+
+    def results(self, b):
+        """Buffer b's outputs as host arrays: verdict, flow_hash, acl_hit (unpacked from the packed words)."""
+        from ppe import abi
+        out = self.bufs[b][2]
+        if self.layout == "packed":
+            return abi.unpack(out["packed"].cpu().numpy())
+        return {"verdict": out["verdict"].cpu().numpy().view(np.uint32),
+                "flow_hash": out["flow_hash"].cpu().numpy().view(np.uint32), "acl_hit": out["acl_hit"].cpu().numpy()}
 
     def arrays(self, k):
         from ppe import abi
@@ -225,9 +247,8 @@ def parity_sample(eng, res, rules, name):
     o = pyoracle.Oracle(rules, default_action=1)
     ref = o.classify_batch(pk["hdr"][:m], pk["len"][:m], cfg=o.cfg(now_seconds=NOW), nthreads=8)
     out = res.bufs[0][2]
-    got_v = out["verdict"][:m].cpu().numpy().view(np.uint32)
-    got_h = out["flow_hash"][:m].cpu().numpy().view(np.uint32)
-    got_a = out["acl_hit"][:m].cpu().numpy()
+    got = res.results(0)
+    got_v, got_h, got_a = got["verdict"][:m], got["flow_hash"][:m], got["acl_hit"][:m]
     far = ref["reach"] > res.stride
     ok = ~far
     act = (got_v >> 8) & 0xFF
@@ -289,10 +310,16 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
     clk = torch.zeros(4, dtype=torch.int64, device=dev)
     nb = min(args.steps, 32, res.nbufs)
     a = _CalibArgs()
+    packed = res.layout == "packed"
     for i in range(nb):
         hdr, lens, out = res.bufs[i][:3]
-        a.b[i] = _CalibBatch(hdr.data_ptr(), lens.data_ptr(), out["verdict"].data_ptr(), out["flow_hash"].data_ptr(),
-                             out["acl_hit"].data_ptr(), out["part8"].data_ptr(), res.n, 0)
+        if packed:  # (mode 4: the 8-B result goes to the packed buffer)
+            a.b[i] = _CalibBatch(hdr.data_ptr(), lens.data_ptr(), out["packed"].data_ptr(), None, None,
+                                 out["part8"].data_ptr(), res.n, 0)
+        else:
+            a.b[i] = _CalibBatch(hdr.data_ptr(), lens.data_ptr(), out["verdict"].data_ptr(),
+                                 out["flow_hash"].data_ptr(), out["acl_hit"].data_ptr(), out["part8"].data_ptr(),
+                                 res.n, 0)
     a.nb, a.clk = nb, clk.data_ptr()
     pk = res.n * nb
 
@@ -300,7 +327,7 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
         c = clk.cpu().tolist()
         return round((c[1] - c[0]) / max(c[3] - c[2], 1) * 100.0, 0)
 
-    def stream_run(mode):  # (mode 2: the skeleton with the kernel's 1-B compact list entry)
+    def stream_run(mode):  # (mode 2: the skeleton with the kernel's 1-B compact list entry; 4: packed 8 + 1 B)
         a.mode = mode
         ms, t = C.c_double(), []
         for _ in range(3):  # one warm launch, then the faster of two
@@ -309,7 +336,7 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
             t.append(ms.value)
         return min(t[1:]), sclk()
 
-    skel_ms, skel_clk = stream_run(2)
+    skel_ms, skel_clk = stream_run(4 if packed else 2)
     ro_ms, ro_clk = stream_run(1)
     nbytes = 1 << 30
     src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -325,11 +352,13 @@ def ceiling(res, args, dev, kern_avg_ms, pk_launch, alg):
     clocks = sample_clocks(lambda: lib.ppe_calib_stream_timed(C.byref(a), 0, sptr, C.byref(ms)))
     torch.cuda.synchronize()
     us_1m = lambda t: round(t * 1e3 / (pk / (1 << 20)), 3)  # noqa: E731
+    wb = res.written_bytes
     return {
         "skeleton": {"us_per_1M_packets": us_1m(skel_ms), "frac": round(alg * pk / (skel_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                     "real_GBps": round(81.0 * pk / (skel_ms / 1e3) / 1e9, 1), "sclk_mhz": skel_clk,
-                     "bytes_per_pkt": "52 + 4 read (68 B of HBM lines), 13 written (the kernel's own traffic: three "
-                                      "4-B results and the 1-B compact list entry)"},
+                     "real_GBps": round((68.0 + wb) * pk / (skel_ms / 1e3) / 1e9, 1), "sclk_mhz": skel_clk,
+                     "bytes_per_pkt": f"52 + 4 read (68 B of HBM lines), {wb:g} written (the kernel's own traffic: "
+                                      + ("one 8-B packed result" if packed else "three 4-B results")
+                                      + " and the 1-B compact list entry)"},
         "read_only": {"us_per_1M_packets": us_1m(ro_ms), "real_GBps": round(68.0 * pk / (ro_ms / 1e3) / 1e9, 1),
                       "frac_at_68B": round(68.0 * pk / (ro_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "sclk_mhz": ro_clk},
         "copy": {"GBps": round(2.0 * nbytes / (copy_ms / 1e3) / 1e9, 1), "bytes": nbytes, "sclk_mhz": copy_clk},
@@ -633,7 +662,7 @@ def measure_config(name, args, dev, world, rank, dist, primary):
     eng.tuning(batches_per_launch=args.batches_per_launch)
     acl = eng.commit(rules, default_action=1)
     cfg = eng.cfg(now_seconds=NOW)
-    res = Resident(name, n, stride, nbufs, rules, rank, dev)
+    res = Resident(name, n, stride, nbufs, rules, rank, dev, layout=args.layout)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
     sptr = C.c_void_p(stream.cuda_stream)
@@ -652,7 +681,11 @@ def measure_config(name, args, dev, world, rank, dist, primary):
 
     warm, timed = res.arrays(max(args.warmup, 1)), res.arrays(args.steps)
     warm_up(lambda: run(warm))
-    # timed region (value): K batches, barrier + synchronize on both sides
+    # timed region (value): K batches, barrier + synchronize on both sides.  The roofline's kernel time comes from the
+    # SAME region: the launches carry their own dispatch start / end timestamps (hipExtLaunchKernelGGL events on the
+    # launch stream), so the kernel time per step can never exceed ms_per_step
+    eng.timing(True)
+    eng.timing_read(reset=True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     ev0.record(stream)
@@ -660,12 +693,6 @@ def measure_config(name, args, dev, world, rank, dist, primary):
     ev1.record(stream)
     barrier()
     my_ms = max(ev0.elapsed_time(ev1), 1e-9)
-    # roofline region: the same call with the kernel's own dispatch timestamps (hipExtLaunchKernelGGL events)
-    eng.timing(True)
-    eng.timing_read(reset=True)
-    barrier()
-    run(timed)
-    barrier()
     kern_ms, launches = eng.timing_read(reset=True)
     eng.timing(False)
     if dist is not None:
@@ -677,6 +704,7 @@ def measure_config(name, args, dev, world, rank, dist, primary):
     rd, wr = algorithmic_bytes(64)
     if res.read_bytes_per_pkt is not None:  # IMIX: min(len, 64) + 4 read per packet
         rd = res.read_bytes_per_pkt
+    wr = res.result_bytes  # (12 B as three words, 8 B packed)
     alg = rd + wr
     pk_launch = n * args.steps / max(launches, 1)
     kern_avg_ms = kern_ms / max(launches, 1)
@@ -693,7 +721,9 @@ def measure_config(name, args, dev, world, rank, dist, primary):
                      "traffic": round(tpp * pk_launch) if tpp else None,
                      "kernel": "ppe_classify_kernel", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                      "launches_timed": launches, "packets_per_launch": int(pk_launch),
-                     "bytes_per_pkt": round(alg, 3), "written_bytes_per_pkt": 13.0,
+                     "bytes_per_pkt": round(alg, 3), "read_bytes_per_pkt": round(rd, 3),
+                     "written_bytes_per_pkt": res.written_bytes, "result_layout": args.layout,
+                     "read_frac": round(rd * pk_launch / (kern_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "us_per_1M_packets": round(kern_avg_ms * 1e3 / (pk_launch / (1 << 20)), 3)},
         "parity_sample_ok": parity, "parity_sample_packets": psample,
         "acl": {**{k: acl[k] for k in ("n_rules", "n_nodes", "max_depth", "blob_bytes", "lds_resident")},
@@ -721,12 +751,14 @@ def run_stateless(args, dev, world, rank, dist):
     eng, res, rules, cfg, n, my_ms = (ctx[k] for k in ("eng", "res", "rules", "cfg", "n", "my_ms"))
 
     # N > 1: the consumer-side verdict gather, timed apart from `value` (the classify path itself
-    # exchanges nothing): all_gather over RCCL of one batch's verdict + flow hash + ACL hit (12 B per packet)
+    # exchanges nothing): all_gather over RCCL of one batch's verdict + flow hash + ACL hit (8 B per packet packed,
+    # 12 B as three words)
     gather = None
     if dist is not None:
         try:
             out0 = res.bufs[0][2]
-            src = torch.stack([out0["verdict"], out0["flow_hash"], out0["acl_hit"]])
+            src = (out0["packed"].view(1, -1) if res.layout == "packed"
+                   else torch.stack([out0["verdict"], out0["flow_hash"], out0["acl_hit"]]))
             # the concatenated output form (rank r's 3 rows at [3r, 3r + 3)): RCCL and gloo both take it
             dst = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=dev)
             ts = []
@@ -740,7 +772,7 @@ def run_stateless(args, dev, world, rank, dist):
             gt = torch.tensor([float(np.median(ts[1:])) * 1e3], dtype=torch.float64, device=dev)
             dist.all_reduce(gt, op=dist.ReduceOp.MAX)
             g_ms = float(gt.item())
-            gather = {"ms_per_batch": round(g_ms, 4), "bytes_per_rank": 12 * n,
+            gather = {"ms_per_batch": round(g_ms, 4), "bytes_per_rank": int(res.result_bytes) * n,
                       "collective": "all_gather (gloo, shared-GPU rehearsal)" if args.shared_gpu else "all_gather (RCCL)",
                       "value_with_gather": round(n * world / ((my_ms / args.steps + g_ms) / 1e3) / 1e6, 2)}
             # the per-reason counters summed over ranks (dp_show_pkt_stat's sum over cores, dp_cmd.c:844; SURVEY.md
@@ -789,10 +821,14 @@ def run_stateless(args, dev, world, rank, dist):
         m = len(pk["len"])
         ph = torch.from_numpy(pk["hdr"]).pin_memory()
         pl = torch.from_numpy(pk["len"].view(np.int32)).pin_memory()
-        hres = {k: torch.empty(m, dtype=torch.int32).pin_memory() for k in ("verdict", "flow_hash", "acl_hit")}
         b = abi.Batch(ph.data_ptr(), pl.data_ptr(), None, m, args.stride)
-        r = abi.Result(hres["verdict"].data_ptr(), hres["flow_hash"].data_ptr(), hres["acl_hit"].data_ptr(),
-                       None, None, None, None)
+        if res.layout == "packed":
+            hres = {"packed": torch.empty(m, dtype=torch.int64).pin_memory()}
+            r = abi.Result(None, None, None, None, None, None, None, None, hres["packed"].data_ptr())
+        else:
+            hres = {k: torch.empty(m, dtype=torch.int32).pin_memory() for k in ("verdict", "flow_hash", "acl_hit")}
+            r = abi.Result(hres["verdict"].data_ptr(), hres["flow_hash"].data_ptr(), hres["acl_hit"].data_ptr(),
+                           None, None, None, None)
         eng.lib.ppe_classify_host(eng.ctx, C.byref(b), C.byref(r), C.byref(cfg), 1 << 18)
         reps = 5
         th = time.perf_counter()
@@ -846,6 +882,9 @@ def run_stateless(args, dev, world, rank, dist):
                        "global_batch": line_cfg["packets_per_gpu"] * world, "rules": line_cfg["rules"],
                        "window_bytes": args.stride, "resident_batches": line_cfg["resident_batches"],
                        "batches_per_launch": args.batches_per_launch or args.steps,
+                       "result_layout": ("packed: 8-B flow hash | status | action | flags | ACL hit + 1, + 1-B "
+                                         "compact partition list" if args.layout == "packed" else
+                                         "soa: 4-B verdict, flow hash, ACL hit + 1-B compact partition list"),
                        "parallelism": f"batch-sharded x{world}"},
             "roofline": rf,
             "cpu_baseline": cpu,

@@ -36,8 +36,10 @@ extern "C" {
 
 /* 2: ppe_tuning_t grew to 20 B (batches_per_launch) and mbuf_t (ppe_decode.h) took the reference's field layout;
  * 3: ppe_tuple's word 3 carries the TCP window-scale option offset (bits 9-15); 4: ppe_result_t.part8;
- * 5: the tuple carries a fragment's Defrag fields and the option-past-the-window bit; strides 64..256 */
-#define PPE_ABI_VERSION 7
+ * 5: the tuple carries a fragment's Defrag fields and the option-past-the-window bit; strides 64..256;
+ * 6: ppe_acl_stats_t cut fields; 7: ppe_rules_stage / _publish; 8: ppe_result_t.packed (8-B verdict + flow hash +
+ * ACL hit) */
+#define PPE_ABI_VERSION 8
 
 /* error codes (negative return values) */
 #define PPE_OK       0
@@ -100,6 +102,19 @@ enum ppe_action { PPE_ACT_FW = 0, PPE_ACT_DROP = 1, PPE_ACT_PUNT = 2 };
 #define PPE_VERDICT_ACTION(v) (((v) >> 8) & 0xffu)
 #define PPE_VERDICT_FLAGS(v)  ((v) >> 16)
 
+/* ---- packed result (ppe_result_t.packed): one 8-B word per packet holding verdict, flow hash and ACL hit ----
+ * bits 0-31 flow hash | 32-36 status | 37-38 action | 39-44 flags (PPE_F_VLAN .. PPE_F_FRAG, the stateless path's
+ * six) | 45-63 acl_hit + 1 (0 = -1).  Exactly the information of the three 4-B words in 8 B (13 → 9 B written per
+ * packet with part8).  ppe_classify / ppe_classify_batches only, classifiers of at most PPE_PACKED_MAX_RULES rule
+ * slots (the `n` of the commit). */
+#define PPE_PACKED_MAX_RULES  ((1u << 19) - 1u)
+#define PPE_PACKED_HASH(x)    ((uint32_t)(x))
+#define PPE_PACKED_STATUS(x)  ((uint32_t)((x) >> 32) & 31u)
+#define PPE_PACKED_ACTION(x)  ((uint32_t)((x) >> 37) & 3u)
+#define PPE_PACKED_FLAGS(x)   ((uint32_t)((x) >> 39) & 63u)
+#define PPE_PACKED_HIT(x)     ((int32_t)((uint32_t)((x) >> 45)) - 1)
+#define PPE_PACKED_VERDICT(x) (PPE_PACKED_STATUS(x) | PPE_PACKED_ACTION(x) << 8 | PPE_PACKED_FLAGS(x) << 16)
+
 /* ---- per-reason counters (sums over every batch since the last clear) ---- */
 enum ppe_counter {
     PPE_C_L2_HEADERLEN_ERR = 0, PPE_C_L2_UNSUPPORT, PPE_C_L2_RX_OK,
@@ -154,6 +169,8 @@ typedef struct {
                                   and tile_cnt NULL): slot [64t + i] of tile t holds the i-th entry of the
                                   partition order above as (packet index - 64t) | action << 6 (PPE_PART8_*);
                                   1 B written per packet instead of 4 (ABI version 4)                         */
+    uint64_t *packed;          /* optional n × 8 B (PPE_PACKED_*), with verdict, flow_hash and acl_hit NULL
+                                  (ABI version 8)                                                             */
 } ppe_result_t;
 
 typedef struct {

@@ -9,6 +9,7 @@
  *   read-only   the same reads, one 4-B word written per 64-packet tile: separates the write mix from the row fetch
  *   skel-12+1   (mode 2) the skeleton with a 1-B partition entry (tile offset | action << 6) instead of the 4-B one
  *   skel-12     (mode 3) the skeleton's three 4-B results only (no partition entry)
+ *   skel-8+1    (mode 4) the packed result layout's writes: one 8-B result (o0 holds n x 8 B) and the 1-B entry
  *   copy        a 16-B-per-lane copy, 4 loads in flight per lane (the guide's float4 copy, MI355X_MICROARCH.md:
  *               6.29 TB/s)
  *
@@ -64,7 +65,16 @@ __global__ __launch_bounds__(512) void calib_kernel(ppe_calib_args a) {
             const uint32_t q3 = *(const uint32_t *)(r + 3);
             const uint32_t l = B.len[p];
             const uint32_t x = q0.x ^ q0.y ^ q0.z ^ q0.w ^ q1.x ^ q1.y ^ q1.z ^ q1.w ^ q2.x ^ q2.y ^ q2.z ^ q2.w ^ q3;
-            if (MODE == 0 || MODE == 2 || MODE == 3) {
+            if (MODE == 4) {
+                if ((t << 6) + lane < B.n) {
+                    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+                    v2u r2;
+                    r2.x = x;
+                    r2.y = x ^ l;
+                    __builtin_nontemporal_store(r2, (v2u *)B.o0 + p);
+                    __builtin_nontemporal_store((uint8_t)((p & 63u) | ((x & 3u) << 6)), (uint8_t *)B.o3 + p);
+                }
+            } else if (MODE == 0 || MODE == 2 || MODE == 3) {
                 if ((t << 6) + lane < B.n) {
                     __builtin_nontemporal_store(x, B.o0 + p);
                     __builtin_nontemporal_store(x ^ l, B.o1 + p);
@@ -132,18 +142,22 @@ static uint32_t default_grid(uint32_t grid) {
 
 extern "C" {
 
-// mode 0 skeleton, 1 read-only, 2 skeleton with a 1-B partition entry, 3 skeleton without it.  grid = workgroups of 512 threads (persistent).  Returns a hipError_t.
+// mode 0 skeleton, 1 read-only, 2 skeleton with a 1-B partition entry, 3 skeleton without it, 4 the packed layout's
+// 8 + 1 B.  grid = workgroups of 512 threads (persistent).  Returns a hipError_t.
 int ppe_calib_stream(const ppe_calib_args *a, uint32_t grid, void *stream, void *ev0, void *ev1) {
     if (!a || a->nb == 0 || a->nb > PPE_CALIB_MAXB) return (int)hipErrorInvalidValue;
     for (uint32_t i = 0; i < a->nb; ++i)
-        if (!a->b[i].hdr || !a->b[i].len || !a->b[i].o0 || a->b[i].n == 0 || (a->mode != 1 && (!a->b[i].o1 ||
-            !a->b[i].o2 || !a->b[i].o3)))
+        if (!a->b[i].hdr || !a->b[i].len || !a->b[i].o0 || a->b[i].n == 0 || (a->mode != 1 && !a->b[i].o3) ||
+            ((a->mode == 0 || a->mode == 2 || a->mode == 3) && (!a->b[i].o1 || !a->b[i].o2)))
             return (int)hipErrorInvalidValue;
     if (a->mode == 0)
         hipExtLaunchKernelGGL(calib_kernel<0>, dim3(grid), dim3(512), 0, (hipStream_t)stream, (hipEvent_t)ev0,
                               (hipEvent_t)ev1, 0, *a);
     else if (a->mode == 2)
         hipExtLaunchKernelGGL(calib_kernel<2>, dim3(grid), dim3(512), 0, (hipStream_t)stream, (hipEvent_t)ev0,
+                              (hipEvent_t)ev1, 0, *a);
+    else if (a->mode == 4)
+        hipExtLaunchKernelGGL(calib_kernel<4>, dim3(grid), dim3(512), 0, (hipStream_t)stream, (hipEvent_t)ev0,
                               (hipEvent_t)ev1, 0, *a);
     else if (a->mode == 3)
         hipExtLaunchKernelGGL(calib_kernel<3>, dim3(grid), dim3(512), 0, (hipStream_t)stream, (hipEvent_t)ev0,

@@ -120,6 +120,7 @@ struct ppe_ctx {
     hipStream_t aux = nullptr;                 // image uploads
     int running = 0;
     int staged = -1;              // ppe_rules_stage: the slot holding an unpublished image (-1: none)
+    uint32_t rule_slots[2] = {0, 0};  // per image: the rule array length it was built from (acl_hit < this)
     uint64_t stage_token = 0, tokens = 0;
     // counters
     unsigned long long *d_cslots = nullptr;
@@ -506,8 +507,18 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
             d.tile_cnt = (uint32_t *)out[i].part8;  // (the kernel reads the compact list from the tile_cnt field)
             d.flags = PPE_BD_PART8;
         }
-        part = part && d.verdict && d.fhash && d.hit && !d.tuple &&
-               ((d.fw_idx && d.fw_idx == d.drop_idx && !d.tile_cnt) || d.flags == PPE_BD_PART8);
+        if (out[i].packed) {
+            if (d.verdict || d.fhash || d.hit)
+                return fail(c, PPE_EINVAL, "packed replaces verdict / flow_hash / acl_hit (pass them NULL)");
+            if (fl) return fail(c, PPE_EINVAL, "the packed result layout is for ppe_classify / ppe_classify_batches");
+            if (c->rule_slots[r] > PPE_PACKED_MAX_RULES)
+                return fail(c, PPE_EINVAL, "packed results hold rule indices below %u (classifier of %u rule slots)",
+                            PPE_PACKED_MAX_RULES, c->rule_slots[r]);
+            d.verdict = (uint32_t *)out[i].packed;  // (the kernel writes the 8-B words through the verdict field)
+            d.flags |= PPE_BD_PACKED;
+        }
+        part = part && ((d.verdict && d.fhash && d.hit) || (d.flags & PPE_BD_PACKED)) && !d.tuple &&
+               ((d.fw_idx && d.fw_idx == d.drop_idx && !d.tile_cnt) || (d.flags & PPE_BD_PART8));
         tiles = std::max(tiles, (in[i].n + 63u) / 64u);
         tiles_total += (uint64_t)((in[i].n + 63u) / 64u);
     }
@@ -784,6 +795,7 @@ int ppe_rules_stage(ppe_ctx_t *c, const RCP_BLOCK_ACL_RULE_TUPLE *rules, const u
     ppe_acl_free_image(words);
     if (rc != PPE_OK) return rc;
     c->staged = back;
+    c->rule_slots[back] = n;
     c->stage_token = ++c->tokens;
     if (token) *token = c->stage_token;
     if (stats) *stats = c->stats[back];
@@ -908,7 +920,7 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         bool ok = (b.hdr = (const uint8_t *)mapped_host(in->hdr)) && (b.len = (const uint32_t *)mapped_host(in->len));
         if (in->ts) ok = ok && (b.ts = (const uint64_t *)mapped_host(in->ts));
         uint32_t **outs[] = {&r.verdict, &r.flow_hash, (uint32_t **)&r.acl_hit, &r.fw_idx, &r.drop_idx, &r.tile_cnt,
-                             &r.tuple, (uint32_t **)&r.part8};
+                             &r.tuple, (uint32_t **)&r.part8, (uint32_t **)&r.packed};
         for (uint32_t **o : outs)
             if (ok && *o) ok = (*o = (uint32_t *)mapped_host(*o)) != nullptr;
         if (ok) {
@@ -918,6 +930,8 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
             return PPE_OK;
         }
     }
+    if (out->packed && out->tuple)  // (the staged path keeps the packed words in the tuple's staging buffer)
+        return fail(c, PPE_EINVAL, "ppe_classify_host: packed with tuple needs device-mapped host buffers");
     if (chunk == 0) chunk = 1u << 18;
     chunk = (chunk + 63u) & ~63u;
     chunk = std::min(chunk, (in->n + 63u) & ~63u);
@@ -959,6 +973,7 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         r.tile_cnt = out->tile_cnt ? h.tcnt : nullptr;
         r.tuple = out->tuple ? h.tuple : nullptr;
         r.part8 = out->part8 ? (uint8_t *)h.fw : nullptr;  // (part8 excludes fw_idx: the staging list is free)
+        r.packed = out->packed ? (uint64_t *)h.tuple : nullptr;
         rc = launch(c, &b, &r, 1, cfg, h.s, 1 + (int)(i % kHostStreams), base);
         if (rc != PPE_OK) return rc;
         if (out->verdict) HIPCHK(c, hipMemcpyAsync(out->verdict + base, h.verdict, (size_t)m * 4, d2h, h.s));
@@ -972,6 +987,7 @@ int ppe_classify_host(ppe_ctx_t *c, const ppe_batch_t *in, const ppe_result_t *o
         if (out->drop_idx && !part)
             HIPCHK(c, hipMemcpyAsync(out->drop_idx + base, h.drop, (size_t)m * 4, d2h, h.s));
         if (out->part8) HIPCHK(c, hipMemcpyAsync(out->part8 + base, h.fw, (size_t)m, d2h, h.s));
+        if (out->packed) HIPCHK(c, hipMemcpyAsync(out->packed + base, h.tuple, (size_t)m * 8, d2h, h.s));
     }
     for (auto &h : c->hs) HIPCHK(c, hipStreamSynchronize(h.s));
     return PPE_OK;

@@ -19,9 +19,11 @@ struct ppe_bdesc {
     uint32_t n;
     uint32_t stride;
     uint32_t idx_base;        /* added to the packet indices written to fw_idx / drop_idx */
-    uint32_t flags;           /* PPE_BD_PART8: tile_cnt carries the compact partition list (ppe_result_t.part8) */
+    uint32_t flags;           /* PPE_BD_PART8: tile_cnt carries the compact partition list (ppe_result_t.part8);
+                                 PPE_BD_PACKED: verdict carries the 8-B packed results (ppe_result_t.packed) */
 };
 #define PPE_BD_PART8 1u
+#define PPE_BD_PACKED 2u
 
 /* Device flow table (ppe_classify_flow; ppe_kernels.hip "flow table").  Open addressing over groups of
  * PPE_FLOW_GROUP slots, linear probing from group flow_hash & gmask; a key lies before the first EMPTY slot of its

@@ -76,6 +76,7 @@ __device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) {
 // completion makes the compiler wait for vmcnt(0) at the next use of any load)
 template <class T> struct GType { typedef T type; };
 template <> struct GType<uint4> { typedef uint32_t __attribute__((ext_vector_type(4))) type; };
+template <> struct GType<uint2> { typedef uint32_t __attribute__((ext_vector_type(2))) type; };
 template <class T> __device__ __forceinline__ T gld(const void *base, uint32_t off) {
     typedef typename GType<T>::type G;
     return __builtin_bit_cast(T, *(const __attribute__((address_space(1))) G *)((const char *)base + off));
@@ -1345,7 +1346,11 @@ void ppe_classify_kernel(ppe_kargs a) {
         const uint32_t st = k.st;
         const uint32_t act = (uint32_t)(act_table >> (2u * st)) & 3u;
         const uint32_t po = 4u * p;  // byte offset of this packet's SoA output words
-        if (valid) {
+        if (valid && !FLOW && (B.flags & PPE_BD_PACKED)) {
+            // the packed layout (ppe_result_t.packed): hash | status, action, flags, hit + 1 in one 8-B store
+            gst_nt<uint2>(B.verdict, 2u * po,
+                          make_uint2(fh, st | (act << 5) | ((k.flags & 63u) << 7) | ((uint32_t)(hit + 1) << 13)));
+        } else if (valid) {
             if (PART || B.verdict) gst_nt<uint32_t>(B.verdict, po, st | (act << 8) | (k.flags << 16));
             if (PART || B.fhash) gst_nt<uint32_t>(B.fhash, po, fh);
             if (PART || B.hit) gst_nt<int32_t>(B.hit, po, hit);

@@ -55,7 +55,21 @@ class Batch(C.Structure):
 class Result(C.Structure):
     _fields_ = [("verdict", C.c_void_p), ("flow_hash", C.c_void_p), ("acl_hit", C.c_void_p),
                 ("fw_idx", C.c_void_p), ("drop_idx", C.c_void_p), ("tile_cnt", C.c_void_p), ("tuple", C.c_void_p),
-                ("part8", C.c_void_p)]  # compact partition list (ABI version 4)
+                ("part8", C.c_void_p),  # compact partition list (ABI version 4)
+                ("packed", C.c_void_p)]  # 8-B verdict + flow hash + ACL hit (ABI version 8)
+
+
+PACKED_MAX_RULES = (1 << 19) - 1  # include/ppe_hip.h PPE_PACKED_MAX_RULES
+
+
+def unpack(packed: np.ndarray) -> dict:
+    """The packed result words (ppe_result_t.packed, PPE_PACKED_* in include/ppe_hip.h) as the three SoA outputs:
+    verdict (status | action << 8 | flags << 16), flow_hash and acl_hit."""
+    x = np.ascontiguousarray(packed).view(np.uint64)
+    hi = (x >> np.uint64(32)).astype(np.uint32)
+    verdict = (hi & 31) | (((hi >> 5) & 3) << 8) | (((hi >> 7) & 63) << 16)
+    return {"verdict": verdict.astype(np.uint32), "flow_hash": (x & np.uint64(0xFFFFFFFF)).astype(np.uint32),
+            "acl_hit": ((hi >> 13).astype(np.int64) - 1).astype(np.int32)}
 
 
 class Cfg(C.Structure):
@@ -206,7 +220,7 @@ EXPORTED_DATA = ["rule_list", "dp_acl_action_default", "gWstDepth", "gAvgDepth",
 _lib = None
 
 
-ABI_VERSION = 7  # include/ppe_hip.h PPE_ABI_VERSION
+ABI_VERSION = 8  # include/ppe_hip.h PPE_ABI_VERSION
 
 
 def load(path: str | os.PathLike | None = None) -> C.CDLL:

@@ -86,7 +86,7 @@ class Engine:
         """Device-pointer form (ppe_classify): enqueue on `stream` (hipStream_t as int) and return."""
         b = abi.Batch(hdr, lens, ts, int(n), int(stride))
         r = abi.Result(out.get("verdict"), out.get("flow_hash"), out.get("acl_hit"), out.get("fw_idx"),
-                       out.get("drop_idx"), out.get("tile_cnt"), out.get("tuple"), out.get("part8"))
+                       out.get("drop_idx"), out.get("tile_cnt"), out.get("tuple"), out.get("part8"), out.get("packed"))
         rc = self.lib.ppe_classify(self.ctx, C.byref(b), C.byref(r), C.byref(cfg or self.cfg()), stream)
         self._check(rc, "ppe_classify")
 
@@ -152,7 +152,8 @@ class Engine:
         b = abi.Batch(hdr.data_ptr(), lens.data_ptr(), ts.data_ptr() if ts is not None else None, lens.numel(),
                       hdr.shape[1])
         r = abi.Result(ptrs.get("verdict"), ptrs.get("flow_hash"), ptrs.get("acl_hit"), ptrs.get("fw_idx"),
-                       ptrs.get("drop_idx"), ptrs.get("tile_cnt"), ptrs.get("tuple"), ptrs.get("part8"))
+                       ptrs.get("drop_idx"), ptrs.get("tile_cnt"), ptrs.get("tuple"), ptrs.get("part8"),
+                       ptrs.get("packed"))
         self._check(self.lib.ppe_classify_flow(self.ctx, C.byref(b), C.byref(r), C.byref(cfg or self.cfg()),
                                                s.cuda_stream), "ppe_classify_flow")
 

@@ -25,7 +25,7 @@ def header_functions():
 
 def test_library_loads():
     lib = abi.load()
-    assert lib.ppe_abi_version() == abi.ABI_VERSION == 7
+    assert lib.ppe_abi_version() == abi.ABI_VERSION == 8
 
 
 def test_every_declared_function_is_exported():
@@ -59,7 +59,7 @@ def test_no_device_means_loud_failure():
 def test_struct_layouts():
     assert abi.RULE_DTYPE.itemsize == 60  # include/rpc-common.h:97-114, packed
     assert C.sizeof(abi.Batch) == 32
-    assert C.sizeof(abi.Result) == 64  # part8 (ABI version 4)
+    assert C.sizeof(abi.Result) == 72  # part8 (ABI version 4), packed (8)
     assert C.sizeof(abi.Cfg) == 16
     assert C.sizeof(abi.Tuning) == 20  # batches_per_launch (ABI version 2)
     assert C.sizeof(abi.Counters) == 256

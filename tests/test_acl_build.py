@@ -395,3 +395,30 @@ def test_cut_lists_of_the_bench_rule_sets():
         cut = o.classify_batch(pk["hdr"], pk["len"], cfg=o.cfg(0, 1, NOW), nthreads=8, use_tree=3)
         for k in ("verdict", "acl_hit", "counters"):
             assert np.array_equal(lin[k], cut[k]), k
+
+
+@pytest.mark.parametrize("lines", ["0", "1"])
+def test_cut_lists_32bit_rule_ids(monkeypatch, lines):
+    """used rule indices past 65,535 (a sparse `used` array over 400,000 slots, the extended API's range)
+    switch the cut lists to 32-bit ids (6 entries per line with the ids in the lines, or the 32-bit id array); the
+    cut walk over that layout equals the linear definition, with the ids in the lines and in their own array."""
+    monkeypatch.setenv("PPE_CUT_LINES", lines)
+    base = synth.make_rules(4096, seed=73)
+    slots = 400_000
+    rules = np.zeros(slots, RULE_DTYPE)
+    used = np.zeros(slots, np.uint8)
+    pos = np.unique(np.concatenate([np.sort(np.random.default_rng(74).choice(np.arange(1, slots), 4093,
+                                                                               replace=False)),
+                                    [65_536, 131_071, slots - 1]]))
+    rules[pos] = base[:len(pos)]
+    used[pos] = 1
+    pk = synth.make_packets(20000, base[:len(pos)], seed=75, stride=64, hit_frac=0.9)
+    img, st, lin = compare(rules, used, pk, default_action=1)
+    assert int(img[22]) != 0, "cut lists expected"
+    h = cut_header(img)
+    assert not h["ids16"] and h["lines_ids"] == (lines == "1")
+    if h["lines_ids"]:
+        assert h["epl"] == 6
+    _, ids = cut_entries(img, h)
+    assert ids.max() > 65_535 and used[ids].all()
+    assert (lin["acl_hit"] > 65_535).sum() > 1000
