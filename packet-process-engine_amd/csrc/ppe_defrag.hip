@@ -113,7 +113,8 @@ struct DfArgs {
     unsigned long long *look;            // admission: per-workgroup look-back words (epoch << 32 | flags | count)
     uint32_t epoch, nlook;               // this call's tag (never 0) and the look-back array's length
     uint32_t look_spins;                 // admission: polls of an unpublished predecessor before giving up
-    uint32_t look_fail_wg;               // test hook (PPE_DF_LOOK_FAIL): this workgroup's look-back fails at once
+    uint32_t look_fail_wg;               // test hook (PPE_DF_LOOK_FAIL): this workgroup's look-back fails at once, in
+                                         // the handle's first ppe_defrag call
     unsigned long long *err_host;        // pinned, device-mapped: set by a failed look-back (ppe_defrag reports it)
     uint64_t *dropped;                   // age: ids of dropped fragments
     uint32_t max_dropped;
@@ -1229,6 +1230,7 @@ int ppe_defrag(ppe_defrag_t *d, const ppe_frag_batch_t *in, const ppe_defrag_out
     if (++d->epoch == 0) d->epoch = 1;   // (0 is the cleared array's tag)
     a.epoch = d->epoch;
     hipLaunchKernelGGL(df_admit_kernel, dim3(g), dim3(kBlock), 0, s, a);
+    d->base.look_fail_wg = ~0u;   // (the test hook fails one call's look-back, the first)
     hipLaunchKernelGGL(df_group_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_process_kernel, dim3(g), dim3(kBlock), 0, s, a);
     hipLaunchKernelGGL(df_place_kernel, dim3(g), dim3(kBlock), 0, s, a);

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--cal-kernel", default="k_row<true>")
     ap.add_argument("--read-per-pkt", type=float, default=68.0, help="algorithmic read bytes per packet (IMIX: "
                     "min(len, 64) + 4 averaged)")
+    ap.add_argument("--write-per-pkt", type=float, default=8.0, help="algorithmic written bytes per packet (the "
+                    "roofline's: verdict + flow hash + ACL hit, 8 packed / 12 as three words; the 1-B list entry is "
+                    "traffic, not algorithmic)")
     ap.add_argument("--config", default="C1")
     ap.add_argument("--kernel", default="ppe_classify_kernel", help="dispatches whose kernel name matches this regular expression")
     ap.add_argument("--calls", type=int, default=0, help="sum every matching dispatch and divide by this many calls "
@@ -50,10 +53,10 @@ def main():
     cw = statistics.median(per_dispatch(a.cal_write, a.cal_kernel, "WRITE_SIZE"))
     cal_rd, cal_wr = a.cal_n * 68, a.cal_n * 16  # skeleton: 64-B window + 4-B length read, 4 x 4-B results written
     kr, kw = cal_rd / cf, cal_wr / cw  # bytes per counter unit for this access pattern
-    alg_rd, alg_wr = n * a.read_per_pkt, n * 16  # written: 12-B verdict + 4-B partition-list entry
+    alg_rd, alg_wr = n * a.read_per_pkt, n * a.write_per_pkt
     if a.calls and a.alg_bytes:  # a whole call's algorithmic bytes (bench.py run_defrag's bytes_call)
         alg_rd, alg_wr = a.alg_bytes, 0.0
-    out = {"config": a.config, "n_packets": n, "read_per_pkt": a.read_per_pkt, "fetch_size_raw": f, "write_size_raw": w, "calib": {"fetch_raw": cf, "write_raw": cw,
+    out = {"config": a.config, "n_packets": n, "read_per_pkt": a.read_per_pkt, "write_per_pkt": a.write_per_pkt, "fetch_size_raw": f, "write_size_raw": w, "calib": {"fetch_raw": cf, "write_raw": cw,
            "bytes_per_fetch_unit": kr, "bytes_per_write_unit": kw, "kernel": a.cal_kernel},
            "read_bytes": f * kr, "write_bytes": w * kw, "traffic_bytes": f * kr + w * kw,
            "algorithmic_bytes": alg_rd + alg_wr,

@@ -26,7 +26,7 @@ for C in $CONFIGS; do
   RP=$(grep -o "algorithmic_read_per_pkt [0-9.]*" $O/fetch_$C.log | awk '{print $2}')
   python3 tools/collect_traffic.py --config $C --fetch $O/fetch_$C/k_counter_collection.csv --write $O/write_$C/k_counter_collection.csv \
     --cal-fetch $O/cal_fetch/cal_counter_collection.csv --cal-write $O/cal_write/cal_counter_collection.csv \
-    --n $((K * 1048576)) --read-per-pkt $RP --out $O/${T}_traffic_$C.json > $O/traffic_$C.log 2>&1 || exit 1
+    --n $((K * 1048576)) --read-per-pkt $RP --write-per-pkt 8 --out $O/${T}_traffic_$C.json > $O/traffic_$C.log 2>&1 || exit 1
   python3 tools/pmc_summary.py $O/tcc_$C/k_counter_collection.csv --tiles $((K * 16384)) --min-us 50 > $O/tcc_$C.txt 2>&1
   if [ $C = C1 ] || [ $C = C3 ] || [ $C = C4 ]; then
     timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES --kernel-trace --output-format csv -d $O/sq_$C -o k -- python3 $R > $O/sq_$C.log 2>&1 || exit 1

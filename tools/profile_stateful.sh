@@ -21,7 +21,7 @@ timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write_F1 -o k -- python3 $B > $O/write_F1.log 2>&1 || exit 1
 python3 tools/collect_traffic.py --config F1 --fetch $O/fetch_F1/k_counter_collection.csv --write $O/write_F1/k_counter_collection.csv \
   --cal-fetch $O/cal_fetch/cal_counter_collection.csv --cal-write $O/cal_write/cal_counter_collection.csv \
-  --n 1048576 --read-per-pkt 92.1 --out $O/${T}_traffic_F1.json > $O/traffic_F1.log 2>&1 || exit 1
+  --n 1048576 --read-per-pkt 92.1 --write-per-pkt 16 --out $O/${T}_traffic_F1.json > $O/traffic_F1.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_D1 -o k -- python3 bench.py --config D1 --no-cpu-baseline > $O/kt_D1.log 2>&1 || exit 1
 # D1 traffic: 8 ppe_defrag calls alone (tools/defrag_run.py), every ppe_defrag kernel's FETCH / WRITE summed per call
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch_D1 -o k -- python3 tools/defrag_run.py --calls 8 > $O/fetch_D1.log 2>&1 || exit 1

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--nbufs", type=int, default=8)
     ap.add_argument("--lib", default=None)
     ap.add_argument("--tune", default="")
+    ap.add_argument("--layout", default="packed", choices=("packed", "soa"), help="result layout (bench.py --layout)")
     a = ap.parse_args()
     a.nbufs = max(a.nbufs, a.batches)  # every batch of a launch distinct (its batch groups run concurrently)
     c = synth.CONFIGS[a.config]
@@ -43,9 +44,14 @@ def main():
         hdr = torch.from_numpy(pk["hdr"]).to(dev)
         lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
         outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(4)]
-        bufs.append((abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, 64),
-                     abi.Result(outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(), None, None, None, None,
-                                outs[3].data_ptr()), hdr, lens, outs))  # the bench's layout: compact list
+        if a.layout == "packed":  # the bench's default: 8-B packed results + the compact list
+            pk8 = torch.empty(n, dtype=torch.int64, device=dev)
+            outs.append(pk8)
+            res = abi.Result(None, None, None, None, None, None, None, outs[3].data_ptr(), pk8.data_ptr())
+        else:
+            res = abi.Result(outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(), None, None, None, None,
+                             outs[3].data_ptr())
+        bufs.append((abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, 64), res, hdr, lens, outs))
     cfg = Engine.cfg(now_seconds=1_700_000_000)
     sp = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     ins = (abi.Batch * a.batches)(*(bufs[i % a.nbufs][0] for i in range(a.batches)))
