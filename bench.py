@@ -93,7 +93,9 @@ def spawn(args_list: list[str], n: int) -> int:
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
+    # 128 batches of 1M packets per timed region: the region's fixed cost (the launch's submission and its dispatch-
+    # timestamp events, ~20 us) is 0.1 us per batch instead of 0.6 at 32 (profiles/r6_ab_runs.md r6c)
+    ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--config", default="C1", choices=sorted(synth.CONFIGS))
     ap.add_argument("--configs", default=",".join(EXTRA_CONFIGS),
@@ -680,7 +682,9 @@ def measure_config(name, args, dev, world, rank, dist, primary):
         torch.cuda.synchronize()
 
     warm, timed = res.arrays(max(args.warmup, 1)), res.arrays(args.steps)
-    warm_up(lambda: run(warm))
+    run(warm)
+    # (warmed up on the timed region's own descriptor set: a ring launch that reuses it uploads nothing)
+    warm_up(lambda: run(timed))
     # timed region (value): K batches, barrier + synchronize on both sides.  The roofline's kernel time comes from the
     # SAME region: the launches carry their own dispatch start / end timestamps (hipExtLaunchKernelGGL events on the
     # launch stream), so the kernel time per step can never exceed ms_per_step
@@ -914,13 +918,14 @@ def flow_owner_update() -> bool:
 
 
 def flow_bytes(stride: int, owner: bool = False) -> float:
-    """Algorithmic bytes per packet of the flow-mode classify kernel on the hit path: the stateless kernel's 84 B
-    (window + length read; verdict, hash, hit, partition entry written), the flow slot's 16-B key read and the 8-B
+    """Algorithmic bytes per packet of the flow-mode classify kernel on the hit path: the stateless kernel's 81 B
+    (window + length read; verdict, hash, hit and the 1-B compact partition entry written: part8, round 6; 84 with
+    round 5's 4-B partition list), the flow slot's 16-B key read and the 8-B
     tile mask per 64 packets, plus the FlowUpdate: in the kernel, the 16-B direction counters read and written (two
     8-B atomics) and the 8-B last-seen store; owner-computed, the 8-B bucket entry the kernel writes
     instead (the update kernel then touches each flow once per batch, outside this kernel's time)."""
     rd, wr = algorithmic_bytes(stride)
-    return rd + wr + 4.0 + 16.0 + (8.0 if owner else 32.0 + 8.0) + 8.0 / 64.0
+    return rd + wr + 1.0 + 16.0 + (8.0 if owner else 32.0 + 8.0) + 8.0 / 64.0
 
 
 def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
@@ -979,7 +984,7 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
         hdr = torch.from_numpy(pk["hdr"]).to(dev)
         lens = torch.from_numpy(pk["len"].view(np.int32)).to(dev)
         out = torch.empty((3, n), dtype=torch.int32, device=dev)
-        part = torch.empty(n, dtype=torch.int32, device=dev)
+        part = torch.empty(n, dtype=torch.uint8, device=dev)  # the compact partition list (part8), as C1 - C4
         bufs.append((hdr, lens, out, part, pk if b == 0 else None))
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
@@ -987,8 +992,8 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     calls = []
     for hdr, lens, out, part, _ in bufs:
         bb = abi.Batch(hdr.data_ptr(), lens.data_ptr(), None, n, stride)
-        rr = abi.Result(out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), part.data_ptr(), part.data_ptr(),
-                        None, None)
+        rr = abi.Result(out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), None, None, None, None,
+                        part.data_ptr())
         calls.append((bb, rr))
     cfgs = [eng.cfg(now_seconds=NOW + i) for i in range(args.warmup + 2 * args.steps + 1)]
     fn = eng.lib.ppe_classify_flow
@@ -1018,6 +1023,11 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     gpu_busy(dev)
     eng.clear_counters()
     new0 = eng.flow_info()["new_flow"]
+    # the classify (FlowFind) kernel alone: the dispatch timestamps of the timed region's own launches
+    # (hipExtLaunchKernelGGL events), so its time per batch never exceeds ms_per_step; a steered
+    # rank's launches are its own share of every batch
+    eng.timing(True)
+    eng.timing_read(reset=True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     ev0.record(stream)
@@ -1026,19 +1036,10 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     ev1.record(stream)
     barrier()
     my_ms = max(ev0.elapsed_time(ev1), 1e-9)
-    cnt = eng.counters()
-    new_timed = eng.flow_info()["new_flow"] - new0
-    # the classify (FlowFind) kernel alone: HIP-event dispatch timestamps of the same launches
-    eng.timing(True)
-    eng.timing_read(reset=True)
-    for i in range(args.steps):
-        if steer:  # the kernel timing runs this rank's own batches through its table, without the exchange
-            bb, rr = calls[i % nbufs]
-            fn(eng.ctx, C.byref(bb), C.byref(rr), C.byref(cfgs[args.warmup + args.steps + i]), sptr)
-        else:
-            step(args.warmup + args.steps + i)
     kern_ms, launches = eng.timing_read(reset=True)
     eng.timing(False)
+    cnt = eng.counters()
+    new_timed = eng.flow_info()["new_flow"] - new0
     info = eng.flow_info()
     if dist is not None:
         t = torch.tensor([my_ms], dtype=torch.float64, device=dev)

@@ -76,6 +76,7 @@ struct FlowTable {
     unsigned long long *tile_miss = nullptr, *tile_new = nullptr;
     // owner-computed FlowUpdate (flow_update_wg in ppe_flow_post_kernel): bucket columns for upd_wgs classify workgroups
     unsigned long long *upd = nullptr;
+    uint32_t *ucnt = nullptr;
     uint32_t upd_wgs = 0, upd_osh = 0, upd_owners = 0, upd_hmask = PPE_UPD_HASH - 1u;
     uint64_t batches = 0;   // ppe_classify_flow calls (the parity selects the miss-tile counter)
     unsigned long long fold_pkts = PPE_PK_FOLD_PKTS, fold_bytes = PPE_PK_FOLD_BYTES;
@@ -292,7 +293,8 @@ StagePlan stage_plan(const ppe_ctx *c, const std::vector<uint32_t> &img, bool si
         p.stage_src = h[4];
         p.cut_gbase_lds = 4u * (h[8] - h[4]);
         p.cut_fp_lds = 4u * (h[9] - h[4]);
-        if (4u * all_words <= bud && env_int("PPE_CUT_ENT_LDS", 1)) {  // everything in LDS (IMG_LDS)
+        // everything in LDS (IMG_LDS: the dense layout only, the kernel's entry addressing assumes it)
+        if (4u * all_words <= bud && !(h[0] & PPE_CUT_LINES) && env_int("PPE_CUT_ENT_LDS", 1)) {
             p.mode = 1;
             p.stage_words = all_words;
             p.cut_ent_lds = 4u * (h[5] - h[4]);
@@ -1244,6 +1246,7 @@ static ppe_flowdev flow_dev(const FlowTable &t, int which) {
     d.gmask = t.nslots / PPE_FLOW_GROUP - 1u;
     d.capacity = t.capacity;
     d.upd = t.upd;
+    d.ucnt = t.ucnt;
     d.upd_wgs = t.upd_wgs;
     d.upd_osh = t.upd_osh;
     d.upd_owners = t.upd_owners;
@@ -1347,6 +1350,7 @@ int ppe_flow_destroy(ppe_ctx_t *c) {
     (void)hipFree(t->tile_miss);
     (void)hipFree(t->tile_new);
     (void)hipFree(t->upd);
+    (void)hipFree(t->ucnt);
     delete t;
     c->flow = nullptr;
     return PPE_OK;
@@ -1398,7 +1402,8 @@ int ppe_flow_create(ppe_ctx_t *c, uint32_t capacity, uint32_t max_batch) {
         // test hook: a smaller LDS hash, so the update kernel's full-hash path runs on small inputs (power of two)
         const int hl = env_int("PPE_FLOW_UPD_HASH", 0);
         if (hl > 0 && hl < (int)PPE_UPD_HASH && (hl & (hl - 1)) == 0) t->upd_hmask = (uint32_t)hl - 1u;
-        if (hipMalloc(&t->upd, (size_t)t->upd_owners * t->upd_wgs * PPE_UPD_CAP * 8u) != hipSuccess)
+        if (hipMalloc(&t->upd, (size_t)t->upd_owners * t->upd_wgs * PPE_UPD_CAP * 8u) != hipSuccess ||
+            hipMalloc(&t->ucnt, (size_t)t->upd_owners * t->upd_wgs * 4u) != hipSuccess)
             rc = fail(c, PPE_ENOMEM, "flow table: out of device memory (update buckets)");
     }
     if (rc == PPE_OK && (hipHostMalloc(&t->snap_h, 64, hipHostMallocMapped) != hipSuccess ||

@@ -62,10 +62,7 @@ enum { PPE_FCTL_LIVE = 0, PPE_FCTL_NEW_FLOW, PPE_FCTL_DEL_FLOW, PPE_FCTL_BATCH_N
 #ifndef PPE_UPD_OWNERS
 #define PPE_UPD_OWNERS 256u
 #endif
-#ifndef PPE_UPD_CAP
-#define PPE_UPD_CAP 8u         /* entries per (owner, classify workgroup) segment, 0 = empty (32 B of 4-B entries, 64 B
-                                  of 8-B ones); a full segment: the direct atomic */
-#endif
+#define PPE_UPD_CAP 16u        /* entries per (owner, classify workgroup) bucket; a full bucket: the direct atomic */
 #ifndef PPE_UPD_HASH
 #define PPE_UPD_HASH 4096u     /* LDS hash entries of an owner workgroup (slots it accumulates; more: direct atomics) */
 #endif
@@ -92,9 +89,8 @@ struct ppe_flowdev {
     unsigned long long seq;       /* batches completed before this one                                                 */
     uint32_t gmask;               /* slot groups - 1                                                                   */
     uint32_t capacity;            /* flow pool size                                                                     */
-    unsigned long long *upd;      /* [owner][upd_wgs] segments of PPE_UPD_CAP entries, written whole (unused entries 0)
-                                     by the classify launch: 4-B {wire length, dir << 16, slot within the owner << 17}
-                                     (upd_osh <= 15), else 8-B {slot | (wire length | dir << 31) << 32}               */
+    unsigned long long *upd;      /* [owner][upd_wgs][PPE_UPD_CAP]: slot | (wire length | dir << 31) << 32             */
+    uint32_t *ucnt;               /* [upd_wgs][owner]: entries in each bucket (written by the classify launch)         */
     uint32_t upd_wgs;             /* classify workgroups with a bucket column (0: every found packet's atomic inline)  */
     uint32_t upd_osh;             /* owner of slot s = s >> upd_osh                                                      */
     uint32_t upd_owners;          /* owners (nslots >> upd_osh)                                                          */

@@ -666,6 +666,9 @@ template <int MODE, int IMGB>
 __device__ __forceinline__ void acl_cut(const uint32_t *__restrict__ gimg, const AclGeo &g, uint32_t sip, uint32_t dip,
                                         uint32_t ports, bool tcp, int32_t &hit, bool &drop) {
     constexpr bool L = MODE != IMG_GLOBAL;
+    // IMG_LDS images have the dense layout (the stage plan gives an image with ids in its lines the L2-entry plan):
+    // entry e at 16 e, its id at cut_idrel + iw e, no line arithmetic
+    constexpr bool DENSE = MODE == IMG_LDS;
     const uint32_t b0 = g.cut & 0xffu, b1 = (g.cut >> 8) & 0xffu;  // (2..14 each)
     const uint32_t bk = ((sip >> (32u - b0)) << b1) | (dip >> (32u - b1));
     const uint32_t gi = bk >> 5, k = bk & 31u;
@@ -689,6 +692,7 @@ __device__ __forceinline__ void acl_cut(const uint32_t *__restrict__ gimg, const
     // entry e: line e / epl (e / epl = umulhi(e, div)), slot e mod epl; byte offset from the entry section
     const uint32_t epl = g.cut_epl;
     auto ebyte = [&](uint32_t e) {
+        if constexpr (DENSE) return 16u * e;
         const uint32_t ln = __umulhi(e, g.cut_div);
         return 128u * ln + 16u * (e - ln * epl);
     };
@@ -698,6 +702,7 @@ __device__ __forceinline__ void acl_cut(const uint32_t *__restrict__ gimg, const
     const uint32_t iw = i16 ? 2u : 4u;
     // the id's byte offset (after the line's epl entries by slot, or in the id array by entry: dense eb = 16 e)
     auto ibyte = [&](uint32_t b) {
+        if constexpr (DENSE) return g.cut_idrel + iw * (b >> 4);
         return (g.cut & PPE_CUT_LINES) ? (b & ~127u) + 16u * epl + iw * ((b & 127u) >> 4) : g.cut_idrel + iw * (b >> 4);
     };
     // entry lines from L2: each candidate's id word is requested right behind its entry, from the same line (the
@@ -721,16 +726,22 @@ __device__ __forceinline__ void acl_cut(const uint32_t *__restrict__ gimg, const
         }
 #pragma unroll
         for (int c = 0; c < W; ++c) {
-            r[c] = make_uint4(0u, 0u, 0u, 0u);
             iv[c] = 0u;
-            if (a[c]) {
-                r[c] = MODE == IMG_LDS ? lds_u128(IMGB + g.cut_ent_lds + be[c]) : gld<uint4>(gimg, 4u * g.cut_ent + be[c]);
-                if (spec) iv[c] = gld<uint32_t>(gimg, 4u * g.cut_ent + (ibyte(be[c]) & ~3u));
+            if constexpr (MODE == IMG_LDS) {
+                // every lane reads (an idle one entry `first`, or past it: inside the staged section, ignored), so
+                // the reads need no exec-mask branches
+                r[c] = lds_u128(IMGB + g.cut_ent_lds + be[c]);
+            } else {
+                r[c] = make_uint4(0u, 0u, 0u, 0u);
+                if (a[c]) {
+                    r[c] = gld<uint4>(gimg, 4u * g.cut_ent + be[c]);
+                    if (spec) iv[c] = gld<uint32_t>(gimg, 4u * g.cut_ent + (ibyte(be[c]) & ~3u));
+                }
             }
         }
 #pragma unroll
-        for (int c = 0; c < W; ++c) {  // the first match wins
-            const bool m = a[c] && !found && cut_match(r[c], ks, kd, ports, tcp);
+        for (int c = 0; c < W; ++c) {  // the first match wins (bitwise: no branch per candidate)
+            const bool m = a[c] & !found & cut_match(r[c], ks, kd, ports, tcp);
             eb = m ? be[c] : eb;
             idw = m ? iv[c] : idw;
             edrop = m ? (r[c].x & 2u) != 0u : edrop;
@@ -1097,12 +1108,13 @@ __device__ __forceinline__ uint32_t flow_account(const ppe_flowdev &f, uint32_t 
     return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
 }
 
-// The classify workgroup collects its FlowUpdate entries in LDS, per owner one segment of PPE_UPD_CAP entries: 4-B
-// entries {wire length (16 bits), dir, slot within the owner (up to 15 bits)} for tables of up to 2^23 slots, 8-B
-// {slot, wire length | dir << 31} beyond.  At its end it writes every segment whole, the unused entries 0 (an entry is
-// never 0: a found packet's wire length is at least 42), so the owner reads one contiguous run of segments and no
-// count: 32 B per (owner, workgroup) where round 5 read a 64-B bucket plus a count word from a strided count array
-__device__ __forceinline__ bool upd_small(const ppe_flowdev &f) { return f.upd_osh <= 15u; }
+// PPE_UPD_LDS: the classify workgroup collects its bucket entries in LDS as 4-B entries {wire length (16 bits), dir,
+// slot within the owner (up to 15 bits)} and writes each bucket out as one 64-B segment at its end, instead of one
+// scattered 8-B store per found packet (tables of up to 2^23 slots; larger ones keep the 8-B global entries)
+#ifndef PPE_UPD_LDS
+#define PPE_UPD_LDS 1
+#endif
+__device__ __forceinline__ bool upd_small(const ppe_flowdev &f) { return PPE_UPD_LDS && f.upd_osh <= 15u; }
 
 // A found packet (classify launch): its direction flag, and its FlowUpdate as an entry in the bucket of its slot's
 // owner in this workgroup's column (flow_update_wg applies it in the next launch, with the last-seen time).
@@ -1117,12 +1129,11 @@ __device__ __forceinline__ uint32_t flow_found(const ppe_flowdev &f, uint32_t *u
         const uint32_t o = s >> f.upd_osh;
         const uint32_t pos = atomicAdd(&ucur[o], 1u);
         if (pos < PPE_UPD_CAP) {
-            if (upd_small(f)) {
+            if (upd_small(f))
                 ubuf[o * PPE_UPD_CAP + pos] = wire_len | (d << 16) | ((s & ((1u << f.upd_osh) - 1u)) << 17);
-            } else {
-                ubuf[2u * (o * PPE_UPD_CAP + pos)] = s;
-                ubuf[2u * (o * PPE_UPD_CAP + pos) + 1u] = wire_len | (d << 31);
-            }
+            else
+                f.upd[((size_t)o * f.upd_wgs + blockIdx.x) * PPE_UPD_CAP + pos] =
+                    (unsigned long long)s | ((unsigned long long)(wire_len | (d << 31)) << 32);
             return PPE_F_FLOW | (to_server ? 0u : PPE_F_TOCLIENT);
         }
     }
@@ -1259,11 +1270,11 @@ void ppe_classify_kernel(ppe_kargs a) {
     constexpr bool CUT = PF == PF_CUT && !FLOW;
     constexpr bool KEYS = MT == 1 && !CUT;  // node walks: per-wave key slots in LDS
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    using L = Lds<BLOCK, KEYS, FLOW ? 4u * PPE_UPD_OWNERS * (1u + 2u * PPE_UPD_CAP) : 0u>;
+    using L = Lds<BLOCK, KEYS, FLOW ? 4u * PPE_UPD_OWNERS * (1u + (PPE_UPD_LDS ? PPE_UPD_CAP : 0u)) : 0u>;
     uint32_t *bins = smem + L::BINS / 4u;    // [PPE_NBINS] packets per (status, flags) bin of this workgroup
     uint32_t *lcnt = bins + PPE_NBINS;       // [32] per-reason counters of this workgroup
     uint32_t *ucur = smem + L::QUEUE / 4u;   // FLOW: [PPE_UPD_OWNERS] entries in this workgroup's owner buckets
-    uint32_t *ubuf = ucur + PPE_UPD_OWNERS;  // FLOW: [PPE_UPD_OWNERS][PPE_UPD_CAP] the segments (4- or 8-B entries)
+    uint32_t *ubuf = ucur + PPE_UPD_OWNERS;  // FLOW, PPE_UPD_LDS: [PPE_UPD_OWNERS][PPE_UPD_CAP] the buckets
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1674,13 +1685,16 @@ void ppe_classify_kernel(ppe_kargs a) {
             for (uint32_t cb = bin_counters(b, act_table); cb; cb &= cb - 1u) atomicAdd(&lcnt[__builtin_ctz(cb)], c);
         }
     }
-    if (FLOW && blockIdx.x < a.flow.upd_wgs) {  // every owner's segment, whole (unused entries 0), for the update
-        const uint32_t ew = upd_small(a.flow) ? 1u : 2u;  // words per entry
-        uint32_t *ub = (uint32_t *)a.flow.upd;
-        for (uint32_t i = tid; i < a.flow.upd_owners * PPE_UPD_CAP * ew; i += BLOCK) {
-            const uint32_t o = i / (PPE_UPD_CAP * ew), e = (i % (PPE_UPD_CAP * ew)) / ew;
-            ub[((size_t)o * a.flow.upd_wgs + blockIdx.x) * PPE_UPD_CAP * ew + (i % (PPE_UPD_CAP * ew))] =
-                e < ucur[o] ? ubuf[i] : 0u;
+    if (FLOW && blockIdx.x < a.flow.upd_wgs) {  // this workgroup's row of bucket counts, for the update kernel
+        for (uint32_t o = tid; o < a.flow.upd_owners; o += BLOCK)
+            a.flow.ucnt[(size_t)blockIdx.x * a.flow.upd_owners + o] = min(ucur[o], PPE_UPD_CAP);
+        if (upd_small(a.flow)) {  // the LDS buckets: 16 lanes write one bucket's 64 B
+            uint32_t *ub = (uint32_t *)a.flow.upd;
+            for (uint32_t i = tid; i < a.flow.upd_owners * PPE_UPD_CAP; i += BLOCK) {
+                const uint32_t o = i / PPE_UPD_CAP, e = i % PPE_UPD_CAP;
+                if (e < ucur[o])
+                    ub[((size_t)o * a.flow.upd_wgs + blockIdx.x) * PPE_UPD_CAP + e] = ubuf[i];
+            }
         }
     }
     __syncthreads();
@@ -1978,31 +1992,32 @@ __device__ __forceinline__ void flow_update_wg(const ppe_flow_kargs &a, uint32_t
     };
     const uint32_t ncol = min(f.upd_grid, f.upd_wgs);
     for (uint32_t w = tid; w < ncol; w += BLOCK) {
-        // this workgroup's segment of column w: 32 B (4-B entries) or 64 B, one contiguous run over the columns of
-        // the owner; every load issued before any entry is used
+        const uint32_t n = min(f.ucnt[(size_t)w * f.upd_owners + o], PPE_UPD_CAP);
+        // the bucket is one 64-B (4-B entries) or 128-B segment: every entry's load issued before any is used
         const bool sm = upd_small(f);
         const size_t bk = (size_t)o * f.upd_wgs + w;
         const uint4 *e = sm ? (const uint4 *)((const uint32_t *)f.upd + bk * PPE_UPD_CAP)
                             : (const uint4 *)(f.upd + bk * PPE_UPD_CAP);
+        // (the segment's loads do not wait for the count: a 4-B-entry bucket is read whole, 64 B, with it)
         uint4 v[PPE_UPD_CAP / 2];
 #pragma unroll
         for (uint32_t q = 0; q < PPE_UPD_CAP / 2; ++q)
-            v[q] = (!sm || q < PPE_UPD_CAP / 4u) ? e[q] : make_uint4(0u, 0u, 0u, 0u);
-        // the segment's entries: slot, direction, wire length (an unused entry, 0: slot ~0, skipped)
+            v[q] = (sm ? q < PPE_UPD_CAP / 4u : 2u * q < n) ? e[q] : make_uint4(0u, 0u, 0u, 0u);
+        // the bucket's entries: slot, direction, wire length (an entry past n: slot ~0, skipped)
         auto entry = [&](uint32_t i, uint32_t &s, uint32_t &d, uint32_t &len) {
             if (sm) {
                 const uint4 q = v[i >> 2];
                 const uint32_t x = (i & 3u) == 0u ? q.x : (i & 3u) == 1u ? q.y : (i & 3u) == 2u ? q.z : q.w;
-                s = x ? (o << f.upd_osh) | (x >> 17) : ~0u;
+                s = (o << f.upd_osh) | (x >> 17);
                 d = (x >> 16) & 1u;
                 len = x & 0xffffu;
             } else {
-                const uint32_t lo = (i & 1u) ? v[i >> 1].z : v[i >> 1].x;
+                s = (i & 1u) ? v[i >> 1].z : v[i >> 1].x;
                 const uint32_t hi = (i & 1u) ? v[i >> 1].w : v[i >> 1].y;
-                s = hi ? lo : ~0u;
                 d = hi >> 31;
                 len = hi & 0x7fffffffu;
             }
+            if (i >= n) s = ~0u;
         };
         // every entry's claim at its home position issued before any result is used (one LDS round trip for the
         // bucket instead of one per entry: the per-entry probe loop was half the update's time, r5w / r5x); the
@@ -2360,7 +2375,7 @@ extern "C" int ppe_classify_occupancy_flow(uint32_t lds_words, int mode, int blo
 
 // classify LDS of a flow-table launch beyond the stateless kernel's: the owner-update bucket cursors (and buckets)
 extern "C" uint32_t ppe_flow_lds_extra() {
-    return 4u * PPE_UPD_OWNERS * (1u + 2u * PPE_UPD_CAP);
+    return 4u * PPE_UPD_OWNERS + (PPE_UPD_LDS ? 4u * PPE_UPD_OWNERS * PPE_UPD_CAP : 0u);
 }
 // waves per SIMD the flow-table classify kernel is compiled for (its LDS share per workgroup)
 extern "C" uint32_t ppe_flow_waves() { return PPE_FLOW_WAVES; }
