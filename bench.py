@@ -93,9 +93,7 @@ def spawn(args_list: list[str], n: int) -> int:
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 128 batches of 1M packets per timed region: the region's fixed cost (the launch's submission and its dispatch-
-    # timestamp events, ~20 us) is 0.1 us per batch instead of 0.6 at 32 (profiles/r6_ab_runs.md r6c)
-    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--config", default="C1", choices=sorted(synth.CONFIGS))
     ap.add_argument("--configs", default=",".join(EXTRA_CONFIGS),
@@ -685,11 +683,12 @@ def measure_config(name, args, dev, world, rank, dist, primary):
     run(warm)
     # (warmed up on the timed region's own descriptor set: a ring launch that reuses it uploads nothing)
     warm_up(lambda: run(timed))
-    # timed region (value): K batches, barrier + synchronize on both sides.  The roofline's kernel time comes from the
-    # SAME region: the launches carry their own dispatch start / end timestamps (hipExtLaunchKernelGGL events on the
-    # launch stream), so the kernel time per step can never exceed ms_per_step
-    eng.timing(True)
-    eng.timing_read(reset=True)
+    # timed region (value): K batches, barrier + synchronize on both sides.  The roofline's launch duration is this
+    # SAME region's: HIP events on the launch stream around the call, which is one launch of all K
+    # batches by default (bpl launches of B batches with --batches-per-launch B), so its time per launch can never
+    # exceed ms_per_step x batches and includes the launch's submission (≈ 5 us).  Dispatch-timestamp events inside
+    # the region would cost ≈ 11 us more per launch (profiles/r6_ab_runs.md r6c); they are taken in a second call
+    # below, for the kernel alone (the rocprofv3 comparison and the same-run skeleton), never for `value` or `frac`.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     ev0.record(stream)
@@ -697,12 +696,21 @@ def measure_config(name, args, dev, world, rank, dist, primary):
     ev1.record(stream)
     barrier()
     my_ms = max(ev0.elapsed_time(ev1), 1e-9)
-    kern_ms, launches = eng.timing_read(reset=True)
+    bpl = args.batches_per_launch or args.steps
+    launches = -(-args.steps // bpl)
+    kern_ms = my_ms
+    # the kernel alone: the same call again with the dispatch's own start / end timestamps (hipExtLaunchKernelGGL)
+    eng.timing(True)
+    eng.timing_read(reset=True)
+    barrier()
+    run(timed)
+    barrier()
+    disp_ms, disp_launches = eng.timing_read(reset=True)
     eng.timing(False)
     if dist is not None:
-        t = torch.tensor([my_ms, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([my_ms, kern_ms, disp_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        my_ms, kern_ms = float(t[0].item()), float(t[1].item())
+        my_ms, kern_ms, disp_ms = float(t[0].item()), float(t[1].item()), float(t[2].item())
     total_pkts = n * args.steps * world
     mpps = total_pkts / (my_ms / 1e3) / 1e6
     rd, wr = algorithmic_bytes(64)
@@ -712,6 +720,7 @@ def measure_config(name, args, dev, world, rank, dist, primary):
     alg = rd + wr
     pk_launch = n * args.steps / max(launches, 1)
     kern_avg_ms = kern_ms / max(launches, 1)
+    disp_avg_ms = disp_ms / max(disp_launches, 1)
     achieved = alg * pk_launch / (kern_avg_ms / 1e3) / 1e9
     tpp = traffic_per_packet(name)
     parity, psample = parity_sample(eng, res, rules, name) if rank == 0 else (None, 0)
@@ -725,10 +734,17 @@ def measure_config(name, args, dev, world, rank, dist, primary):
                      "traffic": round(tpp * pk_launch) if tpp else None,
                      "kernel": "ppe_classify_kernel", "kernel_avg_us": round(kern_avg_ms * 1e3, 3),
                      "launches_timed": launches, "packets_per_launch": int(pk_launch),
+                     "timing": "the value region's own HIP events (launch stream) around its launch(es): the launch "
+                               "duration with its submission",
                      "bytes_per_pkt": round(alg, 3), "read_bytes_per_pkt": round(rd, 3),
                      "written_bytes_per_pkt": res.written_bytes, "result_layout": args.layout,
                      "read_frac": round(rd * pk_launch / (kern_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                     "us_per_1M_packets": round(kern_avg_ms * 1e3 / (pk_launch / (1 << 20)), 3)},
+                     "us_per_1M_packets": round(kern_avg_ms * 1e3 / (pk_launch / (1 << 20)), 3),
+                     "dispatch": {"kernel_avg_us": round(disp_avg_ms * 1e3, 3), "launches": disp_launches,
+                                  "us_per_1M_packets": round(disp_avg_ms * 1e3 / (pk_launch / (1 << 20)), 3),
+                                  "frac": round(alg * pk_launch / (disp_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                  "timing": "the same call again with the dispatch packet's start / end timestamps "
+                                            "(hipExtLaunchKernelGGL events: what rocprofv3 reports): the kernel alone"}},
         "parity_sample_ok": parity, "parity_sample_packets": psample,
         "acl": {**{k: acl[k] for k in ("n_rules", "n_nodes", "max_depth", "blob_bytes", "lds_resident")},
                 "build_ms": round(acl["build_ms"], 3)},
@@ -736,7 +752,7 @@ def measure_config(name, args, dev, world, rank, dist, primary):
     }
     if primary and rank == 0:
         try:
-            out["roofline"]["ceiling"] = ceiling(res, args, dev, kern_avg_ms, pk_launch, alg)
+            out["roofline"]["ceiling"] = ceiling(res, args, dev, disp_avg_ms, pk_launch, alg)
         except Exception as e:  # the ceiling is context, never worth losing the line over
             out["roofline"]["ceiling"] = {"error": str(e)[:200]}
     if not primary and rank == 0 and world == 1 and not args.no_cpu_baseline:
