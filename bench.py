@@ -1153,7 +1153,10 @@ def run_defrag(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     name = name or args.config
     n = (0 if nested else args.n) or cfgd["n"]
     hdr_stride = 128
-    nvar = max(args.warmup, 1) + args.steps
+    # timed calls: at most 24, each creating ≈ 34k fresh FCBs, so the run stays below the config's fcb_max (2^20):
+    # past it the batches would measure FCB_FULL handling, not reassembly (profiles/r6_ab_runs.md r6d)
+    steps = min(args.steps, 24)
+    nvar = max(args.warmup, 1) + steps
     if nvar > 255:
         raise SystemExit("D1: warmup + steps must be <= 255 (one source-address byte per batch)")
     a_full, o_full, l_full = synth.make_fragment_stream(int(n / 3.1) + 64, seed=synth.SEED + 7 + 101 * rank)
@@ -1231,7 +1234,7 @@ def run_defrag(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     ev0.record(stream)
-    for i in range(args.steps):
+    for i in range(steps):
         step(nw + i, NOW + 10**6)
     ev1.record(stream)
     barrier()
@@ -1245,8 +1248,8 @@ def run_defrag(args, cfgd, dev, world, rank, dist, name=None, nested=False):
         t = torch.tensor([my_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         my_ms = float(t.item())
-    mfps = n * args.steps * world / (my_ms / 1e3) / 1e6
-    call_ms = my_ms / args.steps
+    mfps = n * steps * world / (my_ms / 1e3) / 1e6
+    call_ms = my_ms / steps
     # algorithmic bytes of one ppe_defrag call: every frame read once (parse reads its header
     # bytes, the stash or the assembly its data), the frames left held written to their FCB's store slots,
     # every datagram's bytes read (from the input or the store) and written out (whole frame + classify window), and the
@@ -1273,7 +1276,7 @@ def run_defrag(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     if rank == 0:
         line = {
             "metric": DEFRAG_METRIC, "value": round(mfps, 2), "unit": "Mfps", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(call_ms, 5), "higher_is_better": True,
+            "steps": steps, "warmup": args.warmup, "ms_per_step": round(call_ms, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": f"{name}: {n} IPv4 fragments per GPU per batch (make_fragment_stream mix: "
                                    f"UDP/TCP/ICMP, reordered, duplicated, lost, overlapping, oversize), "

@@ -16,4 +16,6 @@ for C in C1 C2 C3 C4 F1 D1; do
   [ -f $P/tcc_$C.txt ] && cp $P/tcc_$C.txt $D/${T}_${C}_tcc.txt
   [ -f $P/sq_$C.txt ] && cp $P/sq_$C.txt $D/${T}_${C}_sq_counters.txt
 done
+# F1: the timed region's dispatches only (tools/f1_timed_stats.py over the kernel trace)
+[ -f $P/${T}_F1_timed.txt ] && cp $P/${T}_F1_timed.txt $D/${T}_F1_timed_region.txt
 ls $D | grep "^${T}_"
