@@ -395,11 +395,14 @@ def warm_up(fn, seconds=WARM_SECONDS):
 
 
 def gpu_busy(dev, seconds=WARM_SECONDS):
-    """Memory-bound filler work right before a stateful config's timed region (its warmup steps change the table, so
-    they are not repeated): the same clock ramp as warm_up()."""
-    x = torch.empty(64 << 20, dtype=torch.int32, device=dev)
-    warm_up(lambda: x.add_(1), seconds)
-    del x
+    """Filler work right before a stateful config's timed region whose warmup steps are not repeated (D1: every call
+    creates FCBs): the same clock ramp as warm_up(), from a 6-MB working set, so the config's own state stays in the
+    Infinity Cache (round 5 streamed 256 MB here, which evicted F1's 64-MB key array: its first timed batches ran
+    at 142 / 91 / 68 / 50 µs against 39 in steady state, profiles/r6h_F1_timed_region.txt)."""
+    a = torch.randn((1024, 1024), dtype=torch.bfloat16, device=dev)
+    b = torch.randn((1024, 1024), dtype=torch.bfloat16, device=dev)
+    warm_up(lambda: [torch.mm(a, b) for _ in range(8)], seconds)
+    del a, b
 
 
 def cpu_baseline(pk, rules, image, seconds, what):
@@ -1011,7 +1014,8 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
         rr = abi.Result(out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), None, None, None, None,
                         part.data_ptr())
         calls.append((bb, rr))
-    cfgs = [eng.cfg(now_seconds=NOW + i) for i in range(args.warmup + 2 * args.steps + 1)]
+    # (the timed batches' times follow every warm-up step's, NOW + warmup + extra < NOW + 1e6)
+    cfgs = [eng.cfg(now_seconds=NOW + i if i < args.warmup else NOW + 10**6 + i) for i in range(args.warmup + 2 * args.steps + 1)]
     fn = eng.lib.ppe_classify_flow
 
     sops = None
@@ -1036,7 +1040,25 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
 
     for i in range(max(args.warmup, 1)):
         step(i)
-    gpu_busy(dev)
+    # then more steps over the same flows until the GPU has been busy for WARM_SECONDS: the clocks ramped and the
+    # table's keys and records resident in the Infinity Cache, as in the steady state the timed batches measure
+    # (filler work that streams other memory would evict them; round 5 did)
+    nextra = [0]
+
+    def extra():
+        bb, rr = calls[nextra[0] % nbufs]
+        cx = eng.cfg(now_seconds=NOW + args.warmup + nextra[0])
+        nextra[0] += 1
+        if steer:
+            steered_classify_flow(sops, dist, bufs[nextra[0] % nbufs][0], bufs[nextra[0] % nbufs][1], cx, world, rank)
+        elif fn(eng.ctx, C.byref(bb), C.byref(rr), C.byref(cx), sptr):
+            raise RuntimeError("ppe_classify_flow failed (warm-up)")
+    if steer:  # (the steered steps exchange batches: every rank runs the same count)
+        for _ in range(8):
+            extra()
+        torch.cuda.synchronize()
+    else:
+        warm_up(extra)
     eng.clear_counters()
     new0 = eng.flow_info()["new_flow"]
     # the classify (FlowFind) kernel alone: the dispatch timestamps of the timed region's own launches
