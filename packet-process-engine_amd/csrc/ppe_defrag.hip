@@ -122,9 +122,6 @@ struct DfArgs {
 };
 
 __device__ __forceinline__ uint32_t ld_be16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
-__device__ __forceinline__ uint32_t ld_be32(const uint8_t *p) {
-    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
-}
 
 __device__ __forceinline__ uint32_t key_hash(uint32_t sip, uint32_t dip, uint32_t id) {
     // bucket choice only (the reference's jhash_3words bucket, decode-defrag.c:108-112, orders nothing observable)
@@ -154,33 +151,47 @@ __global__ void __launch_bounds__(kBlock) df_parse_kernel(DfArgs a) {
     const uint32_t L = tot & 0xffffu;
     uint32_t valid = 0, l2 = 14, ihl4 = 0, sip = 0, dip = 0, idp = 0, offf = 0, dummy = 0;
     if (L >= 14) {
-        bool mac0 = true, mac1 = true;
-        for (int b = 0; b < 6; ++b) {
-            mac0 = mac0 && p[b] == 0;
-            mac1 = mac1 && p[6 + b] == 0;
-        }
-        uint32_t et = ld_be16(p + 12);
+        // the frame's first 40 bytes (Ethernet, a VLAN tag, the IPv4 header's first 20 bytes) as 10 frame-aligned
+        // dwords: 11 aligned loads, all in flight together (not one byte load per field, which the lane's branches
+        // would spread over several round trips), each clamped to the frame's last dword (no read past the frame)
+        const uintptr_t pa = (uintptr_t)p;
+        const uint32_t sh = (uint32_t)(pa & 3u) * 8u;
+        const uint32_t *ap = (const uint32_t *)(pa & ~(uintptr_t)3);
+        const uint32_t lastw = ((uint32_t)(pa & 3u) + L - 1u) >> 2;   // (L >= 14)
+        uint32_t raw[11], fw[10];
+#pragma unroll
+        for (uint32_t k = 0; k < 11; ++k) raw[k] = ap[k < lastw ? k : lastw];
+#pragma unroll
+        for (uint32_t k = 0; k < 10; ++k) fw[k] = sh ? (raw[k] >> sh) | (raw[k + 1] << (32u - sh)) : raw[k];
+        auto byte = [&](uint32_t b) -> uint32_t { return (fw[b >> 2] >> (8u * (b & 3u))) & 0xffu; };
+        auto be16 = [&](uint32_t b) -> uint32_t { return (byte(b) << 8) | byte(b + 1); };
+        auto be32 = [&](uint32_t b) -> uint32_t { return (be16(b) << 16) | be16(b + 2); };
+        const bool mac0 = fw[0] == 0 && (fw[1] & 0xffffu) == 0;   // bytes 0-5
+        const bool mac1 = (fw[1] >> 16) == 0 && fw[2] == 0;       // bytes 6-11
+        const uint32_t et = be16(12);
         bool ok = !mac0 && !mac1;
-        if (ok && (et == 0x8100u || et == 0x9100u)) {
-            ok = L >= 18 && ld_be16(p + 16) == 0x0800u;   // a second tag or another inner type never reaches IPv4
+        const bool tag = et == 0x8100u || et == 0x9100u;
+        if (ok && tag) {
+            ok = L >= 18 && be16(16) == 0x0800u;   // a second tag or another inner type never reaches IPv4
             l2 = 18;
         } else {
             ok = ok && et == 0x0800u;
         }
         if (ok && L >= l2 + 20) {
-            const uint8_t *ip = p + l2;
+            // the IPv4 header's fields at l2 = 14 or 18, both read at compile-time byte positions, then selected
+            const uint32_t b0 = tag ? byte(18) : byte(14);
             const uint32_t l3 = L - l2;
-            ihl4 = (ip[0] & 0x0fu) * 4u;
-            const uint32_t iplen = ld_be16(ip + 2);
-            const uint32_t offw = ld_be16(ip + 6);
-            const uint32_t proto = ip[9];
+            ihl4 = (b0 & 0x0fu) * 4u;
+            const uint32_t iplen = tag ? be16(20) : be16(16);
+            const uint32_t offw = tag ? be16(24) : be16(20);
+            const uint32_t proto = tag ? byte(27) : byte(23);
             const bool is_frag = (offw & 0x1fffu) != 0 || (offw & 0x2000u) != 0;
-            if ((ip[0] >> 4) == 4u && ihl4 >= 20 && iplen >= ihl4 && l3 >= iplen && is_frag && proto != 89u &&
+            if ((b0 >> 4) == 4u && ihl4 >= 20 && iplen >= ihl4 && l3 >= iplen && is_frag && proto != 89u &&
                 l3 - ihl4 != 0) {
                 valid = 1;
-                sip = ld_be32(ip + 12);
-                dip = ld_be32(ip + 16);
-                idp = ld_be16(ip + 4) | (proto << 16) | (((offw >> 13) & 1u) << 24);
+                sip = tag ? be32(30) : be32(26);
+                dip = tag ? be32(34) : be32(30);
+                idp = (tag ? be16(22) : be16(18)) | (proto << 16) | (((offw >> 13) & 1u) << 24);
                 offf = ((offw & 0x1fffu) << 3) | (((l3 - ihl4) & 0xffffu) << 16);
             }
         }
@@ -199,8 +210,8 @@ __global__ void __launch_bounds__(kBlock) df_parse_kernel(DfArgs a) {
             const uint32_t st = a.tstate[s];
             if (st == kEmpty) break;
             if (st == kLive) {
-                const uint32_t *k = a.tkey + (size_t)s * 4;
-                if (k[0] == sip && k[1] == dip && k[2] == (idp & 0xffffu)) {
+                const uint4 k = *(const uint4 *)(a.tkey + (size_t)s * 4);   // one load, not three dependent ones
+                if (k.x == sip && k.y == dip && k.z == (idp & 0xffffu)) {
                     slot = s;
                     break;
                 }
@@ -727,38 +738,59 @@ __global__ void __launch_bounds__(kBlock) df_process_kernel(DfArgs a) {
 #define DF_AB 0
 #endif
 
+// a raw buffer descriptor over [p, p + bytes) from wave-uniform values (readfirstlane: the compiler cannot prove a
+// wave's frame pointer uniform, and a descriptor in VGPRs would be waterfalled)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t df_rsrc(uint64_t p, uint32_t bytes) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)(((uint64_t)hi << 32) | lo), 0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 // ---- stash: copy held frames into their FCB's store slot (PACKET_HW2SW; run in the assembly launch) ------------------
 __device__ __forceinline__ void df_stash_one(const DfArgs &a, uint32_t i) {
     if (DF_AB & 16) return;
+    // the fragment's slot, frame and id read together (one round trip, not two)
     const uint32_t ins = a.inserted[i];
+    const uint64_t off = a.off[i];
+    const uint32_t tot = a.len[i];
+    const uint64_t fid = a.id ? a.id[i] : (uint64_t)i;
     if (ins == kNone) return;
     const uint32_t r = ins >> 8, k = ins & 0xffu;
-    const uint8_t *src = a.pkt + a.off[i];
+    const uint8_t *src = a.pkt + off;
     uint8_t *dst = a.store + ((size_t)r * a.cache_max + k) * a.sstride;
-    const uint32_t tot = a.len[i];
     const uint32_t lane = __lane_id();
     // the held fragment's id, kept with its store slot (the FCB's id list: later datagram plans and aging read it)
-    if (lane == 0) a.rid[(size_t)r * a.cache_max + k] = a.id ? a.id[i] : (uint64_t)i;
-    if (((uintptr_t)src & 3u) == 0) {
-        // all of a pass's loads are issued before its stores (2 KB per pass: one pass for a frag_buf frame)
-        constexpr uint32_t U = 8;
+    if (lane == 0) a.rid[(size_t)r * a.cache_max + k] = fid;
+    // every load of a pass is issued before its stores (2 KB per pass: one pass for a frag_buf frame), through buffer
+    // descriptors whose range check drops the lanes past the frame: no lane-dependent branch, so the stores do not
+    // each wait for the one before (global stores count in vmcnt on gfx950, and a store under a branch after
+    // predicated loads gets a full wait)
+    const uint64_t sp = (uint64_t)(uintptr_t)src, dp = (uint64_t)(uintptr_t)dst;
+    const __amdgpu_buffer_rsrc_t rsb = df_rsrc(sp, tot), rdb = df_rsrc(dp, tot);
+    if ((sp & 3u) == 0) {
         const uint32_t words = tot / 4;
+        const __amdgpu_buffer_rsrc_t rs = df_rsrc(sp, words * 4u), rd = df_rsrc(dp, words * 4u);
+        const uint8_t t = __builtin_amdgcn_raw_buffer_load_b8(rsb, words * 4u + lane, 0, 0);   // the last 0-3 bytes
+        constexpr uint32_t U = 8;
         for (uint32_t base = 0; base < words; base += 64 * U) {
             uint32_t v[U];
 #pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t w = base + u * 64 + lane;
-                v[u] = w < words ? ((const uint32_t *)src)[w] : 0u;
-            }
+            for (uint32_t u = 0; u < U; ++u)
+                v[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, 4u * (base + u * 64 + lane), 0, 0);
 #pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t w = base + u * 64 + lane;
-                if (w < words) ((uint32_t *)dst)[w] = v[u];
-            }
+            for (uint32_t u = 0; u < U; ++u)
+                __builtin_amdgcn_raw_buffer_store_b32(v[u], rd, 4u * (base + u * 64 + lane), 0, 0);
         }
-        for (uint32_t b = words * 4 + lane; b < tot; b += 64) dst[b] = src[b];
-    } else {
-        for (uint32_t b = lane; b < tot; b += 64) dst[b] = src[b];
+        if (lane < 4) __builtin_amdgcn_raw_buffer_store_b8(t, rdb, words * 4u + lane, 0, 0);
+    } else {   // an unaligned frame: bytes, 16 per lane per pass
+        constexpr uint32_t U = 16;
+        for (uint32_t base = 0; base < tot; base += 64 * U) {
+            uint8_t v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b8(rsb, base + u * 64 + lane, 0, 0);
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) __builtin_amdgcn_raw_buffer_store_b8(v[u], rdb, base + u * 64 + lane, 0, 0);
+        }
     }
 }
 
