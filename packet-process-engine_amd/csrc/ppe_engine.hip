@@ -105,6 +105,17 @@ struct FlowTable {
 
 }  // namespace
 
+// A launch that reads an image slot or a descriptor-ring slot, the last one per stream (streams run their launches in
+// order): a classify launch is tracked by its sequence number, which its last workgroup publishes to pinned memory
+// (ppe_kargs.done_*; no event marker behind the launch: a marker cost the F1 stream 4.5 µs per batch, r6o); other
+// launches (ppe_acl_lookup) by an event recorded behind them.
+struct Reader {
+    hipStream_t s;
+    hipEvent_t ev;  // nullptr: tracked by seq
+    uint64_t seq;
+};
+constexpr uint32_t kDoneSlots = 4096;  // launch-completion slots (sequence numbers modulo this)
+
 struct ppe_ctx {
     int device = 0;
     uint32_t n_cu = 256;
@@ -115,8 +126,7 @@ struct ppe_ctx {
     std::vector<uint32_t> level_end[2];  // per image: number of tree nodes at depth <= d (BFS order)
     ppe_acl_stats_t stats[2];
     hipEvent_t img_done[2] = {nullptr, nullptr};
-    std::vector<std::pair<hipStream_t, hipEvent_t>> img_readers[2];  // per slot: launch streams, event behind
-                                                                       // their last launch with it
+    std::vector<Reader> img_readers[2];  // per slot: launch streams, their last launch with it
     hipStream_t aux = nullptr;                 // image uploads
     int running = 0;
     int staged = -1;              // ppe_rules_stage: the slot holding an unpublished image (-1: none)
@@ -140,7 +150,12 @@ struct ppe_ctx {
     // image slots); a launch on another stream that reuses a slot's content waits only for its upload (ring_up)
     ppe_bdesc *d_ring[2] = {nullptr, nullptr};
     ppe_bdesc *h_ring[2] = {nullptr, nullptr};  // pinned staging of the H2D descriptor copy
-    std::vector<std::pair<hipStream_t, hipEvent_t>> ring_readers[2];
+    std::vector<Reader> ring_readers[2];
+    // launch completions (struct Reader): pinned words the launches' last workgroups write, device running counts
+    volatile unsigned long long *done_h = nullptr;
+    unsigned long long *done_hd = nullptr, *done_cnt = nullptr;
+    uint64_t done_cum[kDoneSlots] = {};  // per slot: the running workgroup count its next launch completes
+    uint64_t launch_seq = 0;
     hipEvent_t ring_up[2] = {nullptr, nullptr};  // behind the slot's last upload, on ring_up_stream
     hipStream_t ring_up_stream[2] = {nullptr, nullptr};
     uint32_t ring_n[2] = {0, 0};       // descriptors the slot holds (its content = h_ring[slot][0, ring_n))
@@ -396,40 +411,105 @@ uint32_t blocks_per_cu(ppe_ctx *c, const StagePlan &p, bool flow = false) {
 // behind it, so a rewrite of the slot waits for exactly the launches that read it (the event outlives the stream if
 // the caller frees it).  Events of other streams whose launches have completed are dropped once the list grows, so a
 // caller that uses a new stream per call does not make the list (and every later rewrite's wait) grow without bound.
-int note_reader(ppe_ctx *c, std::vector<std::pair<hipStream_t, hipEvent_t>> &readers, hipStream_t s) {
+// ---- readers of image / descriptor-ring slots (struct Reader) --------------------------------------------------------
+static bool launch_done(const ppe_ctx *c, uint64_t seq) { return c->done_h[seq % kDoneSlots] >= seq; }
+
+// a tracked launch's completion: the pinned word its last workgroup writes, polled (the core yielded between polls,
+// as for the flow snapshot), bounded; past the bound the device is synchronised and the word read once more
+static int wait_launch(ppe_ctx *c, uint64_t seq) {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+    while (!launch_done(c, seq)) {
+        if (std::chrono::steady_clock::now() > until) {
+            HIPCHK(c, hipDeviceSynchronize());
+            if (!launch_done(c, seq)) return fail(c, PPE_EIO, "launch %llu never reported its completion", (unsigned long long)seq);
+            break;
+        }
+        sched_yield();
+    }
+    return PPE_OK;
+}
+static bool reader_done(const ppe_ctx *c, const Reader &x) {
+    return x.ev ? hipEventQuery(x.ev) == hipSuccess : launch_done(c, x.seq);
+}
+static int wait_reader(ppe_ctx *c, Reader &x) {
+    if (!x.ev) return wait_launch(c, x.seq);   // (an entry with an event: its event is behind any seq it had)
+    HIPCHK(c, hipEventSynchronize(x.ev));
+    return PPE_OK;
+}
+static void drop_readers(std::vector<Reader> &v) {
+    for (auto &x : v)
+        if (x.ev) (void)hipEventDestroy(x.ev);
+    v.clear();
+}
+// stream s's entry (created empty), after pruning other streams' completed ones
+static Reader &reader_of(const ppe_ctx *c, std::vector<Reader> &readers, hipStream_t s) {
     constexpr size_t kPruneAt = 8;
     if (readers.size() >= kPruneAt) {
         size_t k = 0;
         for (size_t i = 0; i < readers.size(); ++i) {
-            auto &x = readers[i];
-            if (x.first != s && hipEventQuery(x.second) == hipSuccess) {
-                (void)hipEventDestroy(x.second);
+            Reader &x = readers[i];
+            if (x.s != s && reader_done(c, x)) {
+                if (x.ev) (void)hipEventDestroy(x.ev);
                 continue;
             }
             readers[k++] = x;
         }
         readers.resize(k);
     }
-    hipEvent_t ev = nullptr;
     for (auto &x : readers)
-        if (x.first == s) ev = x.second;
-    if (!ev) {
-        HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        readers.emplace_back(s, ev);
-    }
-    HIPCHK(c, hipEventRecord(ev, s));
+        if (x.s == s) return x;
+    readers.push_back(Reader{s, nullptr, 0});
+    return readers.back();
+}
+// a tracked classify launch (sequence number seq) read the slot on stream s: it completes after every earlier launch
+// on s, so it replaces their entry
+static void note_launch_reader(ppe_ctx *c, std::vector<Reader> &readers, hipStream_t s, uint64_t seq) {
+    Reader &x = reader_of(c, readers, s);
+    if (x.ev) (void)hipEventDestroy(x.ev);
+    x.ev = nullptr;
+    x.seq = seq;
+}
+// an untracked launch read the slot on stream s: an event behind it
+int note_reader(ppe_ctx *c, std::vector<Reader> &readers, hipStream_t s) {
+    Reader &x = reader_of(c, readers, s);
+    if (!x.ev) HIPCHK(c, hipEventCreateWithFlags(&x.ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(x.ev, s));
     return PPE_OK;
 }
 int note_image_reader(ppe_ctx *c, int r, hipStream_t s) { return note_reader(c, c->img_readers[r], s); }
+
+// the next tracked launch's sequence number and completion slot, in its kernel arguments (the slot's previous launch,
+// kDoneSlots launches ago, has completed: at most one launch per slot in flight)
+static int track_launch(ppe_ctx *c, uint32_t grid, ppe_kargs &a) {
+    const uint64_t seq = c->launch_seq + 1u;
+    const uint32_t q = (uint32_t)(seq % kDoneSlots);
+    if (seq > kDoneSlots) {
+        const int rc = wait_launch(c, seq - kDoneSlots);
+        if (rc != PPE_OK) return rc;
+    }
+    c->launch_seq = seq;
+    c->done_cum[q] += grid;
+    a.done_cnt = c->done_cnt + q;
+    a.done_host = c->done_hd + q;
+    a.done_target = c->done_cum[q];
+    a.done_seq = seq;
+    return PPE_OK;
+}
+// the launch did not start: its slot is completed by hand (its workgroups will never count)
+static void untrack_launch(ppe_ctx *c, uint32_t grid, const ppe_kargs &a) {
+    const uint32_t q = (uint32_t)(a.done_seq % kDoneSlots);
+    c->done_cum[q] -= grid;
+    c->done_h[q] = a.done_seq;
+}
 
 int upload_image(ppe_ctx *c, int slot, uint32_t *words, uint32_t n_words, const ppe_acl_stats_t *st) {
     // The back image may still be read by launches queued before the previous swap.  Wait for exactly those (the
     // events recorded behind them, note_image_reader): unrelated work on any stream is never waited on.
     for (auto &x : c->img_readers[slot]) {
-        HIPCHK(c, hipEventSynchronize(x.second));
-        HIPCHK(c, hipEventDestroy(x.second));
+        const int rc = wait_reader(c, x);
+        if (rc != PPE_OK) return rc;
     }
-    c->img_readers[slot].clear();
+    drop_readers(c->img_readers[slot]);
     if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
     const size_t bytes = (size_t)n_words * 4u;
     if (bytes > c->img_cap[slot]) {
@@ -535,11 +615,11 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
         if (rslot < 0) {
             rslot = c->ring_next;
             c->ring_next ^= 1;
-            for (auto &x : c->ring_readers[rslot]) {  // its last readers (then their events are done with)
-                HIPCHK(c, hipEventSynchronize(x.second));
-                HIPCHK(c, hipEventDestroy(x.second));
+            for (auto &x : c->ring_readers[rslot]) {  // its last readers
+                const int rc = wait_reader(c, x);
+                if (rc != PPE_OK) return rc;
             }
-            c->ring_readers[rslot].clear();
+            drop_readers(c->ring_readers[rslot]);
             std::memcpy(c->h_ring[rslot], rd.data(), bytes);
             c->ring_n[rslot] = nb;
             HIPCHK(c, hipMemcpyAsync(c->d_ring[rslot], c->h_ring[rslot], bytes, hipMemcpyHostToDevice, s));
@@ -636,6 +716,10 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     if (grid_out) *grid_out = grid;
 
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    {
+        const int rc0 = track_launch(c, grid, a);
+        if (rc0 != PPE_OK) return rc0;
+    }
     if (c->timing) {
         if (c->ev_used + 2 > c->ev.size()) {
             for (int i = 0; i < 256; ++i) {
@@ -651,12 +735,14 @@ int launch(ppe_ctx *c, const ppe_batch_t *in, const ppe_result_t *out, uint32_t 
     const int rc =
         ppe_launch_classify(&a, grid, plan.mode, plan.pipe, (int)plan.block, fl != nullptr, (void *)s, (void *)e0,
                             (void *)e1);
-    if (rc != 0) return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
-    if (use_ring) {  // every launch that reads the slot: a later rewrite waits for the last of them on each stream
-        const int rc2 = note_reader(c, c->ring_readers[rslot], s);
-        if (rc2 != PPE_OK) return rc2;
+    if (rc != 0) {
+        untrack_launch(c, grid, a);
+        return fail(c, PPE_EIO, "kernel launch failed: %s", hipGetErrorString((hipError_t)rc));
     }
-    return note_image_reader(c, r, s);
+    // the launch reads its image slot (and ring slot): a later rewrite waits for its completion
+    if (use_ring) note_launch_reader(c, c->ring_readers[rslot], s, a.done_seq);
+    note_launch_reader(c, c->img_readers[r], s, a.done_seq);
+    return PPE_OK;
 }
 
 hipError_t use_device(ppe_ctx *c) {
@@ -713,6 +799,16 @@ int ppe_ctx_create(int device, ppe_ctx_t **out) {
         rc = PPE_ENOMEM;
     for (int i = 0; i < 2 && rc == PPE_OK; ++i)
         if (hipEventCreateWithFlags(&c->img_done[i], hipEventDisableTiming) != hipSuccess) rc = PPE_EIO;
+    // launch completions (struct Reader): pinned, device-mapped words and the device running counts
+    if (rc == PPE_OK) {
+        void *h = nullptr;
+        if (hipHostMalloc(&h, kDoneSlots * 8u, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&c->done_hd, h, 0) != hipSuccess ||
+            hipMalloc(&c->done_cnt, kDoneSlots * 8u) != hipSuccess || hipMemset(c->done_cnt, 0, kDoneSlots * 8u) != hipSuccess)
+            rc = PPE_ENOMEM;
+        c->done_h = (volatile unsigned long long *)h;
+        if (h) std::memset(h, 0, kDoneSlots * 8u);
+    }
     // descriptor ring slots (launches over more than PPE_MAX_BATCH batches): allocated here, not on first use, so
     // no batch call pays an allocation
     for (int i = 0; i < 2 && rc == PPE_OK; ++i)
@@ -746,13 +842,14 @@ int ppe_ctx_destroy(ppe_ctx_t *c) {
         if (c->d_ring[i]) (void)hipFree(c->d_ring[i]);
         if (c->h_ring[i]) (void)hipHostFree(c->h_ring[i]);
         if (c->ring_up[i]) (void)hipEventDestroy(c->ring_up[i]);
-        for (auto &x : c->ring_readers[i]) (void)hipEventDestroy(x.second);
+        drop_readers(c->ring_readers[i]);
     }
     for (hipStream_t s : c->pipe)
         if (s) (void)hipStreamDestroy(s);
     if (c->aux) (void)hipStreamDestroy(c->aux);
-    for (auto &v : c->img_readers)
-        for (auto &x : v) (void)hipEventDestroy(x.second);
+    for (auto &v : c->img_readers) drop_readers(v);
+    if (c->done_h) (void)hipHostFree((void *)c->done_h);
+    if (c->done_cnt) (void)hipFree(c->done_cnt);
     for (hipEvent_t e : c->pipe_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->flow) ppe_flow_destroy(c);

@@ -167,6 +167,11 @@ struct ppe_kargs {
     uint32_t off_leaf, off_rules, off_resid; /* image section offsets (words), from the image header: kernel arguments
                                                 (scalar registers, no load in the loop)                               */
     unsigned long long *cslots; /* [grid][PPE_CSLOT_WORDS] counter slots, one per workgroup */
+    /* the launch's completion, for the host's image / descriptor-ring reader bookkeeping (no event marker behind each
+       launch): every workgroup, at its end, adds 1 to *done_cnt (a per-slot running count); the one that brings it to
+       done_target writes done_seq to *done_host (pinned host memory).  done_cnt NULL: not tracked */
+    unsigned long long *done_cnt, *done_host;
+    unsigned long long done_target, done_seq;
     struct ppe_flowdev flow;    /* flow-table launches (ppe_classify_flow, one batch) */
 };
 

@@ -1702,6 +1702,15 @@ void ppe_classify_kernel(ppe_kargs a) {
     if (tid < PPE_C__COUNT && lcnt[tid])
         __hip_atomic_fetch_add(&a.cslots[(size_t)blockIdx.x * PPE_CSLOT_WORDS + tid], (unsigned long long)lcnt[tid],
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the launch's completion for the host's reader bookkeeping: every wave of this workgroup is past its last image
+    // and descriptor read (the barrier above); the workgroup that completes the count publishes the sequence number
+    // (a plain system-scope store: the host needs the completion, not any data, so no release fence)
+    if (a.done_cnt && tid == 0) {
+        const unsigned long long prev = __hip_atomic_fetch_add(a.done_cnt, 1ull, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+        if (prev + 1ull == a.done_target)
+            __hip_atomic_store(a.done_host, a.done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------------------
