@@ -2293,6 +2293,46 @@ __global__ __launch_bounds__(PPE_BLOCK) void ppe_acl_tuple_kernel(ppe_tuple_karg
 
 }  // namespace
 
+#ifdef PPE_TU_HOIST
+// csrc/ppe_kernels_hoist.hip: this file again, built with LLVM's iterative-ILP machine scheduler, exporting only the
+// stateless hoisted-fetch kernels over an LDS-resident image (C1's variant: kernel −2 %, r6s; the cut-list and split
+// variants are slower under it and stay in the default build, profiles/r6_ab_runs.md r6j / r6s)
+template <int B>
+static int launch_hoist_b(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t s, hipEvent_t e0,
+                          hipEvent_t e1) {
+    if (a->part_layout)
+        hipExtLaunchKernelGGL((ppe_classify_kernel<IMG_LDS, PF_HOIST, B, false, true>), dim3(grid), dim3(B), shmem, s,
+                              e0, e1, 0, *a);
+    else
+        hipExtLaunchKernelGGL((ppe_classify_kernel<IMG_LDS, PF_HOIST, B, false>), dim3(grid), dim3(B), shmem, s, e0,
+                              e1, 0, *a);
+    return (int)hipGetLastError();
+}
+extern "C" int ppe_launch_classify_hoist_lds(const ppe_kargs *a, uint32_t grid, size_t shmem, int block, void *stream,
+                                             void *ev_start, void *ev_stop) {
+    const hipStream_t s = (hipStream_t)stream;
+    const hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
+    if (block == 1024) return launch_hoist_b<1024>(a, grid, shmem, s, e0, e1);
+    if (block == 512) return launch_hoist_b<512>(a, grid, shmem, s, e0, e1);
+    return launch_hoist_b<256>(a, grid, shmem, s, e0, e1);
+}
+template <int B>
+static int occ_hoist_b(size_t shmem) {
+    int nb = 0;
+    const hipError_t e =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<IMG_LDS, PF_HOIST, B, false>, B, shmem);
+    return e == hipSuccess ? nb : -1;
+}
+extern "C" int ppe_occupancy_hoist_lds(size_t shmem, int block) {
+    if (block == 1024) return occ_hoist_b<1024>(shmem);
+    if (block == 512) return occ_hoist_b<512>(shmem);
+    return occ_hoist_b<256>(shmem);
+}
+#else
+extern "C" int ppe_launch_classify_hoist_lds(const ppe_kargs *a, uint32_t grid, size_t shmem, int block, void *stream,
+                                             void *ev_start, void *ev_stop);
+extern "C" int ppe_occupancy_hoist_lds(size_t shmem, int block);
+
 template <int M, int P, int B>
 static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
                     int flow) {
@@ -2301,6 +2341,8 @@ static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t
     if (flow) {  // the flow-table variant is built for the default tile fetch only
         hipExtLaunchKernelGGL((ppe_classify_kernel<M, PF_HOIST, B, true>), dim3(grid), dim3(B), shmem, s, e0, e1, 0,
                               *a);
+    } else if constexpr (M == IMG_LDS && P == PF_HOIST) {  // (the iterative-ILP build, ppe_kernels_hoist.hip)
+        return ppe_launch_classify_hoist_lds(a, grid, shmem, B, (void *)s, (void *)e0, (void *)e1);
     } else {
         if (a->part_layout && P != PF_NONE)
             hipExtLaunchKernelGGL((ppe_classify_kernel<M, (P == PF_NONE ? PF_HOIST : P), B, false, true>), dim3(grid),
@@ -2313,6 +2355,8 @@ static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t
 
 template <int M, int P, int B>
 static int occ_t(size_t shmem, bool flow = false) {
+    if constexpr (M == IMG_LDS && P == PF_HOIST)
+        if (!flow) return ppe_occupancy_hoist_lds(shmem, B);
     int nb = 0;
     const hipError_t e =
         flow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, PF_HOIST, B, true>, B, shmem)
@@ -2419,3 +2463,4 @@ extern "C" int ppe_launch_acl_tuples(const ppe_tuple_kargs *a, uint32_t grid, in
     }
     return (int)hipGetLastError();
 }
+#endif  // PPE_TU_HOIST

@@ -1,4 +1,5 @@
 # round 6 diagnostic: what the per-launch image / ring reader event (hipEventRecord after every classify launch)
+# (the PPE_AB_* environment hooks this diagnostic used were removed once r6r replaced the per-launch event)
 # costs: F1 and C1 bench lines with PPE_AB_NO_READER_EVENT=1 (records skipped: unsafe for rule swaps, none here)
 # against the product, alternating processes
 set -o pipefail

@@ -1,4 +1,5 @@
 # round 6 diagnostic: the per-launch reader event's cost by its creation flags (PPE_AB_READER_EV_FLAGS):
+# (the PPE_AB_* environment hooks this diagnostic used were removed once r6r replaced the per-launch event)
 # 2 = DisableTiming (product), 536870914 = + DisableSystemFence, 1073741826 = + ReleaseToDevice, and no record at all
 # (PPE_AB_NO_READER_EVENT=1); F1 bench lines, alternating processes, then an F1 kernel trace per setting
 set -o pipefail

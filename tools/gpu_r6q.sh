@@ -1,4 +1,5 @@
 # round 6 diagnostic: the image-reader event bound to the classify dispatch as its stop event (PPE_AB_READER_BIND=1,
+# (the PPE_AB_* environment hooks this diagnostic used were removed once r6r replaced the per-launch event)
 # no marker packet of its own), created with DisableTiming (2) or default flags (0), against the product's
 # hipEventRecord after the launch and against no record at all; F1 lines alternating, then a kernel trace each
 set -o pipefail
