@@ -1061,11 +1061,8 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
         warm_up(extra)
     eng.clear_counters()
     new0 = eng.flow_info()["new_flow"]
-    # the classify (FlowFind) kernel alone: the dispatch timestamps of the timed region's own launches
-    # (hipExtLaunchKernelGGL events), so its time per batch never exceeds ms_per_step; a steered
-    # rank's launches are its own share of every batch
-    eng.timing(True)
-    eng.timing_read(reset=True)
+    # value: the K timed batches with no dispatch events (a start / end event pair on every classify launch cost the
+    # stream ≈ 6 us per batch, profiles/r6_ab_runs.md r6u)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     ev0.record(stream)
@@ -1074,11 +1071,20 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
     ev1.record(stream)
     barrier()
     my_ms = max(ev0.elapsed_time(ev1), 1e-9)
-    kern_ms, launches = eng.timing_read(reset=True)
-    eng.timing(False)
     cnt = eng.counters()
     new_timed = eng.flow_info()["new_flow"] - new0
     info = eng.flow_info()
+    # the classify (FlowFind) kernel alone: the dispatch timestamps (hipExtLaunchKernelGGL events) of K more batches
+    # over the same flows (their packet times follow the timed ones'); a steered rank's launches are its own share of
+    # every batch
+    eng.timing(True)
+    eng.timing_read(reset=True)
+    barrier()
+    for i in range(args.steps):
+        step(args.warmup + args.steps + i)
+    barrier()
+    kern_ms, launches = eng.timing_read(reset=True)
+    eng.timing(False)
     if dist is not None:
         t = torch.tensor([my_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1114,6 +1120,9 @@ def run_flow(args, cfgd, dev, world, rank, dist, name=None, nested=False):
                                    + ("to the owners' buckets, applied beside finalize by ppe_flow_post_kernel" if owner else
                                       "by one atomic per packet") + "; misses resolved by the flow kernels)",
                          "kernel_avg_us": round(kern_avg_ms * 1e3, 3), "bytes_per_pkt": bpp,
+                         "timing": "batch_avg_us and value: the timed region's HIP events around its K batches (no "
+                                   "dispatch events inside); kernel_avg_us: the dispatch timestamps of the classify "
+                                   "launches of K more batches over the same flows, run right after it",
                          "batch_avg_us": round(my_ms / args.steps * 1e3, 3),
                          "batch_bytes_per_pkt": flow_bytes(stride),
                          "batch_frac": round(batch_achieved / HBM_PEAK_GBPS, 4),
