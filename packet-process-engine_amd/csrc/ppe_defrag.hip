@@ -428,8 +428,11 @@ __device__ __forceinline__ uint32_t df_group_key(const DfArgs &a, uint32_t i) {
     if (s >= kNone - 1 || a.tstate[s] != kLive) return i;
     return a.creator[s];   // the FCB's first fragment in this batch
 }
-constexpr uint32_t kGroupSlots = 15;      // members besides the key fragment held in a group's slots
-constexpr uint32_t kGroupStride = 16;     // words per group in gslot (64 B)
+#ifndef DF_PROC_WIN
+#define DF_PROC_WIN 16   // the process kernel's register window: the group's head + its slots
+#endif
+constexpr uint32_t kGroupSlots = DF_PROC_WIN - 1;  // members besides the key fragment held in a group's slots
+constexpr uint32_t kGroupStride = DF_PROC_WIN;     // words per group in gslot (64 B at 16)
 
 // One lane per fragment: its group key; a member (key != its index) takes a slot of its group by an atomic ticket
 // (claim order, sorted back into batch order by the group's head in df_process_kernel) while slots remain; past
@@ -503,9 +506,6 @@ __device__ __forceinline__ uint32_t chain_at(uint64_t order, uint32_t pos) { ret
 // slots (one 64-B row; a bitonic network puts them in batch order); (2) the head's parsed record, which carries its
 // FCB record and table slot (df_group_kernel), and the members' parsed records; (3) the FCB header (and, for an FCB
 // from an earlier batch, its chain descriptors).  A group with more members than slots steps them one by one.
-#ifndef DF_PROC_WIN
-#define DF_PROC_WIN 16
-#endif
 constexpr uint32_t kWin = DF_PROC_WIN;
 __device__ __forceinline__ void df_process_one(const DfArgs &a, uint32_t j, uint32_t (*cdesc)[kBlock],
                                                uint32_t (*cidx)[kBlock], uint32_t *st, uint32_t &teardrop) {
