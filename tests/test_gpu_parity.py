@@ -2,6 +2,7 @@
 
 Bar: bit-exact verdict word, flow hash, ACL hit index, 5-tuple and counters (integer work — no tolerance)."""
 import ctypes as C
+import time
 
 import numpy as np
 import pytest
@@ -599,6 +600,59 @@ def test_commit_does_not_wait_for_unrelated_streams(eng):
     torch.cuda.synchronize()
     ref = pyoracle.Oracle(rules, default_action=1).classify_batch(pk["hdr"], pk["len"], cfg=pyoracle.Oracle(
         rules, default_action=1).cfg(0, 1, NOW), nthreads=16)
+    assert np.array_equal(o["verdict"].cpu().numpy().view(np.uint32), ref["verdict"])
+
+
+def test_commit_waits_for_a_queued_reader(eng):
+    """A classify launch reports its completion through a pinned word its last workgroup writes (ppe_kargs.done_*,
+    round 6: no event marker behind each launch).  A commit that rewrites the image slot a launch reads waits for
+    that launch even while it is still queued behind other work on its stream, and the launch classifies with the
+    rules it was queued with."""
+    rules = synth.make_rules(256, seed=101)
+    pk = synth.make_packets(50_000, rules, seed=102, stride=64)
+    th = torch.from_numpy(pk["hdr"]).to(DEV)
+    tl = torch.from_numpy(pk["len"].view(np.int32)).to(DEV)
+    work = torch.cuda.Stream(DEV)
+    eng.commit(rules, default_action=1)
+    o = {k: torch.empty(len(pk["len"]), dtype=torch.int32, device=DEV) for k in ("verdict", "acl_hit")}
+    with torch.cuda.stream(work):
+        torch.cuda._sleep(1_000_000_000)  # the launch below waits behind this on its stream
+        eng.classify_torch(th, tl, o, cfg=eng.cfg(now_seconds=NOW))
+        done = torch.cuda.Event()
+        done.record(work)
+    eng.commit(synth.make_rules(256, seed=103), default_action=0)  # the other slot
+    eng.commit(synth.make_rules(256, seed=104), default_action=0)  # rewrites the slot the queued launch reads
+    # the launch had completed when the commit returned (its stream's next marker follows within microseconds; the
+    # spin ahead of it alone would keep the stream busy for a good fraction of a second)
+    t0 = time.perf_counter()
+    while not done.query() and time.perf_counter() - t0 < 0.05:
+        time.sleep(0.001)
+    assert done.query(), "the commit returned before the launch that reads the slot it rewrote had completed"
+    torch.cuda.synchronize()
+    orc = pyoracle.Oracle(rules, default_action=1)
+    ref = orc.classify_batch(pk["hdr"], pk["len"], cfg=orc.cfg(0, 1, NOW), nthreads=16)
+    assert np.array_equal(o["verdict"].cpu().numpy().view(np.uint32), ref["verdict"])
+    assert np.array_equal(o["acl_hit"].cpu().numpy(), ref["acl_hit"])
+
+
+def test_completion_slots_wrap(eng):
+    """More launches than completion slots (4,096): each launch first waits for its slot's previous one, and the
+    commits after them wait for the last reader; the results stay exact."""
+    rules = synth.make_rules(64, seed=105)
+    pk = synth.make_packets(256, rules, seed=106, stride=64)
+    th = torch.from_numpy(pk["hdr"]).to(DEV)
+    tl = torch.from_numpy(pk["len"].view(np.int32)).to(DEV)
+    eng.commit(rules, default_action=1)
+    o = {k: torch.empty(len(pk["len"]), dtype=torch.int32, device=DEV) for k in ("verdict", "acl_hit")}
+    for _ in range(4200):
+        eng.classify_torch(th, tl, o, cfg=eng.cfg(now_seconds=NOW))
+    eng.commit(synth.make_rules(64, seed=107), default_action=0)
+    eng.commit(rules, default_action=1)
+    r = gpu_classify(eng, pk["hdr"], pk["len"])
+    orc = pyoracle.Oracle(rules, default_action=1)
+    ref = orc.classify_batch(pk["hdr"], pk["len"], cfg=orc.cfg(0, 1, NOW), nthreads=1)
+    assert_same(r, ref, keys=("verdict", "acl_hit", "flow_hash"))
+    torch.cuda.synchronize()
     assert np.array_equal(o["verdict"].cpu().numpy().view(np.uint32), ref["verdict"])
 
 
