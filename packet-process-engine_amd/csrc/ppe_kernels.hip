@@ -1257,9 +1257,14 @@ __device__ __forceinline__ uint32_t flow_find_claim(const ppe_flowdev &f, const 
 // PART: every batch of the launch has the throughput layout (verdict, flow hash and ACL hit written, one partition
 // list, no tile counts, no tuple: ppe_kargs.part_layout), so the output checks are compile-time and the kernel holds
 // fewer scalars (C1 step -2..4 %, C4 -3.5 %: fewer SGPR spills to VGPR lanes)
+#ifndef PPE_CUT_LDS_WAVES  // waves per SIMD the cut-list kernel over a whole-LDS image is compiled for (A/B)
+#define PPE_CUT_LDS_WAVES PPE_WAVES_PER_EU
+#endif
 template <int MODE, int PF, int BLOCK, bool FLOW, bool PART = false>
 __global__ __launch_bounds__(BLOCK, (PF == PF_MULTI && !FLOW) ? PPE_MT_WAVES
-                                                             : (FLOW ? PPE_FLOW_WAVES : PPE_WAVES_PER_EU))
+                                    : FLOW                                       ? PPE_FLOW_WAVES
+                                    : (PF == PF_CUT && MODE == IMG_LDS)          ? PPE_CUT_LDS_WAVES
+                                                                                 : PPE_WAVES_PER_EU)
 void ppe_classify_kernel(ppe_kargs a) {
     // the multi-tile kernel over a whole-LDS image runs the software-pipelined round loop: the next round's windows
     // are requested before the walk (vmcnt retires loads in issue order; the walk and the record check there issue
@@ -2343,24 +2348,29 @@ static int launch_t(const ppe_kargs *a, uint32_t grid, size_t shmem, hipStream_t
                               *a);
     } else if constexpr (M == IMG_LDS && P == PF_HOIST) {  // (the iterative-ILP build, ppe_kernels_hoist.hip)
         return ppe_launch_classify_hoist_lds(a, grid, shmem, B, (void *)s, (void *)e0, (void *)e1);
-    } else {
-        if (a->part_layout && P != PF_NONE)
-            hipExtLaunchKernelGGL((ppe_classify_kernel<M, (P == PF_NONE ? PF_HOIST : P), B, false, true>), dim3(grid),
-                                  dim3(B), shmem, s, e0, e1, 0, *a);
+    } else if constexpr (P != PF_NONE) {
+        if (a->part_layout)
+            hipExtLaunchKernelGGL((ppe_classify_kernel<M, P, B, false, true>), dim3(grid), dim3(B), shmem, s, e0, e1, 0,
+                                  *a);
         else
             hipExtLaunchKernelGGL((ppe_classify_kernel<M, P, B, false>), dim3(grid), dim3(B), shmem, s, e0, e1, 0, *a);
+    } else {
+        hipExtLaunchKernelGGL((ppe_classify_kernel<M, P, B, false>), dim3(grid), dim3(B), shmem, s, e0, e1, 0, *a);
     }
     return (int)hipGetLastError();
 }
 
 template <int M, int P, int B>
 static int occ_t(size_t shmem, bool flow = false) {
-    if constexpr (M == IMG_LDS && P == PF_HOIST)
-        if (!flow) return ppe_occupancy_hoist_lds(shmem, B);
     int nb = 0;
-    const hipError_t e =
-        flow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, PF_HOIST, B, true>, B, shmem)
-             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, P, B, false>, B, shmem);
+    hipError_t e;
+    if (flow) {
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, PF_HOIST, B, true>, B, shmem);
+    } else if constexpr (M == IMG_LDS && P == PF_HOIST) {  // (the iterative-ILP build, ppe_kernels_hoist.hip)
+        return ppe_occupancy_hoist_lds(shmem, B);
+    } else {
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ppe_classify_kernel<M, P, B, false>, B, shmem);
+    }
     return e == hipSuccess ? nb : -1;
 }
 
