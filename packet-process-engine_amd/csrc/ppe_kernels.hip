@@ -1260,10 +1260,14 @@ __device__ __forceinline__ uint32_t flow_find_claim(const ppe_flowdev &f, const 
 #ifndef PPE_CUT_LDS_WAVES  // waves per SIMD the cut-list kernel over a whole-LDS image is compiled for (A/B)
 #define PPE_CUT_LDS_WAVES PPE_WAVES_PER_EU
 #endif
+#ifndef PPE_CUT_SPLIT_WAVES  // the same for split images (entries from L2)
+#define PPE_CUT_SPLIT_WAVES PPE_WAVES_PER_EU
+#endif
 template <int MODE, int PF, int BLOCK, bool FLOW, bool PART = false>
 __global__ __launch_bounds__(BLOCK, (PF == PF_MULTI && !FLOW) ? PPE_MT_WAVES
                                     : FLOW                                       ? PPE_FLOW_WAVES
                                     : (PF == PF_CUT && MODE == IMG_LDS)          ? PPE_CUT_LDS_WAVES
+                                    : (PF == PF_CUT && MODE == IMG_SPLIT)        ? PPE_CUT_SPLIT_WAVES
                                                                                  : PPE_WAVES_PER_EU)
 void ppe_classify_kernel(ppe_kargs a) {
     // the multi-tile kernel over a whole-LDS image runs the software-pipelined round loop: the next round's windows
