@@ -150,17 +150,22 @@ __global__ void __launch_bounds__(kBlock) df_parse_kernel(DfArgs a) {
     const uint32_t tot = a.len[i];
     const uint32_t L = tot & 0xffffu;
     uint32_t valid = 0, l2 = 14, ihl4 = 0, sip = 0, dip = 0, idp = 0, offf = 0, dummy = 0;
-    if (L >= 14) {
-        // the frame's first 40 bytes (Ethernet, a VLAN tag, the IPv4 header's first 20 bytes) as 10 frame-aligned
-        // dwords: 11 aligned loads, all in flight together (not one byte load per field, which the lane's branches
-        // would spread over several round trips), each clamped to the frame's last dword (no read past the frame)
-        const uintptr_t pa = (uintptr_t)p;
-        const uint32_t sh = (uint32_t)(pa & 3u) * 8u;
-        const uint32_t *ap = (const uint32_t *)(pa & ~(uintptr_t)3);
-        const uint32_t lastw = ((uint32_t)(pa & 3u) + L - 1u) >> 2;   // (L >= 14)
-        uint32_t raw[11], fw[10];
+    // the frame's first 40 bytes (Ethernet, a VLAN tag, the IPv4 header's first 20 bytes) as 10 frame-aligned dwords:
+    // 11 aligned loads, all in flight together (not one byte load per field, which the lane's branches would spread
+    // over several round trips), each clamped to the frame's last dword (no read past the frame); issued before the
+    // length test, so the frame offset and length loads go out together too (an empty frame reads its length word)
+    const uintptr_t pa = (uintptr_t)p;
+    const uint32_t sh = (uint32_t)(pa & 3u) * 8u;
+    const uint32_t *ap = L ? (const uint32_t *)(pa & ~(uintptr_t)3) : a.len + i;
+    const uint32_t lastw = L ? ((uint32_t)(pa & 3u) + L - 1u) >> 2 : 0u;
+    uint32_t raw[11];
 #pragma unroll
-        for (uint32_t k = 0; k < 11; ++k) raw[k] = ap[k < lastw ? k : lastw];
+    for (uint32_t k = 0; k < 11; ++k) raw[k] = ap[k < lastw ? k : lastw];
+    // (kept ahead of the branch: the compiler would otherwise sink the loads, and the offset load with them, into it)
+#pragma unroll
+    for (uint32_t k = 0; k < 11; ++k) asm volatile("" ::"v"(raw[k]));
+    if (L >= 14) {
+        uint32_t fw[10];
 #pragma unroll
         for (uint32_t k = 0; k < 10; ++k) fw[k] = sh ? (raw[k] >> sh) | (raw[k + 1] << (32u - sh)) : raw[k];
         auto byte = [&](uint32_t b) -> uint32_t { return (fw[b >> 2] >> (8u * (b & 3u))) & 0xffu; };
@@ -207,10 +212,12 @@ __global__ void __launch_bounds__(kBlock) df_parse_kernel(DfArgs a) {
         // re-reads every slot by CAS.
         uint32_t s = h & a.smask;
         for (uint32_t probe = 0; probe <= a.smask; ++probe, s = (s + 1) & a.smask) {
+            // the slot's state and key read together (one round trip per probe, not two)
             const uint32_t st = a.tstate[s];
+            const uint4 k = *(const uint4 *)(a.tkey + (size_t)s * 4);
+            asm volatile("" ::"v"(k.x), "v"(k.y), "v"(k.z));   // (not sunk into the LIVE branch)
             if (st == kEmpty) break;
             if (st == kLive) {
-                const uint4 k = *(const uint4 *)(a.tkey + (size_t)s * 4);   // one load, not three dependent ones
                 if (k.x == sip && k.y == dip && k.z == (idp & 0xffffu)) {
                     slot = s;
                     break;
