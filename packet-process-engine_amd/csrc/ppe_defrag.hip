@@ -900,20 +900,21 @@ __device__ __forceinline__ void df_assemble_slot(const DfArgs &a, uint32_t j, ui
     // out_len = head frame + the later fragments' payloads (reasm_mb->pkt_totallen, decode-defrag.c:240-266)
     uint32_t out_len = head_tot;
     for (uint32_t p = 1; p < nlist; ++p) out_len += __shfl(cd0, p, 64) >> 16;
+    // the IPv4 header's ten 16-bit words, all loaded in one round and the patch computed without a branch (under an
+    // ICMP branch the compiler issued them in two dependent rounds)
+    uint32_t hw16[10];
+#pragma unroll
+    for (uint32_t q = 0; q < 10; ++q) hw16[q] = ld_be16(hsrc + l2 + 2u * q);
     // header patch (non-ICMP: ip_len = ihl*4 + total, ip_off = 0, checksum; ICMP: ip_off = 0)
-    uint32_t w_iplen = ld_be16(hsrc + l2 + 2), w_csum = ld_be16(hsrc + l2 + 10);
-    if (!icmp && !(DF_AB & 4)) {
-        w_iplen = (ihl4 + total) & 0xffffu;
-        // IPV4CalculateChecksum (decode-ipv4.h:117-163) over the patched header: words 0-4, 6-9, then the options
-        uint32_t cs = ld_be16(hsrc + l2) + w_iplen + ld_be16(hsrc + l2 + 4) + 0u /* ip_off */ + ld_be16(hsrc + l2 + 8) +
-                      ld_be16(hsrc + l2 + 12) + ld_be16(hsrc + l2 + 14) + ld_be16(hsrc + l2 + 16) +
-                      ld_be16(hsrc + l2 + 18);
-        if (ihl4 <= 60)
-            for (uint32_t o = 20; o < ihl4; o += 2) cs += ld_be16(hsrc + l2 + o);
-        cs = (cs >> 16) + (cs & 0xffffu);
-        cs += cs >> 16;
-        w_csum = (~cs) & 0xffffu;
-    }
+    const uint32_t iplen_new = (ihl4 + total) & 0xffffu;
+    // IPV4CalculateChecksum (decode-ipv4.h:117-163) over the patched header: words 0-4, 6-9, then the options
+    uint32_t cs = hw16[0] + iplen_new + hw16[2] + 0u /* ip_off */ + hw16[4] + hw16[6] + hw16[7] + hw16[8] + hw16[9];
+    if (!icmp && ihl4 <= 60)
+        for (uint32_t o = 20; o < ihl4; o += 2) cs += ld_be16(hsrc + l2 + o);
+    cs = (cs >> 16) + (cs & 0xffffu);
+    cs += cs >> 16;
+    const bool fix = !icmp && !(DF_AB & 4);
+    const uint32_t w_iplen = fix ? iplen_new : hw16[1], w_csum = fix ? (~cs) & 0xffffu : hw16[5];
     auto patched = [&](uint32_t b, uint32_t v) -> uint32_t {
         const uint32_t o = b - l2;
         if (b < l2 || o >= 12) return v;
